@@ -1,0 +1,127 @@
+"""ctypes mirrors of the structs declared in include/iggy_codec.h (types only)."""
+from __future__ import annotations
+
+import ctypes
+
+u64 = ctypes.c_uint64
+u32 = ctypes.c_uint32
+
+# iggy_error_kind
+OK = 0
+ERR_UNEXPECTED_EOF = 1
+ERR_VALIDATION = 2
+ERR_INVALID_BATCH_CHECKSUM = 3
+ERR_INVALID_MESSAGE_CHECKSUM = 4
+ERR_INVALID_TIMESTAMP_DELTA = 5
+ERR_PAYLOAD_TOO_LARGE = 6
+ERR_INVALID_NUMBER_ENCODING = 20
+ERR_INVALID_MESSAGE_PAYLOAD_LENGTH = 21
+ERR_DEVICE = 100
+ERR_INVALID_ARGUMENT = 101
+ERR_CAPACITY = 102
+ERR_TIMEOUT = 103
+
+# iggy_validation_reason
+V_NONE = 0
+V_BATCH_LENGTH_SHORT = 1
+V_BATCH_RESERVED = 2
+V_FRAMES_DO_NOT_TILE = 3
+V_FRAME_RESERVED = 4
+V_EMPTY_BATCH = 5
+
+INTEGRITY_VERIFY = 0
+INTEGRITY_LAYOUT_ONLY = 1
+POLL_MODE_SDK = 0
+POLL_MODE_ITERATOR = 1
+
+BATCH_HEADER_SIZE = 256
+FRAME_HEADER_SIZE = 48
+
+
+class WireError(ctypes.Structure):
+    _fields_ = [("kind", u32), ("reason", u32), ("a", u64), ("b", u64), ("c", u64)]
+
+    def astuple(self):
+        return (self.kind, self.reason, self.a, self.b, self.c)
+
+    def __repr__(self):
+        return f"WireError(kind={self.kind}, reason={self.reason}, a={self.a:#x}, b={self.b:#x}, c={self.c:#x})"
+
+
+class BatchHeader(ctypes.Structure):
+    _fields_ = [
+        ("partition_id", u64),
+        ("base_offset", u64),
+        ("base_timestamp", u64),
+        ("origin_timestamp", u64),
+        ("batch_length", u64),
+        ("batch_checksum", u64),
+        ("message_count", u32),
+        ("_pad0", u32),
+        ("_pad1", u64),
+    ]
+
+    def astuple(self):
+        return (self.partition_id, self.base_offset, self.base_timestamp, self.origin_timestamp,
+                self.batch_length, self.batch_checksum, self.message_count)
+
+
+class PolledMessage(ctypes.Structure):
+    _fields_ = [
+        ("checksum", u64),
+        ("id_lo", u64),
+        ("id_hi", u64),
+        ("offset", u64),
+        ("timestamp", u64),
+        ("origin_timestamp", u64),
+        ("payload_pos", u64),
+        ("user_headers_pos", u64),
+        ("payload_length", u32),
+        ("user_headers_length", u32),
+        ("_pad", u64),
+    ]
+
+    def astuple(self):
+        return (self.checksum, self.id_lo, self.id_hi, self.offset, self.timestamp,
+                self.origin_timestamp, self.payload_pos, self.user_headers_pos,
+                self.payload_length, self.user_headers_length)
+
+
+class RawMessages(ctypes.Structure):
+    _fields_ = [
+        ("count", u64),
+        ("ids", ctypes.c_void_p),
+        ("origin_timestamps", ctypes.c_void_p),
+        ("payloads", ctypes.c_void_p),
+        ("payload_lengths", ctypes.c_void_p),
+        ("user_headers", ctypes.c_void_p),
+        ("user_headers_lengths", ctypes.c_void_p),
+    ]
+
+
+class DecodeResult(ctypes.Structure):
+    _fields_ = [
+        ("header", BatchHeader),
+        ("error", WireError),
+        ("frame_count", u64),
+        ("computed_checksum", u64),
+        ("path", u32),
+        ("status", u32),
+        ("_pad", u64),
+    ]
+
+
+class EncodeResult(ctypes.Structure):
+    _fields_ = [
+        ("header", BatchHeader),
+        ("error", WireError),
+        ("batch_length", u64),
+        ("_pad", u64 * 3),
+    ]
+
+
+assert ctypes.sizeof(BatchHeader) == 64
+assert ctypes.sizeof(WireError) == 32
+assert ctypes.sizeof(PolledMessage) == 80
+assert ctypes.sizeof(DecodeResult) == 128
+assert ctypes.sizeof(EncodeResult) == 128

@@ -1,0 +1,275 @@
+/*
+ * iggy_codec.h — C ABI of the MI355X-native Iggy message-batch codec.
+ *
+ * This is the drop-in boundary for Iggy's canonical message batch
+ *
+ *     batch = [batch header: 256 B][frame_0 ... frame_{n-1}]
+ *     frame = [frame header: 48 B][payload][user_headers]
+ *
+ * (reference: core/binary_protocol/src/batch.rs:18-30). Every entry point is
+ * plain C: pointers, sizes, PODs. No torch or HIP types appear in a signature;
+ * streams are passed as `void*` (a hipStream_t, NULL = the context's stream).
+ *
+ * Each function names the reference Rust item it replaces (file:line relative
+ * to the apache/iggy tree). INTEGRATION.md shows the Rust `extern "C"` shim a
+ * maintainer would add so those Rust bodies become thin dispatchers.
+ *
+ * Conventions
+ *  - return value: 0 = Ok; IGGY_ERR_* otherwise. Wire-format failures also
+ *    fill an `iggy_wire_error` that mirrors `WireError`
+ *    (core/binary_protocol/src/error.rs:24-68) field by field.
+ *  - the caller owns every buffer; the library never frees caller memory.
+ *  - host-buffer entry points are synchronous; `_device` entry points take
+ *    device pointers, enqueue on `stream` and return immediately (results land
+ *    in a device-resident result struct).
+ *  - a context is used by one thread at a time (Iggy shards are
+ *    thread-per-core); distinct contexts are independent.
+ *  - there is NO CPU fallback: without a usable gfx950 device
+ *    iggy_codec_create fails with IGGY_ERR_DEVICE.
+ */
+#ifndef IGGY_CODEC_H
+#define IGGY_CODEC_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define IGGY_CODEC_ABI_VERSION 1u
+
+/* batch.rs:38, :41, :44, :47, :50 */
+#define IGGY_BATCH_HEADER_SIZE 256u
+#define IGGY_FRAME_HEADER_SIZE 48u
+#define IGGY_BATCH_CHECKSUM_OFFSET 40u
+#define IGGY_BATCH_MESSAGE_COUNT_OFFSET 48u
+#define IGGY_BATCH_RESERVED_OFFSET 52u
+/* batch.rs:55 */
+#define IGGY_MAX_TIMESTAMP_DELTA_MICROS 0xFFFFFFFFull
+
+/* BatchIntegrity, batch.rs:358-365 */
+typedef enum iggy_batch_integrity {
+    IGGY_INTEGRITY_VERIFY = 0,
+    IGGY_INTEGRITY_LAYOUT_ONLY = 1
+} iggy_batch_integrity;
+
+/* WireError variants used by the path (error.rs:27-70) + library failures. */
+typedef enum iggy_error_kind {
+    IGGY_OK = 0,
+    IGGY_ERR_UNEXPECTED_EOF = 1,            /* a=offset b=need c=have      */
+    IGGY_ERR_VALIDATION = 2,                /* reason = iggy_validation_reason */
+    IGGY_ERR_INVALID_BATCH_CHECKSUM = 3,    /* a=stored b=computed c=base_offset */
+    IGGY_ERR_INVALID_MESSAGE_CHECKSUM = 4,  /* a=stored b=computed c=offset */
+    IGGY_ERR_INVALID_TIMESTAMP_DELTA = 5,   /* a=delta                     */
+    IGGY_ERR_PAYLOAD_TOO_LARGE = 6,         /* a=size b=max                */
+    /* IggyError mapping used by the SDK poll decode (polled_messages.rs:59-60) */
+    IGGY_ERR_INVALID_NUMBER_ENCODING = 20,
+    IGGY_ERR_INVALID_MESSAGE_PAYLOAD_LENGTH = 21,
+    /* library-level failures (not wire errors) */
+    IGGY_ERR_DEVICE = 100,
+    IGGY_ERR_INVALID_ARGUMENT = 101,
+    IGGY_ERR_CAPACITY = 102,  /* output capacity too small; a = required */
+    IGGY_ERR_TIMEOUT = 103    /* a device-side bounded wait gave up (bug guard) */
+} iggy_error_kind;
+
+/* The fixed `WireError::Validation` strings of the path, by id. */
+typedef enum iggy_validation_reason {
+    IGGY_V_NONE = 0,
+    IGGY_V_BATCH_LENGTH_SHORT = 1,   /* "batch length must cover the batch header"        batch.rs:109-111 */
+    IGGY_V_BATCH_RESERVED = 2,       /* "batch header reserved bytes must be zero"        batch.rs:120-122 */
+    IGGY_V_FRAMES_DO_NOT_TILE = 3,   /* "batch frames do not tile message_count exactly"  batch.rs:501-503 */
+    IGGY_V_FRAME_RESERVED = 4,       /* "message frame reserved bytes must be zero"       batch.rs:255-257 */
+    IGGY_V_EMPTY_BATCH = 5           /* "cannot encode an empty message batch"  send_messages.rs:97-99 */
+} iggy_validation_reason;
+
+typedef struct iggy_wire_error {
+    uint32_t kind;    /* iggy_error_kind */
+    uint32_t reason;  /* iggy_validation_reason when kind == IGGY_ERR_VALIDATION */
+    uint64_t a, b, c;
+} iggy_wire_error;
+
+/* BatchHeader (batch.rs:64-73). 64 bytes, little-endian host order. */
+typedef struct iggy_batch_header {
+    uint64_t partition_id;
+    uint64_t base_offset;
+    uint64_t base_timestamp;
+    uint64_t origin_timestamp;
+    uint64_t batch_length;
+    uint64_t batch_checksum;
+    uint32_t message_count;
+    uint32_t _pad0;
+    uint64_t _pad1;
+} iggy_batch_header;
+
+/* One polled message, deltas resolved (IggyMessageHeader + payload/user
+ * header ranges; polled_messages.rs:121-143, poll_messages.rs:75-86).
+ * Positions are byte offsets into the caller's input buffer (zero-copy
+ * views, like Bytes::slice). 80 bytes. */
+typedef struct iggy_polled_message {
+    uint64_t checksum;
+    uint64_t id_lo, id_hi;      /* u128 id, little-endian halves */
+    uint64_t offset;            /* base_offset + offset_delta */
+    uint64_t timestamp;         /* base_timestamp (flat per batch) */
+    uint64_t origin_timestamp;  /* origin_timestamp + timestamp_delta */
+    uint64_t payload_pos;
+    uint64_t user_headers_pos;
+    uint32_t payload_length;
+    uint32_t user_headers_length;
+    uint64_t _pad;
+} iggy_polled_message;
+
+/* Encoder input, struct-of-arrays form of `&[RawMessage]`
+ * (requests/messages/send_messages.rs:37-42). Pointers are host pointers for
+ * iggy_codec_encode_batch and device pointers for the _device variant.
+ * payloads / user_headers are the concatenation of every message's bytes in
+ * message order; user_headers and user_headers_lengths may be NULL (= none). */
+typedef struct iggy_raw_messages {
+    uint64_t count;
+    const uint64_t *ids;                 /* 2*count u64: id_lo, id_hi per message */
+    const uint64_t *origin_timestamps;   /* count */
+    const uint8_t *payloads;
+    const uint32_t *payload_lengths;     /* count */
+    const uint8_t *user_headers;
+    const uint32_t *user_headers_lengths;/* count */
+} iggy_raw_messages;
+
+/* Device-resident result of an asynchronous decode. */
+typedef struct iggy_decode_result {
+    iggy_batch_header header;
+    iggy_wire_error error;
+    uint64_t frame_count;        /* frames walked (== message_count on success) */
+    uint64_t computed_checksum;  /* recomputed batch checksum (Verify) */
+    uint32_t path;               /* 1 = uniform-stride kernel, 2 = general walk */
+    uint32_t status;             /* 0 = done; internal otherwise */
+    uint64_t _pad;
+} iggy_decode_result;
+
+/* Device-resident result of an asynchronous encode. */
+typedef struct iggy_encode_result {
+    iggy_batch_header header;
+    iggy_wire_error error;
+    uint64_t batch_length;
+    uint64_t _pad[3];
+} iggy_encode_result;
+
+typedef struct iggy_codec_ctx iggy_codec_ctx;
+
+/* ---------------------------------------------------------------- context */
+uint32_t iggy_codec_abi_version(void);
+/* Binds a context to HIP device `device`, creates its stream and scratch.
+ * Fails with IGGY_ERR_DEVICE when no gfx950 device is usable. */
+int iggy_codec_create(int device, iggy_codec_ctx **out);
+void iggy_codec_destroy(iggy_codec_ctx *ctx);
+/* Pre-size device scratch for batches up to max_batch_bytes (optional;
+ * otherwise grown on demand outside the enqueue path). */
+int iggy_codec_reserve(iggy_codec_ctx *ctx, uint64_t max_batch_bytes, uint64_t max_frames);
+/* The context's own stream (hipStream_t as void*). */
+void *iggy_codec_stream(iggy_codec_ctx *ctx);
+/* Blocks until every operation enqueued on the context's stream is done. */
+int iggy_codec_synchronize(iggy_codec_ctx *ctx);
+
+/* ------------------------------------------------------------ pure host */
+/* BatchHeader::decode (batch.rs:98-134) — 256 bytes, no device work. */
+int iggy_batch_header_decode(const uint8_t *bytes, uint64_t len,
+                             iggy_batch_header *out, iggy_wire_error *err);
+/* BatchHeader::encode_into (batch.rs:138-150). */
+void iggy_batch_header_encode(const iggy_batch_header *h, uint8_t out[256]);
+/* SendMessagesEncoder::encoded_size, batch part (send_messages.rs:69-79). */
+uint64_t iggy_encoded_batch_size(const iggy_raw_messages *msgs);
+
+/* ------------------------------------------------- synchronous (host I/O) */
+/* XxHash3_64::oneshot / calculate_checksum (common/src/utils/checksum.rs:20). */
+int iggy_codec_xxh3_64(iggy_codec_ctx *ctx, const void *data, uint64_t len, uint64_t *out);
+
+/* decode_batch_slice_with (batch.rs:391-422). On Ok, fills *hdr and, if
+ * frame_pos != NULL, the blob-relative start of every frame (up to cap;
+ * IGGY_ERR_CAPACITY if more). `body` may extend past batch_length. */
+int iggy_codec_decode_batch(iggy_codec_ctx *ctx, const uint8_t *body, uint64_t len,
+                            int integrity, iggy_batch_header *hdr,
+                            uint64_t *frame_pos, uint64_t cap, uint64_t *nframes,
+                            iggy_wire_error *err);
+
+/* verify_and_recompute_batch_checksum (batch.rs:474-506). */
+int iggy_codec_verify_and_recompute_batch_checksum(iggy_codec_ctx *ctx,
+                                                   const iggy_batch_header *hdr,
+                                                   const uint8_t *blob, uint64_t blob_len,
+                                                   uint64_t *out, iggy_wire_error *err);
+
+/* calculate_batch_checksum (batch.rs:439-450): frames found by the infallible
+ * walk (BatchIteratorWithOffsets, batch.rs:329-355). */
+int iggy_codec_calculate_batch_checksum(iggy_codec_ctx *ctx, const iggy_batch_header *hdr,
+                                        const uint8_t *blob, uint64_t blob_len,
+                                        uint64_t *out);
+
+/* SendMessagesEncoder::encode batch section (send_messages.rs:89-181) when
+ * partition_id == 0; SendMessagesOwned::from_messages
+ * (server_common/src/send_messages.rs:104-168) with a namespace partition id
+ * otherwise (ids of 0 are NOT minted here: the caller mints, as the SDK does
+ * at common/src/traits/binary_impls/messages.rs:343-347). `out` must hold
+ * iggy_encoded_batch_size(msgs) bytes. */
+int iggy_codec_encode_batch(iggy_codec_ctx *ctx, const iggy_raw_messages *msgs,
+                            uint64_t partition_id, uint8_t *out, uint64_t cap,
+                            uint64_t *out_len, iggy_wire_error *err);
+
+/* Poll-side decode of a stream of batch records (the body after the 16-byte
+ * PollMessages prefix).
+ *  mode 0 = SDK PolledMessages::messages_from_batches
+ *           (common/src/types/message/polled_messages.rs:95-150):
+ *           errors -> IGGY_ERR_INVALID_MESSAGE_PAYLOAD_LENGTH, no count check.
+ *  mode 1 = PolledBatchesIterator (responses/messages/poll_messages.rs:95-165):
+ *           each record decoded LayoutOnly; the first framing error is
+ *           returned after the messages yielded before it (*n is set). */
+#define IGGY_POLL_MODE_SDK 0
+#define IGGY_POLL_MODE_ITERATOR 1
+int iggy_codec_poll_decode(iggy_codec_ctx *ctx, const uint8_t *records, uint64_t len,
+                           int mode, iggy_polled_message *out, uint64_t cap,
+                           uint64_t *n, iggy_wire_error *err);
+
+/* stamp_prepare_for_persistence core (server_common/src/send_messages.rs:642-663):
+ * write base_offset/base_timestamp into the batch header at `batch` and
+ * recompute batch_checksum over its blob. */
+int iggy_codec_stamp_batch(iggy_codec_ctx *ctx, uint8_t *batch, uint64_t len,
+                           uint64_t base_offset, uint64_t base_timestamp,
+                           iggy_batch_header *out, iggy_wire_error *err);
+
+/* ------------------------------------------- asynchronous (device memory) */
+/* decode_batch_slice_with on a device-resident record. Enqueues the whole
+ * decode on `stream`; the outcome lands in *d_result (device memory). */
+int iggy_codec_decode_batch_device(iggy_codec_ctx *ctx, const uint8_t *d_body, uint64_t len,
+                                   int integrity, uint64_t *d_frame_pos, uint64_t cap,
+                                   iggy_decode_result *d_result, void *stream);
+
+/* SendMessagesEncoder::encode on device-resident SoA input (all pointers in
+ * *msgs are device pointers; *msgs itself is a host struct). */
+int iggy_codec_encode_batch_device(iggy_codec_ctx *ctx, const iggy_raw_messages *msgs,
+                                   uint64_t partition_id, uint8_t *d_out, uint64_t cap,
+                                   iggy_encode_result *d_result, void *stream);
+
+/* Batch checksum of a device-resident, already-validated record whose frame
+ * starts are known (d_frame_pos, blob-relative); header fields from *hdr.
+ * Writes the u64 to *d_out. Used by stamp (a17) and slicing (journal.rs:1119). */
+int iggy_codec_batch_checksum_device(iggy_codec_ctx *ctx, const iggy_batch_header *hdr,
+                                     const uint8_t *d_blob, const uint64_t *d_frame_pos,
+                                     uint64_t nframes, uint64_t *d_out, void *stream);
+
+/* XXH3-64 of n independent byte ranges of d_data (offsets u64, lengths u32). */
+int iggy_codec_xxh3_64_ranges_device(iggy_codec_ctx *ctx, const uint8_t *d_data,
+                                     const uint64_t *d_offsets, const uint32_t *d_lengths,
+                                     uint64_t n, uint64_t *d_out, void *stream);
+
+/* ------------------------------------------------------------- profiling */
+/* When enabled, the context brackets the dominant kernel of every decode /
+ * encode with hipEvents on the launch stream and accumulates its duration. */
+int iggy_codec_profile_enable(iggy_codec_ctx *ctx, int enable);
+/* Returns the number of bracketed launches and their summed duration (ms)
+ * for `which` (0 = decode main kernel, 1 = encode main kernel), then resets. */
+int iggy_codec_profile_read(iggy_codec_ctx *ctx, int which, uint64_t *launches, double *total_ms);
+
+/* Human-readable text for an error kind / validation reason. */
+const char *iggy_codec_error_string(uint32_t kind, uint32_t reason);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* IGGY_CODEC_H */

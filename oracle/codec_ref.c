@@ -1,0 +1,468 @@
+/*
+ * codec_ref.c — TEST INFRASTRUCTURE ONLY (see oracle.h).
+ *
+ * Plain-C restatement of the reference message-batch walks, one function per
+ * reference item, each citing the file:line it follows (paths relative to the
+ * apache/iggy tree). Serial, byte-at-a-time semantics exactly as the Rust
+ * code: this is the checker the HIP path is compared against.
+ */
+#include "oracle.h"
+#include <stdlib.h>
+#include <string.h>
+
+#define HDR 256u
+#define FHDR 48u
+
+static inline uint64_t rd64(const uint8_t *p) { uint64_t v; memcpy(&v, p, 8); return v; }
+static inline uint32_t rd32(const uint8_t *p) { uint32_t v; memcpy(&v, p, 4); return v; }
+static inline void wr64(uint8_t *p, uint64_t v) { memcpy(p, &v, 8); }
+static inline void wr32(uint8_t *p, uint32_t v) { memcpy(p, &v, 4); }
+
+static void set_err(iggy_wire_error *e, uint32_t kind, uint32_t reason, uint64_t a, uint64_t b,
+                    uint64_t c) {
+    if (!e) return;
+    e->kind = kind; e->reason = reason; e->a = a; e->b = b; e->c = c;
+}
+
+/* BatchHeader::decode — batch.rs:98-134 */
+int oracle_batch_header_decode(const uint8_t *b, uint64_t len, iggy_batch_header *h,
+                               iggy_wire_error *e) {
+    set_err(e, IGGY_OK, 0, 0, 0, 0);
+    if (len < HDR) {
+        set_err(e, IGGY_ERR_UNEXPECTED_EOF, 0, 0, HDR, len);
+        return IGGY_ERR_UNEXPECTED_EOF;
+    }
+    uint64_t batch_length = rd64(b + 32);
+    if (batch_length < HDR) { /* checked before the reserved bytes (batch.rs:108) */
+        set_err(e, IGGY_ERR_VALIDATION, IGGY_V_BATCH_LENGTH_SHORT, 0, 0, 0);
+        return IGGY_ERR_VALIDATION;
+    }
+    for (uint32_t i = IGGY_BATCH_RESERVED_OFFSET; i < HDR; i++) {
+        if (b[i] != 0) {
+            set_err(e, IGGY_ERR_VALIDATION, IGGY_V_BATCH_RESERVED, 0, 0, 0);
+            return IGGY_ERR_VALIDATION;
+        }
+    }
+    memset(h, 0, sizeof(*h));
+    h->partition_id = rd64(b + 0);
+    h->base_offset = rd64(b + 8);
+    h->base_timestamp = rd64(b + 16);
+    h->origin_timestamp = rd64(b + 24);
+    h->batch_length = batch_length;
+    h->batch_checksum = rd64(b + 40);
+    h->message_count = rd32(b + 48);
+    return 0;
+}
+
+/* BatchHeader::encode_into — batch.rs:138-150 */
+void oracle_batch_header_encode(const iggy_batch_header *h, uint8_t *out) {
+    memset(out, 0, HDR);
+    wr64(out + 0, h->partition_id);
+    wr64(out + 8, h->base_offset);
+    wr64(out + 16, h->base_timestamp);
+    wr64(out + 24, h->origin_timestamp);
+    wr64(out + 32, h->batch_length);
+    wr64(out + 40, h->batch_checksum);
+    wr32(out + 48, h->message_count);
+}
+
+/* One step of BatchIteratorWithOffsets::next — batch.rs:332-354.
+ * Returns 1 and the frame extent on success, 0 when the walk stops. */
+static int walk_next(const uint8_t *blob, uint64_t blob_len, uint64_t pos, uint64_t *end,
+                     uint32_t *pl, uint32_t *uh) {
+    if (pos >= blob_len) return 0;
+    if (blob_len - pos < FHDR) return 0;                  /* BatchMessageHeader::decode EOF */
+    if (rd64(blob + pos + 40) != 0) return 0;             /* reserved, batch.rs:254 */
+    uint32_t p = rd32(blob + pos + 36), u = rd32(blob + pos + 32);
+    uint64_t payload_end = pos + FHDR + p;                 /* batch.rs:340 */
+    uint64_t headers_end = payload_end + u;                /* batch.rs:341 */
+    if (payload_end > blob_len) return 0;                  /* blob.get(..)? */
+    if (headers_end > blob_len) return 0;
+    *end = headers_end;
+    *pl = p; *uh = u;
+    return 1;
+}
+
+/* Batch checksum input = header fields (44 B) || stored checksum of every
+ * walked frame; streaming XXH3 == one-shot over the concatenation
+ * (batch.rs:439-459; pinned by server_common/src/send_messages.rs:833-871). */
+static uint64_t hash_checksum_stream(const iggy_batch_header *h, const uint8_t *blob,
+                                     const uint64_t *starts, uint64_t n) {
+    uint64_t total = 44 + 8 * n;
+    uint8_t *buf = (uint8_t *)malloc(total ? total : 1);
+    wr64(buf + 0, h->partition_id);
+    wr64(buf + 8, h->base_offset);
+    wr64(buf + 16, h->base_timestamp);
+    wr64(buf + 24, h->origin_timestamp);
+    wr64(buf + 32, h->batch_length);
+    wr32(buf + 40, h->message_count);
+    for (uint64_t i = 0; i < n; i++) memcpy(buf + 44 + 8 * i, blob + starts[i], 8);
+    uint64_t r = oracle_xxh3_64(buf, total);
+    free(buf);
+    return r;
+}
+
+/* calculate_batch_checksum — batch.rs:439-450 (infallible walk) */
+uint64_t oracle_calculate_batch_checksum(const iggy_batch_header *h, const uint8_t *blob,
+                                         uint64_t blob_len) {
+    uint64_t cap = blob_len / FHDR + 1, n = 0, pos = 0, end;
+    uint32_t pl, uh;
+    uint64_t *starts = (uint64_t *)malloc(cap * sizeof(uint64_t));
+    while (walk_next(blob, blob_len, pos, &end, &pl, &uh)) {
+        starts[n++] = pos;
+        pos = end;
+    }
+    uint64_t r = hash_checksum_stream(h, blob, starts, n);
+    free(starts);
+    return r;
+}
+
+/* verify_and_recompute_batch_checksum — batch.rs:474-506 */
+int oracle_verify_and_recompute(const iggy_batch_header *h, const uint8_t *blob,
+                                uint64_t blob_len, uint64_t *out, uint64_t *frame_pos,
+                                uint64_t cap, uint64_t *nframes, iggy_wire_error *e) {
+    set_err(e, IGGY_OK, 0, 0, 0, 0);
+    uint64_t scap = blob_len / FHDR + 1, n = 0, pos = 0, end, covered = 0;
+    uint32_t pl, uh;
+    uint64_t *starts = (uint64_t *)malloc(scap * sizeof(uint64_t));
+    while (walk_next(blob, blob_len, pos, &end, &pl, &uh)) {
+        uint64_t stored = rd64(blob + pos);
+        uint64_t expected = oracle_xxh3_64(blob + pos + 8, end - pos - 8);  /* :485 */
+        if (expected != stored) {
+            uint32_t od = rd32(blob + pos + 24);
+            uint64_t off = h->base_offset + od;
+            if (off < h->base_offset) off = UINT64_MAX;  /* saturating_add, :490-493 */
+            set_err(e, IGGY_ERR_INVALID_MESSAGE_CHECKSUM, 0, stored, expected, off);
+            free(starts);
+            return IGGY_ERR_INVALID_MESSAGE_CHECKSUM;
+        }
+        starts[n++] = pos;
+        covered = end;
+        pos = end;
+    }
+    /* verified is a u32 in the reference (:478); n <= blob_len/48 < 2^32 here */
+    if (n != (uint64_t)h->message_count || covered != blob_len) {
+        set_err(e, IGGY_ERR_VALIDATION, IGGY_V_FRAMES_DO_NOT_TILE, 0, 0, 0);
+        free(starts);
+        return IGGY_ERR_VALIDATION;
+    }
+    if (out) *out = hash_checksum_stream(h, blob, starts, n);
+    if (frame_pos) {
+        for (uint64_t i = 0; i < n && i < cap; i++) frame_pos[i] = starts[i];
+    }
+    if (nframes) *nframes = n;
+    free(starts);
+    return 0;
+}
+
+/* validate_batch_layout — batch.rs:513-527 */
+static int validate_layout(const iggy_batch_header *h, const uint8_t *blob, uint64_t blob_len,
+                           uint64_t *frame_pos, uint64_t cap, uint64_t *nframes,
+                           iggy_wire_error *e) {
+    uint64_t n = 0, pos = 0, end, covered = 0;
+    uint32_t pl, uh;
+    while (walk_next(blob, blob_len, pos, &end, &pl, &uh)) {
+        if (frame_pos && n < cap) frame_pos[n] = pos;
+        n++;
+        covered = end;
+        pos = end;
+    }
+    if (n != (uint64_t)h->message_count || covered != blob_len) {
+        set_err(e, IGGY_ERR_VALIDATION, IGGY_V_FRAMES_DO_NOT_TILE, 0, 0, 0);
+        return IGGY_ERR_VALIDATION;
+    }
+    if (nframes) *nframes = n;
+    return 0;
+}
+
+/* decode_batch_slice_with — batch.rs:391-422 */
+int oracle_decode_batch_slice_with(const uint8_t *body, uint64_t len, int integrity,
+                                   iggy_batch_header *h, uint64_t *frame_pos, uint64_t cap,
+                                   uint64_t *nframes, iggy_wire_error *e) {
+    int rc = oracle_batch_header_decode(body, len, h, e);
+    if (rc) return rc;
+    /* blob_len() cannot fail after decode (batch_length >= 256). */
+    if (len < h->batch_length) {
+        set_err(e, IGGY_ERR_UNEXPECTED_EOF, 0, 0, h->batch_length, len);
+        return IGGY_ERR_UNEXPECTED_EOF;
+    }
+    const uint8_t *blob = body + HDR;
+    uint64_t blob_len = h->batch_length - HDR;
+    if (integrity == IGGY_INTEGRITY_VERIFY) {
+        uint64_t computed = 0;
+        rc = oracle_verify_and_recompute(h, blob, blob_len, &computed, frame_pos, cap, nframes, e);
+        if (rc) return rc;
+        if (h->batch_checksum != computed) {
+            set_err(e, IGGY_ERR_INVALID_BATCH_CHECKSUM, 0, h->batch_checksum, computed,
+                    h->base_offset);
+            return IGGY_ERR_INVALID_BATCH_CHECKSUM;
+        }
+        return 0;
+    }
+    return validate_layout(h, blob, blob_len, frame_pos, cap, nframes, e);
+}
+
+/* SendMessagesEncoder::encoded_size batch part — send_messages.rs:69-79 */
+uint64_t oracle_encoded_batch_size(const iggy_raw_messages *m) {
+    uint64_t total = HDR;
+    for (uint64_t i = 0; i < m->count; i++)
+        total += FHDR + m->payload_lengths[i] +
+                 (m->user_headers_lengths ? m->user_headers_lengths[i] : 0);
+    return total;
+}
+
+/* SendMessagesEncoder::encode, batch section — send_messages.rs:89-181
+ * (partition_id != 0: SendMessagesOwned::from_messages,
+ *  server_common/src/send_messages.rs:104-168). */
+int oracle_encode_batch(const iggy_raw_messages *m, uint64_t partition_id, uint8_t *out,
+                        uint64_t cap, uint64_t *out_len, iggy_wire_error *e) {
+    set_err(e, IGGY_OK, 0, 0, 0, 0);
+    if (m->count == 0) {
+        set_err(e, IGGY_ERR_VALIDATION, IGGY_V_EMPTY_BATCH, 0, 0, 0);
+        return IGGY_ERR_VALIDATION;
+    }
+    if (m->count > 0xFFFFFFFFull) {
+        set_err(e, IGGY_ERR_PAYLOAD_TOO_LARGE, 0, m->count, 0xFFFFFFFFull, 0);
+        return IGGY_ERR_PAYLOAD_TOO_LARGE;
+    }
+    uint64_t origin = UINT64_MAX; /* min origin timestamp, :119-123 */
+    for (uint64_t i = 0; i < m->count; i++)
+        if (m->origin_timestamps[i] < origin) origin = m->origin_timestamps[i];
+    uint64_t need = oracle_encoded_batch_size(m);
+    if (need > cap) {
+        set_err(e, IGGY_ERR_CAPACITY, 0, need, cap, 0);
+        return IGGY_ERR_CAPACITY;
+    }
+    uint64_t pos = HDR, psrc = 0, usrc = 0;
+    uint64_t *starts = (uint64_t *)malloc(m->count * sizeof(uint64_t));
+    for (uint64_t i = 0; i < m->count; i++) { /* hot loop :131-164 */
+        uint64_t delta = m->origin_timestamps[i] - origin;
+        if (delta > IGGY_MAX_TIMESTAMP_DELTA_MICROS) {
+            set_err(e, IGGY_ERR_INVALID_TIMESTAMP_DELTA, 0, delta, 0, 0);
+            free(starts);
+            return IGGY_ERR_INVALID_TIMESTAMP_DELTA;
+        }
+        uint32_t pl = m->payload_lengths[i];
+        uint32_t uh = m->user_headers_lengths ? m->user_headers_lengths[i] : 0;
+        uint8_t *f = out + pos;
+        wr64(f + 0, 0);
+        wr64(f + 8, m->ids[2 * i]);
+        wr64(f + 16, m->ids[2 * i + 1]);
+        wr32(f + 24, (uint32_t)i);
+        wr32(f + 28, (uint32_t)delta);
+        wr32(f + 32, uh);
+        wr32(f + 36, pl);
+        wr64(f + 40, 0);
+        memcpy(f + FHDR, m->payloads + psrc, pl); /* payload before user headers, :159-160 */
+        if (uh) memcpy(f + FHDR + pl, m->user_headers + usrc, uh);
+        psrc += pl;
+        usrc += uh;
+        wr64(f, oracle_xxh3_64(f + 8, 40 + (uint64_t)pl + uh)); /* :162-163 */
+        starts[i] = pos - HDR;
+        pos += FHDR + (uint64_t)pl + uh;
+    }
+    /* The SDK caps the batch at u32::MAX (:166-174); the server twin does not. */
+    if (partition_id == 0 && pos > 0xFFFFFFFFull) {
+        set_err(e, IGGY_ERR_PAYLOAD_TOO_LARGE, 0, pos, 0xFFFFFFFFull, 0);
+        free(starts);
+        return IGGY_ERR_PAYLOAD_TOO_LARGE;
+    }
+    iggy_batch_header h;
+    memset(&h, 0, sizeof(h));
+    h.partition_id = partition_id;
+    h.origin_timestamp = origin;
+    h.batch_length = pos;
+    h.message_count = (uint32_t)m->count;
+    h.batch_checksum = hash_checksum_stream(&h, out + HDR, starts, m->count); /* :177 */
+    oracle_batch_header_encode(&h, out);
+    free(starts);
+    if (out_len) *out_len = pos;
+    return 0;
+}
+
+/* Poll decode.
+ * mode SDK:      PolledMessages::messages_from_batches, polled_messages.rs:95-150
+ * mode ITERATOR: PolledBatchesIterator, poll_messages.rs:95-165 */
+int oracle_poll_decode(const uint8_t *buf, uint64_t len, int mode, iggy_polled_message *out,
+                       uint64_t cap, uint64_t *n_out, iggy_wire_error *e) {
+    set_err(e, IGGY_OK, 0, 0, 0, 0);
+    uint64_t n = 0, position = 0;
+    if (n_out) *n_out = 0;
+    while (position < len) {
+        iggy_batch_header h;
+        iggy_wire_error he;
+        if (mode == IGGY_POLL_MODE_SDK) {
+            if (oracle_batch_header_decode(buf + position, len - position, &h, &he)) {
+                set_err(e, IGGY_ERR_INVALID_MESSAGE_PAYLOAD_LENGTH, 0, 0, 0, 0);
+                return IGGY_ERR_INVALID_MESSAGE_PAYLOAD_LENGTH;
+            }
+            uint64_t batch_end = position + h.batch_length;
+            if (batch_end < position || batch_end > len) { /* checked_add + filter, :103-106 */
+                set_err(e, IGGY_ERR_INVALID_MESSAGE_PAYLOAD_LENGTH, 0, 0, 0, 0);
+                return IGGY_ERR_INVALID_MESSAGE_PAYLOAD_LENGTH;
+            }
+            uint64_t cursor = position + HDR;
+            while (cursor < batch_end) {
+                if (batch_end - cursor < FHDR || rd64(buf + cursor + 40) != 0) {
+                    set_err(e, IGGY_ERR_INVALID_MESSAGE_PAYLOAD_LENGTH, 0, 0, 0, 0);
+                    return IGGY_ERR_INVALID_MESSAGE_PAYLOAD_LENGTH;
+                }
+                const uint8_t *f = buf + cursor;
+                uint32_t pl = rd32(f + 36), uh = rd32(f + 32);
+                uint64_t ps = cursor + FHDR, pe = ps + pl, ue = pe + uh;
+                if (ue > batch_end) {
+                    set_err(e, IGGY_ERR_INVALID_MESSAGE_PAYLOAD_LENGTH, 0, 0, 0, 0);
+                    return IGGY_ERR_INVALID_MESSAGE_PAYLOAD_LENGTH;
+                }
+                if (n >= cap) {
+                    set_err(e, IGGY_ERR_CAPACITY, 0, n + 1, cap, 0);
+                    return IGGY_ERR_CAPACITY;
+                }
+                iggy_polled_message *m = &out[n++];
+                memset(m, 0, sizeof(*m));
+                m->checksum = rd64(f);
+                m->id_lo = rd64(f + 8);
+                m->id_hi = rd64(f + 16);
+                m->offset = h.base_offset + rd32(f + 24);          /* wrapping in release */
+                m->timestamp = h.base_timestamp;
+                m->origin_timestamp = h.origin_timestamp + rd32(f + 28);
+                m->payload_pos = ps;
+                m->payload_length = pl;
+                m->user_headers_pos = pe;
+                m->user_headers_length = uh;
+                cursor = ue;
+                if (n_out) *n_out = n;
+            }
+            position = batch_end;
+        } else {
+            uint64_t tmpn = 0;
+            /* advance_batch: decode_batch_slice_with(LayoutOnly), poll_messages.rs:115-129 */
+            int rc = oracle_decode_batch_slice_with(buf + position, len - position,
+                                                    IGGY_INTEGRITY_LAYOUT_ONLY, &h, NULL, 0,
+                                                    &tmpn, e);
+            if (rc) return rc;
+            const uint8_t *blob = buf + position + HDR;
+            uint64_t blob_len = h.batch_length - HDR, pos = 0, end;
+            uint32_t pl, uh;
+            while (walk_next(blob, blob_len, pos, &end, &pl, &uh)) {
+                if (n >= cap) {
+                    set_err(e, IGGY_ERR_CAPACITY, 0, n + 1, cap, 0);
+                    return IGGY_ERR_CAPACITY;
+                }
+                const uint8_t *f = blob + pos;
+                iggy_polled_message *m = &out[n++];
+                memset(m, 0, sizeof(*m));
+                m->checksum = rd64(f);
+                m->id_lo = rd64(f + 8);
+                m->id_hi = rd64(f + 16);
+                m->offset = h.base_offset + rd32(f + 24);
+                m->timestamp = h.base_timestamp;
+                m->origin_timestamp = h.origin_timestamp + rd32(f + 28);
+                m->payload_pos = position + HDR + pos + FHDR;
+                m->payload_length = pl;
+                m->user_headers_pos = m->payload_pos + pl;
+                m->user_headers_length = uh;
+                if (n_out) *n_out = n;
+                pos = end;
+            }
+            position += h.batch_length;
+        }
+    }
+    if (n_out) *n_out = n;
+    return 0;
+}
+
+/* stamp_prepare_for_persistence core — server_common/src/send_messages.rs:642-663 */
+int oracle_stamp_batch(uint8_t *batch, uint64_t len, uint64_t base_offset,
+                       uint64_t base_timestamp, iggy_batch_header *out, iggy_wire_error *e) {
+    iggy_batch_header h;
+    int rc = oracle_batch_header_decode(batch, len, &h, e);
+    if (rc) return rc;
+    if (len < h.batch_length) {
+        set_err(e, IGGY_ERR_UNEXPECTED_EOF, 0, 0, h.batch_length, len);
+        return IGGY_ERR_UNEXPECTED_EOF;
+    }
+    h.base_offset = base_offset;
+    h.base_timestamp = base_timestamp;
+    h.batch_checksum = oracle_calculate_batch_checksum(&h, batch + HDR, h.batch_length - HDR);
+    oracle_batch_header_encode(&h, batch);
+    if (out) *out = h;
+    return 0;
+}
+
+/* ---------------------------------------------------- synthetic inputs */
+static inline uint64_t splitmix64(uint64_t *s) {
+    uint64_t z = (*s += 0x9E3779B97F4A7C15ull);
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+static uint32_t synth_pl(uint64_t *s, uint32_t lo, uint32_t hi) {
+    if (hi <= lo) return lo;
+    return lo + (uint32_t)(splitmix64(s) % ((uint64_t)hi - lo + 1));
+}
+
+uint64_t oracle_synth_batch_size(uint64_t n, uint32_t pl_min, uint32_t pl_max, uint32_t uh_len,
+                                 uint64_t seed) {
+    uint64_t s = seed ^ 0x5151515151515151ull, total = HDR;
+    for (uint64_t i = 0; i < n; i++) total += FHDR + synth_pl(&s, pl_min, pl_max) + uh_len;
+    return total;
+}
+
+uint64_t oracle_synth_batch(uint8_t *out, uint64_t cap, uint64_t n, uint32_t pl_min,
+                            uint32_t pl_max, uint32_t uh_len, uint64_t seed,
+                            uint64_t partition_id) {
+    uint64_t total = oracle_synth_batch_size(n, pl_min, pl_max, uh_len, seed);
+    if (total > cap) return 0;
+    uint64_t sl = seed ^ 0x5151515151515151ull; /* lengths stream (same as _size) */
+    uint64_t sd = seed;                          /* data stream */
+    const uint64_t origin0 = 1700000000000000ull;
+    uint64_t pos = HDR;
+    uint64_t *starts = (uint64_t *)malloc((n ? n : 1) * sizeof(uint64_t));
+    for (uint64_t i = 0; i < n; i++) {
+        uint32_t pl = synth_pl(&sl, pl_min, pl_max);
+        uint8_t *f = out + pos;
+        uint64_t idlo = splitmix64(&sd), idhi = splitmix64(&sd);
+        if ((idlo | idhi) == 0) idlo = 1;
+        wr64(f + 8, idlo);
+        wr64(f + 16, idhi);
+        wr32(f + 24, (uint32_t)i);
+        wr32(f + 28, (uint32_t)i); /* origin_ts_i = origin0 + i */
+        wr32(f + 32, uh_len);
+        wr32(f + 36, pl);
+        wr64(f + 40, 0);
+        uint8_t *d = f + FHDR;
+        uint32_t body = pl + uh_len, k = 0;
+        for (; k + 8 <= body; k += 8) wr64(d + k, splitmix64(&sd));
+        if (k < body) {
+            uint64_t r = splitmix64(&sd);
+            memcpy(d + k, &r, body - k);
+        }
+        wr64(f, oracle_xxh3_64_fast(f + 8, 40 + (uint64_t)body));
+        starts[i] = pos - HDR;
+        pos += FHDR + body;
+    }
+    iggy_batch_header h;
+    memset(&h, 0, sizeof(h));
+    h.partition_id = partition_id;
+    h.base_offset = 0;
+    h.base_timestamp = origin0 + 1000;
+    h.origin_timestamp = origin0;
+    h.batch_length = pos;
+    h.message_count = (uint32_t)n;
+    /* fast streaming-equivalent: one-shot over the 44 + 8n concatenation */
+    {
+        uint64_t tl = 44 + 8 * n;
+        uint8_t *buf = (uint8_t *)malloc(tl);
+        wr64(buf + 0, h.partition_id); wr64(buf + 8, h.base_offset);
+        wr64(buf + 16, h.base_timestamp); wr64(buf + 24, h.origin_timestamp);
+        wr64(buf + 32, h.batch_length); wr32(buf + 40, h.message_count);
+        for (uint64_t i = 0; i < n; i++) memcpy(buf + 44 + 8 * i, out + HDR + starts[i], 8);
+        h.batch_checksum = oracle_xxh3_64_fast(buf, tl);
+        free(buf);
+    }
+    oracle_batch_header_encode(&h, out);
+    free(starts);
+    return pos;
+}

@@ -1,0 +1,78 @@
+/*
+ * oracle.h — TEST INFRASTRUCTURE ONLY.
+ *
+ * CPU restatement of the reference algorithm for Iggy's message-batch codec,
+ * used exclusively as the checker by tests/, __graft_entry__.smoke() and the
+ * cpu_baseline leg of bench.py. Nothing in iggy_amd/ links, loads or calls
+ * it; the product path is the HIP library behind include/iggy_codec.h.
+ *
+ * Parity pins (see DESIGN.md "Oracle"):
+ *  - the reference is Rust and cannot be built here (no cargo/rustc), so this
+ *    is a restatement, not a build of the reference;
+ *  - XXH3-64 comes from the third-party crate twox-hash 2.1.3
+ *    (Cargo.lock:13579-13586), absent from /root/reference; it is restated
+ *    from the published XXH3 specification and pinned against libxxhash 0.8.2
+ *    (python `xxhash` 3.8.1, spec-identical output) for every length class;
+ *  - the codec walks are pinned by the Rust-generated golden vectors in
+ *    foreign/node/src/wire/message/message-batch.test.ts:42-75 and
+ *    foreign/go/binary_serialization/vsr_response_deserializer_test.go:294.
+ * Types come from include/iggy_codec.h (the ABI contract), logic does not.
+ */
+#ifndef IGGY_ORACLE_H
+#define IGGY_ORACLE_H
+#include <stdint.h>
+#include <stddef.h>
+#include "../include/iggy_codec.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+uint64_t oracle_xxh3_64(const void *data, size_t len);
+
+/* streaming: the reference hashes the batch checksum input with a streaming
+ * hasher; XXH3 streaming == one-shot over the concatenation, so the oracle
+ * materialises the concatenation (batch.rs:439-459). */
+int oracle_batch_header_decode(const uint8_t *b, uint64_t len, iggy_batch_header *h,
+                               iggy_wire_error *e);
+void oracle_batch_header_encode(const iggy_batch_header *h, uint8_t *out);
+
+int oracle_decode_batch_slice_with(const uint8_t *body, uint64_t len, int integrity,
+                                   iggy_batch_header *h, uint64_t *frame_pos, uint64_t cap,
+                                   uint64_t *nframes, iggy_wire_error *e);
+int oracle_verify_and_recompute(const iggy_batch_header *h, const uint8_t *blob,
+                                uint64_t blob_len, uint64_t *out, uint64_t *frame_pos,
+                                uint64_t cap, uint64_t *nframes, iggy_wire_error *e);
+uint64_t oracle_calculate_batch_checksum(const iggy_batch_header *h, const uint8_t *blob,
+                                         uint64_t blob_len);
+uint64_t oracle_encoded_batch_size(const iggy_raw_messages *m);
+int oracle_encode_batch(const iggy_raw_messages *m, uint64_t partition_id, uint8_t *out,
+                        uint64_t cap, uint64_t *out_len, iggy_wire_error *e);
+int oracle_poll_decode(const uint8_t *records, uint64_t len, int mode,
+                       iggy_polled_message *out, uint64_t cap, uint64_t *n,
+                       iggy_wire_error *e);
+int oracle_stamp_batch(uint8_t *batch, uint64_t len, uint64_t base_offset,
+                       uint64_t base_timestamp, iggy_batch_header *out, iggy_wire_error *e);
+
+/* synthetic input generator shared by tests and bench (BASELINE.md:
+ * splitmix64, seed 0x16619E3779B97F4A ^ partition). Builds a stamped,
+ * checksummed record of n frames; payload length of frame i =
+ * pl_min + (draw % (pl_max - pl_min + 1)). Returns batch_length. */
+uint64_t oracle_synth_batch(uint8_t *out, uint64_t cap, uint64_t n, uint32_t pl_min,
+                            uint32_t pl_max, uint32_t uh_len, uint64_t seed,
+                            uint64_t partition_id);
+uint64_t oracle_synth_batch_size(uint64_t n, uint32_t pl_min, uint32_t pl_max,
+                                 uint32_t uh_len, uint64_t seed);
+
+/* CPU baseline (bench.py cpu_baseline leg): decode Verify of `reps` copies of
+ * one record on `threads` threads with the AVX2 XXH3 accumulate when the host
+ * has it. Returns seconds of wall time. */
+double oracle_cpu_decode_bench(const uint8_t *body, uint64_t len, int threads, int reps,
+                               uint64_t *checksum_out);
+uint64_t oracle_xxh3_64_fast(const void *data, size_t len);
+int oracle_has_avx2(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

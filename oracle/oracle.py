@@ -1,0 +1,170 @@
+"""ctypes loader for the CPU oracle — TEST INFRASTRUCTURE ONLY.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may import
+this module; it is the checker, never the thing measured or shipped. See
+oracle/oracle.h for what it restates and how it is pinned.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+from iggy_amd.abi import (  # shared ABI struct definitions (types only)
+    BatchHeader,
+    PolledMessage,
+    RawMessages,
+    WireError,
+)
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(_HERE, "liboracle.so")
+_lib = None
+
+u64 = ctypes.c_uint64
+u32 = ctypes.c_uint32
+vp = ctypes.c_void_p
+
+
+def build() -> str:
+    subprocess.run(["make", "-s", "-C", _HERE], check=True)
+    return _LIB_PATH
+
+
+def lib() -> ctypes.CDLL:
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_LIB_PATH):
+            build()
+        L = ctypes.CDLL(_LIB_PATH)
+        L.oracle_xxh3_64.restype = u64
+        L.oracle_xxh3_64.argtypes = [vp, ctypes.c_size_t]
+        L.oracle_xxh3_64_fast.restype = u64
+        L.oracle_xxh3_64_fast.argtypes = [vp, ctypes.c_size_t]
+        L.oracle_batch_header_decode.argtypes = [vp, u64, vp, vp]
+        L.oracle_decode_batch_slice_with.argtypes = [vp, u64, ctypes.c_int, vp, vp, u64, vp, vp]
+        L.oracle_verify_and_recompute.argtypes = [vp, vp, u64, vp, vp, u64, vp, vp]
+        L.oracle_calculate_batch_checksum.restype = u64
+        L.oracle_calculate_batch_checksum.argtypes = [vp, vp, u64]
+        L.oracle_encoded_batch_size.restype = u64
+        L.oracle_encoded_batch_size.argtypes = [vp]
+        L.oracle_encode_batch.argtypes = [vp, u64, vp, u64, vp, vp]
+        L.oracle_poll_decode.argtypes = [vp, u64, ctypes.c_int, vp, u64, vp, vp]
+        L.oracle_stamp_batch.argtypes = [vp, u64, u64, u64, vp, vp]
+        L.oracle_synth_batch.restype = u64
+        L.oracle_synth_batch.argtypes = [vp, u64, u64, u32, u32, u32, u64, u64]
+        L.oracle_synth_batch_size.restype = u64
+        L.oracle_synth_batch_size.argtypes = [u64, u32, u32, u32, u64]
+        L.oracle_cpu_decode_bench.restype = ctypes.c_double
+        L.oracle_cpu_decode_bench.argtypes = [vp, u64, ctypes.c_int, ctypes.c_int, vp]
+        L.oracle_has_avx2.restype = ctypes.c_int
+        _lib = L
+    return _lib
+
+
+def _ptr(buf) -> int:
+    """Address of a bytes/bytearray/numpy buffer (bytes are copied)."""
+    import numpy as np
+
+    if isinstance(buf, np.ndarray):
+        return buf.ctypes.data
+    if isinstance(buf, bytearray):
+        return ctypes.addressof((ctypes.c_char * len(buf)).from_buffer(buf)) if len(buf) else 0
+    raise TypeError("pass bytearray or numpy array")
+
+
+def _as_np(buf):
+    import numpy as np
+
+    if isinstance(buf, np.ndarray):
+        return buf
+    return np.frombuffer(bytes(buf), dtype=np.uint8).copy()
+
+
+def xxh3_64(data: bytes) -> int:
+    a = _as_np(data)
+    return lib().oracle_xxh3_64(a.ctypes.data if a.size else None, a.size)
+
+
+def xxh3_64_fast(data: bytes) -> int:
+    a = _as_np(data)
+    return lib().oracle_xxh3_64_fast(a.ctypes.data if a.size else None, a.size)
+
+
+def decode_batch_slice_with(body, integrity: int = 0, want_frames: bool = True):
+    """-> (rc, WireError, BatchHeader, frame_positions list)"""
+    import numpy as np
+
+    a = _as_np(body)
+    h = BatchHeader()
+    e = WireError()
+    cap = a.size // 48 + 1 if want_frames else 0
+    pos = np.zeros(max(cap, 1), dtype=np.uint64)
+    n = u64(0)
+    rc = lib().oracle_decode_batch_slice_with(
+        a.ctypes.data, a.size, integrity, ctypes.byref(h), pos.ctypes.data if cap else None,
+        cap, ctypes.byref(n), ctypes.byref(e))
+    frames = pos[: n.value].copy() if (rc == 0 and want_frames) else None
+    return rc, e, h, frames
+
+
+def calculate_batch_checksum(h: BatchHeader, blob) -> int:
+    a = _as_np(blob)
+    return lib().oracle_calculate_batch_checksum(ctypes.byref(h), a.ctypes.data if a.size else None, a.size)
+
+
+def encode_batch(raw: "RawMessages", partition_id: int = 0):
+    """raw: iggy_amd.abi.RawMessages bound to host arrays. -> (rc, err, bytes)."""
+    import numpy as np
+
+    need = lib().oracle_encoded_batch_size(ctypes.byref(raw)) if raw.count else 256
+    out = np.zeros(need, dtype=np.uint8)
+    n = u64(0)
+    e = WireError()
+    rc = lib().oracle_encode_batch(ctypes.byref(raw), partition_id, out.ctypes.data, need,
+                                   ctypes.byref(n), ctypes.byref(e))
+    return rc, e, out[: n.value].tobytes() if rc == 0 else b""
+
+
+def poll_decode(records, mode: int = 0, cap: int | None = None):
+    a = _as_np(records)
+    if cap is None:
+        cap = a.size // 48 + 1
+    out = (PolledMessage * max(cap, 1))()
+    n = u64(0)
+    e = WireError()
+    rc = lib().oracle_poll_decode(a.ctypes.data if a.size else None, a.size, mode, out, cap,
+                                  ctypes.byref(n), ctypes.byref(e))
+    return rc, e, [out[i] for i in range(n.value)]
+
+
+def stamp_batch(batch, base_offset: int, base_timestamp: int):
+    a = _as_np(batch)
+    h = BatchHeader()
+    e = WireError()
+    rc = lib().oracle_stamp_batch(a.ctypes.data, a.size, base_offset, base_timestamp,
+                                  ctypes.byref(h), ctypes.byref(e))
+    return rc, e, h, a.tobytes()
+
+
+def synth_batch(n: int, pl_min: int, pl_max: int | None = None, uh_len: int = 0,
+                seed: int = 0x16619E3779B97F4A, partition_id: int = 1, out=None):
+    """Seeded synthetic stamped record (BASELINE.md input spec) as numpy u8."""
+    import numpy as np
+
+    if pl_max is None:
+        pl_max = pl_min
+    size = lib().oracle_synth_batch_size(n, pl_min, pl_max, uh_len, seed)
+    if out is None:
+        out = np.empty(size, dtype=np.uint8)
+    got = lib().oracle_synth_batch(out.ctypes.data, out.size, n, pl_min, pl_max, uh_len, seed,
+                                   partition_id)
+    assert got == size
+    return out[:size]
+
+
+def cpu_decode_bench(body, threads: int, reps: int):
+    a = _as_np(body)
+    c = u64(0)
+    secs = lib().oracle_cpu_decode_bench(a.ctypes.data, a.size, threads, reps, ctypes.byref(c))
+    return secs, c.value
