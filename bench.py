@@ -1,0 +1,230 @@
+"""Benchmark: device-resident message-batch decode on MI355X (BASELINE.json metric).
+
+Workload (BASELINE configs[1], "C2"): one canonical Iggy batch of 1,048,576
+messages x 1 KiB payload per GPU (1,124,073,728 bytes), resident in HBM; one
+step = decode_batch_slice_with(Verify) of that batch
+(core/binary_protocol/src/batch.rs:391-506): every frame walked and
+XXH3-verified, the batch checksum recomputed and compared, the blob-relative
+position of every frame written out (8 B per frame).
+
+Multi-GPU (BASELINE configs[4], "C5"): one rank per GPU, each with its own
+independent partition's batch; no data-path collective (weak scaling). The
+barrier + max-over-ranks timing is the only cross-rank traffic.
+
+The synthetic batches are produced on the GPU by the codec's own encoder
+(SendMessagesEncoder semantics, server-twin form with partition_id = rank+1):
+random full-range payload bytes, random non-zero ids, origin timestamps
+1.7e15 + i microseconds.
+
+Output: ONE JSON line on rank 0 with `roofline` (dominant kernel, HIP events
+on the launch stream) and `cpu_baseline` (the oracle's AVX2 restatement of the
+same decode timed on this host's cores; reported, not optimised against).
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+from iggy_amd import abi  # noqa: E402
+from iggy_amd.codec import Codec  # noqa: E402
+
+METRIC = "GiB/s device-resident message-batch decode, 1M msgs × 1KiB payload"
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s peak
+N_MSG = 1 << 20
+PAYLOAD = 1024
+
+
+def make_batch(cx: Codec, n: int, pl: int, rank: int, dev: torch.device, stream: int):
+    g = torch.Generator(device=dev)
+    g.manual_seed(0x16619E3779B97F4A ^ rank)
+    payload = torch.randint(0, 256, (n * pl,), dtype=torch.uint8, device=dev, generator=g)
+    pls = torch.full((n,), pl, dtype=torch.int32, device=dev)
+    ids = torch.randint(1, 2**62, (2 * n,), dtype=torch.int64, device=dev, generator=g)
+    ots = 1_700_000_000_000_000 + torch.arange(n, dtype=torch.int64, device=dev)
+    total = 256 + n * (48 + pl)
+    out = torch.empty(total, dtype=torch.uint8, device=dev)
+    res = torch.zeros(ctypes.sizeof(abi.EncodeResult), dtype=torch.uint8, device=dev)
+    raw = abi.RawMessages(n, ids.data_ptr(), ots.data_ptr(), payload.data_ptr(), pls.data_ptr(), None, None)
+    rc = cx.encode_device(raw, rank + 1, out.data_ptr(), total, res.data_ptr(), stream)
+    if rc:
+        raise RuntimeError(f"encode_device rc={rc}")
+    torch.cuda.synchronize(dev)
+    er = abi.EncodeResult.from_buffer_copy(res.cpu().numpy().tobytes())
+    if er.error.kind != 0 or er.batch_length != total:
+        raise RuntimeError(f"encode failed: {er.error!r}")
+    del payload, pls, ids, ots
+    return out
+
+
+def cpu_baseline(n_sample: int, seconds: float):
+    """The oracle's restatement of the same decode on host cores (bounded sample)."""
+    from oracle import oracle as O  # cpu_baseline leg: the only bench use of oracle/
+
+    rec = O.synth_batch(n_sample, PAYLOAD, PAYLOAD)
+    nbytes = rec.size
+
+    def rate(threads):
+        reps = 1
+        while True:
+            secs, cs = O.cpu_decode_bench(rec, threads, reps)
+            if cs == 0:
+                raise RuntimeError("cpu baseline decode failed")
+            if secs >= seconds or reps >= 1 << 16:
+                return threads * reps * nbytes / secs / 2**30, secs
+            reps = max(reps * 2, int(reps * seconds / max(secs, 1e-3)) + 1)
+
+    threads = min(16, os.cpu_count() or 1)
+    r1, _ = rate(1)
+    rt, _ = rate(threads)
+    model = ""
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return {
+        "value": round(rt, 3), "unit": "GiB/s", "cores": threads, "kind": "port",
+        "sample": f"{n_sample} msgs x {PAYLOAD} B payload ({nbytes} B record) decoded Verify, "
+                  f"repeated ~{seconds:.0f} s per thread-count; AVX2 XXH3 when available",
+        "single_thread_gib_s": round(r1, 3), "cpu_model": model,
+        "avx2": bool(O.lib().oracle_has_avx2()),
+    }
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--messages", type=int, default=N_MSG)
+    ap.add_argument("--no-cpu", action="store_true", help="skip the cpu_baseline leg")
+    ap.add_argument("--cpu-seconds", type=float, default=5.0)
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+
+        dist.init_process_group("nccl", init_method="env://")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    cx = Codec(local)
+    # an explicit stream: the library enqueues on it and the timing brackets it
+    ts = torch.cuda.Stream(dev)
+    torch.cuda.set_stream(ts)
+    stream = ts.cuda_stream
+
+    n = args.messages
+    batch = make_batch(cx, n, PAYLOAD, rank, dev, stream)
+    L = batch.numel()
+    cx.reserve(L)
+    d_pos = torch.empty(n, dtype=torch.int64, device=dev)
+    d_res = torch.zeros(ctypes.sizeof(abi.DecodeResult), dtype=torch.uint8, device=dev)
+
+    def step():
+        rc = cx.decode_device(batch.data_ptr(), L, abi.INTEGRITY_VERIFY, d_pos.data_ptr(), n,
+                              d_res.data_ptr(), stream)
+        if rc:
+            raise RuntimeError(f"decode_device rc={rc}")
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    res = abi.DecodeResult.from_buffer_copy(d_res.cpu().numpy().tobytes())
+    if res.error.kind != 0 or res.frame_count != n or res.path != 1:
+        raise RuntimeError(f"decode check failed: {res.error!r} frames={res.frame_count} path={res.path}")
+    pos = d_pos[:4].cpu().tolist()
+    assert pos == [i * (48 + PAYLOAD) for i in range(4)], pos
+
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    if dist:
+        dist.barrier()
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    # dominant kernel: k_decode_uniform (frame walk + XXH3 + in-kernel batch-checksum
+    # chain), bracketed by HIP events on the launch stream inside the library
+    cx.profile_enable(True)
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize(dev)
+    launches, total_ms = cx.profile_read(0)
+    cx.profile_enable(False)
+    k_ms = total_ms / max(launches, 1)
+    alg_bytes = L + 8 * n  # read the record once + one 8-B frame position per message
+    achieved = alg_bytes / (k_ms * 1e-3) / 1e9
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu:
+        cpu = cpu_baseline(65536, args.cpu_seconds)
+
+    ms_per_step = elapsed / args.steps * 1e3
+    value = world * L * args.steps / elapsed / 2**30
+    if rank == 0:
+        line = {
+            "metric": METRIC,
+            "value": round(value, 2),
+            "unit": "GiB/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u8",
+            "data": "synthetic (GPU-encoded batches, random payload bytes)",
+            "config": {
+                "workload": "C2: decode_batch_slice_with(Verify) of one device-resident batch per GPU, "
+                            "1,048,576 msgs x 1 KiB payload",
+                "messages_per_gpu": n,
+                "payload_bytes": PAYLOAD,
+                "batch_bytes": L,
+                "outputs": "frame positions (8 B/msg) + result struct",
+                "parallelism": f"{world} independent partitions, one per GPU, no collective",
+            },
+            "roofline": {
+                "bound": "hbm",
+                "achieved": round(achieved, 1),
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 4),
+                "traffic": None,
+                "kernel": "k_decode_uniform<true>",
+                "kernel_ms": round(k_ms, 4),
+                "algorithmic_bytes": alg_bytes,
+            },
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    cx.close()
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

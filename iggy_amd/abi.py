@@ -107,7 +107,7 @@ class DecodeResult(ctypes.Structure):
         ("computed_checksum", u64),
         ("path", u32),
         ("status", u32),
-        ("_pad", u64),
+        ("covered", u64),
     ]
 
 

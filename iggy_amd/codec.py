@@ -1,0 +1,235 @@
+"""Python host binding of the MI355X codec (ctypes over include/iggy_codec.h).
+
+Mirrors the reference interface of the path (names and error behaviour of
+core/binary_protocol/src/batch.rs, requests/messages/send_messages.rs,
+common/src/types/message/polled_messages.rs): every method returns the same
+outcome the Rust function would, with `WireError` fields mirrored by
+iggy_amd.abi.WireError. The library is the product path; there is no CPU
+fallback — constructing a Codec without a gfx950 device raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import re
+
+import numpy as np
+
+from . import abi
+from .abi import BatchHeader, DecodeResult, EncodeResult, PolledMessage, RawMessages, WireError
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libiggy_codec.so")
+HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "iggy_codec.h")
+
+u64 = ctypes.c_uint64
+u32 = ctypes.c_uint32
+vp = ctypes.c_void_p
+ci = ctypes.c_int
+_lib = None
+
+
+class CodecError(RuntimeError):
+    def __init__(self, rc: int, err: WireError | None = None, what: str = ""):
+        self.rc = rc
+        self.err = err
+        super().__init__(f"{what}: rc={rc} {err!r}")
+
+
+def exported_symbols() -> list[str]:
+    """Every function the C ABI header declares."""
+    with open(HEADER_PATH) as f:
+        text = f.read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    names = re.findall(r"^[A-Za-z_][\w\s\*]*?\b(iggy_\w+)\s*\(", text, flags=re.M)
+    return sorted(set(names))
+
+
+def lib() -> ctypes.CDLL:
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise FileNotFoundError(
+            f"{LIB_PATH} missing: build it with `python -c 'import __graft_entry__ as g; g.build()'`")
+    L = ctypes.CDLL(LIB_PATH)
+    L.iggy_codec_abi_version.restype = u32
+    L.iggy_codec_create.argtypes = [ci, ctypes.POINTER(vp)]
+    L.iggy_codec_destroy.argtypes = [vp]
+    L.iggy_codec_destroy.restype = None
+    L.iggy_codec_reserve.argtypes = [vp, u64, u64]
+    L.iggy_codec_stream.argtypes = [vp]
+    L.iggy_codec_stream.restype = vp
+    L.iggy_codec_synchronize.argtypes = [vp]
+    L.iggy_batch_header_decode.argtypes = [vp, u64, vp, vp]
+    L.iggy_batch_header_encode.argtypes = [vp, vp]
+    L.iggy_batch_header_encode.restype = None
+    L.iggy_encoded_batch_size.argtypes = [vp]
+    L.iggy_encoded_batch_size.restype = u64
+    L.iggy_codec_xxh3_64.argtypes = [vp, vp, u64, vp]
+    L.iggy_codec_decode_batch.argtypes = [vp, vp, u64, ci, vp, vp, u64, vp, vp]
+    L.iggy_codec_verify_and_recompute_batch_checksum.argtypes = [vp, vp, vp, u64, vp, vp]
+    L.iggy_codec_calculate_batch_checksum.argtypes = [vp, vp, vp, u64, vp]
+    L.iggy_codec_encode_batch.argtypes = [vp, vp, u64, vp, u64, vp, vp]
+    L.iggy_codec_poll_decode.argtypes = [vp, vp, u64, ci, vp, u64, vp, vp]
+    L.iggy_codec_stamp_batch.argtypes = [vp, vp, u64, u64, u64, vp, vp]
+    L.iggy_codec_decode_batch_device.argtypes = [vp, vp, u64, ci, vp, u64, vp, vp]
+    L.iggy_codec_encode_batch_device.argtypes = [vp, vp, u64, vp, u64, vp, vp]
+    L.iggy_codec_batch_checksum_device.argtypes = [vp, vp, vp, vp, u64, vp, vp]
+    L.iggy_codec_xxh3_64_ranges_device.argtypes = [vp, vp, vp, vp, u64, vp, vp]
+    L.iggy_codec_profile_enable.argtypes = [vp, ci]
+    L.iggy_codec_profile_read.argtypes = [vp, ci, vp, vp]
+    L.iggy_codec_error_string.argtypes = [u32, u32]
+    L.iggy_codec_error_string.restype = ctypes.c_char_p
+    _lib = L
+    return L
+
+
+def _np(buf) -> np.ndarray:
+    if isinstance(buf, np.ndarray):
+        return np.ascontiguousarray(buf).view(np.uint8).reshape(-1)
+    return np.frombuffer(bytes(buf), dtype=np.uint8).copy()
+
+
+def _addr(a: np.ndarray):
+    return a.ctypes.data if a.size else None
+
+
+class Codec:
+    """One codec context bound to one HIP device (thread-per-core shards each own one)."""
+
+    def __init__(self, device: int = 0):
+        self._L = lib()
+        h = vp()
+        rc = self._L.iggy_codec_create(device, ctypes.byref(h))
+        if rc != 0:
+            raise CodecError(rc, None, f"iggy_codec_create(device={device})")
+        self._h = h
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self._L.iggy_codec_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def handle(self):
+        return self._h
+
+    def stream(self) -> int:
+        return self._L.iggy_codec_stream(self._h) or 0
+
+    def reserve(self, max_batch_bytes: int, max_frames: int = 0):
+        rc = self._L.iggy_codec_reserve(self._h, max_batch_bytes, max_frames)
+        if rc:
+            raise CodecError(rc, None, "reserve")
+
+    # ----------------------------------------------------------- host buffers
+    def xxh3_64(self, data) -> int:
+        a = _np(data)
+        out = u64(0)
+        rc = self._L.iggy_codec_xxh3_64(self._h, _addr(a), a.size, ctypes.byref(out))
+        if rc:
+            raise CodecError(rc, None, "xxh3_64")
+        return out.value
+
+    def decode_batch_slice_with(self, body, integrity: int = abi.INTEGRITY_VERIFY,
+                                want_frames: bool = True):
+        """decode_batch_slice_with (batch.rs:391) -> (rc, WireError, BatchHeader, frames)."""
+        a = _np(body)
+        h = BatchHeader()
+        e = WireError()
+        cap = a.size // 48 + 1 if want_frames else 0
+        pos = np.zeros(max(cap, 1), dtype=np.uint64)
+        n = u64(0)
+        rc = self._L.iggy_codec_decode_batch(self._h, _addr(a), a.size, integrity, ctypes.byref(h),
+                                             pos.ctypes.data if cap else None, cap, ctypes.byref(n),
+                                             ctypes.byref(e))
+        frames = pos[: n.value].copy() if (rc == 0 and want_frames) else None
+        return rc, e, h, frames
+
+    def verify_and_recompute_batch_checksum(self, h: BatchHeader, blob):
+        a = _np(blob)
+        out = u64(0)
+        e = WireError()
+        rc = self._L.iggy_codec_verify_and_recompute_batch_checksum(
+            self._h, ctypes.byref(h), _addr(a), a.size, ctypes.byref(out), ctypes.byref(e))
+        return rc, e, out.value
+
+    def calculate_batch_checksum(self, h: BatchHeader, blob) -> int:
+        a = _np(blob)
+        out = u64(0)
+        rc = self._L.iggy_codec_calculate_batch_checksum(self._h, ctypes.byref(h), _addr(a), a.size,
+                                                         ctypes.byref(out))
+        if rc:
+            raise CodecError(rc, None, "calculate_batch_checksum")
+        return out.value
+
+    def encode_batch(self, raw: RawMessages, partition_id: int = 0):
+        """SendMessagesEncoder::encode batch section -> (rc, WireError, bytes)."""
+        need = self._L.iggy_encoded_batch_size(ctypes.byref(raw)) if raw.count else 256
+        out = np.zeros(need, dtype=np.uint8)
+        n = u64(0)
+        e = WireError()
+        rc = self._L.iggy_codec_encode_batch(self._h, ctypes.byref(raw), partition_id, out.ctypes.data,
+                                             need, ctypes.byref(n), ctypes.byref(e))
+        return rc, e, (out[: n.value].tobytes() if rc == 0 else b"")
+
+    def poll_decode(self, records, mode: int = abi.POLL_MODE_SDK, cap: int | None = None):
+        a = _np(records)
+        if cap is None:
+            cap = a.size // 48 + 1
+        out = (PolledMessage * max(cap, 1))()
+        n = u64(0)
+        e = WireError()
+        rc = self._L.iggy_codec_poll_decode(self._h, _addr(a), a.size, mode, out, cap,
+                                            ctypes.byref(n), ctypes.byref(e))
+        return rc, e, [out[i] for i in range(n.value)]
+
+    def stamp_batch(self, batch, base_offset: int, base_timestamp: int):
+        a = _np(batch).copy()
+        h = BatchHeader()
+        e = WireError()
+        rc = self._L.iggy_codec_stamp_batch(self._h, a.ctypes.data, a.size, base_offset,
+                                            base_timestamp, ctypes.byref(h), ctypes.byref(e))
+        return rc, e, h, a.tobytes()
+
+    # --------------------------------------------------------- device buffers
+    def decode_device(self, d_body: int, length: int, integrity: int, d_frame_pos: int | None,
+                      cap: int, d_result: int, stream: int | None = None) -> int:
+        return self._L.iggy_codec_decode_batch_device(self._h, d_body, length, integrity,
+                                                      d_frame_pos, cap, d_result, stream)
+
+    def encode_device(self, raw_dev: RawMessages, partition_id: int, d_out: int, cap: int,
+                      d_result: int, stream: int | None = None) -> int:
+        return self._L.iggy_codec_encode_batch_device(self._h, ctypes.byref(raw_dev), partition_id,
+                                                      d_out, cap, d_result, stream)
+
+    def xxh3_ranges_device(self, d_data, d_offsets, d_lengths, n, d_out, stream=None) -> int:
+        return self._L.iggy_codec_xxh3_64_ranges_device(self._h, d_data, d_offsets, d_lengths, n,
+                                                        d_out, stream)
+
+    def profile_enable(self, on: bool = True):
+        self._L.iggy_codec_profile_enable(self._h, 1 if on else 0)
+
+    def profile_read(self, which: int = 0):
+        n = u64(0)
+        ms = ctypes.c_double(0)
+        self._L.iggy_codec_profile_read(self._h, which, ctypes.byref(n), ctypes.byref(ms))
+        return n.value, ms.value
+
+
+def raw_messages(ids: np.ndarray, origin_timestamps: np.ndarray, payloads: np.ndarray,
+                 payload_lengths: np.ndarray, user_headers: np.ndarray | None = None,
+                 user_headers_lengths: np.ndarray | None = None) -> RawMessages:
+    """Build the SoA `&[RawMessage]` view over host numpy arrays (kept alive by the caller)."""
+    n = len(payload_lengths)
+    return RawMessages(n, ids.ctypes.data, origin_timestamps.ctypes.data,
+                       payloads.ctypes.data if payloads.size else None, payload_lengths.ctypes.data,
+                       user_headers.ctypes.data if user_headers is not None and user_headers.size else None,
+                       user_headers_lengths.ctypes.data if user_headers_lengths is not None else None)

@@ -1,0 +1,224 @@
+// batch_checksum.hip — calculate_batch_checksum (core/binary_protocol/src/batch.rs:439-459)
+// for a record whose walked frames are known: XXH3-64 streamed over the 44
+// header-field bytes followed by every frame's stored 8-byte checksum.
+//
+// The input is 44 + 8N bytes; as XXH3 "long" input it is 1024-B blocks whose
+// 16 stripe contributions commute (computed in parallel, one wave per block,
+// k_bsum_blocks) chained by one scramble per block (k_bsum_chain, one wave,
+// lane j carries accumulator j). Word m of the input (8 bytes at 8m):
+//   m < 5  : partition_id, base_offset, base_timestamp, origin_timestamp, batch_length
+//   m == 5 : message_count | lo32(cs_0) << 32
+//   m >= 6 : hi32(cs_{m-6}) | lo32(cs_{m-5}) << 32
+#include "codec_common.hpp"
+
+namespace iggy {
+
+// where the frame checksums come from
+struct CsSource {
+    const uint64_t *cs;     // dense array (decode general / encode), or
+    const uint8_t *blob;    // gathered at blob + fpos[i]
+    const uint64_t *fpos;
+    __device__ __forceinline__ uint64_t operator()(uint64_t i) const {
+        return cs ? cs[i] : ld64_any(blob + fpos[i]);
+    }
+};
+
+struct CsPlan {
+    uint64_t n, nb, Mreg;
+    bool long_cs;
+};
+__device__ __forceinline__ CsPlan cs_plan(uint64_t nframes) {
+    CsPlan p;
+    p.n = 44 + 8 * nframes;
+    p.long_cs = p.n > 240;
+    p.nb = 0;
+    p.Mreg = 0;
+    if (p.long_cs) {
+        p.nb = (p.n - 1) / 1024;
+        const uint64_t ns = ((p.n - 1) - 1024 * p.nb) / 64;
+        p.Mreg = 8 * (16 * p.nb + ns);
+    }
+    return p;
+}
+
+__device__ __forceinline__ uint64_t cs_word(uint64_t m, const iggy_batch_header &h,
+                                            const CsSource &src) {
+    switch (m) {
+        case 0: return h.partition_id;
+        case 1: return h.base_offset;
+        case 2: return h.base_timestamp;
+        case 3: return h.origin_timestamp;
+        case 4: return h.batch_length;
+        case 5: return (uint64_t)h.message_count | (src(0) << 32);
+        default: return (src(m - 6) >> 32) | (src(m - 5) << 32);
+    }
+}
+
+// header and frame count come from device memory (written by an earlier kernel
+// on the stream) so nothing has to travel back to the host in between.
+__global__ __launch_bounds__(256) void k_bsum_blocks(const iggy_batch_header *hp,
+                                                     const uint64_t *nframes_p, CsSource src,
+                                                     uint64_t *bsums, const uint32_t *skip) {
+    if (skip && *skip) return;
+    const iggy_batch_header h = *hp;
+    const CsPlan pl = cs_plan(*nframes_p);
+    if (!pl.long_cs) return;
+    const int lane = threadIdx.x & 63;
+    const uint64_t wid = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const uint64_t nwaves = ((uint64_t)gridDim.x * blockDim.x) >> 6;
+    for (uint64_t b = wid; b <= pl.nb; b += nwaves) {
+        uint64_t x = 0, y = 0;
+#pragma unroll
+        for (int half = 0; half < 2; ++half) {
+            const uint64_t m = 128 * b + 64 * half + lane;
+            if (m < pl.Mreg) {
+                const uint64_t v = cs_word(m, h, src);
+                y += v;
+                x += mul32x32(v ^ kSecretW8[((m >> 3) & 15) + (m & 7)]);
+            }
+        }
+        x += __shfl_xor(x, 8); y += __shfl_xor(y, 8);
+        x += __shfl_xor(x, 16); y += __shfl_xor(y, 16);
+        x += __shfl_xor(x, 32); y += __shfl_xor(y, 32);
+        const uint64_t t8 = x + __shfl_xor(y, 1);
+        if (lane < 8) bsums[b * 8 + lane] = t8;
+    }
+}
+
+// one wave: out[0] = batch checksum. `small` >= 240 B scratch for short inputs.
+__global__ __launch_bounds__(64) void k_bsum_chain(const iggy_batch_header *hp,
+                                                   const uint64_t *nframes_p, CsSource src,
+                                                   const uint64_t *bsums, uint8_t *small,
+                                                   uint64_t *out, const uint32_t *skip) {
+    if (skip && *skip) return;
+    const iggy_batch_header h = *hp;
+    const uint64_t N = *nframes_p;
+    const CsPlan pl = cs_plan(N);
+    const int lane = threadIdx.x & 63;
+    if (pl.long_cs) {
+        const int j = lane & 7;
+        uint64_t acc = kAccInit[j];
+        const uint64_t key = kSecretW8[16 + j];
+        uint64_t b = 0;
+        // batches of 8 blocks: loads issued ahead of the dependent scrambles
+        for (; b + 8 <= pl.nb; b += 8) {
+            uint64_t v[8];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) v[k] = bsums[(b + k) * 8 + j];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) acc = scramble1(acc + v[k], key);
+        }
+        for (; b < pl.nb; ++b) acc = scramble1(acc + bsums[b * 8 + j], key);
+        acc += bsums[pl.nb * 8 + j];
+        const uint64_t v = src(N - 8 + j);
+        acc += __shfl_xor(v, 1);
+        acc += mul32x32(v ^ kSecretLast[j]);
+        uint64_t a[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) a[i] = __shfl(acc, i);
+        uint64_t r = pl.n * P64_1;
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+            r += fold64(a[2 * i] ^ Secret::w(11 + 16 * i), a[2 * i + 1] ^ Secret::w(19 + 16 * i));
+        if (lane == 0) *out = avalanche(r);
+    } else if (lane == 0) {
+        for (uint64_t m = 0; m < 5; ++m) st64_any(small + 8 * m, cs_word(m, h, src));
+        *(uint32_t *)(small + 40) = h.message_count;
+        for (uint64_t i = 0; i < N; ++i) st64_any(small + 44 + 8 * i, src(i));
+        *out = xxh3_64_lane(small, pl.n);
+    }
+}
+
+// XXH3-64 of independent ranges, one lane per range (calculate_checksum,
+// common/src/utils/checksum.rs:20, applied to many buffers at once).
+__global__ __launch_bounds__(256) void k_xxh3_ranges(const uint8_t *data, const uint64_t *offs,
+                                                     const uint32_t *lens, uint64_t n,
+                                                     uint64_t *out) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+         i += (uint64_t)gridDim.x * blockDim.x)
+        out[i] = xxh3_64_lane(data + offs[i], lens[i]);
+}
+
+// one-shot XXH3-64 of a single large device buffer: per-block stripe sums in
+// parallel, then the scramble chain (same split as the batch checksum).
+__global__ __launch_bounds__(256) void k_xxh3_big_blocks(const uint8_t *p, uint64_t len,
+                                                         uint64_t *bsums) {
+    const int lane = threadIdx.x & 63;
+    const uint64_t nb = (len - 1) / 1024;
+    const uint64_t ns = ((len - 1) - 1024 * nb) / 64;
+    const uint64_t Mreg = 8 * (16 * nb + ns);
+    const uint64_t wid = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const uint64_t nwaves = ((uint64_t)gridDim.x * blockDim.x) >> 6;
+    for (uint64_t b = wid; b <= nb; b += nwaves) {
+        uint64_t x = 0, y = 0;
+#pragma unroll
+        for (int half = 0; half < 2; ++half) {
+            const uint64_t m = 128 * b + 64 * half + lane;
+            if (m < Mreg) {
+                const uint64_t v = ld64_any(p + 8 * m);
+                y += v;
+                x += mul32x32(v ^ kSecretW8[((m >> 3) & 15) + (m & 7)]);
+            }
+        }
+        x += __shfl_xor(x, 8); y += __shfl_xor(y, 8);
+        x += __shfl_xor(x, 16); y += __shfl_xor(y, 16);
+        x += __shfl_xor(x, 32); y += __shfl_xor(y, 32);
+        const uint64_t t8 = x + __shfl_xor(y, 1);
+        if (lane < 8) bsums[b * 8 + lane] = t8;
+    }
+}
+
+__global__ __launch_bounds__(64) void k_xxh3_big_chain(const uint8_t *p, uint64_t len,
+                                                       const uint64_t *bsums, uint64_t *out) {
+    const int lane = threadIdx.x & 63;
+    if (len <= 240) {
+        if (lane == 0) *out = xxh3_64_lane(p, len);
+        return;
+    }
+    const uint64_t nb = (len - 1) / 1024;
+    const int j = lane & 7;
+    uint64_t acc = kAccInit[j];
+    const uint64_t key = kSecretW8[16 + j];
+    uint64_t b = 0;
+    for (; b + 8 <= nb; b += 8) {
+        uint64_t v[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) v[k] = bsums[(b + k) * 8 + j];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) acc = scramble1(acc + v[k], key);
+    }
+    for (; b < nb; ++b) acc = scramble1(acc + bsums[b * 8 + j], key);
+    acc += bsums[nb * 8 + j];
+    const uint64_t v = ld64_any(p + len - 64 + 8 * j);
+    acc += __shfl_xor(v, 1);
+    acc += mul32x32(v ^ kSecretLast[j]);
+    uint64_t a[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) a[i] = __shfl(acc, i);
+    uint64_t r = len * P64_1;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+        r += fold64(a[2 * i] ^ Secret::w(11 + 16 * i), a[2 * i + 1] ^ Secret::w(19 + 16 * i));
+    if (lane == 0) *out = avalanche(r);
+}
+
+// stamp_prepare_for_persistence (server_common/src/send_messages.rs:642-663):
+// header fields -> record bytes (batch.rs:138-150 encode_into)
+__global__ void k_write_header(uint8_t *rec, const iggy_batch_header *hp, const uint64_t *cs) {
+    const int t = threadIdx.x;  // 64 threads x 4 bytes
+    iggy_batch_header h = *hp;
+    if (cs) h.batch_checksum = *cs;
+    uint32_t w = 0;
+    const uint32_t off = 4 * t;
+    if (off < 48) {
+        const uint64_t f[6] = {h.partition_id, h.base_offset, h.base_timestamp,
+                               h.origin_timestamp, h.batch_length, h.batch_checksum};
+        const uint64_t v = f[off / 8];
+        w = (off & 4) ? (uint32_t)(v >> 32) : (uint32_t)v;
+    } else if (off == 48) {
+        w = h.message_count;
+    }
+    *(u32_ua *)(rec + off) = w;
+}
+
+}  // namespace iggy

@@ -1,0 +1,841 @@
+// codec_api.hip — host side of the C ABI declared in include/iggy_codec.h.
+//
+// Unity build: the kernel translation units are included here so the whole
+// library is one code object (libiggy_codec.so). Host code only sizes scratch,
+// enqueues kernels and converts results; every byte of the hot path (frame
+// walk, XXH3, batch checksum, encode) runs on the GPU. There is deliberately
+// no CPU fallback: without a usable gfx950 device iggy_codec_create fails.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+#include <new>
+#include <vector>
+
+#include "../../include/iggy_codec.h"
+#include "batch_checksum.hip"
+#include "decode_general.hip"
+#include "decode_uniform.hip"
+#include "encode.hip"
+#include "poll.hip"
+
+using namespace iggy;
+
+#define HIP_OK(x)                                                              \
+    do {                                                                       \
+        hipError_t e_ = (x);                                                   \
+        if (e_ != hipSuccess) {                                                \
+            if (getenv("IGGY_CODEC_DEBUG"))                                    \
+                fprintf(stderr, "iggy_codec: %s failed: %s (%s:%d)\n", #x,     \
+                        hipGetErrorString(e_), __FILE__, __LINE__);            \
+            return IGGY_ERR_DEVICE;                                            \
+        }                                                                      \
+    } while (0)
+
+namespace {
+
+// one device allocation that grows on demand (never inside an enqueue path
+// whose caller asked for graph-safety: grow happens in reserve / sync APIs)
+struct DevBuf {
+    void *p = nullptr;
+    size_t cap = 0;
+    int ensure(size_t n) {
+        if (n <= cap) return 0;
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+        size_t want = std::max<size_t>(n, 256);
+        if (hipMalloc(&p, want) != hipSuccess) return IGGY_ERR_DEVICE;
+        cap = want;
+        return 0;
+    }
+    template <class T> T *as(size_t off = 0) { return (T *)((uint8_t *)p + off); }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+    }
+};
+
+}  // namespace
+
+struct iggy_codec_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    int ncu = 256;
+    uint32_t epoch = 0;
+    int allow_unaligned = 0;
+    uint32_t dbg = 0;  // IGGY_CODEC_DBG: ablation bits for diagnostics only
+    // decode scratch
+    uint64_t dec_cap_len = 0;
+    DevBuf dsync;    // exited | first_bad | spec_fail | bar[4] | misc[16] | small[512]
+    DevBuf dflags, dsums, derr;
+    DevBuf gtiles_s, gtiles_x, gtiles_cnt, gtiles_list, gtiles_base, gfpos, gcs, gbsums;
+    DevBuf dresult;  // iggy_decode_result + iggy_encode_result + u64 scratch
+    // sync-API staging
+    DevBuf din, dpos, dout;
+    // encode scratch
+    DevBuf epl, euh, etile, ecs, emisc;
+    DevBuf eids, eots, epay, eplen, euhb, euhl;
+    // big one-shot hash
+    DevBuf hbsums;
+    // poll
+    DevBuf ppos, pmsgs;
+    // pinned host mirror of results
+    void *h_pinned = nullptr;
+    // profiling
+    int profile = 0;
+    hipEvent_t ev0[2] = {nullptr, nullptr}, ev1[2] = {nullptr, nullptr};
+    uint64_t prof_n[2] = {0, 0};
+    double prof_ms[2] = {0, 0};
+    bool ev_pending[2] = {false, false};
+};
+
+namespace {
+
+constexpr size_t kSyncExited = 0, kSyncFirstBad = 8, kSyncSpecFail = 16, kSyncBar = 32,
+                 kSyncMisc = 64, kSyncSmall = 256, kSyncBytes = 1024;
+
+int ensure_decode_scratch(iggy_codec_ctx *c, uint64_t len) {
+    if (len <= c->dec_cap_len && c->dsync.p) return 0;
+    const uint64_t L = std::max<uint64_t>(len, 1 << 20);
+    const uint64_t max_frames = L / 48 + 2;
+    const uint64_t max_chunks = (max_frames + 6) / 256 + 2;
+    const uint64_t ntiles = L / kTile + 2;
+    const uint64_t max_blocks = (44 + 8 * max_frames) / 1024 + 2;
+    int r = 0;
+    if (!c->dsync.p) {
+        r |= c->dsync.ensure(kSyncBytes);
+        if (r) return r;
+        HIP_OK(hipMemset(c->dsync.p, 0, kSyncBytes));
+    }
+    r |= c->dflags.ensure(max_chunks * 4);
+    if (!r && c->dflags.p) HIP_OK(hipMemset(c->dflags.p, 0, c->dflags.cap));
+    r |= c->dsums.ensure(2 * max_chunks * 64);
+    r |= c->derr.ensure(max_chunks * 4 * 16);
+    r |= c->gtiles_s.ensure(ntiles * 8);
+    r |= c->gtiles_x.ensure(ntiles * 8);
+    r |= c->gtiles_cnt.ensure(ntiles * 4);
+    r |= c->gtiles_list.ensure(ntiles * kTileCap * 2);
+    r |= c->gtiles_base.ensure(ntiles * 8);
+    r |= c->gfpos.ensure(max_frames * 8);
+    r |= c->gcs.ensure(max_frames * 8);
+    r |= c->gbsums.ensure(max_blocks * 64);
+    if (r) return IGGY_ERR_DEVICE;
+    c->dec_cap_len = L;
+    return 0;
+}
+
+DecodeScratch dscratch(iggy_codec_ctx *c) {
+    DecodeScratch s;
+    s.exited = c->dsync.as<uint32_t>(kSyncExited);
+    s.first_bad = c->dsync.as<uint64_t>(kSyncFirstBad);
+    s.spec_fail = c->dsync.as<uint64_t>(kSyncSpecFail);
+    s.flags = c->dflags.as<uint32_t>();
+    s.sums = c->dsums.as<uint64_t>();
+    s.errslot = c->derr.as<uint64_t>();
+    s.small = c->dsync.as<uint8_t>(kSyncSmall);
+    s.max_chunks = c->dflags.cap / 4;
+    return s;
+}
+
+GeneralScratch gscratch(iggy_codec_ctx *c) {
+    GeneralScratch g;
+    g.tile_s = c->gtiles_s.as<uint64_t>();
+    g.tile_x = c->gtiles_x.as<uint64_t>();
+    g.tile_cnt = c->gtiles_cnt.as<uint32_t>();
+    g.tile_list = c->gtiles_list.as<uint16_t>();
+    g.tile_base = c->gtiles_base.as<uint64_t>();
+    g.fpos = c->gfpos.as<uint64_t>();
+    g.cs = c->gcs.as<uint64_t>();
+    g.bsums = c->gbsums.as<uint64_t>();
+    g.misc = c->dsync.as<uint64_t>(kSyncMisc);
+    g.bar = c->dsync.as<uint32_t>(kSyncBar);
+    g.small = c->dsync.as<uint8_t>(kSyncSmall);
+    g.ntiles = c->gtiles_s.cap / 8;
+    g.max_frames = c->gfpos.cap / 8;
+    g.max_blocks = c->gbsums.cap / 64;
+    return g;
+}
+
+hipStream_t pick(iggy_codec_ctx *c, void *stream) {
+    return stream ? (hipStream_t)stream : c->stream;
+}
+
+void prof_begin(iggy_codec_ctx *c, int which, hipStream_t s) {
+    if (!c->profile) return;
+    if (c->ev_pending[which]) {
+        float ms = 0;
+        if (hipEventSynchronize(c->ev1[which]) == hipSuccess &&
+            hipEventElapsedTime(&ms, c->ev0[which], c->ev1[which]) == hipSuccess) {
+            c->prof_ms[which] += ms;
+            c->prof_n[which] += 1;
+        }
+        c->ev_pending[which] = false;
+    }
+    (void)hipEventRecord(c->ev0[which], s);
+}
+void prof_end(iggy_codec_ctx *c, int which, hipStream_t s) {
+    if (!c->profile) return;
+    (void)hipEventRecord(c->ev1[which], s);
+    c->ev_pending[which] = true;
+}
+
+// launch the whole decode (uniform kernel + guarded general kernel)
+int enqueue_decode(iggy_codec_ctx *c, const uint8_t *d_body, uint64_t len, int integrity,
+                   uint64_t *d_pos, uint64_t cap, iggy_decode_result *d_res, hipStream_t s) {
+    int r = ensure_decode_scratch(c, len);
+    if (r) return r;
+    if (++c->epoch == 0) c->epoch = 1;
+    const bool verify = integrity == IGGY_INTEGRITY_VERIFY;
+    DecodeScratch ds = dscratch(c);
+    GeneralScratch gs = gscratch(c);
+    const uint32_t grid = (uint32_t)std::max(2, c->ncu);
+    prof_begin(c, 0, s);
+    if (verify)
+        hipLaunchKernelGGL(k_decode_uniform<true>, dim3(grid), dim3(256), kLdsBytes, s, d_body, len,
+                           d_pos, cap, d_res, ds, c->epoch, (uint32_t)c->allow_unaligned, c->dbg);
+    else
+        hipLaunchKernelGGL(k_decode_uniform<false>, dim3(grid), dim3(256), kLdsBytes, s, d_body,
+                           len, d_pos, cap, d_res, ds, c->epoch, (uint32_t)c->allow_unaligned, c->dbg);
+    prof_end(c, 0, s);
+    HIP_OK(hipGetLastError());
+    if (verify)
+        hipLaunchKernelGGL(k_decode_general<true>, dim3(c->ncu), dim3(256), 0, s, d_body, len, d_pos,
+                           cap, d_res, gs);
+    else
+        hipLaunchKernelGGL(k_decode_general<false>, dim3(c->ncu), dim3(256), 0, s, d_body, len,
+                           d_pos, cap, d_res, gs);
+    HIP_OK(hipGetLastError());
+    return 0;
+}
+
+void fill_err(iggy_wire_error *err, const iggy_wire_error &e) {
+    if (err) *err = e;
+}
+void set_err(iggy_wire_error *err, uint32_t kind, uint32_t reason = 0, uint64_t a = 0,
+             uint64_t b = 0, uint64_t cc = 0) {
+    if (!err) return;
+    err->kind = kind;
+    err->reason = reason;
+    err->a = a;
+    err->b = b;
+    err->c = cc;
+}
+
+int reset_after_timeout(iggy_codec_ctx *c) {
+    HIP_OK(hipStreamSynchronize(c->stream));
+    HIP_OK(hipMemset(c->dsync.p, 0, kSyncBytes));
+    return 0;
+}
+
+// synchronous decode of a host buffer; also used by stamp / checksum helpers
+int decode_host(iggy_codec_ctx *c, const uint8_t *body, uint64_t len, int integrity,
+                iggy_decode_result *res_out, uint64_t *frame_pos, uint64_t cap, bool keep_on_device) {
+    int r = 0;
+    r |= c->din.ensure(len + 16);
+    const uint64_t pcap = frame_pos ? std::min<uint64_t>(cap, len / 48 + 1) : 0;
+    r |= c->dpos.ensure((pcap + 1) * 8);
+    if (r) return IGGY_ERR_DEVICE;
+    if (len) HIP_OK(hipMemcpyAsync(c->din.p, body, len, hipMemcpyHostToDevice, c->stream));
+    iggy_decode_result *d_res = c->dresult.as<iggy_decode_result>();
+    r = enqueue_decode(c, c->din.as<uint8_t>(), len, integrity, pcap ? c->dpos.as<uint64_t>() : nullptr,
+                       pcap, d_res, c->stream);
+    if (r) return r;
+    iggy_decode_result *h_res = (iggy_decode_result *)c->h_pinned;
+    HIP_OK(hipMemcpyAsync(h_res, d_res, sizeof(*h_res), hipMemcpyDeviceToHost, c->stream));
+    HIP_OK(hipStreamSynchronize(c->stream));
+    *res_out = *h_res;
+    if (res_out->error.kind == IGGY_ERR_TIMEOUT) reset_after_timeout(c);
+    if (frame_pos && pcap && res_out->error.kind == IGGY_OK) {
+        const uint64_t n = std::min<uint64_t>(res_out->frame_count, pcap);
+        if (n) HIP_OK(hipMemcpy(frame_pos, c->dpos.p, n * 8, hipMemcpyDeviceToHost));
+    }
+    (void)keep_on_device;
+    return 0;
+}
+
+}  // namespace
+
+// ===================================================================== ABI
+extern "C" {
+
+uint32_t iggy_codec_abi_version(void) { return IGGY_CODEC_ABI_VERSION; }
+
+int iggy_codec_create(int device, iggy_codec_ctx **out) {
+    if (!out) return IGGY_ERR_INVALID_ARGUMENT;
+    *out = nullptr;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev) return IGGY_ERR_DEVICE;
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device) != hipSuccess) return IGGY_ERR_DEVICE;
+    if (strncmp(prop.gcnArchName, "gfx950", 6) != 0) return IGGY_ERR_DEVICE;
+    iggy_codec_ctx *c = new (std::nothrow) iggy_codec_ctx();
+    if (!c) return IGGY_ERR_DEVICE;
+    c->device = device;
+    c->ncu = prop.multiProcessorCount;
+    if (const char *d = getenv("IGGY_CODEC_DBG")) c->dbg = (uint32_t)strtoul(d, nullptr, 0);
+    if (hipSetDevice(device) != hipSuccess ||
+        hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+        delete c;
+        return IGGY_ERR_DEVICE;
+    }
+    int r = 0;
+    r |= c->dresult.ensure(4096);
+    if (hipHostMalloc(&c->h_pinned, 4096, hipHostMallocDefault) != hipSuccess) r = IGGY_ERR_DEVICE;
+    if (!r) {
+        if (hipFuncSetAttribute((const void *)k_decode_uniform<true>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBytes) != hipSuccess ||
+            hipFuncSetAttribute((const void *)k_decode_uniform<false>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBytes) != hipSuccess)
+            r = IGGY_ERR_DEVICE;
+    }
+    for (int w = 0; w < 2 && !r; ++w)
+        if (hipEventCreate(&c->ev0[w]) != hipSuccess || hipEventCreate(&c->ev1[w]) != hipSuccess)
+            r = IGGY_ERR_DEVICE;
+    if (!r) r = ensure_decode_scratch(c, 1 << 20);
+    if (!r) {
+        // probe: does global_load_lds_dwordx4 honour unaligned sources here?
+        DevBuf pb;
+        if (pb.ensure(8192) == 0) {
+            std::vector<uint8_t> pat(4096);
+            for (size_t i = 0; i < pat.size(); ++i) pat[i] = (uint8_t)(i * 131 + 7);
+            uint32_t *flag = c->dresult.as<uint32_t>(1024);
+            if (hipMemcpy(pb.p, pat.data(), pat.size(), hipMemcpyHostToDevice) == hipSuccess &&
+                hipMemset(flag, 0, 4) == hipSuccess) {
+                hipLaunchKernelGGL(k_probe_glds_unaligned, dim3(1), dim3(64), 16 * 64 * 4, c->stream,
+                                   (const uint8_t *)pb.p, flag);
+                uint32_t ok = 0;
+                if (hipStreamSynchronize(c->stream) == hipSuccess &&
+                    hipMemcpy(&ok, flag, 4, hipMemcpyDeviceToHost) == hipSuccess)
+                    c->allow_unaligned = ok == 1;
+            }
+            pb.release();
+        }
+    }
+    if (r) {
+        iggy_codec_destroy(c);
+        return IGGY_ERR_DEVICE;
+    }
+    *out = c;
+    return 0;
+}
+
+void iggy_codec_destroy(iggy_codec_ctx *c) {
+    if (!c) return;
+    (void)hipSetDevice(c->device);
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    DevBuf *bufs[] = {&c->dsync, &c->dflags, &c->dsums, &c->derr, &c->gtiles_s, &c->gtiles_x,
+                      &c->gtiles_cnt, &c->gtiles_list, &c->gtiles_base, &c->gfpos, &c->gcs,
+                      &c->gbsums, &c->dresult, &c->din, &c->dpos, &c->dout, &c->epl, &c->euh,
+                      &c->etile, &c->ecs, &c->emisc, &c->eids, &c->eots, &c->epay, &c->eplen,
+                      &c->euhb, &c->euhl, &c->hbsums, &c->ppos, &c->pmsgs};
+    for (DevBuf *b : bufs) b->release();
+    if (c->h_pinned) (void)hipHostFree(c->h_pinned);
+    for (int w = 0; w < 2; ++w) {
+        if (c->ev0[w]) (void)hipEventDestroy(c->ev0[w]);
+        if (c->ev1[w]) (void)hipEventDestroy(c->ev1[w]);
+    }
+    if (c->stream) (void)hipStreamDestroy(c->stream);
+    delete c;
+}
+
+int iggy_codec_reserve(iggy_codec_ctx *c, uint64_t max_batch_bytes, uint64_t max_frames) {
+    if (!c) return IGGY_ERR_INVALID_ARGUMENT;
+    HIP_OK(hipSetDevice(c->device));
+    (void)max_frames;
+    return ensure_decode_scratch(c, max_batch_bytes);
+}
+
+void *iggy_codec_stream(iggy_codec_ctx *c) { return c ? (void *)c->stream : nullptr; }
+
+int iggy_codec_synchronize(iggy_codec_ctx *c) {
+    if (!c) return IGGY_ERR_INVALID_ARGUMENT;
+    HIP_OK(hipStreamSynchronize(c->stream));
+    return 0;
+}
+
+// ---------------------------------------------------------------- host pure
+int iggy_batch_header_decode(const uint8_t *b, uint64_t len, iggy_batch_header *h,
+                             iggy_wire_error *err) {
+    set_err(err, IGGY_OK);
+    if (!b && len) return IGGY_ERR_INVALID_ARGUMENT;
+    if (len < 256) {
+        set_err(err, IGGY_ERR_UNEXPECTED_EOF, 0, 0, 256, len);
+        return IGGY_ERR_UNEXPECTED_EOF;
+    }
+    uint64_t bl;
+    memcpy(&bl, b + 32, 8);
+    if (bl < 256) {
+        set_err(err, IGGY_ERR_VALIDATION, IGGY_V_BATCH_LENGTH_SHORT);
+        return IGGY_ERR_VALIDATION;
+    }
+    for (int i = 52; i < 256; ++i)
+        if (b[i]) {
+            set_err(err, IGGY_ERR_VALIDATION, IGGY_V_BATCH_RESERVED);
+            return IGGY_ERR_VALIDATION;
+        }
+    if (h) {
+        memset(h, 0, sizeof(*h));
+        memcpy(&h->partition_id, b + 0, 8);
+        memcpy(&h->base_offset, b + 8, 8);
+        memcpy(&h->base_timestamp, b + 16, 8);
+        memcpy(&h->origin_timestamp, b + 24, 8);
+        h->batch_length = bl;
+        memcpy(&h->batch_checksum, b + 40, 8);
+        memcpy(&h->message_count, b + 48, 4);
+    }
+    return 0;
+}
+
+void iggy_batch_header_encode(const iggy_batch_header *h, uint8_t out[256]) {
+    memset(out, 0, 256);
+    memcpy(out + 0, &h->partition_id, 8);
+    memcpy(out + 8, &h->base_offset, 8);
+    memcpy(out + 16, &h->base_timestamp, 8);
+    memcpy(out + 24, &h->origin_timestamp, 8);
+    memcpy(out + 32, &h->batch_length, 8);
+    memcpy(out + 40, &h->batch_checksum, 8);
+    memcpy(out + 48, &h->message_count, 4);
+}
+
+uint64_t iggy_encoded_batch_size(const iggy_raw_messages *m) {
+    if (!m) return 0;
+    uint64_t t = 256;
+    for (uint64_t i = 0; i < m->count; ++i)
+        t += 48 + (uint64_t)m->payload_lengths[i] + (m->user_headers_lengths ? m->user_headers_lengths[i] : 0);
+    return t;
+}
+
+// ------------------------------------------------------------ synchronous
+int iggy_codec_decode_batch(iggy_codec_ctx *c, const uint8_t *body, uint64_t len, int integrity,
+                            iggy_batch_header *hdr, uint64_t *frame_pos, uint64_t cap,
+                            uint64_t *nframes, iggy_wire_error *err) {
+    if (!c || (!body && len)) return IGGY_ERR_INVALID_ARGUMENT;
+    HIP_OK(hipSetDevice(c->device));
+    iggy_decode_result res;
+    int r = decode_host(c, body, len, integrity, &res, frame_pos, cap, false);
+    if (r) return r;
+    fill_err(err, res.error);
+    if (hdr) *hdr = res.header;
+    if (nframes) *nframes = res.frame_count;
+    if (res.error.kind != IGGY_OK) return (int)res.error.kind;
+    if (frame_pos && res.frame_count > cap) {
+        set_err(err, IGGY_ERR_CAPACITY, 0, res.frame_count, cap);
+        return IGGY_ERR_CAPACITY;
+    }
+    return 0;
+}
+
+int iggy_codec_verify_and_recompute_batch_checksum(iggy_codec_ctx *c, const iggy_batch_header *hdr,
+                                                   const uint8_t *blob, uint64_t blob_len,
+                                                   uint64_t *out, iggy_wire_error *err) {
+    if (!c || !hdr || (!blob && blob_len)) return IGGY_ERR_INVALID_ARGUMENT;
+    // re-materialise the record (header fields as given, batch_length = 256 + blob)
+    std::vector<uint8_t> rec(256 + blob_len);
+    iggy_batch_header h = *hdr;
+    iggy_batch_header_encode(&h, rec.data());
+    uint64_t bl = 256 + blob_len;
+    memcpy(rec.data() + 32, &bl, 8);
+    if (blob_len) memcpy(rec.data() + 256, blob, blob_len);
+    iggy_decode_result res;
+    int r = decode_host(c, rec.data(), rec.size(), IGGY_INTEGRITY_VERIFY, &res, nullptr, 0, false);
+    if (r) return r;
+    if (res.error.kind == IGGY_ERR_INVALID_BATCH_CHECKSUM || res.error.kind == IGGY_OK) {
+        if (out) *out = res.computed_checksum;
+        set_err(err, IGGY_OK);
+        return 0;
+    }
+    fill_err(err, res.error);
+    return (int)res.error.kind;
+}
+
+static int checksum_of_walk(iggy_codec_ctx *c, const iggy_batch_header *hdr, const uint8_t *d_blob,
+                            const uint64_t *d_pos, const uint64_t *d_n, uint64_t *d_out, hipStream_t s) {
+    // hdr is host: stage it in the result area
+    iggy_batch_header *dh = c->dresult.as<iggy_batch_header>(2048);
+    HIP_OK(hipMemcpyAsync(dh, hdr, sizeof(*hdr), hipMemcpyHostToDevice, s));
+    CsSource src{nullptr, d_blob, d_pos};
+    hipLaunchKernelGGL(k_bsum_blocks, dim3(c->ncu * 4), dim3(256), 0, s, dh, d_n, src,
+                       c->gbsums.as<uint64_t>(), nullptr);
+    hipLaunchKernelGGL(k_bsum_chain, dim3(1), dim3(64), 0, s, dh, d_n, src,
+                       (const uint64_t *)c->gbsums.as<uint64_t>(), c->dsync.as<uint8_t>(kSyncSmall), d_out,
+                       nullptr);
+    HIP_OK(hipGetLastError());
+    return 0;
+}
+
+int iggy_codec_calculate_batch_checksum(iggy_codec_ctx *c, const iggy_batch_header *hdr,
+                                        const uint8_t *blob, uint64_t blob_len, uint64_t *out) {
+    if (!c || !hdr || !out || (!blob && blob_len)) return IGGY_ERR_INVALID_ARGUMENT;
+    HIP_OK(hipSetDevice(c->device));
+    // walk the blob (layout) to find the frames the infallible iterator yields
+    std::vector<uint8_t> rec(256 + blob_len);
+    iggy_batch_header h = *hdr;
+    h.batch_length = 256 + blob_len;
+    h.message_count = 0;
+    iggy_batch_header_encode(&h, rec.data());
+    if (blob_len) memcpy(rec.data() + 256, blob, blob_len);
+    iggy_decode_result res;
+    int r = c->dpos.ensure((blob_len / 48 + 2) * 8);
+    if (r) return r;
+    r = decode_host(c, rec.data(), rec.size(), IGGY_INTEGRITY_LAYOUT_ONLY, &res, nullptr, 0, true);
+    if (r) return r;
+    // positions: re-run the walk with the frame_pos output on device
+    r = enqueue_decode(c, c->din.as<uint8_t>(), rec.size(), IGGY_INTEGRITY_LAYOUT_ONLY,
+                       c->dpos.as<uint64_t>(), blob_len / 48 + 1, c->dresult.as<iggy_decode_result>(),
+                       c->stream);
+    if (r) return r;
+    uint64_t *dn = c->dresult.as<uint64_t>(3072);
+    uint64_t n = res.frame_count;
+    HIP_OK(hipMemcpyAsync(dn, &n, 8, hipMemcpyHostToDevice, c->stream));
+    uint64_t *dout = c->dresult.as<uint64_t>(3080);
+    iggy_batch_header hc = *hdr;  // checksum uses the caller's header fields
+    r = checksum_of_walk(c, &hc, c->din.as<uint8_t>(256), c->dpos.as<uint64_t>(), dn, dout, c->stream);
+    if (r) return r;
+    HIP_OK(hipMemcpyAsync(out, dout, 8, hipMemcpyDeviceToHost, c->stream));
+    HIP_OK(hipStreamSynchronize(c->stream));
+    return 0;
+}
+
+int iggy_codec_stamp_batch(iggy_codec_ctx *c, uint8_t *batch, uint64_t len, uint64_t base_offset,
+                           uint64_t base_timestamp, iggy_batch_header *out, iggy_wire_error *err) {
+    if (!c || (!batch && len)) return IGGY_ERR_INVALID_ARGUMENT;
+    iggy_batch_header h;
+    int r = iggy_batch_header_decode(batch, len, &h, err);
+    if (r) return r;
+    if (len < h.batch_length) {
+        set_err(err, IGGY_ERR_UNEXPECTED_EOF, 0, 0, h.batch_length, len);
+        return IGGY_ERR_UNEXPECTED_EOF;
+    }
+    h.base_offset = base_offset;
+    h.base_timestamp = base_timestamp;
+    uint64_t cs = 0;
+    r = iggy_codec_calculate_batch_checksum(c, &h, batch + 256, h.batch_length - 256, &cs);
+    if (r) return r;
+    h.batch_checksum = cs;
+    uint8_t hb[256];
+    iggy_batch_header_encode(&h, hb);
+    memcpy(batch, hb, 256);
+    if (out) *out = h;
+    set_err(err, IGGY_OK);
+    return 0;
+}
+
+int iggy_codec_xxh3_64(iggy_codec_ctx *c, const void *data, uint64_t len, uint64_t *out) {
+    if (!c || !out || (!data && len)) return IGGY_ERR_INVALID_ARGUMENT;
+    HIP_OK(hipSetDevice(c->device));
+    int r = c->din.ensure(len + 16);
+    const uint64_t nb = len ? (len - 1) / 1024 + 1 : 1;
+    r |= c->hbsums.ensure(nb * 64 + 64);
+    if (r) return IGGY_ERR_DEVICE;
+    if (len) HIP_OK(hipMemcpyAsync(c->din.p, data, len, hipMemcpyHostToDevice, c->stream));
+    uint64_t *dout = c->dresult.as<uint64_t>(3088);
+    if (len > 240)
+        hipLaunchKernelGGL(k_xxh3_big_blocks, dim3(c->ncu * 4), dim3(256), 0, c->stream,
+                           c->din.as<uint8_t>(), len, c->hbsums.as<uint64_t>());
+    hipLaunchKernelGGL(k_xxh3_big_chain, dim3(1), dim3(64), 0, c->stream, c->din.as<uint8_t>(), len,
+                       (const uint64_t *)c->hbsums.as<uint64_t>(), dout);
+    HIP_OK(hipGetLastError());
+    HIP_OK(hipMemcpyAsync(out, dout, 8, hipMemcpyDeviceToHost, c->stream));
+    HIP_OK(hipStreamSynchronize(c->stream));
+    return 0;
+}
+
+// ---------------------------------------------------------------- encode
+static int enqueue_encode(iggy_codec_ctx *c, const iggy_raw_messages *dm, uint64_t partition_id,
+                          uint8_t *d_out, iggy_encode_result *d_res, hipStream_t s) {
+    const uint64_t n = dm->count;
+    const uint64_t ntiles = (n + kEncTile - 1) / kEncTile;
+    int r = 0;
+    r |= c->epl.ensure(n * 8);
+    r |= c->euh.ensure(n * 8);
+    r |= c->etile.ensure(ntiles * 24 + 64);
+    r |= c->ecs.ensure(n * 8);
+    r |= c->emisc.ensure(512);
+    const uint64_t nbk = (44 + 8 * n) / 1024 + 2;
+    r |= c->gbsums.ensure(nbk * 64);
+    if (r) return IGGY_ERR_DEVICE;
+    EncScratch es;
+    es.pl_local = c->epl.as<uint64_t>();
+    es.uh_local = c->euh.as<uint64_t>();
+    es.tile_pl = c->etile.as<uint64_t>();
+    es.tile_uh = c->etile.as<uint64_t>(ntiles * 8);
+    es.tile_min = c->etile.as<uint64_t>(ntiles * 16);
+    es.cs = c->ecs.as<uint64_t>();
+    es.misc = c->emisc.as<uint64_t>();
+    es.hdr = c->emisc.as<iggy_batch_header>(128);
+    iggy_raw_messages m = *dm;
+    prof_begin(c, 1, s);
+    hipLaunchKernelGGL(k_enc_prep, dim3(ntiles), dim3(256), 0, s, m, es);
+    hipLaunchKernelGGL(k_enc_scan, dim3(1), dim3(256), 0, s, ntiles, n, partition_id, es);
+    const uint64_t waves = std::min<uint64_t>(n, (uint64_t)c->ncu * 32);
+    hipLaunchKernelGGL(k_enc_frames, dim3((waves + 3) / 4), dim3(256), 0, s, m, es, d_out);
+    prof_end(c, 1, s);
+    CsSource src{es.cs, nullptr, nullptr};
+    hipLaunchKernelGGL(k_bsum_blocks, dim3(c->ncu * 4), dim3(256), 0, s, (const iggy_batch_header *)es.hdr,
+                       (const uint64_t *)&es.misc[3], src, c->gbsums.as<uint64_t>(), nullptr);
+    uint64_t *dcs = c->emisc.as<uint64_t>(256);
+    hipLaunchKernelGGL(k_bsum_chain, dim3(1), dim3(64), 0, s, (const iggy_batch_header *)es.hdr,
+                       (const uint64_t *)&es.misc[3], src, (const uint64_t *)c->gbsums.as<uint64_t>(),
+                       c->emisc.as<uint8_t>(320) /* 192 B of small */, dcs, nullptr);
+    hipLaunchKernelGGL(k_enc_finish, dim3(1), dim3(64), 0, s, m, es, partition_id,
+                       (const uint64_t *)dcs, d_out, d_res);
+    HIP_OK(hipGetLastError());
+    return 0;
+}
+
+int iggy_codec_encode_batch(iggy_codec_ctx *c, const iggy_raw_messages *m, uint64_t partition_id,
+                            uint8_t *out, uint64_t cap, uint64_t *out_len, iggy_wire_error *err) {
+    if (!c || !m) return IGGY_ERR_INVALID_ARGUMENT;
+    set_err(err, IGGY_OK);
+    if (m->count == 0) {
+        set_err(err, IGGY_ERR_VALIDATION, IGGY_V_EMPTY_BATCH);
+        return IGGY_ERR_VALIDATION;
+    }
+    if (m->count > 0xFFFFFFFFull) {
+        set_err(err, IGGY_ERR_PAYLOAD_TOO_LARGE, 0, m->count, 0xFFFFFFFFull);
+        return IGGY_ERR_PAYLOAD_TOO_LARGE;
+    }
+    HIP_OK(hipSetDevice(c->device));
+    const uint64_t n = m->count;
+    uint64_t spl = 0, suh = 0;
+    for (uint64_t i = 0; i < n; ++i) {
+        spl += m->payload_lengths[i];
+        suh += m->user_headers_lengths ? m->user_headers_lengths[i] : 0;
+    }
+    const uint64_t need = 256 + 48 * n + spl + suh;
+    if (cap < need || !out) {
+        set_err(err, IGGY_ERR_CAPACITY, 0, need, cap);
+        return IGGY_ERR_CAPACITY;
+    }
+    int r = 0;
+    r |= c->eids.ensure(n * 16);
+    r |= c->eots.ensure(n * 8);
+    r |= c->epay.ensure(spl + 16);
+    r |= c->eplen.ensure(n * 4);
+    r |= c->euhb.ensure(suh + 16);
+    r |= c->euhl.ensure(n * 4);
+    r |= c->dout.ensure(need + 16);
+    if (r) return IGGY_ERR_DEVICE;
+    hipStream_t s = c->stream;
+    HIP_OK(hipMemcpyAsync(c->eids.p, m->ids, n * 16, hipMemcpyHostToDevice, s));
+    HIP_OK(hipMemcpyAsync(c->eots.p, m->origin_timestamps, n * 8, hipMemcpyHostToDevice, s));
+    if (spl) HIP_OK(hipMemcpyAsync(c->epay.p, m->payloads, spl, hipMemcpyHostToDevice, s));
+    HIP_OK(hipMemcpyAsync(c->eplen.p, m->payload_lengths, n * 4, hipMemcpyHostToDevice, s));
+    const bool has_uh = m->user_headers_lengths != nullptr;
+    if (has_uh) {
+        if (suh) HIP_OK(hipMemcpyAsync(c->euhb.p, m->user_headers, suh, hipMemcpyHostToDevice, s));
+        HIP_OK(hipMemcpyAsync(c->euhl.p, m->user_headers_lengths, n * 4, hipMemcpyHostToDevice, s));
+    }
+    iggy_raw_messages dm;
+    dm.count = n;
+    dm.ids = c->eids.as<uint64_t>();
+    dm.origin_timestamps = c->eots.as<uint64_t>();
+    dm.payloads = c->epay.as<uint8_t>();
+    dm.payload_lengths = c->eplen.as<uint32_t>();
+    dm.user_headers = has_uh ? c->euhb.as<uint8_t>() : nullptr;
+    dm.user_headers_lengths = has_uh ? c->euhl.as<uint32_t>() : nullptr;
+    iggy_encode_result *d_res = c->dresult.as<iggy_encode_result>(512);
+    r = enqueue_encode(c, &dm, partition_id, c->dout.as<uint8_t>(), d_res, s);
+    if (r) return r;
+    iggy_encode_result *h_res = (iggy_encode_result *)((uint8_t *)c->h_pinned + 512);
+    HIP_OK(hipMemcpyAsync(h_res, d_res, sizeof(*h_res), hipMemcpyDeviceToHost, s));
+    HIP_OK(hipStreamSynchronize(s));
+    if (h_res->error.kind != IGGY_OK) {
+        fill_err(err, h_res->error);
+        return (int)h_res->error.kind;
+    }
+    HIP_OK(hipMemcpy(out, c->dout.p, need, hipMemcpyDeviceToHost));
+    if (out_len) *out_len = need;
+    return 0;
+}
+
+int iggy_codec_encode_batch_device(iggy_codec_ctx *c, const iggy_raw_messages *msgs,
+                                   uint64_t partition_id, uint8_t *d_out, uint64_t cap,
+                                   iggy_encode_result *d_result, void *stream) {
+    if (!c || !msgs || !d_out || !d_result || msgs->count == 0 || msgs->count > 0xFFFFFFFFull)
+        return IGGY_ERR_INVALID_ARGUMENT;
+    (void)cap;
+    return enqueue_encode(c, msgs, partition_id, d_out, d_result, pick(c, stream));
+}
+
+// ------------------------------------------------------------- poll decode
+int iggy_codec_poll_decode(iggy_codec_ctx *c, const uint8_t *buf, uint64_t len, int mode,
+                           iggy_polled_message *out, uint64_t cap, uint64_t *n_out,
+                           iggy_wire_error *err) {
+    if (!c || (!buf && len)) return IGGY_ERR_INVALID_ARGUMENT;
+    HIP_OK(hipSetDevice(c->device));
+    set_err(err, IGGY_OK);
+    uint64_t n = 0, position = 0;
+    if (n_out) *n_out = 0;
+    int r = 0;
+    r |= c->din.ensure(len + 16);
+    r |= c->ppos.ensure((len / 48 + 2) * 8);
+    r |= c->pmsgs.ensure((len / 48 + 2) * sizeof(iggy_polled_message));
+    if (r) return IGGY_ERR_DEVICE;
+    if (len) HIP_OK(hipMemcpyAsync(c->din.p, buf, len, hipMemcpyHostToDevice, c->stream));
+    iggy_decode_result *d_res = c->dresult.as<iggy_decode_result>();
+    iggy_decode_result *h_res = (iggy_decode_result *)c->h_pinned;
+    // copy the messages decoded so far back to the caller (the iterator yields
+    // them before its error, poll_messages.rs:135-163)
+    auto flush = [&](uint64_t count) -> int {
+        if (count) {
+            HIP_OK(hipMemcpyAsync(out, c->pmsgs.p, count * sizeof(iggy_polled_message),
+                                  hipMemcpyDeviceToHost, c->stream));
+        }
+        HIP_OK(hipStreamSynchronize(c->stream));
+        if (n_out) *n_out = count;
+        return 0;
+    };
+    while (position < len) {
+        // record header: host-side (256 B), per polled_messages.rs:99-106 / poll_messages.rs:123-125
+        iggy_batch_header h;
+        iggy_wire_error he;
+        const int hr = iggy_batch_header_decode(buf + position, len - position, &h, &he);
+        if (mode == IGGY_POLL_MODE_SDK) {
+            if (hr || h.batch_length > len - position) {
+                set_err(err, IGGY_ERR_INVALID_MESSAGE_PAYLOAD_LENGTH);
+                return IGGY_ERR_INVALID_MESSAGE_PAYLOAD_LENGTH;
+            }
+        } else if (hr) {
+            fill_err(err, he);
+            if ((r = flush(n))) return r;
+            return hr;
+        }
+        // frame walk of this record on the device (layout only)
+        r = enqueue_decode(c, c->din.as<uint8_t>(position), len - position, IGGY_INTEGRITY_LAYOUT_ONLY,
+                           c->ppos.as<uint64_t>(), len / 48 + 1, d_res, c->stream);
+        if (r) return r;
+        HIP_OK(hipMemcpyAsync(h_res, d_res, sizeof(*h_res), hipMemcpyDeviceToHost, c->stream));
+        HIP_OK(hipStreamSynchronize(c->stream));
+        const iggy_decode_result res = *h_res;
+        if (res.error.kind == IGGY_ERR_TIMEOUT) {
+            reset_after_timeout(c);
+            fill_err(err, res.error);
+            return IGGY_ERR_TIMEOUT;
+        }
+        const uint64_t bl = h.batch_length - 256;
+        const uint64_t nf = res.frame_count;
+        if (mode == IGGY_POLL_MODE_SDK) {
+            // the SDK walk only needs the frames to tile the record (no count check)
+            if (res.covered != bl) {
+                set_err(err, IGGY_ERR_INVALID_MESSAGE_PAYLOAD_LENGTH);
+                return IGGY_ERR_INVALID_MESSAGE_PAYLOAD_LENGTH;
+            }
+        } else if (res.error.kind != IGGY_OK) {
+            fill_err(err, res.error);
+            if ((r = flush(n))) return r;
+            return (int)res.error.kind;
+        }
+        if (n + nf > cap) {
+            set_err(err, IGGY_ERR_CAPACITY, 0, n + nf, cap);
+            if (n_out) *n_out = n;
+            return IGGY_ERR_CAPACITY;
+        }
+        if (nf) {
+            hipLaunchKernelGGL(k_poll_fill, dim3((uint32_t)std::min<uint64_t>((nf + 255) / 256, 65535)), dim3(256), 0,
+                               c->stream, c->din.as<uint8_t>(), position, c->ppos.as<uint64_t>(), nf,
+                               c->pmsgs.as<iggy_polled_message>(n * sizeof(iggy_polled_message)));
+            HIP_OK(hipGetLastError());
+        }
+        n += nf;
+        position += h.batch_length;
+    }
+    return flush(n);
+}
+
+// ------------------------------------------------------------ device APIs
+int iggy_codec_decode_batch_device(iggy_codec_ctx *c, const uint8_t *d_body, uint64_t len,
+                                   int integrity, uint64_t *d_frame_pos, uint64_t cap,
+                                   iggy_decode_result *d_result, void *stream) {
+    if (!c || !d_result || (!d_body && len)) return IGGY_ERR_INVALID_ARGUMENT;
+    return enqueue_decode(c, d_body, len, integrity, d_frame_pos, d_frame_pos ? cap : 0, d_result,
+                          pick(c, stream));
+}
+
+int iggy_codec_batch_checksum_device(iggy_codec_ctx *c, const iggy_batch_header *hdr,
+                                     const uint8_t *d_blob, const uint64_t *d_frame_pos,
+                                     uint64_t nframes, uint64_t *d_out, void *stream) {
+    if (!c || !hdr || !d_out) return IGGY_ERR_INVALID_ARGUMENT;
+    hipStream_t s = pick(c, stream);
+    int r = c->gbsums.ensure(((44 + 8 * nframes) / 1024 + 2) * 64);
+    if (r) return r;
+    uint64_t *dn = c->dresult.as<uint64_t>(3096);
+    HIP_OK(hipMemcpyAsync(dn, &nframes, 8, hipMemcpyHostToDevice, s));
+    return checksum_of_walk(c, hdr, d_blob, d_frame_pos, dn, d_out, s);
+}
+
+int iggy_codec_xxh3_64_ranges_device(iggy_codec_ctx *c, const uint8_t *d_data, const uint64_t *d_offsets,
+                                     const uint32_t *d_lengths, uint64_t n, uint64_t *d_out,
+                                     void *stream) {
+    if (!c || !d_out || (n && (!d_data || !d_offsets || !d_lengths))) return IGGY_ERR_INVALID_ARGUMENT;
+    if (!n) return 0;
+    const uint64_t blocks = std::min<uint64_t>((n + 255) / 256, (uint64_t)c->ncu * 16);
+    hipLaunchKernelGGL(k_xxh3_ranges, dim3((uint32_t)blocks), dim3(256), 0, pick(c, stream), d_data,
+                       d_offsets, d_lengths, n, d_out);
+    HIP_OK(hipGetLastError());
+    return 0;
+}
+
+// -------------------------------------------------------------- profiling
+int iggy_codec_profile_enable(iggy_codec_ctx *c, int enable) {
+    if (!c) return IGGY_ERR_INVALID_ARGUMENT;
+    c->profile = enable ? 1 : 0;
+    for (int w = 0; w < 2; ++w) {
+        c->prof_n[w] = 0;
+        c->prof_ms[w] = 0;
+        c->ev_pending[w] = false;
+    }
+    return 0;
+}
+
+int iggy_codec_profile_read(iggy_codec_ctx *c, int which, uint64_t *launches, double *total_ms) {
+    if (!c || which < 0 || which > 1) return IGGY_ERR_INVALID_ARGUMENT;
+    if (c->ev_pending[which]) {
+        float ms = 0;
+        HIP_OK(hipEventSynchronize(c->ev1[which]));
+        if (hipEventElapsedTime(&ms, c->ev0[which], c->ev1[which]) == hipSuccess) {
+            c->prof_ms[which] += ms;
+            c->prof_n[which] += 1;
+        }
+        c->ev_pending[which] = false;
+    }
+    if (launches) *launches = c->prof_n[which];
+    if (total_ms) *total_ms = c->prof_ms[which];
+    c->prof_n[which] = 0;
+    c->prof_ms[which] = 0;
+    return 0;
+}
+
+const char *iggy_codec_error_string(uint32_t kind, uint32_t reason) {
+    switch (kind) {
+        case IGGY_OK: return "ok";
+        case IGGY_ERR_UNEXPECTED_EOF: return "unexpected end of buffer";
+        case IGGY_ERR_VALIDATION:
+            switch (reason) {
+                case IGGY_V_BATCH_LENGTH_SHORT: return "batch length must cover the batch header";
+                case IGGY_V_BATCH_RESERVED: return "batch header reserved bytes must be zero";
+                case IGGY_V_FRAMES_DO_NOT_TILE: return "batch frames do not tile message_count exactly";
+                case IGGY_V_FRAME_RESERVED: return "message frame reserved bytes must be zero";
+                case IGGY_V_EMPTY_BATCH: return "cannot encode an empty message batch";
+                default: return "validation failed";
+            }
+        case IGGY_ERR_INVALID_BATCH_CHECKSUM: return "invalid batch checksum";
+        case IGGY_ERR_INVALID_MESSAGE_CHECKSUM: return "invalid message checksum";
+        case IGGY_ERR_INVALID_TIMESTAMP_DELTA: return "message timestamp delta exceeds the batch maximum";
+        case IGGY_ERR_PAYLOAD_TOO_LARGE: return "payload too large";
+        case IGGY_ERR_INVALID_NUMBER_ENCODING: return "invalid number encoding";
+        case IGGY_ERR_INVALID_MESSAGE_PAYLOAD_LENGTH: return "invalid message payload length";
+        case IGGY_ERR_DEVICE: return "device error";
+        case IGGY_ERR_INVALID_ARGUMENT: return "invalid argument";
+        case IGGY_ERR_CAPACITY: return "output capacity too small";
+        case IGGY_ERR_TIMEOUT: return "device wait timed out";
+        default: return "unknown";
+    }
+}
+
+}  // extern "C"

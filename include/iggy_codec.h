@@ -142,7 +142,7 @@ typedef struct iggy_decode_result {
     uint64_t computed_checksum;  /* recomputed batch checksum (Verify) */
     uint32_t path;               /* 1 = uniform-stride kernel, 2 = general walk */
     uint32_t status;             /* 0 = done; internal otherwise */
-    uint64_t _pad;
+    uint64_t covered;            /* end of the last walked frame (blob-relative) */
 } iggy_decode_result;
 
 /* Device-resident result of an asynchronous encode. */

@@ -294,25 +294,29 @@ int oracle_poll_decode(const uint8_t *buf, uint64_t len, int mode, iggy_polled_m
         if (mode == IGGY_POLL_MODE_SDK) {
             if (oracle_batch_header_decode(buf + position, len - position, &h, &he)) {
                 set_err(e, IGGY_ERR_INVALID_MESSAGE_PAYLOAD_LENGTH, 0, 0, 0, 0);
+                if (n_out) *n_out = 0;
                 return IGGY_ERR_INVALID_MESSAGE_PAYLOAD_LENGTH;
             }
             uint64_t batch_end = position + h.batch_length;
             if (batch_end < position || batch_end > len) { /* checked_add + filter, :103-106 */
                 set_err(e, IGGY_ERR_INVALID_MESSAGE_PAYLOAD_LENGTH, 0, 0, 0, 0);
+                if (n_out) *n_out = 0;
                 return IGGY_ERR_INVALID_MESSAGE_PAYLOAD_LENGTH;
             }
             uint64_t cursor = position + HDR;
             while (cursor < batch_end) {
                 if (batch_end - cursor < FHDR || rd64(buf + cursor + 40) != 0) {
                     set_err(e, IGGY_ERR_INVALID_MESSAGE_PAYLOAD_LENGTH, 0, 0, 0, 0);
-                    return IGGY_ERR_INVALID_MESSAGE_PAYLOAD_LENGTH;
+                    if (n_out) *n_out = 0;
+                return IGGY_ERR_INVALID_MESSAGE_PAYLOAD_LENGTH;
                 }
                 const uint8_t *f = buf + cursor;
                 uint32_t pl = rd32(f + 36), uh = rd32(f + 32);
                 uint64_t ps = cursor + FHDR, pe = ps + pl, ue = pe + uh;
                 if (ue > batch_end) {
                     set_err(e, IGGY_ERR_INVALID_MESSAGE_PAYLOAD_LENGTH, 0, 0, 0, 0);
-                    return IGGY_ERR_INVALID_MESSAGE_PAYLOAD_LENGTH;
+                    if (n_out) *n_out = 0;
+                return IGGY_ERR_INVALID_MESSAGE_PAYLOAD_LENGTH;
                 }
                 if (n >= cap) {
                     set_err(e, IGGY_ERR_CAPACITY, 0, n + 1, cap, 0);

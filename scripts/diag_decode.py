@@ -1,0 +1,67 @@
+"""Diagnostic A/B of the uniform decode kernel's roles (not part of the bench).
+
+IGGY_CODEC_DBG bits (read at context creation): 1 = consumer skips the serial
+batch-checksum chain, 2 = producers skip hashing, 4 = feeder skips loading sums.
+All variants run interleaved in one process on the same batch.
+"""
+import ctypes
+import os
+import sys
+import time
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from iggy_amd import abi  # noqa: E402
+from iggy_amd.codec import Codec  # noqa: E402
+import bench  # noqa: E402
+
+
+def main():
+    n = int(sys.argv[1]) if len(sys.argv) > 1 else 1 << 20
+    pl = int(sys.argv[2]) if len(sys.argv) > 2 else 1024
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(0)
+    variants = [0, 1, 2, 3, 5, 7]
+    ctxs = {}
+    for v in variants:
+        os.environ["IGGY_CODEC_DBG"] = str(v)
+        ctxs[v] = Codec(0)
+    os.environ.pop("IGGY_CODEC_DBG")
+    ts = torch.cuda.Stream()
+    torch.cuda.set_stream(ts)
+    stream = ts.cuda_stream
+    assert stream != 0
+    batch = bench.make_batch(ctxs[0], n, pl, 0, dev, stream)
+    L = batch.numel()
+    d_pos = torch.empty(n, dtype=torch.int64, device=dev)
+    d_res = torch.zeros(ctypes.sizeof(abi.DecodeResult), dtype=torch.uint8, device=dev)
+    for v, cx in ctxs.items():
+        cx.reserve(L)
+    res = {v: [] for v in variants}
+    for integ in (0, 1):
+        for rnd in range(3):
+            for v, cx in ctxs.items():
+                if integ == 1 and v != 0:
+                    continue
+                for _ in range(2):
+                    rc = cx.decode_device(batch.data_ptr(), L, integ, d_pos.data_ptr(), n, d_res.data_ptr(), stream)
+                    assert rc == 0, rc
+                torch.cuda.synchronize()
+                e0 = torch.cuda.Event(enable_timing=True)
+                e1 = torch.cuda.Event(enable_timing=True)
+                e0.record()
+                d_res.zero_()
+                for _ in range(10):
+                    rc = cx.decode_device(batch.data_ptr(), L, integ, d_pos.data_ptr(), n, d_res.data_ptr(), stream)
+                    assert rc == 0, rc
+                e1.record()
+                torch.cuda.synchronize()
+                ms = e0.elapsed_time(e1) / 10
+                r = abi.DecodeResult.from_buffer_copy(d_res.cpu().numpy().tobytes())
+                print(f"integ={integ} dbg={v} round={rnd} ms={ms:.4f} GiB/s={L/ms/1e-3/2**30:.1f} "
+                      f"err={r.error.kind} frames={r.frame_count} path={r.path}", flush=True)
+
+
+if __name__ == "__main__":
+    main()
