@@ -112,9 +112,9 @@ int ensure_decode_scratch(iggy_codec_ctx *c, uint64_t len) {
         if (r) return r;
         HIP_OK(hipMemset(c->dsync.p, 0, kSyncBytes));
     }
-    r |= c->dflags.ensure(max_chunks * 4);
+    r |= c->dflags.ensure(max_chunks * 16);  // u32 per (chunk, wave)
     if (!r && c->dflags.p) HIP_OK(hipMemset(c->dflags.p, 0, c->dflags.cap));
-    r |= c->dsums.ensure(2 * max_chunks * 64);
+    r |= c->dsums.ensure(max_chunks * 4 * 64);  // 8 x u64 per (chunk, wave)
     r |= c->derr.ensure(max_chunks * 4 * 16);
     r |= c->gtiles_s.ensure(ntiles * 8);
     r |= c->gtiles_x.ensure(ntiles * 8);
@@ -138,7 +138,7 @@ DecodeScratch dscratch(iggy_codec_ctx *c) {
     s.sums = c->dsums.as<uint64_t>();
     s.errslot = c->derr.as<uint64_t>();
     s.small = c->dsync.as<uint8_t>(kSyncSmall);
-    s.max_chunks = c->dflags.cap / 4;
+    s.max_chunks = c->dflags.cap / 16;
     return s;
 }
 

@@ -11,20 +11,25 @@
 //
 // Work layout (MI355X: 256 CUs, wave64, 160 KiB LDS):
 //  * grid = 1 consumer WG + NPROD producer WGs (one per CU, 256 threads,
-//    ~154 KiB LDS). Producer g handles chunks g, g+NPROD, ... statically.
+//    152 KiB LDS). Producer g handles chunks g, g+NPROD, ... statically.
 //  * a chunk = 256 consecutive frames [256c-6, 256c+250); the -6 aligns the
 //    chunk with two 1024-B blocks of the batch-checksum input
-//    (44 header bytes + 8 bytes per frame => word m = frame + 6).
-//  * each wave owns 64 frames (one per lane) and streams them through a
-//    double-buffered 16 KiB LDS image with global_load_lds_dwordx4: one
-//    wave-instruction moves 4 frames x 256 contiguous bytes (full lines),
-//    the image is XOR-swizzled so every lane's ds_read_b128 is conflict-free.
+//    (44 header bytes + 8 bytes per frame => checksum word m = frame + 6).
+//  * each wave owns 64 frames (one per lane) and runs independently (no
+//    workgroup barrier anywhere in the producer): it streams its frames
+//    through a 4-slot LDS ring with global_load_lds_dwordx4, three phases of
+//    8 x 16 B per lane in flight (24 KiB per wave, 96 KiB per CU). One
+//    wave-instruction moves 8 frames x 128 contiguous bytes (full lines); the
+//    image is XOR-swizzled so the per-lane ds_read_b128 are bank-balanced.
+//    Short frames (S <= 248) use 2 slots of 16 chunks (whole frame per slot).
 //  * XXH3 per lane: stripe words accumulate in registers, scramble at block
 //    ends, last stripe from a per-lane side copy, merge.
-//  * batch checksum: each chunk reduces its 256 checksum-input words to the
-//    8 accumulator sums of its two XXH3 blocks and publishes them
-//    (write-through sc1 stores + flag); the consumer WG runs the serial
-//    8192-step scramble chain concurrently, fed through an LDS ring.
+//  * batch checksum: each wave reduces its 63 interior checksum-input words to
+//    8 accumulator partial sums and publishes them (write-through sc1 stores,
+//    then a per-wave flag once its vmcnt covers the stores). The consumer WG's
+//    single wave gathers 64 chunks at a time (partials + wave-boundary words),
+//    stages them in LDS and runs the serial 1-scramble-per-block chain while
+//    the next 64 chunks' loads are in flight.
 #include "codec_common.hpp"
 
 #include <utility>
@@ -32,32 +37,38 @@
 namespace iggy {
 
 struct DecodeScratch {
-    uint32_t *exited;     // producer WGs that finished (reset by consumer)
+    uint32_t *exited;     // producer waves that finished (reset by consumer)
     uint64_t *first_bad;  // ~index of first checksum mismatch (max-encoded), 0 = none
     uint64_t *spec_fail;  // ~index of first frame whose header breaks the stride
-    uint32_t *flags;      // [max_chunks] = epoch when the chunk's sums are published
-    uint64_t *sums;       // [2*max_chunks][8] per-block accumulator sums
+    uint32_t *flags;      // [max_chunks*4] = epoch when wave w's sums of chunk c are published
+    uint64_t *sums;       // [max_chunks*4][8] per-wave accumulator partial sums
     uint64_t *errslot;    // [max_chunks*4][2] (stored, computed) per wave
     uint8_t *small;       // >= 512 B: short batch-checksum inputs
     uint64_t max_chunks;
 };
 
 // ---- LDS map of a producer WG (dynamic LDS only, base offset 0) ----------
-constexpr uint32_t kWaveBuf = 16384;                  // one phase: 64 lanes x 16 chunks x 16 B
-constexpr uint32_t kSideOff = 4 * 2 * kWaveBuf;      // 131072
-constexpr uint32_t kSideLane = 96;                    // 6 chunks per lane
-constexpr uint32_t kXchgOff = kSideOff + 4 * 64 * kSideLane;  // 155648
-constexpr uint32_t kRedOff = kXchgOff + 256 * 8;      // 157696
-constexpr uint32_t kLdsBytes = kRedOff + 4 * 8 * 8;   // 157952
-// consumer WG reuses the space: ring of per-chunk sums + control words
-constexpr uint32_t kRing = 1024;                      // chunks (128 B each) = 128 KiB
-constexpr uint32_t kCtrlOff = kRing * 128;            // 131072
+constexpr uint32_t kWaveRing = 32768;                          // per wave: 4 x 8 KiB or 2 x 16 KiB
+constexpr uint32_t kSideOff = 4 * kWaveRing;                   // 131072
+constexpr uint32_t kSideLane = 96;                             // 6 chunks per lane
+constexpr uint32_t kLdsBytes = kSideOff + 4 * 64 * kSideLane;  // 155648
+// consumer WG: ring of kRing batches of 64 chunks' block sums (16 x u64 per chunk),
+// filled by kGatherWaves gatherer waves, drained by the chain wave
+constexpr uint32_t kBatch = 64;
+constexpr uint32_t kRing = 8;
+constexpr uint32_t kGatherWaves = 3;
+constexpr uint32_t kCtlOff = kRing * kBatch * 16 * 8;  // 64 KiB
+struct ChainCtl {
+    uint32_t ready[kRing];  // batch index + 1 staged in the slot
+    uint32_t consumed;      // batches the chain wave has finished
+    uint32_t abort;         // a gatherer or the chain wave gave up (spin limit)
+};
+static_assert(kCtlOff + sizeof(ChainCtl) <= kLdsBytes, "consumer LDS");
 static_assert(kLdsBytes <= 160 * 1024, "LDS budget");
-
 
 struct UPlan {
     uint32_t state;  // 0 run, 1 result known early, 2 need general
-    uint32_t nck, nph, q_side0;
+    uint32_t nck, nph, q_side0, ph;
     uint64_t S, N, L, nchunks;
     uint64_t nbF, Kreg;          // per-frame hash: full blocks, regular words
     uint64_t n, nb, Mreg;        // batch checksum input: bytes, full blocks, regular words
@@ -74,6 +85,7 @@ __device__ inline void make_plan(const HeaderInfo &hi, const uint8_t *blob, uint
     p.ekind = IGGY_OK; p.ereason = 0; p.ea = p.eb = p.ec = 0;
     p.S = p.N = p.L = p.nchunks = 0;
     p.nck = p.nph = p.q_side0 = 0;
+    p.ph = 16;
     p.nbF = p.Kreg = p.n = p.nb = p.Mreg = 0;
     p.long_frames = p.long_cs = false;
     if (hi.err_kind != IGGY_OK) {
@@ -91,7 +103,7 @@ __device__ inline void make_plan(const HeaderInfo &hi, const uint8_t *blob, uint
         p.state = 1; p.ekind = IGGY_ERR_VALIDATION; p.ereason = IGGY_V_FRAMES_DO_NOT_TILE;
         return;
     }
-    uint64_t S = kFrameHdr + (uint64_t)ld32_any(blob + 36) + (uint64_t)ld32_any(blob + 32);
+    const uint64_t S = kFrameHdr + (uint64_t)ld32_any(blob + 36) + (uint64_t)ld32_any(blob + 32);
     if (S > bl) {
         p.state = 1; p.ekind = IGGY_ERR_VALIDATION; p.ereason = IGGY_V_FRAMES_DO_NOT_TILE;
         return;
@@ -107,8 +119,9 @@ __device__ inline void make_plan(const HeaderInfo &hi, const uint8_t *blob, uint
         p.nck = (uint32_t)((S + 15) / 16);
         p.long_frames = p.L > 240;
         if (p.long_frames) {
+            p.ph = 8;
             p.nbF = (p.L - 1) / 1024;
-            uint64_t ns = ((p.L - 1) - 1024 * p.nbF) / 64;
+            const uint64_t ns = ((p.L - 1) - 1024 * p.nbF) / 64;
             p.Kreg = 8 * (16 * p.nbF + ns);
             p.q_side0 = (uint32_t)((S - 64) >> 4);
         }
@@ -116,13 +129,13 @@ __device__ inline void make_plan(const HeaderInfo &hi, const uint8_t *blob, uint
         p.long_cs = p.n > 240;
         if (p.long_cs) {
             p.nb = (p.n - 1) / 1024;
-            uint64_t ns = ((p.n - 1) - 1024 * p.nb) / 64;
+            const uint64_t ns = ((p.n - 1) - 1024 * p.nb) / 64;
             p.Mreg = 8 * (16 * p.nb + ns);
         }
     } else {
         p.nck = 3;  // header bytes 0..47 only
     }
-    p.nph = (p.nck + 15) / 16;
+    p.nph = (p.nck + p.ph - 1) / p.ph;
     p.tail_unsafe = hi.h.batch_length + (16ull * p.nck - S) > len;
     p.state = 0;
 }
@@ -137,39 +150,56 @@ __device__ __forceinline__ void glds16(const void *gsrc, uint32_t lds_addr) {
         "global_load_lds_dwordx4 %1, off\n\t"
         "s_mov_b32 m0, %0"
         : "=&s"(keep)
-        : "v"(gsrc), "s"(lds_addr)
+        : "v"(gsrc), "s"(__builtin_amdgcn_readfirstlane(lds_addr))
         : "memory");
 }
-__device__ __forceinline__ void wait_vm16() { asm volatile("s_waitcnt vmcnt(16)" ::: "memory"); }
-__device__ __forceinline__ void wait_vm0() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
-__device__ __forceinline__ void lds_fence_barrier() {
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
+__device__ __forceinline__ void wait_vm(uint32_t n) {
+    // n = glds instructions allowed to stay in flight (multiples of 8)
+    switch (n) {
+        case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+        case 8: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
+        case 16: asm volatile("s_waitcnt vmcnt(16)" ::: "memory"); break;
+        case 24: asm volatile("s_waitcnt vmcnt(24)" ::: "memory"); break;
+        default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+    }
 }
 
 __device__ __forceinline__ uint64_t funnel64(uint64_t lo, uint64_t hi, uint32_t t) {
     return t ? ((lo >> (8 * t)) | (hi << (64 - 8 * t))) : lo;
 }
 
-// issue one phase (16 chunks per frame) for the wave's 64 frames of chunk c:
-// instruction k moves frames 4k..4k+3 (16 lanes each = 256 contiguous bytes)
+// one XXH3 block step on the carried value y = acc + S_b: returns scramble(y) + S_{b+1}.
+// The form measured fastest on gfx950 (26 ns/step: v_lshl_add_u64, v_xor, v_mul_lo_u32,
+// v_mad_u64_u32; scripts/chain_micro.hip); the mad's 64-bit addend form is slower.
+__device__ __forceinline__ uint64_t chain_step(uint64_t y, uint64_t s, uint32_t klo, uint32_t khi) {
+    const uint32_t hi = (uint32_t)(y >> 32);
+    const uint32_t lo = (uint32_t)y ^ (hi >> 15) ^ klo;
+    const uint32_t h2 = hi ^ khi;
+    uint64_t t = (uint64_t)lo * P32_1 + ((uint64_t)(h2 * P32_1) << 32);
+    asm volatile("" : "+v"(t));  // keep s out of the mad's addend (that form is 1.8x slower)
+    return t + s;
+}
+
+// issue phase p of this wave's 64 frames of chunk c: instruction k moves frames
+// (64/PH)k .. (64/PH)k + 64/PH - 1, PH lanes x 16 B = PH*16 contiguous bytes each
+template <int PH>
 __device__ __forceinline__ void issue_phase(const uint8_t *blob, const UPlan &pl, int64_t iw0,
-                                            uint32_t p, uint32_t lds_buf, int lane) {
-    const int fsub = lane >> 4;
+                                            uint32_t p, uint32_t lds_slot, int lane) {
+    constexpr int FPI = 64 / PH;  // frames per instruction
+    const int fsub = lane / PH;
     int64_t i = iw0 + fsub;
-    const uint8_t *fb = blob + (uint64_t)i * pl.S;  // frame base (maybe bogus if i invalid)
-    const uint64_t step = 4 * pl.S;
+    const uint8_t *fb = blob + (uint64_t)i * pl.S;
+    const uint64_t step = (uint64_t)FPI * pl.S;
 #pragma unroll
-    for (int k = 0; k < 16; ++k) {
-        const int f = 4 * k + fsub;
-        const uint32_t cidx = (uint32_t)((lane & 15) ^ (f & 15));
-        const uint32_t q = 16 * p + cidx;
+    for (int k = 0; k < PH; ++k) {
+        const int f = FPI * k + fsub;
+        const uint32_t cidx = (uint32_t)((lane % PH) ^ (f % PH));
+        const uint32_t q = PH * p + cidx;
         const bool ok = (i >= 0) && ((uint64_t)i < pl.N) && (q < pl.nck) &&
                         !(pl.tail_unsafe && (uint64_t)i == pl.N - 1 && 16ull * q + 16 > pl.S);
         const uint8_t *src = ok ? fb + 16ull * q : blob;
-        glds16(src, lds_buf + 1024u * k);
-        i += 4;
+        glds16(src, lds_slot + 1024u * k);
+        i += FPI;
         fb += step;
     }
 }
@@ -181,35 +211,35 @@ struct PhaseState {
     uint32_t uh, plen;
 };
 
-// chunk C (compile-time) of phase p (p % 4 == P4) for this lane's frame.
+// chunk C (compile-time) of phase p (p % (64/PH) == PM) for this lane's frame.
 // Returns true when the frame has no chunk C (end of the phase loop).
-template <int P4, bool CHECKED, bool VERIFY, int C>
+template <int PH, int PM, bool CHECKED, bool VERIFY, int C>
 __device__ __forceinline__ bool chunk_step(const uint8_t *lbase, uint32_t sw, uint8_t *side,
                                            uint32_t p, const UPlan &pl, PhaseState &st) {
-    const uint32_t q = 16 * p + C;
+    const uint32_t q = PH * p + C;
     if (CHECKED && q >= pl.nck) return true;
     const uint4 D = *(const uint4 *)(lbase + 16u * ((uint32_t)C ^ sw));
     const uint64_t u0 = (uint64_t)D.x | ((uint64_t)D.y << 32);
     const uint64_t u1 = (uint64_t)D.z | ((uint64_t)D.w << 32);
-    if (P4 == 0 && C == 0 && CHECKED) {
+    if (PM == 0 && C == 0 && CHECKED) {
         if (p == 0) st.stored = u0;
     }
-    if (P4 == 0 && C == 2 && CHECKED) {
+    if (PM == 0 && C == 2 && CHECKED) {
         if (p == 0) { st.uh = D.x; st.plen = D.y; st.resv = u1; }
     }
-    if (!VERIFY || !pl.long_frames) return false;
+    if (!VERIFY || PH != 8) return false;  // hashing here only for long frames (PH == 8)
     if (CHECKED && q >= pl.q_side0) *(uint4 *)(side + 16u * (q - pl.q_side0)) = D;
     // unit 2q -> hashed word k = 2q-1 ; unit 2q+1 -> word 2q
     constexpr int J0 = (2 * C - 1) & 7;
-    constexpr int SIB0 = (4 * P4 + ((2 * C - 1) >> 3)) & 15;
+    constexpr int SIB0 = ((PH / 4) * PM + ((2 * C - 1) >> 3)) & 15;
     constexpr int J1 = (2 * C) & 7;
-    constexpr int SIB1 = (4 * P4 + ((2 * C) >> 3)) & 15;
+    constexpr int SIB1 = ((PH / 4) * PM + ((2 * C) >> 3)) & 15;
     {
         const int64_t k0 = 2 * (int64_t)q - 1;
         const bool reg0 = CHECKED ? (k0 >= 0 && (uint64_t)k0 < pl.Kreg) : true;
         if (reg0) st.acc.word<J0>(u0, Secret::w(8 * (SIB0 + J0)));
-        if (C == 0 && P4 == 0) {
-            if (p >= 4 && (uint64_t)(p / 4 - 1) < pl.nbF) st.acc.scramble();
+        if (C == 0 && PM == 0) {  // word 128b+127 closes block b = p*PH/64 - 1
+            if (p > 0 && (uint64_t)(p * PH / 64 - 1) < pl.nbF) st.acc.scramble();
         }
     }
     {
@@ -220,61 +250,55 @@ __device__ __forceinline__ bool chunk_step(const uint8_t *lbase, uint32_t sw, ui
     return false;
 }
 
-template <int P4, bool CHECKED, bool VERIFY, int... Cs>
+template <int PH, int PM, bool CHECKED, bool VERIFY, int... Cs>
 __device__ __forceinline__ void phase_chunks(std::integer_sequence<int, Cs...>, const uint8_t *lbase,
                                              uint32_t sw, uint8_t *side, uint32_t p,
                                              const UPlan &pl, PhaseState &st) {
-    (void)(chunk_step<P4, CHECKED, VERIFY, Cs>(lbase, sw, side, p, pl, st) || ...);
+    (void)(chunk_step<PH, PM, CHECKED, VERIFY, Cs>(lbase, sw, side, p, pl, st) || ...);
 }
 
-// Processes the 16 chunks of phase p for this lane's frame.
-// CHECKED: some word of the phase may be non-regular / need side capture /
-// be the frame header (p == 0).
-template <int P4, bool CHECKED, bool VERIFY>
-__device__ __forceinline__ void phase_body(const uint8_t *buf, uint8_t *side, int lane, uint32_t p,
+template <int PH, int PM, bool CHECKED, bool VERIFY>
+__device__ __forceinline__ void phase_body(const uint8_t *slot, uint8_t *side, int lane, uint32_t p,
                                            const UPlan &pl, PhaseState &st) {
-    phase_chunks<P4, CHECKED, VERIFY>(std::make_integer_sequence<int, 16>{},
-                                      buf + (uint32_t)lane * 256u, (uint32_t)(lane & 15), side, p,
-                                      pl, st);
+    phase_chunks<PH, PM, CHECKED, VERIFY>(std::make_integer_sequence<int, PH>{},
+                                          slot + (uint32_t)lane * (PH * 16u),
+                                          (uint32_t)(lane % PH), side, p, pl, st);
 }
 
-template <bool VERIFY>
-__device__ __forceinline__ void run_phase(const uint8_t *buf, uint8_t *side, int lane, uint32_t p,
-                                          const UPlan &pl, PhaseState &st) {
+template <int PH, bool VERIFY, int... PMs>
+__device__ __forceinline__ void run_phase_impl(std::integer_sequence<int, PMs...>, const uint8_t *slot,
+                                               uint8_t *side, int lane, uint32_t p, const UPlan &pl,
+                                               PhaseState &st) {
+    constexpr uint32_t NPM = 64 / PH;
     // a phase is "full" when all its words are regular and none needs side capture
-    const bool full = VERIFY && pl.long_frames && p > 0 && (16 * p + 15 < pl.nck) &&
-                      (32ull * p + 30 < pl.Kreg) && (16 * p + 15 < pl.q_side0);
-    switch (p & 3) {
-        case 0:
-            if (full) phase_body<0, false, VERIFY>(buf, side, lane, p, pl, st);
-            else phase_body<0, true, VERIFY>(buf, side, lane, p, pl, st);
-            break;
-        case 1:
-            if (full) phase_body<1, false, VERIFY>(buf, side, lane, p, pl, st);
-            else phase_body<1, true, VERIFY>(buf, side, lane, p, pl, st);
-            break;
-        case 2:
-            if (full) phase_body<2, false, VERIFY>(buf, side, lane, p, pl, st);
-            else phase_body<2, true, VERIFY>(buf, side, lane, p, pl, st);
-            break;
-        default:
-            if (full) phase_body<3, false, VERIFY>(buf, side, lane, p, pl, st);
-            else phase_body<3, true, VERIFY>(buf, side, lane, p, pl, st);
-            break;
-    }
+    const bool full = VERIFY && PH == 8 && p > 0 && (PH * p + PH - 1 < pl.nck) &&
+                      (2ull * (PH * p + PH - 1) < pl.Kreg) && (PH * p + PH - 1 < pl.q_side0);
+    const uint32_t pm = p % NPM;
+    (void)((pm == (uint32_t)PMs
+                ? (full ? phase_body<PH, PMs, false, VERIFY>(slot, side, lane, p, pl, st)
+                        : phase_body<PH, PMs, true, VERIFY>(slot, side, lane, p, pl, st),
+                   true)
+                : false) ||
+           ...);
 }
 
-// short frames (hashed length 40..240): random access inside phase 0 image
-__device__ inline uint64_t short_hash(const uint8_t *buf0, int lane, uint64_t L) {
+template <int PH, bool VERIFY>
+__device__ __forceinline__ void run_phase(const uint8_t *slot, uint8_t *side, int lane, uint32_t p,
+                                          const UPlan &pl, PhaseState &st) {
+    run_phase_impl<PH, VERIFY>(std::make_integer_sequence<int, 64 / PH>{}, slot, side, lane, p, pl, st);
+}
+
+// short frames (hashed length 40..240): random access inside the 16-chunk image
+__device__ inline uint64_t short_hash(const uint8_t *slot, int lane, uint64_t L) {
     const uint32_t sw = (uint32_t)(lane & 15);
-    const uint8_t *lbase = buf0 + (uint32_t)lane * 256u;
+    const uint8_t *lbase = slot + (uint32_t)lane * 256u;
     auto unit = [&](uint32_t u) -> uint64_t {
         return *(const uint64_t *)(lbase + 16u * ((u >> 1) ^ sw) + 8u * (u & 1));
     };
     auto rd = [&](uint64_t hoff) -> uint64_t {  // hashed offset -> stream offset 8 + hoff
-        uint64_t o = 8 + hoff;
-        uint32_t u = (uint32_t)(o >> 3), t = (uint32_t)(o & 7);
-        uint64_t lo = unit(u);
+        const uint64_t o = 8 + hoff;
+        const uint32_t u = (uint32_t)(o >> 3), t = (uint32_t)(o & 7);
+        const uint64_t lo = unit(u);
         return t ? funnel64(lo, unit(u + 1), t) : lo;
     };
     auto mix16 = [&](uint64_t off, uint64_t s0, uint64_t s1) {
@@ -311,20 +335,226 @@ __device__ inline uint64_t short_hash(const uint8_t *buf0, int lane, uint64_t L)
     return avalanche(acc);
 }
 
+// ------------------------------------------------------------- producer
+// One wave's whole life: every chunk of this WG, streamed through its ring.
+template <int PH, int NSLOT, int DEPTH, bool VERIFY>
+__device__ __forceinline__ void produce(const uint8_t *blob, const UPlan &pl, uint64_t *frame_pos, uint64_t cap,
+                        const DecodeScratch &sc, uint32_t epoch, uint32_t g, uint32_t nprod,
+                        uint32_t wave, int lane, uint8_t *smem, uint32_t dbg) {
+    constexpr uint32_t kSlot = 64u * PH * 16u;
+    static_assert(NSLOT * kSlot <= kWaveRing, "ring");
+    const uint32_t ring = wave * kWaveRing;
+    uint8_t *side = smem + kSideOff + wave * 64 * kSideLane + (uint32_t)lane * kSideLane;
+    const uint32_t tid = wave * 64 + (uint32_t)lane;
+    const uint64_t cs_sec = kSecretW8[((tid >> 3) & 15) + (tid & 7)];
+
+    // flat stream of steps (chunk, phase) issued DEPTH ahead of the compute side
+    uint64_t ic = g;
+    uint32_t ip = 0, iss = 0, k = 0;
+    auto issue_next = [&]() {
+        if (ic >= pl.nchunks) return;
+        issue_phase<PH>(blob, pl, (int64_t)(256 * ic) - 6 + 64 * (int64_t)wave, ip,
+                        ring + (iss % NSLOT) * kSlot, lane);
+        ++iss;
+        if (++ip == pl.nph) { ip = 0; ic += nprod; }
+    };
+    for (int d = 0; d < DEPTH; ++d) issue_next();
+
+    // chunks whose partial sums are stored but not yet covered by a vmcnt wait:
+    // FIFO (pub_c, pub_c + nprod, ...), the head ready once step pub_k has landed
+    uint64_t pub_c = g;
+    uint32_t pub_k = 0, npend = 0;
+    auto publish_ready = [&](uint32_t kk) {
+        while (npend && pub_k <= kk) {
+            if (lane == 0)
+                __hip_atomic_store(&sc.flags[pub_c * 4 + wave], epoch, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+            pub_c += nprod;
+            pub_k += pl.nph;
+            --npend;
+        }
+    };
+
+    for (uint64_t c = g; c < pl.nchunks; c += nprod) {
+        const int64_t i = (int64_t)(256 * c) - 6 + 64 * (int64_t)wave + lane;
+        const bool fvalid = i >= 0 && (uint64_t)i < pl.N;
+        PhaseState st;
+        st.acc.init();
+        st.stored = 0; st.resv = 0; st.uh = 0; st.plen = 0;
+        uint32_t slot_last = 0;
+        for (uint32_t p = 0; p < pl.nph; ++p) {
+            issue_next();
+            wait_vm(PH * (iss - 1 - k));  // step k landed; later steps may stay in flight
+            if (npend) publish_ready(k);
+            slot_last = ring + (k % NSLOT) * kSlot;
+            if (dbg & 2) run_phase<PH, false>(smem + slot_last, side, lane, p, pl, st);
+            else run_phase<PH, VERIFY>(smem + slot_last, side, lane, p, pl, st);
+            ++k;
+        }
+        // ---- per-frame result
+        uint64_t h = 0;
+        if (VERIFY) {
+            if (pl.long_frames) {
+                // last stripe: hashed bytes [L-64, L) = stream [S-64, S) from the side copy
+                const uint64_t o = pl.S - 64;
+                const uint32_t t = (uint32_t)(o & 7);
+                const uint32_t u0 = (uint32_t)(o >> 3) - 2 * pl.q_side0;
+                uint64_t U[9];
+#pragma unroll
+                for (int x = 0; x < 9; ++x) U[x] = (x < 8 || t) ? *(const uint64_t *)(side + 8u * (u0 + x)) : 0;
+                st.acc.word<0>(funnel64(U[0], U[1], t), Secret::w(121));
+                st.acc.word<1>(funnel64(U[1], U[2], t), Secret::w(129));
+                st.acc.word<2>(funnel64(U[2], U[3], t), Secret::w(137));
+                st.acc.word<3>(funnel64(U[3], U[4], t), Secret::w(145));
+                st.acc.word<4>(funnel64(U[4], U[5], t), Secret::w(153));
+                st.acc.word<5>(funnel64(U[5], U[6], t), Secret::w(161));
+                st.acc.word<6>(funnel64(U[6], U[7], t), Secret::w(169));
+                st.acc.word<7>(funnel64(U[7], U[8], t), Secret::w(177));
+                h = st.acc.merge(pl.L);
+            } else {
+                h = short_hash(smem + slot_last, lane, pl.L);
+            }
+        }
+        const uint64_t stored = st.stored;
+        const bool spec_bad = fvalid && (st.resv != 0 || (uint64_t)kFrameHdr + st.plen + st.uh != pl.S);
+        // the last frame of a record that ends at the buffer end is verified by the
+        // consumer from exact-extent reads (its last chunk was not staged)
+        const bool mism = VERIFY && fvalid && h != stored && !(pl.tail_unsafe && (uint64_t)i == pl.N - 1);
+        if (frame_pos && fvalid && (uint64_t)i < cap) frame_pos[i] = (uint64_t)i * pl.S;
+        const uint64_t mb = __ballot(mism);
+        if (mb) {
+            const int leader = __builtin_ctzll(mb);
+            if (lane == leader) {
+                atomicMax((unsigned long long *)sc.first_bad, (unsigned long long)~(uint64_t)i);
+                const uint64_t slot = c * 4 + wave;
+                __hip_atomic_store(&sc.errslot[2 * slot], stored, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(&sc.errslot[2 * slot + 1], h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
+        const uint64_t sb = __ballot(spec_bad);
+        if (sb) {
+            const int leader = __builtin_ctzll(sb);
+            if (lane == leader) atomicMax((unsigned long long *)sc.spec_fail, (unsigned long long)~(uint64_t)i);
+        }
+        // ---- this wave's interior batch-checksum words m = 256c + 64w + lane (lane < 63)
+        if (VERIFY && pl.long_cs) {
+            const uint64_t next = __shfl_down(stored, 1);
+            const uint64_t m = 256 * c + tid;
+            uint64_t x = 0, y = 0;  // x -> acc[j], y -> acc[j^1]
+            if (lane < 63 && m >= 6 && m < pl.Mreg) {
+                const uint64_t v = (stored >> 32) | (next << 32);
+                y = v;
+                x = mul32x32(v ^ cs_sec);
+            }
+            x += __shfl_xor(x, 8); y += __shfl_xor(y, 8);
+            x += __shfl_xor(x, 16); y += __shfl_xor(y, 16);
+            x += __shfl_xor(x, 32); y += __shfl_xor(y, 32);
+            const uint64_t t8 = x + __shfl_xor(y, 1);  // lane t (< 8): partial acc[t]
+            if (lane < 8)
+                __hip_atomic_store(&sc.sums[(c * 4 + wave) * 8 + lane], t8, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+            // covered by the wait of step (last step of c) + DEPTH
+            if (npend == 0) pub_k = (k - 1) + DEPTH;  // FIFO head: this chunk
+            ++npend;
+        }
+    }
+    wait_vm(0);
+    publish_ready(~0u);
+    if (lane == 0) __hip_atomic_fetch_add(sc.exited, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // ------------------------------------------------------------- consumer
-template <bool VERIFY>
-__device__ void consumer_wg(const uint8_t *body, const HeaderInfo &hi, const UPlan &pl,
-                            uint64_t *frame_pos, iggy_decode_result *result,
-                            const DecodeScratch &sc, uint32_t epoch, uint32_t nprod,
-                            uint8_t *smem, uint32_t dbg) {
+__device__ __forceinline__ uint64_t chain_batches(const UPlan &pl) {
+    return ((pl.nb >> 1) + 1 + kBatch - 1) / kBatch;  // chunks 0 .. nb/2 hold blocks 0 .. nb
+}
+
+// Gatherer wave gw (0..kGatherWaves-1) of the consumer WG: batches gw, gw + 3, ...
+// Waits for the 4 producer waves of each of its 64 chunks, loads their partial
+// sums and the 4 wave-boundary words, and stages 16 block-sum words per chunk.
+__device__ __forceinline__ void gather(const uint8_t *blob, const UPlan &pl, const DecodeScratch &sc,
+                                       uint32_t epoch, uint32_t gw, uint8_t *smem, uint64_t t_start) {
     const int lane = threadIdx.x & 63;
-    const int wave = threadIdx.x >> 6;
-    const uint8_t *blob = body + kHdr;
+    ChainCtl *ctl = (ChainCtl *)(smem + kCtlOff);
     uint64_t *ring = (uint64_t *)smem;
-    uint32_t *ctrl = (uint32_t *)(smem + kCtrlOff);  // [0]=ready [1]=consumed [2]=alldone [3]=timeout
-    if (threadIdx.x == 0) { ctrl[0] = 0; ctrl[1] = 0; ctrl[2] = 0; ctrl[3] = 0; }
-    __syncthreads();
-    if (wave >= 2) return;
+    const uint64_t need = (pl.nb >> 1) + 1;
+    const uint64_t nbatch = chain_batches(pl);
+    auto give_up = [&]() -> bool {
+        return __hip_atomic_load(&ctl->abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != 0 ||
+               rt_now() - t_start > kSpinLimitTicks;
+    };
+    for (uint64_t bi = gw; bi < nbatch; bi += kGatherWaves) {
+        const uint32_t slot = (uint32_t)(bi % kRing);
+        bool abort = false;
+        while (bi >= kRing && (uint64_t)__hip_atomic_load(&ctl->consumed, __ATOMIC_ACQUIRE,
+                                                          __HIP_MEMORY_SCOPE_WORKGROUP) + kRing <= bi) {
+            __builtin_amdgcn_s_sleep(1);
+            if (give_up()) { abort = true; break; }
+        }
+        const uint64_t c = bi * kBatch + lane;
+        const bool live = c < need && c < pl.nchunks;
+        while (!abort) {
+            bool ok = true;
+            if (live) {
+#pragma unroll
+                for (int w = 0; w < 4; ++w)
+                    ok &= __hip_atomic_load(&sc.flags[c * 4 + w], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == epoch;
+            }
+            if (__ballot(!ok) == 0) break;
+            __builtin_amdgcn_s_sleep(2);
+            if (give_up()) abort = true;
+        }
+        if (abort) {
+            if (lane == 0) __hip_atomic_store(&ctl->abort, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            return;
+        }
+        uint64_t P[32], CS[8];
+#pragma unroll
+        for (int x = 0; x < 32; ++x)
+            P[x] = live ? __hip_atomic_load(&sc.sums[c * 32 + x], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
+#pragma unroll
+        for (int w = 0; w < 4; ++w) {
+            // wave-boundary word m = 256c + 64w + 63 = hi32(cs_{m-6}) | lo32(cs_{m-5}) << 32
+            const uint64_t m = 256 * c + 64 * w + 63;
+            const bool need_w = live && m >= 6 && m < pl.Mreg;
+            const uint64_t fi = m - 6;
+            CS[2 * w] = need_w ? ld64_any(blob + fi * pl.S) : 0;
+            CS[2 * w + 1] = need_w ? ld64_any(blob + (fi + 1) * pl.S) : 0;
+        }
+        uint64_t B[16];
+#pragma unroll
+        for (int t = 0; t < 8; ++t) {
+            B[t] = P[t] + P[8 + t];            // block 2c   = waves 0, 1 of the chunk
+            B[8 + t] = P[16 + t] + P[24 + t];  // block 2c+1 = waves 2, 3
+        }
+#pragma unroll
+        for (int w = 0; w < 4; ++w) {
+            const uint64_t m = 256 * c + 64 * w + 63;
+            if (live && m >= 6 && m < pl.Mreg) {
+                const uint64_t v = (CS[2 * w] >> 32) | (CS[2 * w + 1] << 32);
+                // lane j = 7 of stripe (8w + 7) mod 16: acc[6] += v, acc[7] += mul
+                const int hb = w >> 1;
+                B[8 * hb + 6] += v;
+                B[8 * hb + 7] += mul32x32(v ^ kSecretW8[((8 * w + 7) & 15) + 7]);
+            }
+        }
+        uint64_t *dst = ring + ((uint64_t)slot * kBatch + lane) * 16;
+#pragma unroll
+        for (int t = 0; t < 16; ++t) dst[t] = B[t];
+        if (lane == 0)
+            __hip_atomic_store(&ctl->ready[slot], (uint32_t)(bi + 1), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+}
+
+// The consumer WG (block 0): wave 0 runs the serial batch-checksum chain
+// (batch.rs:439-459 / 474-505) and the precedence resolution of
+// decode_batch_slice_with (batch.rs:395-421); waves 1..3 gather its inputs.
+template <bool VERIFY>
+__device__ __forceinline__ void consumer(const uint8_t *body, const HeaderInfo &hi, const UPlan &pl,
+                                         iggy_decode_result *result, const DecodeScratch &sc,
+                                         uint32_t epoch, uint32_t nwaves_prod, uint32_t wave,
+                                         uint8_t *smem, uint32_t dbg) {
+    const int lane = threadIdx.x & 63;
+    const uint8_t *blob = body + kHdr;
 
     if (pl.state != 0) {
         if (wave != 0) return;
@@ -338,11 +568,10 @@ __device__ void consumer_wg(const uint8_t *body, const HeaderInfo &hi, const UPl
             // zero frames: checksum over the 44 header bytes (batch.rs:452-458)
             if (lane == 0) {
                 uint8_t *s = sc.small;
-                uint64_t w[5] = {hi.h.partition_id, hi.h.base_offset, hi.h.base_timestamp,
-                                 hi.h.origin_timestamp, hi.h.batch_length};
-                for (int i = 0; i < 5; ++i)
-                    for (int k = 0; k < 8; ++k) s[8 * i + k] = (uint8_t)(w[i] >> (8 * k));
-                for (int k = 0; k < 4; ++k) s[40 + k] = (uint8_t)(hi.h.message_count >> (8 * k));
+                const uint64_t w[5] = {hi.h.partition_id, hi.h.base_offset, hi.h.base_timestamp,
+                                       hi.h.origin_timestamp, hi.h.batch_length};
+                for (int i = 0; i < 5; ++i) st64_any(s + 8 * i, w[i]);
+                *(u32_ua *)(s + 40) = hi.h.message_count;
                 computed = xxh3_64_lane(s, 44);
                 if (computed != hi.h.batch_checksum) {
                     kind = IGGY_ERR_INVALID_BATCH_CHECKSUM; reason = 0;
@@ -350,82 +579,29 @@ __device__ void consumer_wg(const uint8_t *body, const HeaderInfo &hi, const UPl
                 }
             }
         }
-        if (lane == 0)
-            write_result(result, hi, kind, reason, a, b, c, 0, computed, 1, status, 0);
+        if (lane == 0) write_result(result, hi, kind, reason, a, b, c, 0, computed, 1, status, 0);
         return;
     }
 
     const uint64_t t_start = rt_now();
-    if (wave == 1) {
-        // ---------------- feeder: flags -> LDS ring (sc1 loads, Guideline 16 R1)
-        const uint64_t need = (VERIFY && pl.long_cs && !(dbg & 1)) ? (pl.nb >> 1) + 1 : 0;
-        uint64_t c = 0;
-        bool timed_out = false;
-        while (c < need) {
-            const uint32_t consumed = __hip_atomic_load(&ctrl[1], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
-            const uint64_t space = kRing - (c - consumed);
-            uint64_t win = need - c;
-            if (win > 64) win = 64;
-            if (win > space) win = space;
-            bool ready = false;
-            if ((uint64_t)lane < win) {
-                const uint64_t cc = c + lane;
-                ready = cc >= pl.nchunks ||
-                        __hip_atomic_load(&sc.flags[cc], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == epoch;
-            }
-            const uint64_t mask = __ballot(ready);
-            const uint32_t r = (~mask == 0) ? 64u : (uint32_t)__builtin_ctzll(~mask);  // consecutive ready
-            if (r == 0) {
-                __builtin_amdgcn_s_sleep(2);
-                if (rt_now() - t_start > kSpinLimitTicks) { timed_out = true; break; }
-                continue;
-            }
-            // 16 sums per chunk; + the chunk-boundary checksum word m = 256cc+255
-            for (uint32_t idx = lane; idx < ((dbg & 4) ? 0u : 16 * r); idx += 64) {
-                const uint64_t cc = c + idx / 16;
-                const uint32_t e = idx % 16;
-                uint64_t v = 0;
-                if (cc < pl.nchunks)
-                    v = __hip_atomic_load(&sc.sums[(2 * cc) * 8 + e], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                if (e >= 14) {
-                    const uint64_t m = 256 * cc + 255;
-                    const uint64_t ia = 256 * cc + 249;  // frame whose hi32 starts word m
-                    if (m < pl.Mreg && ia + 1 < pl.N) {
-                        const uint64_t csa = ld64_any(blob + ia * pl.S);
-                        const uint64_t csb = ld64_any(blob + (ia + 1) * pl.S);
-                        const uint64_t wv = (csa >> 32) | (csb << 32);
-                        // word j = 7 of stripe 15: acc[6] += v, acc[7] += mul(v ^ sec[15+7])
-                        if (e == 14) v += wv;
-                        else v += mul32x32(wv ^ Secret::w(8 * 22));
-                    }
-                }
-                ring[(cc % kRing) * 16 + e] = v;
-            }
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            if (lane == 0)
-                __hip_atomic_store(&ctrl[0], (uint32_t)(c + r), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-            c += r;
-        }
-        // every producer done => every chunk's stores / atomics are visible
-        while (!timed_out &&
-               __hip_atomic_load(sc.exited, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != nprod) {
-            __builtin_amdgcn_s_sleep(4);
-            if (rt_now() - t_start > kSpinLimitTicks) timed_out = true;
-        }
-        if (lane == 0) {
-            if (timed_out) __hip_atomic_store(&ctrl[3], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            __hip_atomic_store(&ctrl[2], 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-        }
+    bool timed_out = false;
+    uint64_t computed = 0;
+    const bool chain = VERIFY && pl.long_cs && !(dbg & 1);
+    if (chain) {
+        if (threadIdx.x < sizeof(ChainCtl) / 4) ((uint32_t *)(smem + kCtlOff))[threadIdx.x] = 0;
+        __syncthreads();
+    }
+    if (wave != 0) {  // gatherer waves feed the chain wave through the LDS ring
+        if (chain) gather(blob, pl, sc, epoch, wave - 1, smem, t_start);
         return;
     }
-
-    // ---------------- wave 0: serial batch-checksum chain + resolution
-    uint64_t computed = 0;
-    bool timed_out = false;
-    if (VERIFY && pl.long_cs && !(dbg & 1)) {
+    if (chain) {
+        ChainCtl *ctl = (ChainCtl *)(smem + kCtlOff);
+        const uint64_t *ring = (const uint64_t *)smem;
         const int j = lane & 7;
         uint64_t acc = kAccInit[j];
         const uint64_t key = kSecretW8[16 + j];
+        const uint32_t klo = (uint32_t)key, khi = (uint32_t)(key >> 32);
         // words 0..5 of stripe 0: header fields, then count | lo32(cs_0)
         {
             const uint64_t cs0 = ld64_any(blob);
@@ -438,37 +614,63 @@ __device__ void consumer_wg(const uint8_t *body, const HeaderInfo &hi, const UPl
                 if (j == m) acc += mul32x32(w6[m] ^ Secret::w(8 * m));
             }
         }
-        uint32_t ready = 0;
-        uint64_t b = 0;
-        while (b <= pl.nb) {
-            const uint64_t cc = b >> 1;
-            if (cc >= ready) {
-                ready = __hip_atomic_load(&ctrl[0], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
-                if (cc >= ready) {
-                    if (__hip_atomic_load(&ctrl[2], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP)) {
-                        timed_out = true;  // feeder gave up
-                        break;
-                    }
-                    __builtin_amdgcn_s_sleep(1);
-                    continue;
+        // y = acc + (sum of the current block); block b >= 1: y = scramble(y) + S_b.
+        // Only blocks 0 .. nb-1 are scrambled: the partial block nb just adds.
+        const uint64_t nbatch = chain_batches(pl);
+        uint64_t y = acc;
+        for (uint64_t bi = 0; bi < nbatch && !timed_out; ++bi) {
+            const uint32_t slot = (uint32_t)(bi % kRing);
+            while (__hip_atomic_load(&ctl->ready[slot], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) !=
+                   (uint32_t)(bi + 1)) {
+                __builtin_amdgcn_s_sleep(1);
+                if (__hip_atomic_load(&ctl->abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) ||
+                    rt_now() - t_start > kSpinLimitTicks) {
+                    timed_out = true;
+                    break;
                 }
             }
-            // run every block that is ready without re-polling
-            uint64_t bend = 2 * (uint64_t)ready;
+            if (timed_out) break;
+            const uint64_t b0 = 2 * kBatch * bi;
+            uint64_t bend = b0 + 2 * kBatch;
             if (bend > pl.nb + 1) bend = pl.nb + 1;
-            for (; b < bend; ++b) {
-                acc += ring[((b >> 1) % kRing) * 16 + (b & 1) * 8 + j];
-                if (b < pl.nb) acc = scramble1(acc, key);
-                if ((b & 1) && lane == 0)
-                    __hip_atomic_store(&ctrl[1], (uint32_t)((b >> 1) + 1), __ATOMIC_RELAXED,
-                                       __HIP_MEMORY_SCOPE_WORKGROUP);
+            // block b of this batch at src[8 * (b - b0)]
+            const uint64_t *src = ring + (uint64_t)slot * (kBatch * 16) + j;
+            uint32_t k = 0;
+            const uint32_t kend = (uint32_t)(bend - b0);
+            if (bi == 0) { y += src[0]; k = 1; }
+            // groups of 16 blocks, next group's LDS reads in flight during this group
+            uint64_t va[16], vb[16];
+            auto ld16 = [&](uint64_t *v, uint32_t k0) {
+#pragma unroll
+                for (int x = 0; x < 16; ++x) v[x] = src[8 * (k0 + x)];
+            };
+            auto run16 = [&](const uint64_t *v) {
+#pragma unroll
+                for (int x = 0; x < 16; ++x) y = chain_step(y, v[x], klo, khi);
+            };
+            if (k + 16 <= kend) ld16(va, k);
+            while (k + 16 <= kend) {
+                const bool more = k + 32 <= kend;
+                if (more) ld16(vb, k + 16);
+                run16(va);
+                k += 16;
+                if (!more) break;
+                const bool more2 = k + 32 <= kend;
+                if (more2) ld16(va, k + 16);
+                run16(vb);
+                k += 16;
+                if (!more2) break;
             }
+            for (; k < kend; ++k) y = chain_step(y, src[8 * k], klo, khi);
+            __hip_atomic_store(&ctl->consumed, (uint32_t)(bi + 1), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
         }
-        if (!timed_out) {
+        if (timed_out) {
+            __hip_atomic_store(&ctl->abort, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        } else {
+            acc = y;
             // last stripe = stored checksums of frames N-8 .. N-1 (secret offset 121)
             const uint64_t v = ld64_any(blob + (pl.N - 8 + j) * pl.S);
-            const uint64_t vx = __shfl_xor(v, 1);
-            acc += vx;
+            acc += __shfl_xor(v, 1);
             acc += mul32x32(v ^ kSecretLast[j]);
             uint64_t a[8];
 #pragma unroll
@@ -483,15 +685,11 @@ __device__ void consumer_wg(const uint8_t *body, const HeaderInfo &hi, const UPl
         // short checksum input (N <= 24): hash it directly
         if (lane == 0) {
             uint8_t *s = sc.small;
-            uint64_t w[5] = {hi.h.partition_id, hi.h.base_offset, hi.h.base_timestamp,
-                             hi.h.origin_timestamp, hi.h.batch_length};
-            for (int i = 0; i < 5; ++i)
-                for (int k = 0; k < 8; ++k) s[8 * i + k] = (uint8_t)(w[i] >> (8 * k));
-            for (int k = 0; k < 4; ++k) s[40 + k] = (uint8_t)(hi.h.message_count >> (8 * k));
-            for (uint64_t i = 0; i < pl.N; ++i) {
-                const uint64_t cs = ld64_any(blob + i * pl.S);
-                for (int k = 0; k < 8; ++k) s[44 + 8 * i + k] = (uint8_t)(cs >> (8 * k));
-            }
+            const uint64_t w[5] = {hi.h.partition_id, hi.h.base_offset, hi.h.base_timestamp,
+                                   hi.h.origin_timestamp, hi.h.batch_length};
+            for (int i = 0; i < 5; ++i) st64_any(s + 8 * i, w[i]);
+            *(u32_ua *)(s + 40) = hi.h.message_count;
+            for (uint64_t i = 0; i < pl.N; ++i) st64_any(s + 44 + 8 * i, ld64_any(blob + i * pl.S));
             computed = xxh3_64_lane(s, pl.n);
         }
     }
@@ -504,10 +702,12 @@ __device__ void consumer_wg(const uint8_t *body, const HeaderInfo &hi, const UPl
         tail_computed = xxh3_64_lane(f + 8, pl.L);
         tail_bad = tail_stored != tail_computed;
     }
-    // wait for the feeder's "all producers done"
-    while (!__hip_atomic_load(&ctrl[2], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP))
-        __builtin_amdgcn_s_sleep(2);
-    if (__hip_atomic_load(&ctrl[3], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) timed_out = true;
+    // every producer wave done => their stores / atomics are visible
+    while (!timed_out &&
+           __hip_atomic_load(sc.exited, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != nwaves_prod) {
+        __builtin_amdgcn_s_sleep(4);
+        if (rt_now() - t_start > kSpinLimitTicks) timed_out = true;
+    }
     if (lane != 0) return;
     if (timed_out) {
         write_result(result, hi, IGGY_ERR_TIMEOUT, 0, 0, 0, 0, 0, 0, 1, kStatusDone, 0);
@@ -568,7 +768,7 @@ __global__ __launch_bounds__(256, 1) void k_decode_uniform(const uint8_t *__rest
                                                            uint32_t allow_unaligned, uint32_t dbg) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const int lane = threadIdx.x & 63;
-    const int wave = threadIdx.x >> 6;
+    const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t nprod = gridDim.x - 1;
     HeaderInfo hi;
     parse_header(body, len, hi);
@@ -576,150 +776,16 @@ __global__ __launch_bounds__(256, 1) void k_decode_uniform(const uint8_t *__rest
     make_plan(hi, body + kHdr, len, VERIFY, sc.max_chunks, allow_unaligned != 0, pl);
 
     if (blockIdx.x == 0) {
-        consumer_wg<VERIFY>(body, hi, pl, frame_pos, result, sc, epoch, nprod, smem, dbg);
+        consumer<VERIFY>(body, hi, pl, result, sc, epoch, 4 * nprod, wave, smem, dbg);
         return;
     }
-    if (pl.state != 0) return;  // nothing for producers; consumer resolves
-
+    if (pl.state != 0) return;  // nothing for producers; the consumer resolves
     const uint8_t *blob = body + kHdr;
     const uint32_t g = blockIdx.x - 1;
-    const uint32_t wave_u = (uint32_t)__builtin_amdgcn_readfirstlane(wave);
-    const uint32_t buf0 = wave_u * 2 * kWaveBuf;
-    uint8_t *side = smem + kSideOff + wave_u * 64 * kSideLane + (uint32_t)lane * kSideLane;
-    uint64_t *xchg = (uint64_t *)(smem + kXchgOff);
-    uint64_t *red = (uint64_t *)(smem + kRedOff);
-
-    // per-thread constant of the checksum-input word it owns in every chunk
-    const uint32_t tid = threadIdx.x;
-    const uint64_t cs_sec = kSecretW8[((tid >> 3) & 15) + (tid & 7)];
-
-    uint64_t c = g;
-    uint32_t bi = 0;
-    bool have_prev = false;
-    uint64_t c_prev = 0;
-    if (c < pl.nchunks) issue_phase(blob, pl, (int64_t)(256 * c) - 6 + 64 * wave, 0, buf0, lane);
-
-    for (; c < pl.nchunks; c += nprod) {
-        const uint64_t cn = c + nprod;
-        const int64_t iw0 = (int64_t)(256 * c) - 6 + 64 * wave;
-        const int64_t i = iw0 + lane;
-        const bool fvalid = i >= 0 && (uint64_t)i < pl.N;
-        PhaseState st;
-        st.acc.init();
-        st.stored = 0;
-        st.resv = 0;
-        st.uh = 0;
-        st.plen = 0;
-        for (uint32_t p = 0; p < pl.nph; ++p) {
-            const uint32_t nb_ = buf0 + (bi ^ 1) * kWaveBuf;
-            bool issued = true;
-            if (p + 1 < pl.nph) issue_phase(blob, pl, iw0, p + 1, nb_, lane);
-            else if (cn < pl.nchunks) issue_phase(blob, pl, (int64_t)(256 * cn) - 6 + 64 * wave, 0, nb_, lane);
-            else issued = false;
-            if (issued) wait_vm16(); else wait_vm0();
-            if (p == 0) {
-                // everything older than the phase just issued has landed in every
-                // wave, including the previous chunk's sc1 stores: publish it
-                lds_fence_barrier();
-                if (have_prev && threadIdx.x == 0)
-                    __hip_atomic_store(&sc.flags[c_prev], epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
-            if (dbg & 2) run_phase<false>(smem + buf0 + bi * kWaveBuf, side, lane, p, pl, st);
-            else run_phase<VERIFY>(smem + buf0 + bi * kWaveBuf, side, lane, p, pl, st);
-            bi ^= 1;
-        }
-        // ---- per-frame result
-        uint64_t h = 0;
-        if (VERIFY) {
-            if (pl.long_frames) {
-                // last stripe: hashed bytes [L-64, L) = stream [S-64, S) from the side copy
-                const uint64_t o = pl.S - 64;
-                const uint32_t t = (uint32_t)(o & 7);
-                const uint32_t u0 = (uint32_t)(o >> 3) - 2 * pl.q_side0;
-                uint64_t U[9];
-#pragma unroll
-                for (int k = 0; k < 9; ++k) {
-                    if (k < 8 || t) U[k] = *(const uint64_t *)(side + 8u * (u0 + k));
-                    else U[k] = 0;
-                }
-#pragma unroll
-                for (int k = 0; k < 8; ++k) {
-                    const uint64_t w = funnel64(U[k], U[k + 1], t);
-                    switch (k) {
-                        case 0: st.acc.word<0>(w, Secret::w(121)); break;
-                        case 1: st.acc.word<1>(w, Secret::w(129)); break;
-                        case 2: st.acc.word<2>(w, Secret::w(137)); break;
-                        case 3: st.acc.word<3>(w, Secret::w(145)); break;
-                        case 4: st.acc.word<4>(w, Secret::w(153)); break;
-                        case 5: st.acc.word<5>(w, Secret::w(161)); break;
-                        case 6: st.acc.word<6>(w, Secret::w(169)); break;
-                        default: st.acc.word<7>(w, Secret::w(177)); break;
-                    }
-                }
-                h = st.acc.merge(pl.L);
-            } else {
-                // single phase; its image is buffer (bi ^ 1) now
-                h = short_hash(smem + buf0 + (bi ^ 1) * kWaveBuf, lane, pl.L);
-            }
-        }
-        const uint64_t stored = st.stored;
-        const bool spec_bad = fvalid && (st.resv != 0 || (uint64_t)kFrameHdr + st.plen + st.uh != pl.S);
-        // the last frame of a record that ends at the buffer end is verified by the
-        // consumer from exact-extent reads (its last chunk was not staged)
-        const bool mism = VERIFY && fvalid && h != stored &&
-                          !(pl.tail_unsafe && (uint64_t)i == pl.N - 1);
-        if (frame_pos && fvalid && (uint64_t)i < cap) frame_pos[i] = (uint64_t)i * pl.S;
-        const uint64_t mb = __ballot(mism);
-        if (mb) {
-            const int leader = __builtin_ctzll(mb);
-            if (lane == leader) {
-                atomicMax((unsigned long long *)sc.first_bad, (unsigned long long)~(uint64_t)i);
-                const uint64_t slot = c * 4 + wave;
-                __hip_atomic_store(&sc.errslot[2 * slot], stored, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                __hip_atomic_store(&sc.errslot[2 * slot + 1], h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
-        }
-        const uint64_t sb = __ballot(spec_bad);
-        if (sb) {
-            const int leader = __builtin_ctzll(sb);
-            if (lane == leader) atomicMax((unsigned long long *)sc.spec_fail, (unsigned long long)~(uint64_t)i);
-        }
-        // ---- batch-checksum words of this chunk: m = 256c + tid (tid < 255)
-        if (VERIFY && pl.long_cs) {
-            xchg[tid] = stored;
-            lds_fence_barrier();
-            const uint64_t m = 256 * c + tid;
-            uint64_t x = 0, y = 0;  // x -> acc[j], y -> acc[j^1]
-            if (tid < 255 && m >= 6 && m < pl.Mreg) {
-                const uint64_t v = (stored >> 32) | (xchg[tid + 1] << 32);
-                y = v;
-                x = mul32x32(v ^ cs_sec);
-            }
-            // sum lanes with equal (lane & 7): xor 8, 16, 32
-            x += __shfl_xor(x, 8); y += __shfl_xor(y, 8);
-            x += __shfl_xor(x, 16); y += __shfl_xor(y, 16);
-            x += __shfl_xor(x, 32); y += __shfl_xor(y, 32);
-            const uint64_t t8 = x + __shfl_xor(y, 1);  // lane t (<8): acc[t] sum
-            if (lane < 8) red[wave * 8 + lane] = t8;
-            lds_fence_barrier();
-            if (wave == 0 && lane < 16) {
-                const int half = lane >> 3, t = lane & 7;
-                const uint64_t s = red[(2 * half) * 8 + t] + red[(2 * half + 1) * 8 + t];
-                __hip_atomic_store(&sc.sums[(2 * c + half) * 8 + t], s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
-        }
-        have_prev = true;
-        c_prev = c;
-    }
-    // drain every wave's stores, then publish the last chunk and retire
-    wait_vm0();
-    lds_fence_barrier();
-    if (threadIdx.x == 0) {
-        if (have_prev)
-            __hip_atomic_store(&sc.flags[c_prev], epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __hip_atomic_fetch_add(sc.exited, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
+    if (VERIFY && pl.long_frames)
+        produce<8, 4, 3, VERIFY>(blob, pl, frame_pos, cap, sc, epoch, g, nprod, wave, lane, smem, dbg);
+    else
+        produce<16, 2, 1, VERIFY>(blob, pl, frame_pos, cap, sc, epoch, g, nprod, wave, lane, smem, dbg);
 }
 
 template __global__ void k_decode_uniform<true>(const uint8_t *__restrict__, uint64_t, uint64_t *,
