@@ -40,14 +40,15 @@ struct DecodeScratch {
     uint32_t *exited;     // producer waves that finished (reset by consumer)
     uint64_t *first_bad;  // ~index of first checksum mismatch (max-encoded), 0 = none
     uint64_t *spec_fail;  // ~index of first frame whose header breaks the stride
-    uint32_t *flags;      // [max_chunks*4] = epoch when wave w's sums of chunk c are published
-    uint64_t *sums;       // [max_chunks*4][8] per-wave accumulator partial sums
+    uint64_t *sums;       // [max_chunks*4][16] per-unit accumulator partial sums, 32-bit halves
+                          // tagged with the launch epoch: (half | epoch << 32)
     uint64_t *errslot;    // [max_chunks*4][2] (stored, computed) per wave
     uint8_t *small;       // >= 512 B: short batch-checksum inputs
     uint64_t max_chunks;
 };
 
 // ---- LDS map of a producer WG (dynamic LDS only, base offset 0) ----------
+constexpr uint32_t kUniformThreads = 512;                      // lane-group producers: 8 waves per WG
 constexpr uint32_t kWaveRing = 32768;                          // per wave: 4 x 8 KiB or 2 x 16 KiB
 constexpr uint32_t kSideOff = 4 * kWaveRing;                   // 131072
 constexpr uint32_t kSideLane = 96;                             // 6 chunks per lane
@@ -63,18 +64,20 @@ struct ChainCtl {
     uint32_t consumed;      // batches the chain wave has finished
     uint32_t abort;         // a gatherer or the chain wave gave up (spin limit)
 };
-static_assert(kCtlOff + sizeof(ChainCtl) <= kLdsBytes, "consumer LDS");
+constexpr uint32_t kConsumerLds = kCtlOff + 64;
+static_assert(kCtlOff + sizeof(ChainCtl) <= kConsumerLds, "consumer LDS");
 static_assert(kLdsBytes <= 160 * 1024, "LDS budget");
 
 struct UPlan {
     uint32_t state;  // 0 run, 1 result known early, 2 need general
     uint32_t nck, nph, q_side0, ph;
     uint64_t S, N, L, nchunks;
-    uint64_t nbF, Kreg;          // per-frame hash: full blocks, regular words
+    uint64_t nbF, Kreg, ns;      // per-frame hash: full blocks, regular words, partial stripes
     uint64_t n, nb, Mreg;        // batch checksum input: bytes, full blocks, regular words
     uint32_t ekind, ereason;
     uint64_t ea, eb, ec;
     bool long_frames, long_cs;
+    bool nt;           // diagnostics: non-temporal LDS-DMA loads
     bool tail_unsafe;  // last frame's last 16-B chunk would read past the caller's buffer
 };
 
@@ -82,11 +85,12 @@ __device__ inline void make_plan(const HeaderInfo &hi, const uint8_t *blob, uint
                                  bool verify, uint64_t max_chunks, bool allow_unaligned, UPlan &p) {
     p.state = 2;
     p.tail_unsafe = false;
+    p.nt = false;
     p.ekind = IGGY_OK; p.ereason = 0; p.ea = p.eb = p.ec = 0;
     p.S = p.N = p.L = p.nchunks = 0;
     p.nck = p.nph = p.q_side0 = 0;
     p.ph = 16;
-    p.nbF = p.Kreg = p.n = p.nb = p.Mreg = 0;
+    p.nbF = p.Kreg = p.ns = p.n = p.nb = p.Mreg = 0;
     p.long_frames = p.long_cs = false;
     if (hi.err_kind != IGGY_OK) {
         p.state = 1; p.ekind = hi.err_kind; p.ereason = hi.err_reason;
@@ -121,8 +125,8 @@ __device__ inline void make_plan(const HeaderInfo &hi, const uint8_t *blob, uint
         if (p.long_frames) {
             p.ph = 8;
             p.nbF = (p.L - 1) / 1024;
-            const uint64_t ns = ((p.L - 1) - 1024 * p.nbF) / 64;
-            p.Kreg = 8 * (16 * p.nbF + ns);
+            p.ns = ((p.L - 1) - 1024 * p.nbF) / 64;
+            p.Kreg = 8 * (16 * p.nbF + p.ns);
             p.q_side0 = (uint32_t)((S - 64) >> 4);
         }
         p.n = 44 + 8 * p.N;
@@ -141,8 +145,20 @@ __device__ inline void make_plan(const HeaderInfo &hi, const uint8_t *blob, uint
 }
 
 // ------------------------------------------------------------ primitives
-__device__ __forceinline__ void glds16(const void *gsrc, uint32_t lds_addr) {
+__device__ __forceinline__ void glds16(const void *gsrc, uint32_t lds_addr, bool nt = false) {
     uint32_t keep;
+    if (nt) {
+        asm volatile(
+            "s_mov_b32 %0, m0\n\t"
+            "s_mov_b32 m0, %2\n\t"
+            "s_nop 0\n\t"
+            "global_load_lds_dwordx4 %1, off nt\n\t"
+            "s_mov_b32 m0, %0"
+            : "=&s"(keep)
+            : "v"(gsrc), "s"(__builtin_amdgcn_readfirstlane(lds_addr))
+            : "memory");
+        return;
+    }
     asm volatile(
         "s_mov_b32 %0, m0\n\t"
         "s_mov_b32 m0, %2\n\t"
@@ -198,7 +214,7 @@ __device__ __forceinline__ void issue_phase(const uint8_t *blob, const UPlan &pl
         const bool ok = (i >= 0) && ((uint64_t)i < pl.N) && (q < pl.nck) &&
                         !(pl.tail_unsafe && (uint64_t)i == pl.N - 1 && 16ull * q + 16 > pl.S);
         const uint8_t *src = ok ? fb + 16ull * q : blob;
-        glds16(src, lds_slot + 1024u * k);
+        glds16(src, lds_slot + 1024u * k, pl.nt);
         i += FPI;
         fb += step;
     }
@@ -335,6 +351,41 @@ __device__ inline uint64_t short_hash(const uint8_t *slot, int lane, uint64_t L)
     return avalanche(acc);
 }
 
+// ------------------------------------------------------------- unit sums
+// A unit = 64 consecutive frames [256c - 6 + 64w, +64) (chunk c, quarter w).
+// Its interior batch-checksum words m = 256c + 64w + t (t < 63) are
+// hi32(cs_{m-6}) | lo32(cs_{m-5}) << 32: reduce them to 8 accumulator partial
+// sums and publish them as 16 epoch-tagged 32-bit halves (no flag, no fence:
+// each 8-B store is single-copy atomic, the gatherer checks every tag).
+// `stored` = stored checksum of frame 256c - 6 + 64w + lane.
+// cs_sec = secret word of checksum word m (stripe (m >> 3) & 15, lane m & 7)
+__device__ __forceinline__ uint64_t unit_cs_secret(uint64_t unit, int lane) {
+    const uint32_t tid = (uint32_t)((unit & 3) * 64 + lane);
+    return kSecretW8[((tid >> 3) & 15) + (tid & 7)];
+}
+__device__ __forceinline__ void publish_unit_sums(const UPlan &pl, const DecodeScratch &sc, uint32_t epoch,
+                                                  uint64_t unit, int lane, uint64_t stored, uint64_t cs_sec) {
+    const uint32_t tid = (uint32_t)((unit & 3) * 64 + lane);
+    const uint64_t next = __shfl_down(stored, 1);
+    const uint64_t m = 256 * (unit >> 2) + tid;
+    uint64_t x = 0, y = 0;  // x -> acc[j], y -> acc[j^1]
+    if (lane < 63 && m >= 6 && m < pl.Mreg) {
+        const uint64_t v = (stored >> 32) | (next << 32);
+        y = v;
+        x = mul32x32(v ^ cs_sec);
+    }
+    x += __shfl_xor(x, 8); y += __shfl_xor(y, 8);
+    x += __shfl_xor(x, 16); y += __shfl_xor(y, 16);
+    x += __shfl_xor(x, 32); y += __shfl_xor(y, 32);
+    const uint64_t t8 = x + __shfl_xor(y, 1);  // lane t (< 8): partial acc[t]
+    if (lane < 8) {
+        const uint64_t tag = (uint64_t)epoch << 32;
+        uint64_t *dst = sc.sums + unit * 16 + 2 * lane;
+        __hip_atomic_store(dst, (t8 & 0xffffffffull) | tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(dst + 1, (t8 >> 32) | tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
 // ------------------------------------------------------------- producer
 // One wave's whole life: every chunk of this WG, streamed through its ring.
 template <int PH, int NSLOT, int DEPTH, bool VERIFY>
@@ -360,21 +411,6 @@ __device__ __forceinline__ void produce(const uint8_t *blob, const UPlan &pl, ui
     };
     for (int d = 0; d < DEPTH; ++d) issue_next();
 
-    // chunks whose partial sums are stored but not yet covered by a vmcnt wait:
-    // FIFO (pub_c, pub_c + nprod, ...), the head ready once step pub_k has landed
-    uint64_t pub_c = g;
-    uint32_t pub_k = 0, npend = 0;
-    auto publish_ready = [&](uint32_t kk) {
-        while (npend && pub_k <= kk) {
-            if (lane == 0)
-                __hip_atomic_store(&sc.flags[pub_c * 4 + wave], epoch, __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_AGENT);
-            pub_c += nprod;
-            pub_k += pl.nph;
-            --npend;
-        }
-    };
-
     for (uint64_t c = g; c < pl.nchunks; c += nprod) {
         const int64_t i = (int64_t)(256 * c) - 6 + 64 * (int64_t)wave + lane;
         const bool fvalid = i >= 0 && (uint64_t)i < pl.N;
@@ -385,12 +421,13 @@ __device__ __forceinline__ void produce(const uint8_t *blob, const UPlan &pl, ui
         for (uint32_t p = 0; p < pl.nph; ++p) {
             issue_next();
             wait_vm(PH * (iss - 1 - k));  // step k landed; later steps may stay in flight
-            if (npend) publish_ready(k);
             slot_last = ring + (k % NSLOT) * kSlot;
+            if (dbg & 8) { ++k; continue; }  // diagnostics: loads only
             if (dbg & 2) run_phase<PH, false>(smem + slot_last, side, lane, p, pl, st);
             else run_phase<PH, VERIFY>(smem + slot_last, side, lane, p, pl, st);
             ++k;
         }
+        if (dbg & 8) continue;
         // ---- per-frame result
         uint64_t h = 0;
         if (VERIFY) {
@@ -436,31 +473,219 @@ __device__ __forceinline__ void produce(const uint8_t *blob, const UPlan &pl, ui
             const int leader = __builtin_ctzll(sb);
             if (lane == leader) atomicMax((unsigned long long *)sc.spec_fail, (unsigned long long)~(uint64_t)i);
         }
-        // ---- this wave's interior batch-checksum words m = 256c + 64w + lane (lane < 63)
-        if (VERIFY && pl.long_cs) {
-            const uint64_t next = __shfl_down(stored, 1);
-            const uint64_t m = 256 * c + tid;
-            uint64_t x = 0, y = 0;  // x -> acc[j], y -> acc[j^1]
-            if (lane < 63 && m >= 6 && m < pl.Mreg) {
-                const uint64_t v = (stored >> 32) | (next << 32);
-                y = v;
-                x = mul32x32(v ^ cs_sec);
-            }
-            x += __shfl_xor(x, 8); y += __shfl_xor(y, 8);
-            x += __shfl_xor(x, 16); y += __shfl_xor(y, 16);
-            x += __shfl_xor(x, 32); y += __shfl_xor(y, 32);
-            const uint64_t t8 = x + __shfl_xor(y, 1);  // lane t (< 8): partial acc[t]
-            if (lane < 8)
-                __hip_atomic_store(&sc.sums[(c * 4 + wave) * 8 + lane], t8, __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_AGENT);
-            // covered by the wait of step (last step of c) + DEPTH
-            if (npend == 0) pub_k = (k - 1) + DEPTH;  // FIFO head: this chunk
-            ++npend;
-        }
+        if (VERIFY && pl.long_cs)
+            publish_unit_sums(pl, sc, epoch, c * 4 + wave, lane, stored, unit_cs_secret(c * 4 + wave, lane));
     }
     wait_vm(0);
-    publish_ready(~0u);
     if (lane == 0) __hip_atomic_fetch_add(sc.exited, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// ------------------------------------------------------- lane-group producer
+// Long frames (hashed length L > 240) under Verify. No LDS: 8 lanes per frame,
+// 8 frames per wave-instruction, every lane loading 16 B straight into VGPRs,
+// so one instruction reads 8 x 128 contiguous bytes (one 128-B segment of each
+// of 8 frames). This register-direct shape streams at ~6.4 TB/s on MI355X
+// (scripts/bw_micro.hip) where the LDS-DMA shape peaked at ~5.3 TB/s.
+//
+// Lane l of a frame group loads piece (m = l>>1) of stripe (2q + (l&1)) of
+// segment q: hashed words 2m, 2m+1, i.e. accumulators acc[2m], acc[2m+1] of
+// that stripe (acc[j] += mul32x32(w_j ^ s), acc[j^1] += w_j stays lane-local).
+// The two lanes of a pair hold partial sums of even / odd stripes; they are
+// combined (DPP quad_perm) at every 1024-B block end, scrambled, and carried
+// by the even lane. A unit = 64 frames = 8 groups processed in order; the next
+// (group, block) step's loads are in flight while the current one hashes.
+template <int CTRL>
+__device__ __forceinline__ uint64_t dpp64(uint64_t x) {
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_mov_dpp((int)(uint32_t)x, CTRL, 0xF, 0xF, false);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_mov_dpp((int)(uint32_t)(x >> 32), CTRL, 0xF, 0xF, false);
+    return (uint64_t)lo | ((uint64_t)hi << 32);
+}
+constexpr int kDppXor1 = 0xB1;  // quad_perm [1,0,3,2]
+constexpr int kDppXor2 = 0x4E;  // quad_perm [2,3,0,1]
+__device__ __forceinline__ uint64_t swz_xor4(uint64_t x) {  // ds_swizzle bit mode, xor_mask 4
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_ds_swizzle((int)(uint32_t)x, 0x101F);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_ds_swizzle((int)(uint32_t)(x >> 32), 0x101F);
+    return (uint64_t)lo | ((uint64_t)hi << 32);
+}
+
+struct LgBuf {
+    uint4 v[8];       // 8 segments x 16 B of one block (or the partial block)
+    uint4 last;       // last stripe piece (final step only)
+    uint64_t stored;  // stored checksum (final step only)
+};
+
+struct LgLane {  // per-lane constants
+    uint32_t l, m, par, fg, poff;
+    uint64_t s0[8], s1[8];
+    uint64_t key0, key1, init0, init1, last0, last1, mrg0, mrg1;
+    uint64_t css0, css1;  // batch-checksum word secrets for even / odd units
+};
+
+__device__ __forceinline__ int64_t lg_frame_index(uint64_t u, uint32_t g, uint32_t fg) {
+    return (int64_t)(256 * (u >> 2)) - 6 + 64 * (int64_t)(u & 3) + 8 * (int64_t)g + fg;
+}
+
+// Exactly 10 loads per step (8 pieces, last-stripe piece, stored checksum) on
+// both paths, every value consumed by lg_process (full steps fold `last` and
+// `stored` into a sink), so the compiler's vmcnt bookkeeping can wait for
+// this step's loads while the next step's 10 stay in flight. Full-block steps
+// re-read the frame start for `last` / `stored` (cache hits).
+// uses of x cannot move above this point; forces x to be materialised here
+__device__ __forceinline__ void pin_after_wait(uint64_t &x) { asm volatile("" : "+v"(x)); }
+
+__device__ __forceinline__ void lg_issue(const uint8_t *blob, const UPlan &pl, const LgLane &c, uint64_t u,
+                                         uint32_t g, uint32_t b, LgBuf &B) {
+    const int64_t i = lg_frame_index(u, g, c.fg);
+    const bool valid = i >= 0 && (uint64_t)i < pl.N;
+    const uint8_t *fb = blob + (valid ? (uint64_t)i : 0) * pl.S;
+    const uint8_t *hb = fb + 8 + 1024ull * b + c.poff;
+    const bool full = b < pl.nbF;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) B.v[q] = ld128_any((full || 2 * q + c.par < pl.ns) ? hb + 128 * q : fb);
+    B.last = ld128_any(full ? fb : fb + 8 + pl.L - 64 + 16 * c.m);
+    B.stored = ld64_any(fb);
+}
+
+__device__ __forceinline__ void lg_piece(uint64_t &a0, uint64_t &a1, uint4 p, uint64_t s0, uint64_t s1) {
+    const uint64_t w0 = (uint64_t)p.x | ((uint64_t)p.y << 32);
+    const uint64_t w1 = (uint64_t)p.z | ((uint64_t)p.w << 32);
+    a0 += mul32x32(w0 ^ s0) + w1;
+    a1 += mul32x32(w1 ^ s1) + w0;
+}
+
+struct LgState {
+    uint64_t a0, a1, cs_mine;
+    uint32_t sink;  // full steps' `last` / `stored` values land here (keeps their loads live)
+    bool sbad, unit_err;
+};
+
+__device__ __forceinline__ void lg_process(const UPlan &pl, const LgLane &c, const DecodeScratch &sc,
+                                           uint32_t epoch, uint64_t *frame_pos, uint64_t cap, uint64_t u,
+                                           uint32_t g, uint32_t b, const LgBuf &B, LgState &st, int lane) {
+    if (b == 0) {
+        if (g == 0) st.unit_err = false;
+        st.a0 = c.init0;
+        st.a1 = c.init1;
+        // frame header: hashed word 3 = user_headers_len | payload_len (lane 2),
+        // hashed word 4 = reserved (lane 4); both in the first segment
+        const int64_t i = lg_frame_index(u, g, c.fg);
+        const bool valid = i >= 0 && (uint64_t)i < pl.N;
+        const uint4 h0 = B.v[0];
+        st.sbad = valid && ((c.l == 2 && (uint64_t)kFrameHdr + h0.z + h0.w != pl.S) ||
+                            (c.l == 4 && (h0.x | h0.y) != 0));
+    }
+    if (b < pl.nbF) {
+#pragma unroll
+        for (int q = 0; q < 8; ++q) lg_piece(st.a0, st.a1, B.v[q], c.s0[q], c.s1[q]);
+        st.a0 += dpp64<kDppXor1>(st.a0);
+        st.a1 += dpp64<kDppXor1>(st.a1);
+        st.a0 = scramble1(st.a0, c.key0);
+        st.a1 = scramble1(st.a1, c.key1);
+        if (c.par) { st.a0 = 0; st.a1 = 0; }
+        st.sink += B.last.x ^ (uint32_t)B.stored;
+        return;
+    }
+    // final step of the frame group: partial block, last stripe, merge, checks
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+        if (2 * q < pl.ns && 2 * q + c.par < pl.ns) lg_piece(st.a0, st.a1, B.v[q], c.s0[q], c.s1[q]);
+        else st.sink += B.v[q].x;  // unused piece: keep its load live
+    }
+    st.a0 += dpp64<kDppXor1>(st.a0);
+    st.a1 += dpp64<kDppXor1>(st.a1);
+    lg_piece(st.a0, st.a1, B.last, c.last0, c.last1);
+    uint64_t t = fold64(st.a0 ^ c.mrg0, st.a1 ^ c.mrg1);
+    t += dpp64<kDppXor2>(t);
+    t += swz_xor4(t);
+    const uint64_t h = avalanche(pl.L * P64_1 + t);
+    const int64_t i = lg_frame_index(u, g, c.fg);
+    const bool valid = i >= 0 && (uint64_t)i < pl.N;
+    const uint64_t stored = B.stored;
+    const bool mism = valid && h != stored;
+    // stored checksums, lane-per-frame, for the unit's batch-checksum words
+    const uint64_t mine = __shfl(stored, (int)(8 * c.l));
+    if (c.fg == g) st.cs_mine = mine;  // lane 8g + k <- frame 8g + k
+    const uint64_t mb = __ballot(mism);
+    if (mb && !st.unit_err) {  // groups run in index order: the first one is the unit's first
+        st.unit_err = true;
+        const int leader = __builtin_ctzll(mb);
+        if (lane == leader) {
+            atomicMax((unsigned long long *)sc.first_bad, (unsigned long long)~(uint64_t)i);
+            __hip_atomic_store(&sc.errslot[2 * u], stored, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(&sc.errslot[2 * u + 1], h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+    const uint64_t sb = __ballot(st.sbad);
+    if (sb) {
+        const int leader = __builtin_ctzll(sb);
+        if (lane == leader) atomicMax((unsigned long long *)sc.spec_fail, (unsigned long long)~(uint64_t)i);
+    }
+    if (g == 7) {  // unit complete
+        const int64_t fi = lg_frame_index(u, 0, 0) + lane;
+        if (frame_pos && fi >= 0 && (uint64_t)fi < pl.N && (uint64_t)fi < cap) frame_pos[fi] = (uint64_t)fi * pl.S;
+        if (pl.long_cs) publish_unit_sums(pl, sc, epoch, u, lane, st.cs_mine, (u & 1) ? c.css1 : c.css0);
+    }
+}
+
+__device__ __forceinline__ void produce_lg(const uint8_t *blob, const UPlan &pl, uint64_t *frame_pos, uint64_t cap,
+                                           const DecodeScratch &sc, uint32_t epoch, uint32_t gw, uint32_t nw,
+                                           int lane) {
+    LgLane c;
+    c.l = lane & 7; c.m = c.l >> 1; c.par = c.l & 1; c.fg = (uint32_t)lane >> 3;
+    c.poff = 16 * (c.m + 4 * c.par);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+        c.s0[q] = kSecretW8[2 * q + c.par + 2 * c.m];
+        c.s1[q] = kSecretW8[2 * q + c.par + 2 * c.m + 1];
+    }
+    c.key0 = kSecretW8[16 + 2 * c.m]; c.key1 = kSecretW8[17 + 2 * c.m];
+    c.init0 = c.par ? 0 : kAccInit[2 * c.m]; c.init1 = c.par ? 0 : kAccInit[2 * c.m + 1];
+    c.last0 = kSecretLast[2 * c.m]; c.last1 = kSecretLast[2 * c.m + 1];
+    c.mrg0 = kSecretMerge[2 * c.m]; c.mrg1 = kSecretMerge[2 * c.m + 1];
+    c.css0 = unit_cs_secret(0, lane); c.css1 = unit_cs_secret(1, lane);
+    // materialise every lane constant here: the hot loop then holds no
+    // compiler-tracked load, so its only vmcnt waits are the explicit ones
+#pragma unroll
+    for (int q = 0; q < 8; ++q) { pin_after_wait(c.s0[q]); pin_after_wait(c.s1[q]); }
+    pin_after_wait(c.key0); pin_after_wait(c.key1); pin_after_wait(c.init0); pin_after_wait(c.init1);
+    pin_after_wait(c.last0); pin_after_wait(c.last1); pin_after_wait(c.mrg0); pin_after_wait(c.mrg1);
+    pin_after_wait(c.css0); pin_after_wait(c.css1);
+    const uint64_t units = 4 * pl.nchunks;
+    const uint32_t nblk = (uint32_t)pl.nbF + 1;  // steps per frame group
+    if (gw >= units) return;
+
+    LgState st;
+    st.a0 = c.init0; st.a1 = c.init1; st.cs_mine = 0; st.sbad = false; st.unit_err = false; st.sink = 0;
+    // processing cursor (pu, pg, pb) and issue cursor one step ahead (iu, ig, ib)
+    uint64_t pu = gw, iu = gw;
+    uint32_t pg = 0, pb = 0, ig = 0, ib = 0;
+    auto advance = [&](uint64_t &u, uint32_t &g, uint32_t &b) {
+        if (++b == nblk) { b = 0; if (++g == 8) { g = 0; u += nw; } }
+    };
+    LgBuf A, Bq;
+    lg_issue(blob, pl, c, iu, ig, ib, A);
+    advance(iu, ig, ib);
+    // the next step is always issued (a past-the-end step re-reads the wave's
+    // first step, unused) and a compiler barrier keeps those loads above the
+    // hashing of the current step
+    auto issue_next = [&](LgBuf &B) -> bool {
+        const bool more = iu < units;
+        lg_issue(blob, pl, c, more ? iu : gw, more ? ig : 0, more ? ib : 0, B);
+        if (more) advance(iu, ig, ib);
+        asm volatile("" ::: "memory");
+        return more;
+    };
+    while (true) {
+        const bool more1 = issue_next(Bq);
+        lg_process(pl, c, sc, epoch, frame_pos, cap, pu, pg, pb, A, st, lane);
+        advance(pu, pg, pb);
+        if (!more1) break;
+        const bool more2 = issue_next(A);
+        lg_process(pl, c, sc, epoch, frame_pos, cap, pu, pg, pb, Bq, st, lane);
+        advance(pu, pg, pb);
+        if (!more2) break;
+    }
+    if (st.sink == 0x5eed5eedu && pl.N == 0) sc.small[lane] = 1;  // never true (N >= 1); keeps `sink` live
 }
 
 // ------------------------------------------------------------- consumer
@@ -492,25 +717,47 @@ __device__ __forceinline__ void gather(const uint8_t *blob, const UPlan &pl, con
         }
         const uint64_t c = bi * kBatch + lane;
         const bool live = c < need && c < pl.nchunks;
+        const uint64_t *src = sc.sums + c * 64;  // 4 units x 16 tagged halves
+        auto tag_ok = [&](uint64_t v) { return (uint32_t)(v >> 32) == epoch; };
+        // cheap poll: the last half of each unit, then everything with a full tag check
         while (!abort) {
             bool ok = true;
             if (live) {
 #pragma unroll
                 for (int w = 0; w < 4; ++w)
-                    ok &= __hip_atomic_load(&sc.flags[c * 4 + w], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == epoch;
+                    ok &= tag_ok(__hip_atomic_load(src + 16 * w + 15, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
             }
             if (__ballot(!ok) == 0) break;
             __builtin_amdgcn_s_sleep(2);
+            if (give_up()) abort = true;
+        }
+        uint64_t B[16];
+        while (!abort) {
+            bool ok = true;
+#pragma unroll
+            for (int t = 0; t < 16; ++t) B[t] = 0;
+            if (live) {
+#pragma unroll
+                for (int w = 0; w < 4; ++w) {
+#pragma unroll
+                    for (int t = 0; t < 8; ++t) {
+                        const uint64_t lo = __hip_atomic_load(src + 16 * w + 2 * t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        const uint64_t hi = __hip_atomic_load(src + 16 * w + 2 * t + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        ok &= tag_ok(lo) & tag_ok(hi);
+                        // units 0, 1 of chunk c -> block 2c; units 2, 3 -> block 2c+1
+                        B[8 * (w >> 1) + t] += (lo & 0xffffffffull) | (hi << 32);
+                    }
+                }
+            }
+            if (__ballot(!ok) == 0) break;
+            __builtin_amdgcn_s_sleep(1);
             if (give_up()) abort = true;
         }
         if (abort) {
             if (lane == 0) __hip_atomic_store(&ctl->abort, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             return;
         }
-        uint64_t P[32], CS[8];
-#pragma unroll
-        for (int x = 0; x < 32; ++x)
-            P[x] = live ? __hip_atomic_load(&sc.sums[c * 32 + x], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
+        uint64_t CS[8];
 #pragma unroll
         for (int w = 0; w < 4; ++w) {
             // wave-boundary word m = 256c + 64w + 63 = hi32(cs_{m-6}) | lo32(cs_{m-5}) << 32
@@ -519,12 +766,6 @@ __device__ __forceinline__ void gather(const uint8_t *blob, const UPlan &pl, con
             const uint64_t fi = m - 6;
             CS[2 * w] = need_w ? ld64_any(blob + fi * pl.S) : 0;
             CS[2 * w + 1] = need_w ? ld64_any(blob + (fi + 1) * pl.S) : 0;
-        }
-        uint64_t B[16];
-#pragma unroll
-        for (int t = 0; t < 8; ++t) {
-            B[t] = P[t] + P[8 + t];            // block 2c   = waves 0, 1 of the chunk
-            B[8 + t] = P[16 + t] + P[24 + t];  // block 2c+1 = waves 2, 3
         }
 #pragma unroll
         for (int w = 0; w < 4; ++w) {
@@ -592,7 +833,7 @@ __device__ __forceinline__ void consumer(const uint8_t *body, const HeaderInfo &
         __syncthreads();
     }
     if (wave != 0) {  // gatherer waves feed the chain wave through the LDS ring
-        if (chain) gather(blob, pl, sc, epoch, wave - 1, smem, t_start);
+        if (chain && wave <= kGatherWaves) gather(blob, pl, sc, epoch, wave - 1, smem, t_start);
         return;
     }
     if (chain) {
@@ -759,40 +1000,77 @@ __device__ __forceinline__ void consumer(const uint8_t *body, const HeaderInfo &
     __hip_atomic_store(sc.spec_fail, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// ------------------------------------------------------------- kernel
+// ------------------------------------------------------------- kernels
+// Three launches per decode (codec_api.hip enqueue_decode): the consumer WG on
+// the context's side stream, then the LDS-staged producers and the lane-group
+// producers on the caller's stream. Exactly one producer kind runs (the other
+// exits at once after reading the header); the producer grids leave one CU for
+// the consumer, and no producer ever waits for the consumer.
 template <bool VERIFY>
-__global__ __launch_bounds__(256, 1) void k_decode_uniform(const uint8_t *__restrict__ body,
-                                                           uint64_t len, uint64_t *frame_pos,
-                                                           uint64_t cap, iggy_decode_result *result,
-                                                           DecodeScratch sc, uint32_t epoch,
-                                                           uint32_t allow_unaligned, uint32_t dbg) {
+__device__ __forceinline__ bool uniform_uses_lg(const UPlan &pl, uint32_t dbg) {
+    return VERIFY && pl.long_frames && !(dbg & 32);  // dbg bit 32: force the LDS form (A/B only)
+}
+
+template <bool VERIFY>
+__global__ __launch_bounds__(256, 1) void k_uniform_consumer(const uint8_t *__restrict__ body, uint64_t len,
+                                                             iggy_decode_result *result, DecodeScratch sc,
+                                                             uint32_t epoch, uint32_t allow_unaligned,
+                                                             uint32_t waves_lg, uint32_t waves_lds,
+                                                             uint32_t dbg) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    const int lane = threadIdx.x & 63;
     const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const uint32_t nprod = gridDim.x - 1;
     HeaderInfo hi;
     parse_header(body, len, hi);
     UPlan pl;
     make_plan(hi, body + kHdr, len, VERIFY, sc.max_chunks, allow_unaligned != 0, pl);
-
-    if (blockIdx.x == 0) {
-        consumer<VERIFY>(body, hi, pl, result, sc, epoch, 4 * nprod, wave, smem, dbg);
-        return;
-    }
-    if (pl.state != 0) return;  // nothing for producers; the consumer resolves
-    const uint8_t *blob = body + kHdr;
-    const uint32_t g = blockIdx.x - 1;
-    if (VERIFY && pl.long_frames)
-        produce<8, 4, 3, VERIFY>(blob, pl, frame_pos, cap, sc, epoch, g, nprod, wave, lane, smem, dbg);
-    else
-        produce<16, 2, 1, VERIFY>(blob, pl, frame_pos, cap, sc, epoch, g, nprod, wave, lane, smem, dbg);
+    const uint32_t nwaves = uniform_uses_lg<VERIFY>(pl, dbg) ? waves_lg : waves_lds;
+    consumer<VERIFY>(body, hi, pl, result, sc, epoch, nwaves, wave, smem, dbg);
 }
 
-template __global__ void k_decode_uniform<true>(const uint8_t *__restrict__, uint64_t, uint64_t *,
-                                                uint64_t, iggy_decode_result *, DecodeScratch,
-                                                uint32_t, uint32_t, uint32_t);
-template __global__ void k_decode_uniform<false>(const uint8_t *__restrict__, uint64_t, uint64_t *,
-                                                 uint64_t, iggy_decode_result *, DecodeScratch,
-                                                 uint32_t, uint32_t, uint32_t);
+template <bool VERIFY>
+__global__ __launch_bounds__(256, 1) void k_uniform_lds(const uint8_t *__restrict__ body, uint64_t len,
+                                                        uint64_t *frame_pos, uint64_t cap, DecodeScratch sc,
+                                                        uint32_t epoch, uint32_t allow_unaligned,
+                                                        uint32_t dbg) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const int lane = threadIdx.x & 63;
+    const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    HeaderInfo hi;
+    parse_header(body, len, hi);
+    UPlan pl;
+    make_plan(hi, body + kHdr, len, VERIFY, sc.max_chunks, allow_unaligned != 0, pl);
+    pl.nt = (dbg & 16) != 0;
+    if (pl.state != 0 || uniform_uses_lg<VERIFY>(pl, dbg)) return;
+    const uint8_t *blob = body + kHdr;
+    if (VERIFY && pl.long_frames)
+        produce<8, 4, 3, VERIFY>(blob, pl, frame_pos, cap, sc, epoch, blockIdx.x, gridDim.x, wave, lane, smem, dbg);
+    else
+        produce<16, 2, 1, VERIFY>(blob, pl, frame_pos, cap, sc, epoch, blockIdx.x, gridDim.x, wave, lane, smem, dbg);
+}
+
+__global__ __launch_bounds__(kUniformThreads, 1) void k_uniform_lg(const uint8_t *__restrict__ body, uint64_t len,
+                                                                  uint64_t *frame_pos, uint64_t cap,
+                                                                  DecodeScratch sc, uint32_t epoch,
+                                                                  uint32_t allow_unaligned, uint32_t dbg) {
+    const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    HeaderInfo hi;
+    parse_header(body, len, hi);
+    UPlan pl;
+    make_plan(hi, body + kHdr, len, true, sc.max_chunks, allow_unaligned != 0, pl);
+    if (pl.state != 0 || !uniform_uses_lg<true>(pl, dbg)) return;
+    produce_lg(body + kHdr, pl, frame_pos, cap, sc, epoch, blockIdx.x * 8 + wave, gridDim.x * 8,
+               threadIdx.x & 63);
+    if ((threadIdx.x & 63) == 0)
+        __hip_atomic_fetch_add(sc.exited, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+template __global__ void k_uniform_consumer<true>(const uint8_t *__restrict__, uint64_t, iggy_decode_result *,
+                                                  DecodeScratch, uint32_t, uint32_t, uint32_t, uint32_t, uint32_t);
+template __global__ void k_uniform_consumer<false>(const uint8_t *__restrict__, uint64_t, iggy_decode_result *,
+                                                   DecodeScratch, uint32_t, uint32_t, uint32_t, uint32_t, uint32_t);
+template __global__ void k_uniform_lds<true>(const uint8_t *__restrict__, uint64_t, uint64_t *, uint64_t,
+                                             DecodeScratch, uint32_t, uint32_t, uint32_t);
+template __global__ void k_uniform_lds<false>(const uint8_t *__restrict__, uint64_t, uint64_t *, uint64_t,
+                                              DecodeScratch, uint32_t, uint32_t, uint32_t);
 
 }  // namespace iggy

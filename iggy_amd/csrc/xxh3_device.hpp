@@ -63,6 +63,10 @@ __constant__ static const uint64_t kSecretW8[24] = {
 __constant__ static const uint64_t kSecretLast[8] = {
     Secret::w(121), Secret::w(129), Secret::w(137), Secret::w(145),
     Secret::w(153), Secret::w(161), Secret::w(169), Secret::w(177)};
+// Secret words of the XXH3 long-path merge: acc[2i] ^ w(11 + 16i), acc[2i+1] ^ w(19 + 16i).
+__constant__ static const uint64_t kSecretMerge[8] = {
+    Secret::w(11), Secret::w(19), Secret::w(27), Secret::w(35),
+    Secret::w(43), Secret::w(51), Secret::w(59), Secret::w(67)};
 // Initial accumulators of the XXH3 long path.
 __constant__ static const uint64_t kAccInit[8] = {P32_3, P64_1, P64_2, P64_3,
                                                   P64_4, P32_2, P64_5, P32_1};

@@ -1,0 +1,90 @@
+// HBM read-bandwidth calibration (diagnostic, not product): how fast can this
+// box stream a ~1.1 GB device buffer with (a) coalesced global_load_dwordx4 into
+// VGPRs, (b) 8 lanes x 16 B per frame-segment at a 1072-B stride (the
+// lane-group frame layout), at several grid shapes.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+
+__global__ void rd_coalesced(const uint4 *__restrict__ p, uint64_t n16, uint64_t *out, int unroll) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    uint32_t x = 0;
+    for (; i + 7 * stride < n16; i += 8 * stride) {
+        uint4 v[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) v[k] = p[i + k * stride];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) x ^= v[k].x ^ v[k].y ^ v[k].z ^ v[k].w;
+    }
+    for (; i < n16; i += stride) { uint4 v = p[i]; x ^= v.x ^ v.y ^ v.z ^ v.w; }
+    if (x == 0x12345678) out[0] = x;
+}
+
+// wave = 8 frame groups of 8 lanes; each lane loads 16 B at frame + 8 + 128 q + 16 (l%8)
+template <int DEPTH>
+__global__ void rd_frames(const uint8_t *__restrict__ blob, uint64_t S, uint64_t N, uint64_t *out) {
+    const int lane = threadIdx.x & 63;
+    const uint64_t gw = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const uint64_t nw = ((uint64_t)gridDim.x * blockDim.x) >> 6;
+    const uint32_t nseg = (uint32_t)((S - 8 + 127) / 128);
+    uint32_t x = 0;
+    for (uint64_t f0 = gw * 8; f0 < N; f0 += nw * 8) {
+        const uint64_t f = f0 + (lane >> 3);
+        const uint8_t *base = blob + f * S + 8 + 16 * (lane & 7);
+        const bool ok = f < N;
+        for (uint32_t q = 0; q < nseg; q += DEPTH) {
+            uint4 v[DEPTH];
+#pragma unroll
+            for (int d = 0; d < DEPTH; ++d) {
+                const uint64_t off = 128ull * (q + d);
+                v[d] = (ok && q + d < nseg && off + 16 * (lane & 7) + 24 <= S)
+                           ? *(const uint4 *)(base + off) : make_uint4(0, 0, 0, 0);
+            }
+#pragma unroll
+            for (int d = 0; d < DEPTH; ++d) x ^= v[d].x ^ v[d].y ^ v[d].z ^ v[d].w;
+        }
+    }
+    if (x == 0x12345678) out[0] = x;
+}
+
+int main() {
+    const uint64_t N = 1 << 20, S = 1072, L = 256 + N * S;
+    uint8_t *d;
+    uint64_t *o;
+    hipMalloc(&d, L + 4096);
+    hipMalloc(&o, 64);
+    hipMemset(d, 0x5a, L + 4096);
+    hipEvent_t e0, e1;
+    hipEventCreate(&e0);
+    hipEventCreate(&e1);
+    auto timeit = [&](const char *name, auto launch) {
+        for (int w = 0; w < 3; ++w) launch();
+        hipDeviceSynchronize();
+        hipEventRecord(e0);
+        const int reps = 20;
+        for (int r = 0; r < reps; ++r) launch();
+        hipEventRecord(e1);
+        hipEventSynchronize(e1);
+        float ms;
+        hipEventElapsedTime(&ms, e0, e1);
+        ms /= reps;
+        printf("%-40s %8.4f ms  %7.1f GB/s\n", name, ms, L / (ms * 1e-3) / 1e9);
+    };
+    char nm[128];
+    for (int blocks : {256, 512, 1024, 2048, 4096}) {
+        for (int th : {256, 512}) {
+            snprintf(nm, sizeof nm, "coalesced grid=%d x %d", blocks, th);
+            timeit(nm, [&] { hipLaunchKernelGGL(rd_coalesced, blocks, th, 0, 0, (const uint4 *)d, L / 16, o, 8); });
+        }
+    }
+    for (int blocks : {256, 512, 1024, 2048}) {
+        for (int th : {256, 512, 1024}) {
+            snprintf(nm, sizeof nm, "frames d4 grid=%d x %d", blocks, th);
+            timeit(nm, [&] { hipLaunchKernelGGL(rd_frames<4>, blocks, th, 0, 0, d + 256, S, N, o); });
+            snprintf(nm, sizeof nm, "frames d9 grid=%d x %d", blocks, th);
+            timeit(nm, [&] { hipLaunchKernelGGL(rd_frames<9>, blocks, th, 0, 0, d + 256, S, N, o); });
+        }
+    }
+    return 0;
+}

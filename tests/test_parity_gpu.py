@@ -202,3 +202,67 @@ def test_poll_multi_record(cx, mode):
     orc, oe, om = O.poll_decode(bad, mode)
     _same(rc, e, orc, oe)
     assert len(msgs) == len(om)
+
+
+# ---- full-size parity (BASELINE config C2 and a 256K-message record): many more
+# chunks than producer waves, every LDS ring slot of the chain reused, and the
+# per-call epoch tags exercised by repeated calls on one context
+@pytest.fixture(scope="module")
+def big_record():
+    return O.synth_batch(1 << 18, 1024, 1024, 0, seed=0x5EED)
+
+
+def test_c2_full_size_decode(cx):
+    rec = O.synth_batch(1 << 20, 1024, 1024, 0, seed=0x16619E3779B97F4A)
+    assert rec.size == 1_124_073_728
+    orc, oe, oh, of = O.decode_batch_slice_with(rec, 0)
+    assert orc == 0
+    for _ in range(2):
+        rc, e, h, frames = cx.decode_batch_slice_with(rec, 0)
+        assert rc == 0, e
+        assert h.astuple() == oh.astuple()
+        assert np.array_equal(frames, of)
+
+
+def test_large_uniform_repeated(cx, big_record):
+    orc, oe, oh, of = O.decode_batch_slice_with(big_record, 0)
+    for integrity in (0, 1, 0, 0):
+        rc, e, h, frames = cx.decode_batch_slice_with(big_record, integrity)
+        assert rc == orc == 0, e
+        assert h.astuple() == oh.astuple()
+        assert np.array_equal(frames, of)
+
+
+@pytest.mark.parametrize("where", ["payload_late", "payload_first", "stored_cs_mid", "batch_cs",
+                                   "reserved_late", "count", "last_frame_byte", "two_errors"])
+def test_large_uniform_corruption(cx, big_record, where):
+    rec = big_record.copy()
+    S = 1072
+    if where == "payload_late":
+        rec[256 + S * 250_000 + 500] ^= 0x40
+    elif where == "payload_first":
+        rec[256 + 100] ^= 1
+    elif where == "stored_cs_mid":
+        rec[256 + S * 131_071 + 3] ^= 0x10
+    elif where == "batch_cs":
+        rec[56] ^= 0x80
+    elif where == "reserved_late":
+        rec[256 + S * 200_000 + 45] = 7
+    elif where == "count":
+        struct.pack_into("<I", rec, 48, (1 << 18) - 1)
+    elif where == "last_frame_byte":
+        rec[-1] ^= 0xFF
+    elif where == "two_errors":
+        rec[256 + S * 180_000 + 300] ^= 2
+        rec[256 + S * 70_000 + 900] ^= 4
+    for integrity in (0, 1):
+        _check_decode_integrity(cx, rec, integrity)
+
+
+def _check_decode_integrity(cx, rec, integrity):
+    rc, e, h, frames = cx.decode_batch_slice_with(rec, integrity)
+    orc, oe, oh, of = O.decode_batch_slice_with(rec, integrity)
+    _same(rc, e, orc, oe)
+    if rc == 0:
+        assert h.astuple() == oh.astuple()
+        assert np.array_equal(frames, of)
