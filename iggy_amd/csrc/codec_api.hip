@@ -202,17 +202,17 @@ int enqueue_decode(iggy_codec_ctx *c, const uint8_t *d_body, uint64_t len, int i
     HIP_OK(hipEventRecord(c->ev_fork, s));
     HIP_OK(hipStreamWaitEvent(c->side, c->ev_fork, 0));
     if (verify)
-        hipLaunchKernelGGL(k_uniform_consumer<true>, dim3(1), dim3(256), kConsumerLds, c->side, d_body, len,
-                           d_res, ds, c->epoch, au, grid * 8, grid * 4, c->dbg);
+        hipLaunchKernelGGL(k_uniform_consumer<true>, dim3(1), dim3(kConsumerThreads), kConsumerLds, c->side, d_body, len,
+                           d_res, ds, c->epoch, au, grid * (kUniformThreads / 64), grid * 4, c->dbg);
     else
-        hipLaunchKernelGGL(k_uniform_consumer<false>, dim3(1), dim3(256), kConsumerLds, c->side, d_body, len,
-                           d_res, ds, c->epoch, au, grid * 8, grid * 4, c->dbg);
+        hipLaunchKernelGGL(k_uniform_consumer<false>, dim3(1), dim3(kConsumerThreads), kConsumerLds, c->side, d_body, len,
+                           d_res, ds, c->epoch, au, grid * (kUniformThreads / 64), grid * 4, c->dbg);
     HIP_OK(hipGetLastError());
     if (verify) {
         hipLaunchKernelGGL(k_uniform_lds<true>, dim3(grid), dim3(256), kLdsBytes, s, d_body, len, d_pos, cap,
                            ds, c->epoch, au, c->dbg);
-        hipLaunchKernelGGL(k_uniform_lg, dim3(grid), dim3(kUniformThreads), 0, s, d_body, len, d_pos, cap, ds,
-                           c->epoch, au, c->dbg);
+        hipLaunchKernelGGL(k_uniform_lg, dim3(grid), dim3(kUniformThreads), kLgLds, s, d_body, len, d_pos,
+                           cap, ds, c->epoch, au, c->dbg);
     } else {
         hipLaunchKernelGGL(k_uniform_lds<false>, dim3(grid), dim3(256), kLdsBytes, s, d_body, len, d_pos, cap,
                            ds, c->epoch, au, c->dbg);
@@ -312,6 +312,8 @@ int iggy_codec_create(int device, iggy_codec_ctx **out) {
                                 hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBytes) != hipSuccess ||
             hipFuncSetAttribute((const void *)k_uniform_lds<false>,
                                 hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBytes) != hipSuccess ||
+            hipFuncSetAttribute((const void *)k_uniform_lg,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, kLgLds) != hipSuccess ||
             hipFuncSetAttribute((const void *)k_uniform_consumer<true>,
                                 hipFuncAttributeMaxDynamicSharedMemorySize, kConsumerLds) != hipSuccess ||
             hipFuncSetAttribute((const void *)k_uniform_consumer<false>,

@@ -48,7 +48,7 @@ struct DecodeScratch {
 };
 
 // ---- LDS map of a producer WG (dynamic LDS only, base offset 0) ----------
-constexpr uint32_t kUniformThreads = 512;                      // lane-group producers: 8 waves per WG
+constexpr uint32_t kUniformThreads = 256;                      // lane-group producers: 4 waves per WG
 constexpr uint32_t kWaveRing = 32768;                          // per wave: 4 x 8 KiB or 2 x 16 KiB
 constexpr uint32_t kSideOff = 4 * kWaveRing;                   // 131072
 constexpr uint32_t kSideLane = 96;                             // 6 chunks per lane
@@ -57,7 +57,8 @@ constexpr uint32_t kLdsBytes = kSideOff + 4 * 64 * kSideLane;  // 155648
 // filled by kGatherWaves gatherer waves, drained by the chain wave
 constexpr uint32_t kBatch = 64;
 constexpr uint32_t kRing = 8;
-constexpr uint32_t kGatherWaves = 3;
+constexpr uint32_t kGatherWaves = 7;
+constexpr uint32_t kConsumerThreads = 64 * (kGatherWaves + 1);
 constexpr uint32_t kCtlOff = kRing * kBatch * 16 * 8;  // 64 KiB
 struct ChainCtl {
     uint32_t ready[kRing];  // batch index + 1 staged in the slot
@@ -65,6 +66,10 @@ struct ChainCtl {
     uint32_t abort;         // a gatherer or the chain wave gave up (spin limit)
 };
 constexpr uint32_t kConsumerLds = kCtlOff + 64;
+// lane-group producers: kLgSlots x 10 KiB per wave (set where kLgSlots is); at
+// >= 96 KiB per WG the consumer WG (kConsumerLds) can never share a CU with one
+constexpr uint32_t kLgLds = 4 * 3 * 10 * 1024;
+static_assert(kLgLds + kConsumerLds > 160 * 1024, "consumer must not fit beside a producer WG");
 static_assert(kCtlOff + sizeof(ChainCtl) <= kConsumerLds, "consumer LDS");
 static_assert(kLdsBytes <= 160 * 1024, "LDS budget");
 
@@ -174,6 +179,9 @@ __device__ __forceinline__ void wait_vm(uint32_t n) {
     switch (n) {
         case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
         case 8: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
+        case 10: asm volatile("s_waitcnt vmcnt(10)" ::: "memory"); break;
+        case 20: asm volatile("s_waitcnt vmcnt(20)" ::: "memory"); break;
+        case 30: asm volatile("s_waitcnt vmcnt(30)" ::: "memory"); break;
         case 16: asm volatile("s_waitcnt vmcnt(16)" ::: "memory"); break;
         case 24: asm volatile("s_waitcnt vmcnt(24)" ::: "memory"); break;
         default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
@@ -525,25 +533,46 @@ __device__ __forceinline__ int64_t lg_frame_index(uint64_t u, uint32_t g, uint32
     return (int64_t)(256 * (u >> 2)) - 6 + 64 * (int64_t)(u & 3) + 8 * (int64_t)g + fg;
 }
 
-// Exactly 10 loads per step (8 pieces, last-stripe piece, stored checksum) on
-// both paths, every value consumed by lg_process (full steps fold `last` and
-// `stored` into a sink), so the compiler's vmcnt bookkeeping can wait for
-// this step's loads while the next step's 10 stay in flight. Full-block steps
-// re-read the frame start for `last` / `stored` (cache hits).
+// A frame group takes nsteps = nbF + (ns > 0) steps (at least 1): one per full
+// 1024-B block, plus one for the partial block when it has stripes. Every step
+// issues exactly 10 loads (8 pieces, last-stripe piece, stored checksum); the
+// last two are real only on the group's final step (elsewhere they re-read the
+// frame start and land in a sink). The constant count lets the compiler's
+// vmcnt bookkeeping wait for THIS step's loads while the next step's stay in
+// flight. C2 (L = 1064: nbF = 1, ns = 0) runs one 10-load step per group.
 // uses of x cannot move above this point; forces x to be materialised here
 __device__ __forceinline__ void pin_after_wait(uint64_t &x) { asm volatile("" : "+v"(x)); }
 
+__device__ __forceinline__ uint32_t lg_nsteps(const UPlan &pl) {
+    const uint32_t n = (uint32_t)pl.nbF + (pl.ns > 0 ? 1u : 0u);
+    return n ? n : 1u;
+}
+
+// Issue one step: 10 x global_load_lds_dwordx4 (8 pieces, last-stripe piece,
+// frame start for the stored checksum) into the 10-KiB LDS slot `slot`; lane i
+// of instruction k lands at slot + 1024k + 16i, so each lane later reads back
+// exactly its own 16 B. The loads bypass VGPRs: the wave waits for them with an
+// explicit vmcnt, and never blocks on the step it has just issued.
+constexpr uint32_t kLgStepBytes = 10 * 1024;
 __device__ __forceinline__ void lg_issue(const uint8_t *blob, const UPlan &pl, const LgLane &c, uint64_t u,
-                                         uint32_t g, uint32_t b, LgBuf &B) {
+                                         uint32_t g, uint32_t b, uint32_t nsteps, uint32_t slot) {
     const int64_t i = lg_frame_index(u, g, c.fg);
     const bool valid = i >= 0 && (uint64_t)i < pl.N;
     const uint8_t *fb = blob + (valid ? (uint64_t)i : 0) * pl.S;
     const uint8_t *hb = fb + 8 + 1024ull * b + c.poff;
     const bool full = b < pl.nbF;
+    const bool fin = b + 1 == nsteps;
 #pragma unroll
-    for (int q = 0; q < 8; ++q) B.v[q] = ld128_any((full || 2 * q + c.par < pl.ns) ? hb + 128 * q : fb);
-    B.last = ld128_any(full ? fb : fb + 8 + pl.L - 64 + 16 * c.m);
-    B.stored = ld64_any(fb);
+    for (int q = 0; q < 8; ++q) glds16((full || 2 * q + c.par < pl.ns) ? hb + 128 * q : fb, slot + 1024u * q);
+    glds16(fin ? fb + 8 + pl.L - 64 + 16 * c.m : fb, slot + 8u * 1024u);
+    glds16(fb, slot + 9u * 1024u);
+}
+__device__ __forceinline__ void lg_read(const uint8_t *smem, uint32_t slot, int lane, LgBuf &B) {
+    const uint8_t *p = smem + slot + 16u * (uint32_t)lane;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) B.v[q] = *(const uint4 *)(p + 1024u * q);
+    B.last = *(const uint4 *)(p + 8u * 1024u);
+    B.stored = *(const uint64_t *)(p + 9u * 1024u);
 }
 
 __device__ __forceinline__ void lg_piece(uint64_t &a0, uint64_t &a1, uint4 p, uint64_t s0, uint64_t s1) {
@@ -561,7 +590,8 @@ struct LgState {
 
 __device__ __forceinline__ void lg_process(const UPlan &pl, const LgLane &c, const DecodeScratch &sc,
                                            uint32_t epoch, uint64_t *frame_pos, uint64_t cap, uint64_t u,
-                                           uint32_t g, uint32_t b, const LgBuf &B, LgState &st, int lane) {
+                                           uint32_t g, uint32_t b, uint32_t nsteps, const LgBuf &B, LgState &st,
+                                           int lane) {
     if (b == 0) {
         if (g == 0) st.unit_err = false;
         st.a0 = c.init0;
@@ -574,7 +604,7 @@ __device__ __forceinline__ void lg_process(const UPlan &pl, const LgLane &c, con
         st.sbad = valid && ((c.l == 2 && (uint64_t)kFrameHdr + h0.z + h0.w != pl.S) ||
                             (c.l == 4 && (h0.x | h0.y) != 0));
     }
-    if (b < pl.nbF) {
+    if (b < pl.nbF) {  // a full block: accumulate, fold the pair, scramble
 #pragma unroll
         for (int q = 0; q < 8; ++q) lg_piece(st.a0, st.a1, B.v[q], c.s0[q], c.s1[q]);
         st.a0 += dpp64<kDppXor1>(st.a0);
@@ -582,15 +612,19 @@ __device__ __forceinline__ void lg_process(const UPlan &pl, const LgLane &c, con
         st.a0 = scramble1(st.a0, c.key0);
         st.a1 = scramble1(st.a1, c.key1);
         if (c.par) { st.a0 = 0; st.a1 = 0; }
-        st.sink += B.last.x ^ (uint32_t)B.stored;
+    } else {  // the partial block's stripes (only when ns > 0)
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            if (2 * q < pl.ns && 2 * q + c.par < pl.ns) lg_piece(st.a0, st.a1, B.v[q], c.s0[q], c.s1[q]);
+            else st.sink += B.v[q].x ^ B.v[q].y ^ B.v[q].z ^ B.v[q].w;  // unused piece: keep its load live
+        }
+    }
+    if (b + 1 != nsteps) {
+        // not the final step: those loads were fillers (consume every register they write)
+        st.sink += B.last.x ^ B.last.y ^ B.last.z ^ B.last.w ^ (uint32_t)B.stored ^ (uint32_t)(B.stored >> 32);
         return;
     }
-    // final step of the frame group: partial block, last stripe, merge, checks
-#pragma unroll
-    for (int q = 0; q < 8; ++q) {
-        if (2 * q < pl.ns && 2 * q + c.par < pl.ns) lg_piece(st.a0, st.a1, B.v[q], c.s0[q], c.s1[q]);
-        else st.sink += B.v[q].x;  // unused piece: keep its load live
-    }
+    // final step of the frame group: fold the pair, last stripe, merge, checks
     st.a0 += dpp64<kDppXor1>(st.a0);
     st.a1 += dpp64<kDppXor1>(st.a1);
     lg_piece(st.a0, st.a1, B.last, c.last0, c.last1);
@@ -627,9 +661,11 @@ __device__ __forceinline__ void lg_process(const UPlan &pl, const LgLane &c, con
     }
 }
 
+constexpr uint32_t kLgSlots = 3;  // per wave: 1 step being hashed + 2 in flight (30 KiB)
+static_assert(4 * kLgSlots * kLgStepBytes == kLgLds, "LDS sizing");
 __device__ __forceinline__ void produce_lg(const uint8_t *blob, const UPlan &pl, uint64_t *frame_pos, uint64_t cap,
                                            const DecodeScratch &sc, uint32_t epoch, uint32_t gw, uint32_t nw,
-                                           int lane) {
+                                           uint32_t wave, int lane, uint8_t *smem) {
     LgLane c;
     c.l = lane & 7; c.m = c.l >> 1; c.par = c.l & 1; c.fg = (uint32_t)lane >> 3;
     c.poff = 16 * (c.m + 4 * c.par);
@@ -651,40 +687,37 @@ __device__ __forceinline__ void produce_lg(const uint8_t *blob, const UPlan &pl,
     pin_after_wait(c.last0); pin_after_wait(c.last1); pin_after_wait(c.mrg0); pin_after_wait(c.mrg1);
     pin_after_wait(c.css0); pin_after_wait(c.css1);
     const uint64_t units = 4 * pl.nchunks;
-    const uint32_t nblk = (uint32_t)pl.nbF + 1;  // steps per frame group
+    const uint32_t nblk = lg_nsteps(pl);  // steps per frame group
     if (gw >= units) return;
 
     LgState st;
     st.a0 = c.init0; st.a1 = c.init1; st.cs_mine = 0; st.sbad = false; st.unit_err = false; st.sink = 0;
-    // processing cursor (pu, pg, pb) and issue cursor one step ahead (iu, ig, ib)
+    // processing cursor (pu, pg, pb) and issue cursor (iu, ig, ib) up to kLgSlots-1 steps ahead
     uint64_t pu = gw, iu = gw;
     uint32_t pg = 0, pb = 0, ig = 0, ib = 0;
     auto advance = [&](uint64_t &u, uint32_t &g, uint32_t &b) {
         if (++b == nblk) { b = 0; if (++g == 8) { g = 0; u += nw; } }
     };
-    LgBuf A, Bq;
-    lg_issue(blob, pl, c, iu, ig, ib, A);
-    advance(iu, ig, ib);
-    // the next step is always issued (a past-the-end step re-reads the wave's
-    // first step, unused) and a compiler barrier keeps those loads above the
-    // hashing of the current step
-    auto issue_next = [&](LgBuf &B) -> bool {
-        const bool more = iu < units;
-        lg_issue(blob, pl, c, more ? iu : gw, more ? ig : 0, more ? ib : 0, B);
-        if (more) advance(iu, ig, ib);
-        asm volatile("" ::: "memory");
-        return more;
+    const uint32_t ring = wave * (kLgSlots * kLgStepBytes);
+    uint32_t iss = 0;  // steps issued
+    auto issue_next = [&]() {
+        if (iu >= units) return;
+        lg_issue(blob, pl, c, iu, ig, ib, nblk, ring + (iss % kLgSlots) * kLgStepBytes);
+        advance(iu, ig, ib);
+        ++iss;
     };
-    while (true) {
-        const bool more1 = issue_next(Bq);
-        lg_process(pl, c, sc, epoch, frame_pos, cap, pu, pg, pb, A, st, lane);
+    for (uint32_t d = 0; d + 1 < kLgSlots; ++d) issue_next();
+    for (uint32_t k = 0; pu < units; ++k) {
+        wait_vm(10 * (iss - 1 - k));  // step k landed; the later steps stay in flight
+        LgBuf B;
+        const uint32_t slot = ring + (k % kLgSlots) * kLgStepBytes;
+        lg_read(smem, slot, lane, B);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // slot read out before it is refilled
+        issue_next();
+        lg_process(pl, c, sc, epoch, frame_pos, cap, pu, pg, pb, nblk, B, st, lane);
         advance(pu, pg, pb);
-        if (!more1) break;
-        const bool more2 = issue_next(A);
-        lg_process(pl, c, sc, epoch, frame_pos, cap, pu, pg, pb, Bq, st, lane);
-        advance(pu, pg, pb);
-        if (!more2) break;
     }
+    wait_vm(0);
     if (st.sink == 0x5eed5eedu && pl.N == 0) sc.small[lane] = 1;  // never true (N >= 1); keeps `sink` live
 }
 
@@ -693,7 +726,7 @@ __device__ __forceinline__ uint64_t chain_batches(const UPlan &pl) {
     return ((pl.nb >> 1) + 1 + kBatch - 1) / kBatch;  // chunks 0 .. nb/2 hold blocks 0 .. nb
 }
 
-// Gatherer wave gw (0..kGatherWaves-1) of the consumer WG: batches gw, gw + 3, ...
+// Gatherer wave gw (0..kGatherWaves-1) of the consumer WG: batches gw, gw + kGatherWaves, ...
 // Waits for the 4 producer waves of each of its 64 chunks, loads their partial
 // sums and the 4 wave-boundary words, and stages 16 block-sum words per chunk.
 __device__ __forceinline__ void gather(const uint8_t *blob, const UPlan &pl, const DecodeScratch &sc,
@@ -1012,7 +1045,7 @@ __device__ __forceinline__ bool uniform_uses_lg(const UPlan &pl, uint32_t dbg) {
 }
 
 template <bool VERIFY>
-__global__ __launch_bounds__(256, 1) void k_uniform_consumer(const uint8_t *__restrict__ body, uint64_t len,
+__global__ __launch_bounds__(kConsumerThreads, 1) void k_uniform_consumer(const uint8_t *__restrict__ body, uint64_t len,
                                                              iggy_decode_result *result, DecodeScratch sc,
                                                              uint32_t epoch, uint32_t allow_unaligned,
                                                              uint32_t waves_lg, uint32_t waves_lds,
@@ -1052,14 +1085,15 @@ __global__ __launch_bounds__(kUniformThreads, 1) void k_uniform_lg(const uint8_t
                                                                   uint64_t *frame_pos, uint64_t cap,
                                                                   DecodeScratch sc, uint32_t epoch,
                                                                   uint32_t allow_unaligned, uint32_t dbg) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     HeaderInfo hi;
     parse_header(body, len, hi);
     UPlan pl;
     make_plan(hi, body + kHdr, len, true, sc.max_chunks, allow_unaligned != 0, pl);
     if (pl.state != 0 || !uniform_uses_lg<true>(pl, dbg)) return;
-    produce_lg(body + kHdr, pl, frame_pos, cap, sc, epoch, blockIdx.x * 8 + wave, gridDim.x * 8,
-               threadIdx.x & 63);
+    produce_lg(body + kHdr, pl, frame_pos, cap, sc, epoch, blockIdx.x * (kUniformThreads / 64) + wave,
+               gridDim.x * (kUniformThreads / 64), wave, threadIdx.x & 63, smem);
     if ((threadIdx.x & 63) == 0)
         __hip_atomic_fetch_add(sc.exited, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
 }

@@ -21,15 +21,18 @@ __global__ void rd_coalesced(const uint4 *__restrict__ p, uint64_t n16, uint64_t
     if (x == 0x12345678) out[0] = x;
 }
 
-// wave = 8 frame groups of 8 lanes; each lane loads 16 B at frame + 8 + 128 q + 16 (l%8)
-template <int DEPTH>
+// wave = 8 frame groups of 8 lanes; each lane loads 16 B at frame + 8 + 128 q + 16 (l%8).
+// UNIT = frames a wave walks before jumping by nw*UNIT (8: 17 MB window, 64: 139 MB window)
+template <int DEPTH, int UNIT = 8>
 __global__ void rd_frames(const uint8_t *__restrict__ blob, uint64_t S, uint64_t N, uint64_t *out) {
     const int lane = threadIdx.x & 63;
     const uint64_t gw = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     const uint64_t nw = ((uint64_t)gridDim.x * blockDim.x) >> 6;
     const uint32_t nseg = (uint32_t)((S - 8 + 127) / 128);
     uint32_t x = 0;
-    for (uint64_t f0 = gw * 8; f0 < N; f0 += nw * 8) {
+    for (uint64_t ff = 0; ff < N; ff += 8) {
+        const uint64_t f0 = (ff / UNIT) * nw * UNIT + gw * UNIT + (ff % UNIT);
+        if (f0 >= N) break;
         const uint64_t f = f0 + (lane >> 3);
         const uint8_t *base = blob + f * S + 8 + 16 * (lane & 7);
         const bool ok = f < N;
@@ -72,14 +75,20 @@ int main() {
         printf("%-40s %8.4f ms  %7.1f GB/s\n", name, ms, L / (ms * 1e-3) / 1e9);
     };
     char nm[128];
-    for (int blocks : {256, 512, 1024, 2048, 4096}) {
+    for (int blocks : {255}) {
+        timeit("frames d9 unit64 grid=255 x 512", [&] { hipLaunchKernelGGL((rd_frames<9, 64>), 255, 512, 0, 0, d + 256, S, N, o); });
+        timeit("frames d9 unit8 grid=255 x 512", [&] { hipLaunchKernelGGL((rd_frames<9, 8>), 255, 512, 0, 0, d + 256, S, N, o); });
+        timeit("frames d4 unit64 grid=255 x 512", [&] { hipLaunchKernelGGL((rd_frames<4, 64>), 255, 512, 0, 0, d + 256, S, N, o); });
+        timeit("frames d9 unit64 grid=255 x 1024", [&] { hipLaunchKernelGGL((rd_frames<9, 64>), 255, 1024, 0, 0, d + 256, S, N, o); });
+    }
+    for (int blocks : {256, 1024}) {
         for (int th : {256, 512}) {
             snprintf(nm, sizeof nm, "coalesced grid=%d x %d", blocks, th);
             timeit(nm, [&] { hipLaunchKernelGGL(rd_coalesced, blocks, th, 0, 0, (const uint4 *)d, L / 16, o, 8); });
         }
     }
-    for (int blocks : {256, 512, 1024, 2048}) {
-        for (int th : {256, 512, 1024}) {
+    for (int blocks : {256, 1024}) {
+        for (int th : {512}) {
             snprintf(nm, sizeof nm, "frames d4 grid=%d x %d", blocks, th);
             timeit(nm, [&] { hipLaunchKernelGGL(rd_frames<4>, blocks, th, 0, 0, d + 256, S, N, o); });
             snprintf(nm, sizeof nm, "frames d9 grid=%d x %d", blocks, th);

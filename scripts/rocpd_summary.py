@@ -25,3 +25,10 @@ def main():
 
 if __name__ == "__main__":
     main()
+
+
+def per_kernel_sequence(path, name_sub):
+    """Durations (us) of every dispatch whose name contains name_sub, in order."""
+    db = sqlite3.connect(path)
+    return [d / 1e3 for (n, d) in db.execute("select name, duration from kernels order by start")
+            if name_sub in n]
