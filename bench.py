@@ -67,25 +67,30 @@ def make_batch(cx: Codec, n: int, pl: int, rank: int, dev: torch.device, stream:
 
 
 def cpu_baseline(n_sample: int, seconds: float):
-    """The oracle's restatement of the same decode on host cores (bounded sample)."""
+    """The oracle's restatement of the same decode on host cores (bounded sample).
+
+    The sample is a full C2-shaped record (not cache-resident: 1.05 GiB), each
+    thread walking and verifying the whole record serially (the reference's
+    execution model: one shard thread per batch); T threads decode independent
+    walks of it concurrently."""
     from oracle import oracle as O  # cpu_baseline leg: the only bench use of oracle/
 
     rec = O.synth_batch(n_sample, PAYLOAD, PAYLOAD)
     nbytes = rec.size
 
     def rate(threads):
-        reps = 1
-        while True:
+        reps, total_secs, total_reps = 1, 0.0, 0
+        while total_secs < seconds:
             secs, cs = O.cpu_decode_bench(rec, threads, reps)
             if cs == 0:
                 raise RuntimeError("cpu baseline decode failed")
-            if secs >= seconds or reps >= 1 << 16:
-                return threads * reps * nbytes / secs / 2**30, secs
-            reps = max(reps * 2, int(reps * seconds / max(secs, 1e-3)) + 1)
+            total_secs += secs
+            total_reps += reps
+        return threads * total_reps * nbytes / total_secs / 2**30
 
     threads = min(16, os.cpu_count() or 1)
-    r1, _ = rate(1)
-    rt, _ = rate(threads)
+    r1 = rate(1)
+    rt = rate(threads)
     model = ""
     try:
         with open("/proc/cpuinfo") as f:
@@ -95,13 +100,44 @@ def cpu_baseline(n_sample: int, seconds: float):
                     break
     except OSError:
         pass
+    del rec
     return {
         "value": round(rt, 3), "unit": "GiB/s", "cores": threads, "kind": "port",
-        "sample": f"{n_sample} msgs x {PAYLOAD} B payload ({nbytes} B record) decoded Verify, "
-                  f"repeated ~{seconds:.0f} s per thread-count; AVX2 XXH3 when available",
+        "sample": f"{n_sample} msgs x {PAYLOAD} B payload ({nbytes} B record, not cache-resident), "
+                  f"decode_batch_slice_with(Verify) walked serially per thread, >= {seconds:.0f} s per "
+                  f"thread count; oracle C restatement with AVX2 XXH3, -O3 -march=native",
         "single_thread_gib_s": round(r1, 3), "cpu_model": model,
         "avx2": bool(O.lib().oracle_has_avx2()),
     }
+
+
+def pmc_traffic(n: int):
+    """HBM bytes per decode from the committed rocprofv3 PMC summary (FETCH_SIZE of the
+    producer kernel, x2 per MI355X_MICROARCH.md for gfx950) when it matches this config."""
+    path = os.path.join(ROOT, "profiles", "pmc_fetch.json")
+    try:
+        with open(path) as f:
+            d = json.load(f)
+    except (OSError, ValueError):
+        return None, None
+    if d.get("messages") != n or d.get("payload") != PAYLOAD:
+        return None, None
+    return d.get("hbm_bytes_per_decode"), d.get("source")
+
+
+def max_over_ranks(x: float, dist, device) -> float:
+    """The bench's only cross-rank traffic: max of a per-rank scalar (RCCL on GPUs,
+    gloo in the CPU tests). No data-path collective exists: partitions are independent."""
+    if dist is None:
+        return x
+    t = torch.tensor([x], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def whole_job_gib_s(world: int, batch_bytes: int, steps: int, elapsed: float) -> float:
+    """Aggregate throughput: every rank decodes `steps` batches of `batch_bytes` (weak scaling)."""
+    return world * batch_bytes * steps / elapsed / 2**30
 
 
 def main():
@@ -111,7 +147,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--messages", type=int, default=N_MSG)
     ap.add_argument("--no-cpu", action="store_true", help="skip the cpu_baseline leg")
-    ap.add_argument("--cpu-seconds", type=float, default=5.0)
+    ap.add_argument("--cpu-seconds", type=float, default=4.0)
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -162,12 +198,11 @@ def main():
     elapsed = time.perf_counter() - t0
     if dist:
         dist.barrier()
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed = max_over_ranks(elapsed, dist, dev)
 
-    # dominant kernel: k_decode_uniform (frame walk + XXH3 + in-kernel batch-checksum
-    # chain), bracketed by HIP events on the launch stream inside the library
+    # the decode's device phase: the lane-group producer kernel on the launch stream
+    # plus the chain/consumer WG forked onto the context's side stream and joined
+    # back, bracketed by HIP events on the launch stream inside the library
     cx.profile_enable(True)
     for _ in range(args.steps):
         step()
@@ -180,10 +215,11 @@ def main():
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
-        cpu = cpu_baseline(65536, args.cpu_seconds)
+        cpu = cpu_baseline(N_MSG, args.cpu_seconds)
 
+    traffic, traffic_src = pmc_traffic(n)
     ms_per_step = elapsed / args.steps * 1e3
-    value = world * L * args.steps / elapsed / 2**30
+    value = whole_job_gib_s(world, L, args.steps, elapsed)
     if rank == 0:
         line = {
             "metric": METRIC,
@@ -213,8 +249,9 @@ def main():
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
-                "traffic": None,
-                "kernel": "k_decode_uniform<true>",
+                "traffic": traffic,
+                "traffic_source": traffic_src,
+                "kernel": "k_uniform_lg + k_uniform_consumer (fork/join on the launch stream)",
                 "kernel_ms": round(k_ms, 4),
                 "algorithmic_bytes": alg_bytes,
             },

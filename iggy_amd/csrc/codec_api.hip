@@ -65,8 +65,6 @@ struct DevBuf {
 struct iggy_codec_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
-    hipStream_t side = nullptr;  // the uniform decode's consumer WG runs here, beside the producers
-    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     int ncu = 256;
     uint32_t epoch = 0;
     int allow_unaligned = 0;
@@ -116,7 +114,7 @@ int ensure_decode_scratch(iggy_codec_ctx *c, uint64_t len) {
     }
     // 16 epoch-tagged halves per unit (64 frames), 4 units per chunk; zeroed so
     // no stale tag can match a live epoch
-    r |= c->dsums.ensure(max_chunks * 4 * 16 * 8);
+    r |= c->dsums.ensure(max_chunks * kUnitSumRows * 8 + 64);
     if (!r && c->dsums.p) HIP_OK(hipMemset(c->dsums.p, 0, c->dsums.cap));
     r |= c->derr.ensure(max_chunks * 4 * 16);
     r |= c->gtiles_s.ensure(ntiles * 8);
@@ -140,7 +138,7 @@ DecodeScratch dscratch(iggy_codec_ctx *c) {
     s.sums = c->dsums.as<uint64_t>();
     s.errslot = c->derr.as<uint64_t>();
     s.small = c->dsync.as<uint8_t>(kSyncSmall);
-    s.max_chunks = c->dsums.cap / (4 * 16 * 8);
+    s.max_chunks = (c->dsums.cap - 64) / (kUnitSumRows * 8);
     return s;
 }
 
@@ -195,31 +193,19 @@ int enqueue_decode(iggy_codec_ctx *c, const uint8_t *d_body, uint64_t len, int i
     const bool verify = integrity == IGGY_INTEGRITY_VERIFY;
     DecodeScratch ds = dscratch(c);
     GeneralScratch gs = gscratch(c);
-    // one CU stays free for the consumer WG (its chain overlaps the producers)
-    const uint32_t grid = (uint32_t)std::max(1, c->ncu - 1);
+    // persistent grids: one WG per CU, block 0 the consumer (chain) WG
+    const uint32_t grid = (uint32_t)std::max(2, c->ncu);
     const uint32_t au = (uint32_t)c->allow_unaligned;
     prof_begin(c, 0, s);
-    HIP_OK(hipEventRecord(c->ev_fork, s));
-    HIP_OK(hipStreamWaitEvent(c->side, c->ev_fork, 0));
-    if (verify)
-        hipLaunchKernelGGL(k_uniform_consumer<true>, dim3(1), dim3(kConsumerThreads), kConsumerLds, c->side, d_body, len,
-                           d_res, ds, c->epoch, au, grid * (kUniformThreads / 64), grid * 4, c->dbg);
-    else
-        hipLaunchKernelGGL(k_uniform_consumer<false>, dim3(1), dim3(kConsumerThreads), kConsumerLds, c->side, d_body, len,
-                           d_res, ds, c->epoch, au, grid * (kUniformThreads / 64), grid * 4, c->dbg);
-    HIP_OK(hipGetLastError());
     if (verify) {
         hipLaunchKernelGGL(k_uniform_lds<true>, dim3(grid), dim3(256), kLdsBytes, s, d_body, len, d_pos, cap,
-                           ds, c->epoch, au, c->dbg);
+                           d_res, ds, c->epoch, au, c->dbg);
         hipLaunchKernelGGL(k_uniform_lg, dim3(grid), dim3(kUniformThreads), kLgLds, s, d_body, len, d_pos,
-                           cap, ds, c->epoch, au, c->dbg);
+                           cap, d_res, ds, c->epoch, au, c->dbg);
     } else {
         hipLaunchKernelGGL(k_uniform_lds<false>, dim3(grid), dim3(256), kLdsBytes, s, d_body, len, d_pos, cap,
-                           ds, c->epoch, au, c->dbg);
+                           d_res, ds, c->epoch, au, c->dbg);
     }
-    HIP_OK(hipGetLastError());
-    HIP_OK(hipEventRecord(c->ev_join, c->side));
-    HIP_OK(hipStreamWaitEvent(s, c->ev_join, 0));
     prof_end(c, 0, s);
     HIP_OK(hipGetLastError());
     if (verify)
@@ -298,9 +284,7 @@ int iggy_codec_create(int device, iggy_codec_ctx **out) {
     c->ncu = prop.multiProcessorCount;
     if (const char *d = getenv("IGGY_CODEC_DBG")) c->dbg = (uint32_t)strtoul(d, nullptr, 0);
     if (hipSetDevice(device) != hipSuccess ||
-        hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
-        hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking) != hipSuccess) {
-        if (c->stream) (void)hipStreamDestroy(c->stream);
+        hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
         delete c;
         return IGGY_ERR_DEVICE;
     }
@@ -313,14 +297,7 @@ int iggy_codec_create(int device, iggy_codec_ctx **out) {
             hipFuncSetAttribute((const void *)k_uniform_lds<false>,
                                 hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBytes) != hipSuccess ||
             hipFuncSetAttribute((const void *)k_uniform_lg,
-                                hipFuncAttributeMaxDynamicSharedMemorySize, kLgLds) != hipSuccess ||
-            hipFuncSetAttribute((const void *)k_uniform_consumer<true>,
-                                hipFuncAttributeMaxDynamicSharedMemorySize, kConsumerLds) != hipSuccess ||
-            hipFuncSetAttribute((const void *)k_uniform_consumer<false>,
-                                hipFuncAttributeMaxDynamicSharedMemorySize, kConsumerLds) != hipSuccess)
-            r = IGGY_ERR_DEVICE;
-        if (hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming) != hipSuccess ||
-            hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming) != hipSuccess)
+                                hipFuncAttributeMaxDynamicSharedMemorySize, kLgLds) != hipSuccess)
             r = IGGY_ERR_DEVICE;
     }
     for (int w = 0; w < 2 && !r; ++w)
@@ -358,7 +335,6 @@ void iggy_codec_destroy(iggy_codec_ctx *c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
-    if (c->side) (void)hipStreamSynchronize(c->side);
     DevBuf *bufs[] = {&c->dsync, &c->dsums, &c->derr, &c->gtiles_s, &c->gtiles_x,
                       &c->gtiles_cnt, &c->gtiles_list, &c->gtiles_base, &c->gfpos, &c->gcs,
                       &c->gbsums, &c->dresult, &c->din, &c->dpos, &c->dout, &c->epl, &c->euh,
@@ -370,9 +346,6 @@ void iggy_codec_destroy(iggy_codec_ctx *c) {
         if (c->ev0[w]) (void)hipEventDestroy(c->ev0[w]);
         if (c->ev1[w]) (void)hipEventDestroy(c->ev1[w]);
     }
-    if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
-    if (c->ev_join) (void)hipEventDestroy(c->ev_join);
-    if (c->side) (void)hipStreamDestroy(c->side);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
 }

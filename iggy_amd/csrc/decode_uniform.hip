@@ -40,8 +40,8 @@ struct DecodeScratch {
     uint32_t *exited;     // producer waves that finished (reset by consumer)
     uint64_t *first_bad;  // ~index of first checksum mismatch (max-encoded), 0 = none
     uint64_t *spec_fail;  // ~index of first frame whose header breaks the stride
-    uint64_t *sums;       // [max_chunks*4][16] per-unit accumulator partial sums, 32-bit halves
-                          // tagged with the launch epoch: (half | epoch << 32)
+    uint64_t *sums;       // [kUnitSumRows][max_chunks] column-per-chunk, epoch-tagged 32-bit halves
+                          // (half | epoch << 32); see publish_unit_sums
     uint64_t *errslot;    // [max_chunks*4][2] (stored, computed) per wave
     uint8_t *small;       // >= 512 B: short batch-checksum inputs
     uint64_t max_chunks;
@@ -57,8 +57,7 @@ constexpr uint32_t kLdsBytes = kSideOff + 4 * 64 * kSideLane;  // 155648
 // filled by kGatherWaves gatherer waves, drained by the chain wave
 constexpr uint32_t kBatch = 64;
 constexpr uint32_t kRing = 8;
-constexpr uint32_t kGatherWaves = 7;
-constexpr uint32_t kConsumerThreads = 64 * (kGatherWaves + 1);
+constexpr uint32_t kGatherWaves = 3;  // consumer WG waves 1..3; wave 0 (the chain) has SIMD 0 alone
 constexpr uint32_t kCtlOff = kRing * kBatch * 16 * 8;  // 64 KiB
 struct ChainCtl {
     uint32_t ready[kRing];  // batch index + 1 staged in the slot
@@ -66,10 +65,9 @@ struct ChainCtl {
     uint32_t abort;         // a gatherer or the chain wave gave up (spin limit)
 };
 constexpr uint32_t kConsumerLds = kCtlOff + 64;
-// lane-group producers: kLgSlots x 10 KiB per wave (set where kLgSlots is); at
-// >= 96 KiB per WG the consumer WG (kConsumerLds) can never share a CU with one
-constexpr uint32_t kLgLds = 4 * 3 * 10 * 1024;
-static_assert(kLgLds + kConsumerLds > 160 * 1024, "consumer must not fit beside a producer WG");
+// lane-group producers: kLgSlots x 10 KiB per wave (set where kLgSlots is)
+constexpr uint32_t kLgLds = 4 * 4 * 10 * 1024;
+static_assert(kConsumerLds <= kLgLds && kConsumerLds <= kLdsBytes, "consumer WG runs inside both grids");
 static_assert(kCtlOff + sizeof(ChainCtl) <= kConsumerLds, "consumer LDS");
 static_assert(kLdsBytes <= 160 * 1024, "LDS budget");
 
@@ -172,6 +170,21 @@ __device__ __forceinline__ void glds16(const void *gsrc, uint32_t lds_addr, bool
         "s_mov_b32 m0, %0"
         : "=&s"(keep)
         : "v"(gsrc), "s"(__builtin_amdgcn_readfirstlane(lds_addr))
+        : "memory");
+}
+// gsrc + OFF -> lds_addr. The instruction offset is added to the LDS address too
+// (LDS_ADDR = M0 + inst_offset + 16 * lane), so M0 gets lds_addr - OFF.
+template <int OFF>
+__device__ __forceinline__ void glds16o(const void *gsrc, uint32_t lds_addr) {
+    uint32_t keep;
+    asm volatile(
+        "s_mov_b32 %0, m0\n\t"
+        "s_mov_b32 m0, %2\n\t"
+        "s_nop 0\n\t"
+        "global_load_lds_dwordx4 %1, off offset:%3\n\t"
+        "s_mov_b32 m0, %0"
+        : "=&s"(keep)
+        : "v"(gsrc), "s"(__builtin_amdgcn_readfirstlane(lds_addr - OFF)), "i"(OFF)
         : "memory");
 }
 __device__ __forceinline__ void wait_vm(uint32_t n) {
@@ -363,9 +376,18 @@ __device__ inline uint64_t short_hash(const uint8_t *slot, int lane, uint64_t L)
 // A unit = 64 consecutive frames [256c - 6 + 64w, +64) (chunk c, quarter w).
 // Its interior batch-checksum words m = 256c + 64w + t (t < 63) are
 // hi32(cs_{m-6}) | lo32(cs_{m-5}) << 32: reduce them to 8 accumulator partial
-// sums and publish them as 16 epoch-tagged 32-bit halves (no flag, no fence:
-// each 8-B store is single-copy atomic, the gatherer checks every tag).
+// sums and publish them as 16 epoch-tagged 32-bit halves, plus the two halves
+// of the unit's boundary words (lo32 of its first frame's checksum, hi32 of its
+// last), so the gatherer never reads the record. No flag, no fence: each 8-B
+// store is single-copy atomic and the gatherer checks every tag.
+// Layout: row (18w + t), column c, so a gatherer wave (lane = chunk) reads
+// every row with one coalesced 512-B load.
 // `stored` = stored checksum of frame 256c - 6 + 64w + lane.
+constexpr uint32_t kUnitRows = 18;
+constexpr uint32_t kUnitSumRows = 4 * kUnitRows;
+__device__ __forceinline__ uint64_t *unit_row(const DecodeScratch &sc, uint64_t c, uint32_t w, uint32_t t) {
+    return sc.sums + (uint64_t)(w * kUnitRows + t) * sc.max_chunks + c;
+}
 // cs_sec = secret word of checksum word m (stripe (m >> 3) & 15, lane m & 7)
 __device__ __forceinline__ uint64_t unit_cs_secret(uint64_t unit, int lane) {
     const uint32_t tid = (uint32_t)((unit & 3) * 64 + lane);
@@ -386,12 +408,21 @@ __device__ __forceinline__ void publish_unit_sums(const UPlan &pl, const DecodeS
     x += __shfl_xor(x, 16); y += __shfl_xor(y, 16);
     x += __shfl_xor(x, 32); y += __shfl_xor(y, 32);
     const uint64_t t8 = x + __shfl_xor(y, 1);  // lane t (< 8): partial acc[t]
+    const uint64_t tag = (uint64_t)epoch << 32;
+    const uint64_t c = unit >> 2;
+    const uint32_t w = (uint32_t)(unit & 3);
     if (lane < 8) {
-        const uint64_t tag = (uint64_t)epoch << 32;
-        uint64_t *dst = sc.sums + unit * 16 + 2 * lane;
-        __hip_atomic_store(dst, (t8 & 0xffffffffull) | tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(dst + 1, (t8 >> 32) | tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(unit_row(sc, c, w, 2 * lane), (t8 & 0xffffffffull) | tag, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(unit_row(sc, c, w, 2 * lane + 1), (t8 >> 32) | tag, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
     }
+    if (lane == 0)
+        __hip_atomic_store(unit_row(sc, c, w, 16), (stored & 0xffffffffull) | tag, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+    if (lane == 63)
+        __hip_atomic_store(unit_row(sc, c, w, 17), (stored >> 32) | tag, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // ------------------------------------------------------------- producer
@@ -562,8 +593,19 @@ __device__ __forceinline__ void lg_issue(const uint8_t *blob, const UPlan &pl, c
     const uint8_t *hb = fb + 8 + 1024ull * b + c.poff;
     const bool full = b < pl.nbF;
     const bool fin = b + 1 == nsteps;
+    if (full) {  // one base address, immediate offsets
+        glds16o<0>(hb, slot);
+        glds16o<128>(hb, slot + 1024u);
+        glds16o<256>(hb, slot + 2048u);
+        glds16o<384>(hb, slot + 3072u);
+        glds16o<512>(hb, slot + 4096u);
+        glds16o<640>(hb, slot + 5120u);
+        glds16o<768>(hb, slot + 6144u);
+        glds16o<896>(hb, slot + 7168u);
+    } else {
 #pragma unroll
-    for (int q = 0; q < 8; ++q) glds16((full || 2 * q + c.par < pl.ns) ? hb + 128 * q : fb, slot + 1024u * q);
+        for (int q = 0; q < 8; ++q) glds16((2 * q + c.par < pl.ns) ? hb + 128 * q : fb, slot + 1024u * q);
+    }
     glds16(fin ? fb + 8 + pl.L - 64 + 16 * c.m : fb, slot + 8u * 1024u);
     glds16(fb, slot + 9u * 1024u);
 }
@@ -661,8 +703,9 @@ __device__ __forceinline__ void lg_process(const UPlan &pl, const LgLane &c, con
     }
 }
 
-constexpr uint32_t kLgSlots = 3;  // per wave: 1 step being hashed + 2 in flight (30 KiB)
+constexpr uint32_t kLgSlots = 4;  // per wave: 1 step being hashed + 3 in flight (40 KiB)
 static_assert(4 * kLgSlots * kLgStepBytes == kLgLds, "LDS sizing");
+template <uint32_t SLOTS>
 __device__ __forceinline__ void produce_lg(const uint8_t *blob, const UPlan &pl, uint64_t *frame_pos, uint64_t cap,
                                            const DecodeScratch &sc, uint32_t epoch, uint32_t gw, uint32_t nw,
                                            uint32_t wave, int lane, uint8_t *smem) {
@@ -692,25 +735,25 @@ __device__ __forceinline__ void produce_lg(const uint8_t *blob, const UPlan &pl,
 
     LgState st;
     st.a0 = c.init0; st.a1 = c.init1; st.cs_mine = 0; st.sbad = false; st.unit_err = false; st.sink = 0;
-    // processing cursor (pu, pg, pb) and issue cursor (iu, ig, ib) up to kLgSlots-1 steps ahead
+    // processing cursor (pu, pg, pb) and issue cursor (iu, ig, ib) up to SLOTS-1 steps ahead
     uint64_t pu = gw, iu = gw;
     uint32_t pg = 0, pb = 0, ig = 0, ib = 0;
     auto advance = [&](uint64_t &u, uint32_t &g, uint32_t &b) {
         if (++b == nblk) { b = 0; if (++g == 8) { g = 0; u += nw; } }
     };
-    const uint32_t ring = wave * (kLgSlots * kLgStepBytes);
+    const uint32_t ring = wave * (SLOTS * kLgStepBytes);
     uint32_t iss = 0;  // steps issued
     auto issue_next = [&]() {
         if (iu >= units) return;
-        lg_issue(blob, pl, c, iu, ig, ib, nblk, ring + (iss % kLgSlots) * kLgStepBytes);
+        lg_issue(blob, pl, c, iu, ig, ib, nblk, ring + (iss % SLOTS) * kLgStepBytes);
         advance(iu, ig, ib);
         ++iss;
     };
-    for (uint32_t d = 0; d + 1 < kLgSlots; ++d) issue_next();
+    for (uint32_t d = 0; d + 1 < SLOTS; ++d) issue_next();
     for (uint32_t k = 0; pu < units; ++k) {
         wait_vm(10 * (iss - 1 - k));  // step k landed; the later steps stay in flight
         LgBuf B;
-        const uint32_t slot = ring + (k % kLgSlots) * kLgStepBytes;
+        const uint32_t slot = ring + (k % SLOTS) * kLgStepBytes;
         lg_read(smem, slot, lane, B);
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // slot read out before it is refilled
         issue_next();
@@ -750,61 +793,78 @@ __device__ __forceinline__ void gather(const uint8_t *blob, const UPlan &pl, con
         }
         const uint64_t c = bi * kBatch + lane;
         const bool live = c < need && c < pl.nchunks;
-        const uint64_t *src = sc.sums + c * 64;  // 4 units x 16 tagged halves
+        const bool has_next = live && c + 1 < pl.nchunks;
         auto tag_ok = [&](uint64_t v) { return (uint32_t)(v >> 32) == epoch; };
-        // cheap poll: the last half of each unit, then everything with a full tag check
-        while (!abort) {
-            bool ok = true;
-            if (live) {
-#pragma unroll
-                for (int w = 0; w < 4; ++w)
-                    ok &= tag_ok(__hip_atomic_load(src + 16 * w + 15, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-            }
-            if (__ballot(!ok) == 0) break;
-            __builtin_amdgcn_s_sleep(2);
-            if (give_up()) abort = true;
-        }
+        // one round trip when the producers are ahead: 73 coalesced loads (16 sum halves
+        // + 2 boundary halves per unit, and the next chunk's first boundary half), every
+        // tag checked; otherwise poll one tagged word per unit, then reload
         uint64_t B[16];
-        while (!abort) {
+        uint32_t first_lo[5], last_hi[4];
+        for (bool first = true; !abort; first = false) {
+            if (!first) {
+                while (!abort) {
+                    bool ok = true;
+                    if (live) {
+#pragma unroll
+                        for (int w = 0; w < 4; ++w)
+                            ok &= tag_ok(__hip_atomic_load(unit_row(sc, c, w, 17), __ATOMIC_RELAXED,
+                                                           __HIP_MEMORY_SCOPE_AGENT));
+                    }
+                    if (__ballot(!ok) == 0) break;
+                    __builtin_amdgcn_s_sleep(2);
+                    if (give_up()) abort = true;
+                }
+                if (abort) break;
+            }
             bool ok = true;
 #pragma unroll
             for (int t = 0; t < 16; ++t) B[t] = 0;
+#pragma unroll
+            for (int w = 0; w < 5; ++w) first_lo[w] = 0;
+#pragma unroll
+            for (int w = 0; w < 4; ++w) last_hi[w] = 0;
             if (live) {
 #pragma unroll
                 for (int w = 0; w < 4; ++w) {
 #pragma unroll
                     for (int t = 0; t < 8; ++t) {
-                        const uint64_t lo = __hip_atomic_load(src + 16 * w + 2 * t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                        const uint64_t hi = __hip_atomic_load(src + 16 * w + 2 * t + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        const uint64_t lo = __hip_atomic_load(unit_row(sc, c, w, 2 * t), __ATOMIC_RELAXED,
+                                                              __HIP_MEMORY_SCOPE_AGENT);
+                        const uint64_t hi = __hip_atomic_load(unit_row(sc, c, w, 2 * t + 1), __ATOMIC_RELAXED,
+                                                              __HIP_MEMORY_SCOPE_AGENT);
                         ok &= tag_ok(lo) & tag_ok(hi);
                         // units 0, 1 of chunk c -> block 2c; units 2, 3 -> block 2c+1
                         B[8 * (w >> 1) + t] += (lo & 0xffffffffull) | (hi << 32);
                     }
+                    const uint64_t f = __hip_atomic_load(unit_row(sc, c, w, 16), __ATOMIC_RELAXED,
+                                                         __HIP_MEMORY_SCOPE_AGENT);
+                    const uint64_t l = __hip_atomic_load(unit_row(sc, c, w, 17), __ATOMIC_RELAXED,
+                                                         __HIP_MEMORY_SCOPE_AGENT);
+                    ok &= tag_ok(f) & tag_ok(l);
+                    first_lo[w] = (uint32_t)f;
+                    last_hi[w] = (uint32_t)l;
                 }
             }
+            if (has_next) {
+                const uint64_t f = __hip_atomic_load(unit_row(sc, c + 1, 0, 16), __ATOMIC_RELAXED,
+                                                     __HIP_MEMORY_SCOPE_AGENT);
+                ok &= tag_ok(f);
+                first_lo[4] = (uint32_t)f;
+            }
             if (__ballot(!ok) == 0) break;
-            __builtin_amdgcn_s_sleep(1);
             if (give_up()) abort = true;
         }
         if (abort) {
             if (lane == 0) __hip_atomic_store(&ctl->abort, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             return;
         }
-        uint64_t CS[8];
 #pragma unroll
         for (int w = 0; w < 4; ++w) {
-            // wave-boundary word m = 256c + 64w + 63 = hi32(cs_{m-6}) | lo32(cs_{m-5}) << 32
-            const uint64_t m = 256 * c + 64 * w + 63;
-            const bool need_w = live && m >= 6 && m < pl.Mreg;
-            const uint64_t fi = m - 6;
-            CS[2 * w] = need_w ? ld64_any(blob + fi * pl.S) : 0;
-            CS[2 * w + 1] = need_w ? ld64_any(blob + (fi + 1) * pl.S) : 0;
-        }
-#pragma unroll
-        for (int w = 0; w < 4; ++w) {
+            // unit-boundary word m = 256c + 64w + 63 = hi32(cs of the unit's last frame)
+            //                                        | lo32(cs of the next unit's first frame) << 32
             const uint64_t m = 256 * c + 64 * w + 63;
             if (live && m >= 6 && m < pl.Mreg) {
-                const uint64_t v = (CS[2 * w] >> 32) | (CS[2 * w + 1] << 32);
+                const uint64_t v = (uint64_t)last_hi[w] | ((uint64_t)first_lo[w + 1] << 32);
                 // lane j = 7 of stripe (8w + 7) mod 16: acc[6] += v, acc[7] += mul
                 const int hb = w >> 1;
                 B[8 * hb + 6] += v;
@@ -1034,35 +1094,23 @@ __device__ __forceinline__ void consumer(const uint8_t *body, const HeaderInfo &
 }
 
 // ------------------------------------------------------------- kernels
-// Three launches per decode (codec_api.hip enqueue_decode): the consumer WG on
-// the context's side stream, then the LDS-staged producers and the lane-group
-// producers on the caller's stream. Exactly one producer kind runs (the other
-// exits at once after reading the header); the producer grids leave one CU for
-// the consumer, and no producer ever waits for the consumer.
+// Two launches per decode (codec_api.hip enqueue_decode), each a persistent grid
+// of one WG per CU whose block 0 is the consumer WG (chain wave + gatherers):
+//  * k_uniform_lds: LDS-staged producers (short frames, LayoutOnly), and the
+//    consumer for every plan that is not lane-group (incl. early results);
+//  * k_uniform_lg: lane-group producers for long frames under Verify.
+// Exactly one of them does work; the other exits after reading the header.
+// Producers never wait for the consumer, so a grid that is only partly resident
+// (or kernels serialised by a profiler) still completes.
 template <bool VERIFY>
 __device__ __forceinline__ bool uniform_uses_lg(const UPlan &pl, uint32_t dbg) {
-    return VERIFY && pl.long_frames && !(dbg & 32);  // dbg bit 32: force the LDS form (A/B only)
-}
-
-template <bool VERIFY>
-__global__ __launch_bounds__(kConsumerThreads, 1) void k_uniform_consumer(const uint8_t *__restrict__ body, uint64_t len,
-                                                             iggy_decode_result *result, DecodeScratch sc,
-                                                             uint32_t epoch, uint32_t allow_unaligned,
-                                                             uint32_t waves_lg, uint32_t waves_lds,
-                                                             uint32_t dbg) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    HeaderInfo hi;
-    parse_header(body, len, hi);
-    UPlan pl;
-    make_plan(hi, body + kHdr, len, VERIFY, sc.max_chunks, allow_unaligned != 0, pl);
-    const uint32_t nwaves = uniform_uses_lg<VERIFY>(pl, dbg) ? waves_lg : waves_lds;
-    consumer<VERIFY>(body, hi, pl, result, sc, epoch, nwaves, wave, smem, dbg);
+    return VERIFY && pl.state == 0 && pl.long_frames && !(dbg & 32);  // dbg bit 32: force the LDS form
 }
 
 template <bool VERIFY>
 __global__ __launch_bounds__(256, 1) void k_uniform_lds(const uint8_t *__restrict__ body, uint64_t len,
-                                                        uint64_t *frame_pos, uint64_t cap, DecodeScratch sc,
+                                                        uint64_t *frame_pos, uint64_t cap,
+                                                        iggy_decode_result *result, DecodeScratch sc,
                                                         uint32_t epoch, uint32_t allow_unaligned,
                                                         uint32_t dbg) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
@@ -1073,38 +1121,50 @@ __global__ __launch_bounds__(256, 1) void k_uniform_lds(const uint8_t *__restric
     UPlan pl;
     make_plan(hi, body + kHdr, len, VERIFY, sc.max_chunks, allow_unaligned != 0, pl);
     pl.nt = (dbg & 16) != 0;
-    if (pl.state != 0 || uniform_uses_lg<VERIFY>(pl, dbg)) return;
+    if (uniform_uses_lg<VERIFY>(pl, dbg)) return;
+    const uint32_t nprod = gridDim.x - 1;
+    if (blockIdx.x == 0) {
+        consumer<VERIFY>(body, hi, pl, result, sc, epoch, 4 * nprod, wave, smem, dbg);
+        return;
+    }
+    if (pl.state != 0) return;
     const uint8_t *blob = body + kHdr;
+    const uint32_t g = blockIdx.x - 1;
     if (VERIFY && pl.long_frames)
-        produce<8, 4, 3, VERIFY>(blob, pl, frame_pos, cap, sc, epoch, blockIdx.x, gridDim.x, wave, lane, smem, dbg);
+        produce<8, 4, 3, VERIFY>(blob, pl, frame_pos, cap, sc, epoch, g, nprod, wave, lane, smem, dbg);
     else
-        produce<16, 2, 1, VERIFY>(blob, pl, frame_pos, cap, sc, epoch, blockIdx.x, gridDim.x, wave, lane, smem, dbg);
+        produce<16, 2, 1, VERIFY>(blob, pl, frame_pos, cap, sc, epoch, g, nprod, wave, lane, smem, dbg);
 }
 
 __global__ __launch_bounds__(kUniformThreads, 1) void k_uniform_lg(const uint8_t *__restrict__ body, uint64_t len,
                                                                   uint64_t *frame_pos, uint64_t cap,
-                                                                  DecodeScratch sc, uint32_t epoch,
-                                                                  uint32_t allow_unaligned, uint32_t dbg) {
+                                                                  iggy_decode_result *result, DecodeScratch sc,
+                                                                  uint32_t epoch, uint32_t allow_unaligned,
+                                                                  uint32_t dbg) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     HeaderInfo hi;
     parse_header(body, len, hi);
     UPlan pl;
     make_plan(hi, body + kHdr, len, true, sc.max_chunks, allow_unaligned != 0, pl);
-    if (pl.state != 0 || !uniform_uses_lg<true>(pl, dbg)) return;
-    produce_lg(body + kHdr, pl, frame_pos, cap, sc, epoch, blockIdx.x * (kUniformThreads / 64) + wave,
-               gridDim.x * (kUniformThreads / 64), wave, threadIdx.x & 63, smem);
+    if (!uniform_uses_lg<true>(pl, dbg)) return;
+    const uint32_t nprod = gridDim.x - 1;
+    if (blockIdx.x == 0) {
+        consumer<true>(body, hi, pl, result, sc, epoch, (kUniformThreads / 64) * nprod, wave, smem, dbg);
+        return;
+    }
+    const uint32_t gw = (blockIdx.x - 1) * (kUniformThreads / 64) + wave, nw = nprod * (kUniformThreads / 64);
+    if (dbg & 256)  // A/B: 3-slot ring
+        produce_lg<3>(body + kHdr, pl, frame_pos, cap, sc, epoch, gw, nw, wave, threadIdx.x & 63, smem);
+    else
+        produce_lg<kLgSlots>(body + kHdr, pl, frame_pos, cap, sc, epoch, gw, nw, wave, threadIdx.x & 63, smem);
     if ((threadIdx.x & 63) == 0)
         __hip_atomic_fetch_add(sc.exited, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-template __global__ void k_uniform_consumer<true>(const uint8_t *__restrict__, uint64_t, iggy_decode_result *,
-                                                  DecodeScratch, uint32_t, uint32_t, uint32_t, uint32_t, uint32_t);
-template __global__ void k_uniform_consumer<false>(const uint8_t *__restrict__, uint64_t, iggy_decode_result *,
-                                                   DecodeScratch, uint32_t, uint32_t, uint32_t, uint32_t, uint32_t);
 template __global__ void k_uniform_lds<true>(const uint8_t *__restrict__, uint64_t, uint64_t *, uint64_t,
-                                             DecodeScratch, uint32_t, uint32_t, uint32_t);
+                                             iggy_decode_result *, DecodeScratch, uint32_t, uint32_t, uint32_t);
 template __global__ void k_uniform_lds<false>(const uint8_t *__restrict__, uint64_t, uint64_t *, uint64_t,
-                                              DecodeScratch, uint32_t, uint32_t, uint32_t);
+                                              iggy_decode_result *, DecodeScratch, uint32_t, uint32_t, uint32_t);
 
 }  // namespace iggy
