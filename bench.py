@@ -251,7 +251,7 @@ def main():
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": traffic,
                 "traffic_source": traffic_src,
-                "kernel": "k_uniform_lg + k_uniform_consumer (fork/join on the launch stream)",
+                "kernel": "k_decode_uniform<true> (one persistent grid: lane-group producers + chain WG)",
                 "kernel_ms": round(k_ms, 4),
                 "algorithmic_bytes": alg_bytes,
             },

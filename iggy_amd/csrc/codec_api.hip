@@ -193,19 +193,16 @@ int enqueue_decode(iggy_codec_ctx *c, const uint8_t *d_body, uint64_t len, int i
     const bool verify = integrity == IGGY_INTEGRITY_VERIFY;
     DecodeScratch ds = dscratch(c);
     GeneralScratch gs = gscratch(c);
-    // persistent grids: one WG per CU, block 0 the consumer (chain) WG
+    // one persistent grid: one WG per CU, block 0 the consumer (chain) WG
     const uint32_t grid = (uint32_t)std::max(2, c->ncu);
     const uint32_t au = (uint32_t)c->allow_unaligned;
     prof_begin(c, 0, s);
-    if (verify) {
-        hipLaunchKernelGGL(k_uniform_lds<true>, dim3(grid), dim3(256), kLdsBytes, s, d_body, len, d_pos, cap,
-                           d_res, ds, c->epoch, au, c->dbg);
-        hipLaunchKernelGGL(k_uniform_lg, dim3(grid), dim3(kUniformThreads), kLgLds, s, d_body, len, d_pos,
+    if (verify)
+        hipLaunchKernelGGL(k_decode_uniform<true>, dim3(grid), dim3(256), kUniformLds, s, d_body, len, d_pos,
                            cap, d_res, ds, c->epoch, au, c->dbg);
-    } else {
-        hipLaunchKernelGGL(k_uniform_lds<false>, dim3(grid), dim3(256), kLdsBytes, s, d_body, len, d_pos, cap,
-                           d_res, ds, c->epoch, au, c->dbg);
-    }
+    else
+        hipLaunchKernelGGL(k_decode_uniform<false>, dim3(grid), dim3(256), kUniformLds, s, d_body, len, d_pos,
+                           cap, d_res, ds, c->epoch, au, c->dbg);
     prof_end(c, 0, s);
     HIP_OK(hipGetLastError());
     if (verify)
@@ -292,12 +289,10 @@ int iggy_codec_create(int device, iggy_codec_ctx **out) {
     r |= c->dresult.ensure(4096);
     if (hipHostMalloc(&c->h_pinned, 4096, hipHostMallocDefault) != hipSuccess) r = IGGY_ERR_DEVICE;
     if (!r) {
-        if (hipFuncSetAttribute((const void *)k_uniform_lds<true>,
-                                hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBytes) != hipSuccess ||
-            hipFuncSetAttribute((const void *)k_uniform_lds<false>,
-                                hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBytes) != hipSuccess ||
-            hipFuncSetAttribute((const void *)k_uniform_lg,
-                                hipFuncAttributeMaxDynamicSharedMemorySize, kLgLds) != hipSuccess)
+        if (hipFuncSetAttribute((const void *)k_decode_uniform<true>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, kUniformLds) != hipSuccess ||
+            hipFuncSetAttribute((const void *)k_decode_uniform<false>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, kUniformLds) != hipSuccess)
             r = IGGY_ERR_DEVICE;
     }
     for (int w = 0; w < 2 && !r; ++w)

@@ -48,7 +48,6 @@ struct DecodeScratch {
 };
 
 // ---- LDS map of a producer WG (dynamic LDS only, base offset 0) ----------
-constexpr uint32_t kUniformThreads = 256;                      // lane-group producers: 4 waves per WG
 constexpr uint32_t kWaveRing = 32768;                          // per wave: 4 x 8 KiB or 2 x 16 KiB
 constexpr uint32_t kSideOff = 4 * kWaveRing;                   // 131072
 constexpr uint32_t kSideLane = 96;                             // 6 chunks per lane
@@ -67,7 +66,8 @@ struct ChainCtl {
 constexpr uint32_t kConsumerLds = kCtlOff + 64;
 // lane-group producers: kLgSlots x 10 KiB per wave (set where kLgSlots is)
 constexpr uint32_t kLgLds = 4 * 4 * 10 * 1024;
-static_assert(kConsumerLds <= kLgLds && kConsumerLds <= kLdsBytes, "consumer WG runs inside both grids");
+constexpr uint32_t kUniformLds = kLgLds > kLdsBytes ? kLgLds : kLdsBytes;  // the grid's dynamic LDS
+static_assert(kConsumerLds <= kLgLds && kConsumerLds <= kLdsBytes, "consumer WG fits the grid's LDS");
 static_assert(kCtlOff + sizeof(ChainCtl) <= kConsumerLds, "consumer LDS");
 static_assert(kLdsBytes <= 160 * 1024, "LDS budget");
 
@@ -148,44 +148,38 @@ __device__ inline void make_plan(const HeaderInfo &hi, const uint8_t *blob, uint
 }
 
 // ------------------------------------------------------------ primitives
+// M0 carries the LDS destination; it is declared clobbered (the compiler
+// re-materialises M0 itself wherever it needs it) instead of saved/restored.
 __device__ __forceinline__ void glds16(const void *gsrc, uint32_t lds_addr, bool nt = false) {
-    uint32_t keep;
     if (nt) {
         asm volatile(
-            "s_mov_b32 %0, m0\n\t"
-            "s_mov_b32 m0, %2\n\t"
+            "s_mov_b32 m0, %1\n\t"
             "s_nop 0\n\t"
-            "global_load_lds_dwordx4 %1, off nt\n\t"
-            "s_mov_b32 m0, %0"
-            : "=&s"(keep)
+            "global_load_lds_dwordx4 %0, off nt"
+            :
             : "v"(gsrc), "s"(__builtin_amdgcn_readfirstlane(lds_addr))
-            : "memory");
+            : "memory", "m0");
         return;
     }
     asm volatile(
-        "s_mov_b32 %0, m0\n\t"
-        "s_mov_b32 m0, %2\n\t"
+        "s_mov_b32 m0, %1\n\t"
         "s_nop 0\n\t"
-        "global_load_lds_dwordx4 %1, off\n\t"
-        "s_mov_b32 m0, %0"
-        : "=&s"(keep)
+        "global_load_lds_dwordx4 %0, off"
+        :
         : "v"(gsrc), "s"(__builtin_amdgcn_readfirstlane(lds_addr))
-        : "memory");
+        : "memory", "m0");
 }
 // gsrc + OFF -> lds_addr. The instruction offset is added to the LDS address too
 // (LDS_ADDR = M0 + inst_offset + 16 * lane), so M0 gets lds_addr - OFF.
 template <int OFF>
 __device__ __forceinline__ void glds16o(const void *gsrc, uint32_t lds_addr) {
-    uint32_t keep;
     asm volatile(
-        "s_mov_b32 %0, m0\n\t"
-        "s_mov_b32 m0, %2\n\t"
+        "s_mov_b32 m0, %1\n\t"
         "s_nop 0\n\t"
-        "global_load_lds_dwordx4 %1, off offset:%3\n\t"
-        "s_mov_b32 m0, %0"
-        : "=&s"(keep)
+        "global_load_lds_dwordx4 %0, off offset:%2"
+        :
         : "v"(gsrc), "s"(__builtin_amdgcn_readfirstlane(lds_addr - OFF)), "i"(OFF)
-        : "memory");
+        : "memory", "m0");
 }
 __device__ __forceinline__ void wait_vm(uint32_t n) {
     // n = glds instructions allowed to stay in flight (multiples of 8)
@@ -634,6 +628,12 @@ __device__ __forceinline__ void lg_process(const UPlan &pl, const LgLane &c, con
                                            uint32_t epoch, uint64_t *frame_pos, uint64_t cap, uint64_t u,
                                            uint32_t g, uint32_t b, uint32_t nsteps, const LgBuf &B, LgState &st,
                                            int lane) {
+    if (pl.nt) {  // diagnostics (dbg bit 64): staging only, no hashing
+#pragma unroll
+        for (int q = 0; q < 8; ++q) st.sink += B.v[q].x ^ B.v[q].w;
+        st.sink += B.last.y ^ (uint32_t)B.stored;
+        return;
+    }
     if (b == 0) {
         if (g == 0) st.unit_err = false;
         st.a0 = c.init0;
@@ -647,8 +647,13 @@ __device__ __forceinline__ void lg_process(const UPlan &pl, const LgLane &c, con
                             (c.l == 4 && (h0.x | h0.y) != 0));
     }
     if (b < pl.nbF) {  // a full block: accumulate, fold the pair, scramble
+        // four independent partial sums per accumulator: the 16 mads overlap instead
+        // of forming two dependent chains of 8 (sums commute inside a block)
+        uint64_t p0[4] = {0, 0, 0, 0}, p1[4] = {0, 0, 0, 0};
 #pragma unroll
-        for (int q = 0; q < 8; ++q) lg_piece(st.a0, st.a1, B.v[q], c.s0[q], c.s1[q]);
+        for (int q = 0; q < 8; ++q) lg_piece(p0[q & 3], p1[q & 3], B.v[q], c.s0[q], c.s1[q]);
+        st.a0 += (p0[0] + p0[1]) + (p0[2] + p0[3]);
+        st.a1 += (p1[0] + p1[1]) + (p1[2] + p1[3]);
         st.a0 += dpp64<kDppXor1>(st.a0);
         st.a1 += dpp64<kDppXor1>(st.a1);
         st.a0 = scramble1(st.a0, c.key0);
@@ -703,6 +708,29 @@ __device__ __forceinline__ void lg_process(const UPlan &pl, const LgLane &c, con
     }
 }
 
+template <bool PIN>
+__device__ __forceinline__ void lg_lane_init(LgLane &c, int lane) {
+    c.l = lane & 7; c.m = c.l >> 1; c.par = c.l & 1; c.fg = (uint32_t)lane >> 3;
+    c.poff = 16 * (c.m + 4 * c.par);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+        c.s0[q] = kSecretW8[2 * q + c.par + 2 * c.m];
+        c.s1[q] = kSecretW8[2 * q + c.par + 2 * c.m + 1];
+    }
+    c.key0 = kSecretW8[16 + 2 * c.m]; c.key1 = kSecretW8[17 + 2 * c.m];
+    c.init0 = c.par ? 0 : kAccInit[2 * c.m]; c.init1 = c.par ? 0 : kAccInit[2 * c.m + 1];
+    c.last0 = kSecretLast[2 * c.m]; c.last1 = kSecretLast[2 * c.m + 1];
+    c.mrg0 = kSecretMerge[2 * c.m]; c.mrg1 = kSecretMerge[2 * c.m + 1];
+    c.css0 = unit_cs_secret(0, lane); c.css1 = unit_cs_secret(1, lane);
+    if (PIN) {
+#pragma unroll
+        for (int q = 0; q < 8; ++q) { pin_after_wait(c.s0[q]); pin_after_wait(c.s1[q]); }
+        pin_after_wait(c.key0); pin_after_wait(c.key1); pin_after_wait(c.init0); pin_after_wait(c.init1);
+        pin_after_wait(c.last0); pin_after_wait(c.last1); pin_after_wait(c.mrg0); pin_after_wait(c.mrg1);
+        pin_after_wait(c.css0); pin_after_wait(c.css1);
+    }
+}
+
 constexpr uint32_t kLgSlots = 4;  // per wave: 1 step being hashed + 3 in flight (40 KiB)
 static_assert(4 * kLgSlots * kLgStepBytes == kLgLds, "LDS sizing");
 template <uint32_t SLOTS>
@@ -749,14 +777,16 @@ __device__ __forceinline__ void produce_lg(const uint8_t *blob, const UPlan &pl,
         advance(iu, ig, ib);
         ++iss;
     };
-    for (uint32_t d = 0; d + 1 < SLOTS; ++d) issue_next();
+    // every slot holds a step in flight; a slot is refilled as soon as its step has
+    // been read into registers, so SLOTS steps stay in flight while one is hashed
+    for (uint32_t d = 0; d < SLOTS; ++d) issue_next();
     for (uint32_t k = 0; pu < units; ++k) {
         wait_vm(10 * (iss - 1 - k));  // step k landed; the later steps stay in flight
         LgBuf B;
         const uint32_t slot = ring + (k % SLOTS) * kLgStepBytes;
         lg_read(smem, slot, lane, B);
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // slot read out before it is refilled
-        issue_next();
+        issue_next();  // step k + SLOTS into the slot just read
         lg_process(pl, c, sc, epoch, frame_pos, cap, pu, pg, pb, nblk, B, st, lane);
         advance(pu, pg, pb);
     }
@@ -1093,26 +1123,23 @@ __device__ __forceinline__ void consumer(const uint8_t *body, const HeaderInfo &
     __hip_atomic_store(sc.spec_fail, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// ------------------------------------------------------------- kernels
-// Two launches per decode (codec_api.hip enqueue_decode), each a persistent grid
-// of one WG per CU whose block 0 is the consumer WG (chain wave + gatherers):
-//  * k_uniform_lds: LDS-staged producers (short frames, LayoutOnly), and the
-//    consumer for every plan that is not lane-group (incl. early results);
-//  * k_uniform_lg: lane-group producers for long frames under Verify.
-// Exactly one of them does work; the other exits after reading the header.
-// Producers never wait for the consumer, so a grid that is only partly resident
-// (or kernels serialised by a profiler) still completes.
+// ------------------------------------------------------------- kernel
 template <bool VERIFY>
 __device__ __forceinline__ bool uniform_uses_lg(const UPlan &pl, uint32_t dbg) {
     return VERIFY && pl.state == 0 && pl.long_frames && !(dbg & 32);  // dbg bit 32: force the LDS form
 }
 
+// One persistent grid of one WG per CU (256 threads, up to 160 KiB LDS): block 0
+// is the consumer WG (chain wave + gatherers), blocks 1.. the producers, either
+// lane-group (long frames under Verify) or LDS-staged (short frames, LayoutOnly).
+// Producers never wait for the consumer, so a grid that is only partly resident
+// (or kernels serialised by a profiler) still completes.
 template <bool VERIFY>
-__global__ __launch_bounds__(256, 1) void k_uniform_lds(const uint8_t *__restrict__ body, uint64_t len,
-                                                        uint64_t *frame_pos, uint64_t cap,
-                                                        iggy_decode_result *result, DecodeScratch sc,
-                                                        uint32_t epoch, uint32_t allow_unaligned,
-                                                        uint32_t dbg) {
+__global__ __launch_bounds__(256, 1) void k_decode_uniform(const uint8_t *__restrict__ body, uint64_t len,
+                                                           uint64_t *frame_pos, uint64_t cap,
+                                                           iggy_decode_result *result, DecodeScratch sc,
+                                                           uint32_t epoch, uint32_t allow_unaligned,
+                                                           uint32_t dbg) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const int lane = threadIdx.x & 63;
     const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -1120,8 +1147,8 @@ __global__ __launch_bounds__(256, 1) void k_uniform_lds(const uint8_t *__restric
     parse_header(body, len, hi);
     UPlan pl;
     make_plan(hi, body + kHdr, len, VERIFY, sc.max_chunks, allow_unaligned != 0, pl);
-    pl.nt = (dbg & 16) != 0;
-    if (uniform_uses_lg<VERIFY>(pl, dbg)) return;
+    const bool lg = uniform_uses_lg<VERIFY>(pl, dbg);
+    pl.nt = (dbg & 64) != 0;
     const uint32_t nprod = gridDim.x - 1;
     if (blockIdx.x == 0) {
         consumer<VERIFY>(body, hi, pl, result, sc, epoch, 4 * nprod, wave, smem, dbg);
@@ -1130,41 +1157,21 @@ __global__ __launch_bounds__(256, 1) void k_uniform_lds(const uint8_t *__restric
     if (pl.state != 0) return;
     const uint8_t *blob = body + kHdr;
     const uint32_t g = blockIdx.x - 1;
+    if (VERIFY && lg) {
+        produce_lg<kLgSlots>(blob, pl, frame_pos, cap, sc, epoch, g * 4 + wave, nprod * 4, wave, lane, smem);
+        if (lane == 0) __hip_atomic_fetch_add(sc.exited, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        return;
+    }
+    pl.nt = (dbg & 16) != 0;
     if (VERIFY && pl.long_frames)
         produce<8, 4, 3, VERIFY>(blob, pl, frame_pos, cap, sc, epoch, g, nprod, wave, lane, smem, dbg);
     else
         produce<16, 2, 1, VERIFY>(blob, pl, frame_pos, cap, sc, epoch, g, nprod, wave, lane, smem, dbg);
 }
 
-__global__ __launch_bounds__(kUniformThreads, 1) void k_uniform_lg(const uint8_t *__restrict__ body, uint64_t len,
-                                                                  uint64_t *frame_pos, uint64_t cap,
-                                                                  iggy_decode_result *result, DecodeScratch sc,
-                                                                  uint32_t epoch, uint32_t allow_unaligned,
-                                                                  uint32_t dbg) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    HeaderInfo hi;
-    parse_header(body, len, hi);
-    UPlan pl;
-    make_plan(hi, body + kHdr, len, true, sc.max_chunks, allow_unaligned != 0, pl);
-    if (!uniform_uses_lg<true>(pl, dbg)) return;
-    const uint32_t nprod = gridDim.x - 1;
-    if (blockIdx.x == 0) {
-        consumer<true>(body, hi, pl, result, sc, epoch, (kUniformThreads / 64) * nprod, wave, smem, dbg);
-        return;
-    }
-    const uint32_t gw = (blockIdx.x - 1) * (kUniformThreads / 64) + wave, nw = nprod * (kUniformThreads / 64);
-    if (dbg & 256)  // A/B: 3-slot ring
-        produce_lg<3>(body + kHdr, pl, frame_pos, cap, sc, epoch, gw, nw, wave, threadIdx.x & 63, smem);
-    else
-        produce_lg<kLgSlots>(body + kHdr, pl, frame_pos, cap, sc, epoch, gw, nw, wave, threadIdx.x & 63, smem);
-    if ((threadIdx.x & 63) == 0)
-        __hip_atomic_fetch_add(sc.exited, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-template __global__ void k_uniform_lds<true>(const uint8_t *__restrict__, uint64_t, uint64_t *, uint64_t,
-                                             iggy_decode_result *, DecodeScratch, uint32_t, uint32_t, uint32_t);
-template __global__ void k_uniform_lds<false>(const uint8_t *__restrict__, uint64_t, uint64_t *, uint64_t,
-                                              iggy_decode_result *, DecodeScratch, uint32_t, uint32_t, uint32_t);
+template __global__ void k_decode_uniform<true>(const uint8_t *__restrict__, uint64_t, uint64_t *, uint64_t,
+                                                iggy_decode_result *, DecodeScratch, uint32_t, uint32_t, uint32_t);
+template __global__ void k_decode_uniform<false>(const uint8_t *__restrict__, uint64_t, uint64_t *, uint64_t,
+                                                 iggy_decode_result *, DecodeScratch, uint32_t, uint32_t, uint32_t);
 
 }  // namespace iggy

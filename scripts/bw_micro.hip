@@ -51,6 +51,74 @@ __global__ void rd_frames(const uint8_t *__restrict__ blob, uint64_t S, uint64_t
     if (x == 0x12345678) out[0] = x;
 }
 
+
+// ---- LDS-DMA staging variants (no compute): 4 waves per WG, SLOTS x 10 x 1 KiB ring per wave
+__device__ __forceinline__ void glds(const void *g, uint32_t lds) {
+    asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off"
+                 :: "v"(g), "s"(__builtin_amdgcn_readfirstlane(lds)) : "memory", "m0");
+}
+__device__ __forceinline__ void wvm(int n) {
+    if (n >= 30) asm volatile("s_waitcnt vmcnt(30)" ::: "memory");
+    else if (n >= 20) asm volatile("s_waitcnt vmcnt(20)" ::: "memory");
+    else if (n >= 10) asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+// MODE 0: segment pattern (lane group = frame, 8 frames x 128 B per instruction), 8 seg + 2 extra loads/step
+// MODE 1: per-frame contiguous blocks (instruction k = frame k's 1 KiB), 8 + 1 loads/step
+// UNIT: frames per wave-unit before jumping (64 or 8)
+template <int MODE, int UNIT, int SLOTS>
+__global__ __launch_bounds__(256, 1) void lds_frames(const uint8_t *__restrict__ blob, uint64_t S, uint64_t N, uint64_t *out) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const int lane = threadIdx.x & 63;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint64_t gw = (uint64_t)blockIdx.x * 4 + wave, nw = (uint64_t)gridDim.x * 4;
+    const uint32_t ring = wave * SLOTS * 10240;
+    const int l = lane & 7, fg = lane >> 3, m = l >> 1, par = l & 1;
+    const uint32_t poff = 16 * (m + 4 * par);
+    uint64_t issued = 0, done = 0;
+    const uint64_t nsteps_total = (N + 7) / 8;  // groups
+    // group sequence for this wave
+    auto group_of = [&](uint64_t k) -> uint64_t {  // k-th group of this wave
+        const uint64_t per = UNIT / 8;
+        return (k / per) * nw * per + gw * per + (k % per);
+    };
+    auto issue = [&](uint64_t k) {
+        const uint64_t grp = group_of(k);
+        const uint32_t slot = ring + (uint32_t)(k % SLOTS) * 10240;
+        if (MODE == 0) {
+            const uint64_t f = grp * 8 + fg;
+            const uint8_t *fb = blob + (f < N ? f : 0) * S;
+            for (int q = 0; q < 8; ++q) glds(fb + 8 + 128 * q + poff, slot + 1024 * q);
+            glds(fb + 8 + 1000 + 16 * m, slot + 8192);
+            glds(fb, slot + 9216);
+        } else {
+            for (int k2 = 0; k2 < 8; ++k2) {
+                const uint64_t f = grp * 8 + k2;
+                const uint8_t *fb = blob + (f < N ? f : 0) * S;
+                glds(fb + 8 + 16 * lane, slot + 1040 * k2);
+            }
+            const uint64_t f = grp * 8 + fg;
+            const uint8_t *fb = blob + (f < N ? f : 0) * S;
+            glds(l < 4 ? fb + 8 + 1000 + 16 * l : fb, slot + 8320);
+        }
+    };
+    uint32_t x = 0;
+    uint64_t mine = 0;
+    while (group_of(mine) < nsteps_total) ++mine;
+    for (; issued < SLOTS && issued < mine; ++issued) issue(issued);
+    for (uint64_t k = 0; k < mine; ++k) {
+        const int ahead = (int)(issued - 1 - k);
+        wvm((MODE == 0 ? 10 : 9) * ahead >= 30 ? 30 : (MODE == 0 ? 10 : 9) * ahead >= 20 ? 20 : (MODE == 0 ? 10 : 9) * ahead >= 10 ? 10 : 0);
+        const uint8_t *p = smem + ring + (k % SLOTS) * 10240 + 16 * lane;
+        uint4 v = *(const uint4 *)p;
+        x ^= v.x ^ v.w;
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if (issued < mine) { issue(issued); ++issued; }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (x == 0x12345678) out[0] = x;
+}
+
 int main() {
     const uint64_t N = 1 << 20, S = 1072, L = 256 + N * S;
     uint8_t *d;
@@ -75,6 +143,16 @@ int main() {
         printf("%-40s %8.4f ms  %7.1f GB/s\n", name, ms, L / (ms * 1e-3) / 1e9);
     };
     char nm[128];
+    hipFuncSetAttribute((const void *)lds_frames<0, 64, 4>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
+    hipFuncSetAttribute((const void *)lds_frames<0, 8, 4>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
+    hipFuncSetAttribute((const void *)lds_frames<1, 64, 4>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
+    hipFuncSetAttribute((const void *)lds_frames<1, 8, 4>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
+    hipFuncSetAttribute((const void *)lds_frames<0, 64, 3>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
+    timeit("ldsdma seg unit64 4slot", [&] { hipLaunchKernelGGL((lds_frames<0, 64, 4>), 255, 256, 163840, 0, d + 256, S, N, o); });
+    timeit("ldsdma seg unit8 4slot", [&] { hipLaunchKernelGGL((lds_frames<0, 8, 4>), 255, 256, 163840, 0, d + 256, S, N, o); });
+    timeit("ldsdma contig unit64 4slot", [&] { hipLaunchKernelGGL((lds_frames<1, 64, 4>), 255, 256, 163840, 0, d + 256, S, N, o); });
+    timeit("ldsdma contig unit8 4slot", [&] { hipLaunchKernelGGL((lds_frames<1, 8, 4>), 255, 256, 163840, 0, d + 256, S, N, o); });
+    timeit("ldsdma seg unit64 3slot", [&] { hipLaunchKernelGGL((lds_frames<0, 64, 3>), 255, 256, 163840, 0, d + 256, S, N, o); });
     for (int blocks : {255}) {
         timeit("frames d9 unit64 grid=255 x 512", [&] { hipLaunchKernelGGL((rd_frames<9, 64>), 255, 512, 0, 0, d + 256, S, N, o); });
         timeit("frames d9 unit8 grid=255 x 512", [&] { hipLaunchKernelGGL((rd_frames<9, 8>), 255, 512, 0, 0, d + 256, S, N, o); });

@@ -22,7 +22,7 @@ def main():
     pl = int(sys.argv[2]) if len(sys.argv) > 2 else 1024
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(0)
-    variants = [0, 1, 256, 257]
+    variants = [0, 1, 65, 32]
     ctxs = {}
     for v in variants:
         os.environ["IGGY_CODEC_DBG"] = str(v)
