@@ -120,7 +120,7 @@ def pmc_traffic(n: int):
             d = json.load(f)
     except (OSError, ValueError):
         return None, None
-    if d.get("messages") != n or d.get("payload") != PAYLOAD:
+    if d.get("messages") != n or d.get("payload") != PAYLOAD or "k_decode_uniform" not in d.get("kernel", ""):
         return None, None
     return d.get("hbm_bytes_per_decode"), d.get("source")
 

@@ -25,11 +25,11 @@ def main():
     per_kernel = {}
     for name, kb, _ in rows:
         per_kernel.setdefault(name.split("(")[0], []).append(kb)
-    target = [k for k in per_kernel if "k_uniform_lg" in k]
+    target = [k for k in per_kernel if "k_decode_uniform" in k]
     if not target:
-        raise SystemExit(f"no k_uniform_lg dispatches in {db_path}: {sorted(per_kernel)}")
-    # decodes timed by bench.py: every k_uniform_lg dispatch with real work (the
-    # encode-side and torch kernels are separate names)
+        raise SystemExit(f"no k_decode_uniform dispatches in {db_path}: {sorted(per_kernel)}")
+    # decodes timed by bench.py: every k_decode_uniform dispatch (the encode-side
+    # and torch kernels are separate names)
     vals = per_kernel[target[0]]
     kb = statistics.median(vals)
     hbm_bytes = kb * 1024 * 2  # gfx950 correction: FETCH_SIZE = half of the streamed bytes
