@@ -197,6 +197,9 @@ int enqueue_decode(iggy_codec_ctx *c, const uint8_t *d_body, uint64_t len, int i
     const uint32_t grid = (uint32_t)std::max(2, c->ncu);
     const uint32_t au = (uint32_t)c->allow_unaligned;
     prof_begin(c, 0, s);
+    if (verify)  // lane-group grid first: it returns at once unless the record is its shape
+        hipLaunchKernelGGL(k_decode_lg, dim3(grid), dim3(256), kLgLds, s, d_body, len, d_pos, cap, d_res, ds,
+                           c->epoch, au, c->dbg);
     if (verify)
         hipLaunchKernelGGL(k_decode_uniform<true>, dim3(grid), dim3(256), kUniformLds, s, d_body, len, d_pos,
                            cap, d_res, ds, c->epoch, au, c->dbg);
@@ -289,7 +292,9 @@ int iggy_codec_create(int device, iggy_codec_ctx **out) {
     r |= c->dresult.ensure(4096);
     if (hipHostMalloc(&c->h_pinned, 4096, hipHostMallocDefault) != hipSuccess) r = IGGY_ERR_DEVICE;
     if (!r) {
-        if (hipFuncSetAttribute((const void *)k_decode_uniform<true>,
+        if (hipFuncSetAttribute((const void *)k_decode_lg, hipFuncAttributeMaxDynamicSharedMemorySize, kLgLds) !=
+                hipSuccess ||
+            hipFuncSetAttribute((const void *)k_decode_uniform<true>,
                                 hipFuncAttributeMaxDynamicSharedMemorySize, kUniformLds) != hipSuccess ||
             hipFuncSetAttribute((const void *)k_decode_uniform<false>,
                                 hipFuncAttributeMaxDynamicSharedMemorySize, kUniformLds) != hipSuccess)

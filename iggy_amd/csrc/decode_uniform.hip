@@ -66,8 +66,8 @@ struct ChainCtl {
 constexpr uint32_t kConsumerLds = kCtlOff + 64;
 // lane-group producers: kLgSlots x 10 KiB per wave (set where kLgSlots is)
 constexpr uint32_t kLgLds = 4 * 4 * 10 * 1024;
-constexpr uint32_t kUniformLds = kLgLds > kLdsBytes ? kLgLds : kLdsBytes;  // the grid's dynamic LDS
-static_assert(kConsumerLds <= kLgLds && kConsumerLds <= kLdsBytes, "consumer WG fits the grid's LDS");
+constexpr uint32_t kUniformLds = kLdsBytes;  // dynamic LDS of the LDS-staged grid (kLgLds: lane-group grid)
+static_assert(kConsumerLds <= kLgLds && kConsumerLds <= kLdsBytes, "consumer WG fits either grid's LDS");
 static_assert(kCtlOff + sizeof(ChainCtl) <= kConsumerLds, "consumer LDS");
 static_assert(kLdsBytes <= 160 * 1024, "LDS budget");
 
@@ -81,6 +81,7 @@ struct UPlan {
     uint64_t ea, eb, ec;
     bool long_frames, long_cs;
     bool nt;           // diagnostics: non-temporal LDS-DMA loads
+    bool nopub;        // diagnostics (dbg bit 128): lane-group producers publish nothing
     bool tail_unsafe;  // last frame's last 16-B chunk would read past the caller's buffer
 };
 
@@ -89,6 +90,7 @@ __device__ inline void make_plan(const HeaderInfo &hi, const uint8_t *blob, uint
     p.state = 2;
     p.tail_unsafe = false;
     p.nt = false;
+    p.nopub = false;
     p.ekind = IGGY_OK; p.ereason = 0; p.ea = p.eb = p.ec = 0;
     p.S = p.N = p.L = p.nchunks = 0;
     p.nck = p.nph = p.q_side0 = 0;
@@ -193,6 +195,12 @@ __device__ __forceinline__ void wait_vm(uint32_t n) {
         case 24: asm volatile("s_waitcnt vmcnt(24)" ::: "memory"); break;
         default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
     }
+}
+
+template <int N>
+__device__ __forceinline__ void wait_vm_const() {
+    static_assert(N >= 0 && N <= 63, "vmcnt range");
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
 __device__ __forceinline__ uint64_t funnel64(uint64_t lo, uint64_t hi, uint32_t t) {
@@ -387,13 +395,13 @@ __device__ __forceinline__ uint64_t unit_cs_secret(uint64_t unit, int lane) {
     const uint32_t tid = (uint32_t)((unit & 3) * 64 + lane);
     return kSecretW8[((tid >> 3) & 15) + (tid & 7)];
 }
-__device__ __forceinline__ void publish_unit_sums(const UPlan &pl, const DecodeScratch &sc, uint32_t epoch,
+__device__ __forceinline__ void publish_unit_sums(uint64_t Mreg, const DecodeScratch &sc, uint32_t epoch,
                                                   uint64_t unit, int lane, uint64_t stored, uint64_t cs_sec) {
     const uint32_t tid = (uint32_t)((unit & 3) * 64 + lane);
     const uint64_t next = __shfl_down(stored, 1);
     const uint64_t m = 256 * (unit >> 2) + tid;
     uint64_t x = 0, y = 0;  // x -> acc[j], y -> acc[j^1]
-    if (lane < 63 && m >= 6 && m < pl.Mreg) {
+    if (lane < 63 && m >= 6 && m < Mreg) {
         const uint64_t v = (stored >> 32) | (next << 32);
         y = v;
         x = mul32x32(v ^ cs_sec);
@@ -507,7 +515,7 @@ __device__ __forceinline__ void produce(const uint8_t *blob, const UPlan &pl, ui
             if (lane == leader) atomicMax((unsigned long long *)sc.spec_fail, (unsigned long long)~(uint64_t)i);
         }
         if (VERIFY && pl.long_cs)
-            publish_unit_sums(pl, sc, epoch, c * 4 + wave, lane, stored, unit_cs_secret(c * 4 + wave, lane));
+            publish_unit_sums(pl.Mreg, sc, epoch, c * 4 + wave, lane, stored, unit_cs_secret(c * 4 + wave, lane));
     }
     wait_vm(0);
     if (lane == 0) __hip_atomic_fetch_add(sc.exited, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -541,6 +549,19 @@ __device__ __forceinline__ uint64_t swz_xor4(uint64_t x) {  // ds_swizzle bit mo
     return (uint64_t)lo | ((uint64_t)hi << 32);
 }
 
+// The lane-group producer's whole view of the record (a small subset of UPlan,
+// so the producer loop of k_decode_lg carries no state of the other forms).
+struct LgPlan {
+    uint64_t S, N, L, nbF, ns, nchunks, Mreg;
+    bool long_cs, nt, nopub;
+};
+__device__ __forceinline__ LgPlan lg_plan(const UPlan &p) {
+    LgPlan q;
+    q.S = p.S; q.N = p.N; q.L = p.L; q.nbF = p.nbF; q.ns = p.ns; q.nchunks = p.nchunks; q.Mreg = p.Mreg;
+    q.long_cs = p.long_cs; q.nt = p.nt; q.nopub = p.nopub;
+    return q;
+}
+
 struct LgBuf {
     uint4 v[8];       // 8 segments x 16 B of one block (or the partial block)
     uint4 last;       // last stripe piece (final step only)
@@ -568,7 +589,7 @@ __device__ __forceinline__ int64_t lg_frame_index(uint64_t u, uint32_t g, uint32
 // uses of x cannot move above this point; forces x to be materialised here
 __device__ __forceinline__ void pin_after_wait(uint64_t &x) { asm volatile("" : "+v"(x)); }
 
-__device__ __forceinline__ uint32_t lg_nsteps(const UPlan &pl) {
+__device__ __forceinline__ uint32_t lg_nsteps(const LgPlan &pl) {
     const uint32_t n = (uint32_t)pl.nbF + (pl.ns > 0 ? 1u : 0u);
     return n ? n : 1u;
 }
@@ -579,14 +600,15 @@ __device__ __forceinline__ uint32_t lg_nsteps(const UPlan &pl) {
 // exactly its own 16 B. The loads bypass VGPRs: the wave waits for them with an
 // explicit vmcnt, and never blocks on the step it has just issued.
 constexpr uint32_t kLgStepBytes = 10 * 1024;
-__device__ __forceinline__ void lg_issue(const uint8_t *blob, const UPlan &pl, const LgLane &c, uint64_t u,
+template <bool ONE>
+__device__ __forceinline__ void lg_issue(const uint8_t *blob, const LgPlan &pl, const LgLane &c, uint64_t u,
                                          uint32_t g, uint32_t b, uint32_t nsteps, uint32_t slot) {
     const int64_t i = lg_frame_index(u, g, c.fg);
     const bool valid = i >= 0 && (uint64_t)i < pl.N;
     const uint8_t *fb = blob + (valid ? (uint64_t)i : 0) * pl.S;
     const uint8_t *hb = fb + 8 + 1024ull * b + c.poff;
-    const bool full = b < pl.nbF;
-    const bool fin = b + 1 == nsteps;
+    const bool full = ONE || b < pl.nbF;
+    const bool fin = ONE || b + 1 == nsteps;
     if (full) {  // one base address, immediate offsets
         glds16o<0>(hb, slot);
         glds16o<128>(hb, slot + 1024u);
@@ -624,7 +646,8 @@ struct LgState {
     bool sbad, unit_err;
 };
 
-__device__ __forceinline__ void lg_process(const UPlan &pl, const LgLane &c, const DecodeScratch &sc,
+template <bool ONE>
+__device__ __forceinline__ void lg_process(const LgPlan &pl, const LgLane &c, const DecodeScratch &sc,
                                            uint32_t epoch, uint64_t *frame_pos, uint64_t cap, uint64_t u,
                                            uint32_t g, uint32_t b, uint32_t nsteps, const LgBuf &B, LgState &st,
                                            int lane) {
@@ -634,7 +657,7 @@ __device__ __forceinline__ void lg_process(const UPlan &pl, const LgLane &c, con
         st.sink += B.last.y ^ (uint32_t)B.stored;
         return;
     }
-    if (b == 0) {
+    if (ONE || b == 0) {
         if (g == 0) st.unit_err = false;
         st.a0 = c.init0;
         st.a1 = c.init1;
@@ -646,7 +669,7 @@ __device__ __forceinline__ void lg_process(const UPlan &pl, const LgLane &c, con
         st.sbad = valid && ((c.l == 2 && (uint64_t)kFrameHdr + h0.z + h0.w != pl.S) ||
                             (c.l == 4 && (h0.x | h0.y) != 0));
     }
-    if (b < pl.nbF) {  // a full block: accumulate, fold the pair, scramble
+    if (ONE || b < pl.nbF) {  // a full block: accumulate, fold the pair, scramble
         // four independent partial sums per accumulator: the 16 mads overlap instead
         // of forming two dependent chains of 8 (sums commute inside a block)
         uint64_t p0[4] = {0, 0, 0, 0}, p1[4] = {0, 0, 0, 0};
@@ -666,7 +689,7 @@ __device__ __forceinline__ void lg_process(const UPlan &pl, const LgLane &c, con
             else st.sink += B.v[q].x ^ B.v[q].y ^ B.v[q].z ^ B.v[q].w;  // unused piece: keep its load live
         }
     }
-    if (b + 1 != nsteps) {
+    if (!ONE && b + 1 != nsteps) {
         // not the final step: those loads were fillers (consume every register they write)
         st.sink += B.last.x ^ B.last.y ^ B.last.z ^ B.last.w ^ (uint32_t)B.stored ^ (uint32_t)(B.stored >> 32);
         return;
@@ -701,10 +724,10 @@ __device__ __forceinline__ void lg_process(const UPlan &pl, const LgLane &c, con
         const int leader = __builtin_ctzll(sb);
         if (lane == leader) atomicMax((unsigned long long *)sc.spec_fail, (unsigned long long)~(uint64_t)i);
     }
-    if (g == 7) {  // unit complete
+    if (g == 7 && !pl.nopub) {  // unit complete
         const int64_t fi = lg_frame_index(u, 0, 0) + lane;
         if (frame_pos && fi >= 0 && (uint64_t)fi < pl.N && (uint64_t)fi < cap) frame_pos[fi] = (uint64_t)fi * pl.S;
-        if (pl.long_cs) publish_unit_sums(pl, sc, epoch, u, lane, st.cs_mine, (u & 1) ? c.css1 : c.css0);
+        if (pl.long_cs) publish_unit_sums(pl.Mreg, sc, epoch, u, lane, st.cs_mine, (u & 1) ? c.css1 : c.css0);
     }
 }
 
@@ -733,8 +756,11 @@ __device__ __forceinline__ void lg_lane_init(LgLane &c, int lane) {
 
 constexpr uint32_t kLgSlots = 4;  // per wave: 1 step being hashed + 3 in flight (40 KiB)
 static_assert(4 * kLgSlots * kLgStepBytes == kLgLds, "LDS sizing");
-template <uint32_t SLOTS>
-__device__ __forceinline__ void produce_lg(const uint8_t *blob, const UPlan &pl, uint64_t *frame_pos, uint64_t cap,
+// ONE: every frame group is a single full-block step (nbF == 1, ns == 0, i.e.
+// 1024 < L <= 1088: the C2 shape), so the step code has no partial-block or
+// filler paths.
+template <uint32_t SLOTS, bool ONE>
+__device__ __forceinline__ void produce_lg(const uint8_t *blob, const LgPlan &pl, uint64_t *frame_pos, uint64_t cap,
                                            const DecodeScratch &sc, uint32_t epoch, uint32_t gw, uint32_t nw,
                                            uint32_t wave, int lane, uint8_t *smem) {
     LgLane c;
@@ -758,8 +784,9 @@ __device__ __forceinline__ void produce_lg(const uint8_t *blob, const UPlan &pl,
     pin_after_wait(c.last0); pin_after_wait(c.last1); pin_after_wait(c.mrg0); pin_after_wait(c.mrg1);
     pin_after_wait(c.css0); pin_after_wait(c.css1);
     const uint64_t units = 4 * pl.nchunks;
-    const uint32_t nblk = lg_nsteps(pl);  // steps per frame group
+    const uint32_t nblk = ONE ? 1u : lg_nsteps(pl);  // steps per frame group
     if (gw >= units) return;
+    const uint64_t total = (units - gw + nw - 1) / nw * 8 * nblk;  // steps of this wave
 
     LgState st;
     st.a0 = c.init0; st.a1 = c.init1; st.cs_mine = 0; st.sbad = false; st.unit_err = false; st.sink = 0;
@@ -767,27 +794,29 @@ __device__ __forceinline__ void produce_lg(const uint8_t *blob, const UPlan &pl,
     uint64_t pu = gw, iu = gw;
     uint32_t pg = 0, pb = 0, ig = 0, ib = 0;
     auto advance = [&](uint64_t &u, uint32_t &g, uint32_t &b) {
-        if (++b == nblk) { b = 0; if (++g == 8) { g = 0; u += nw; } }
+        if (ONE || ++b == nblk) { b = 0; if (++g == 8) { g = 0; u += nw; } }
     };
     const uint32_t ring = wave * (SLOTS * kLgStepBytes);
     uint32_t iss = 0;  // steps issued
     auto issue_next = [&]() {
         if (iu >= units) return;
-        lg_issue(blob, pl, c, iu, ig, ib, nblk, ring + (iss % SLOTS) * kLgStepBytes);
+        lg_issue<ONE>(blob, pl, c, iu, ig, ib, nblk, ring + (iss % SLOTS) * kLgStepBytes);
         advance(iu, ig, ib);
         ++iss;
     };
     // every slot holds a step in flight; a slot is refilled as soon as its step has
     // been read into registers, so SLOTS steps stay in flight while one is hashed
     for (uint32_t d = 0; d < SLOTS; ++d) issue_next();
-    for (uint32_t k = 0; pu < units; ++k) {
-        wait_vm(10 * (iss - 1 - k));  // step k landed; the later steps stay in flight
+    for (uint64_t k = 0; k < total; ++k) {
+        // step k landed; the later steps stay in flight (the last SLOTS-1 steps drain all)
+        if (k + SLOTS <= total) wait_vm_const<10 * (SLOTS - 1)>();
+        else wait_vm_const<0>();
         LgBuf B;
         const uint32_t slot = ring + (k % SLOTS) * kLgStepBytes;
         lg_read(smem, slot, lane, B);
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // slot read out before it is refilled
         issue_next();  // step k + SLOTS into the slot just read
-        lg_process(pl, c, sc, epoch, frame_pos, cap, pu, pg, pb, nblk, B, st, lane);
+        lg_process<ONE>(pl, c, sc, epoch, frame_pos, cap, pu, pg, pb, nblk, B, st, lane);
         advance(pu, pg, pb);
     }
     wait_vm(0);
@@ -1147,8 +1176,7 @@ __global__ __launch_bounds__(256, 1) void k_decode_uniform(const uint8_t *__rest
     parse_header(body, len, hi);
     UPlan pl;
     make_plan(hi, body + kHdr, len, VERIFY, sc.max_chunks, allow_unaligned != 0, pl);
-    const bool lg = uniform_uses_lg<VERIFY>(pl, dbg);
-    pl.nt = (dbg & 64) != 0;
+    if (uniform_uses_lg<VERIFY>(pl, dbg)) return;  // k_decode_lg decoded this record
     const uint32_t nprod = gridDim.x - 1;
     if (blockIdx.x == 0) {
         consumer<VERIFY>(body, hi, pl, result, sc, epoch, 4 * nprod, wave, smem, dbg);
@@ -1157,16 +1185,113 @@ __global__ __launch_bounds__(256, 1) void k_decode_uniform(const uint8_t *__rest
     if (pl.state != 0) return;
     const uint8_t *blob = body + kHdr;
     const uint32_t g = blockIdx.x - 1;
-    if (VERIFY && lg) {
-        produce_lg<kLgSlots>(blob, pl, frame_pos, cap, sc, epoch, g * 4 + wave, nprod * 4, wave, lane, smem);
-        if (lane == 0) __hip_atomic_fetch_add(sc.exited, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-        return;
-    }
     pl.nt = (dbg & 16) != 0;
     if (VERIFY && pl.long_frames)
         produce<8, 4, 3, VERIFY>(blob, pl, frame_pos, cap, sc, epoch, g, nprod, wave, lane, smem, dbg);
     else
         produce<16, 2, 1, VERIFY>(blob, pl, frame_pos, cap, sc, epoch, g, nprod, wave, lane, smem, dbg);
+}
+
+// diagnostics (dbg bit 256): scripts/lg_micro.hip's staging loop (unit64, 4 slots,
+// no hashing) verbatim inside this kernel, to separate loop code from environment
+__device__ __attribute__((noinline)) void lg_micro_loop(const uint8_t *blob, uint64_t S, uint64_t N, uint32_t gw,
+                                                        uint32_t nw, uint32_t wave, int lane, uint8_t *smem,
+                                                        uint8_t *sink) {
+    constexpr int SLOTS = 4;
+    const uint32_t ring = wave * SLOTS * 10240;
+    const uint32_t l = lane & 7, fg = lane >> 3, m = l >> 1, par = l & 1;
+    const uint32_t poff = 16 * (m + 4 * par);
+    const uint64_t L = S - 8;
+    const uint64_t ngroups = (N + 7) / 8;
+    auto group_of = [&](uint64_t k) -> uint64_t { return (k / 8) * nw * 8 + (uint64_t)gw * 8 + (k % 8); };
+    uint64_t mine = 0;
+    while (group_of(mine) < ngroups) ++mine;
+    auto issue = [&](uint64_t k) {
+        const uint64_t f = group_of(k) * 8 + fg;
+        const uint8_t *fb = blob + (f < N ? f : 0) * S;
+        const uint32_t slot = ring + (uint32_t)(k % SLOTS) * 10240;
+        for (int q = 0; q < 8; ++q) glds16(fb + 8 + 128 * q + poff, slot + 1024 * q);
+        glds16(fb + 8 + L - 64 + 16 * m, slot + 8192);
+        glds16(fb, slot + 9216);
+    };
+    uint32_t x = 0;
+    for (uint64_t k = 0; k < SLOTS && k < mine; ++k) issue(k);
+    for (uint64_t k = 0; k < mine; ++k) {
+        if (k + SLOTS <= mine) wait_vm_const<30>(); else wait_vm_const<0>();
+        const uint8_t *p = smem + ring + (k % SLOTS) * 10240 + 16 * lane;
+        uint4 v[8];
+        for (int q = 0; q < 8; ++q) v[q] = *(const uint4 *)(p + 1024 * q);
+        const uint4 lastp = *(const uint4 *)(p + 8192);
+        const uint64_t stored = *(const uint64_t *)(p + 9216);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if (k + SLOTS < mine) issue(k + SLOTS);
+        for (int q = 0; q < 8; ++q) x ^= v[q].x ^ v[q].w;
+        x ^= lastp.y ^ (uint32_t)stored;
+    }
+    wait_vm_const<0>();
+    if (x == 0x12345678) sink[lane] = 1;
+}
+
+// The lane-group grid's consumer WG as a real call: the chain/gather code's
+// register pressure then stays out of the producer loop's allocation.
+__device__ __attribute__((noinline)) void consumer_lg(const uint8_t *body, const HeaderInfo &hi, const UPlan &pl,
+                                                      iggy_decode_result *result, const DecodeScratch &sc,
+                                                      uint32_t epoch, uint32_t nwaves_prod, uint32_t wave,
+                                                      uint8_t *smem, uint32_t dbg) {
+    consumer<true>(body, hi, pl, result, sc, epoch, nwaves_prod, wave, smem, dbg);
+}
+
+// Lane-group uniform grid (the C2 path: long frames under Verify): one WG per CU
+// (256 threads, 160 KiB LDS), block 0 the consumer WG, blocks 1.. the
+// lane-group producers. Enqueued ahead of k_decode_uniform for every Verify
+// decode; returns at once unless the record takes this form.
+__global__ __launch_bounds__(256, 1) void k_decode_lg(const uint8_t *__restrict__ body, uint64_t len,
+                                                      uint64_t *frame_pos, uint64_t cap, iggy_decode_result *result,
+                                                      DecodeScratch sc, uint32_t epoch, uint32_t allow_unaligned,
+                                                      uint32_t dbg) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const int lane = threadIdx.x & 63;
+    const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t nprod = gridDim.x - 1;
+    if (blockIdx.x == 0) {
+        HeaderInfo hi;
+        parse_header(body, len, hi);
+        UPlan pl;
+        make_plan(hi, body + kHdr, len, true, sc.max_chunks, allow_unaligned != 0, pl);
+        if (!uniform_uses_lg<true>(pl, dbg)) return;
+        pl.tail_unsafe = false;  // every lane-group load stays inside its frame
+        consumer_lg(body, hi, pl, result, sc, epoch, 4 * nprod, wave, smem, dbg);
+        return;
+    }
+    LgPlan lp;
+    {
+        HeaderInfo hi;
+        parse_header(body, len, hi);
+        UPlan pl;
+        make_plan(hi, body + kHdr, len, true, sc.max_chunks, allow_unaligned != 0, pl);
+        if (!uniform_uses_lg<true>(pl, dbg)) return;
+        pl.nt = (dbg & 64) != 0;
+        pl.nopub = (dbg & 128) != 0;
+        lp = lg_plan(pl);
+    }
+    const uint8_t *blob = body + kHdr;
+    const uint32_t g = blockIdx.x - 1;
+    if (dbg & 256) {
+        lg_micro_loop(blob, lp.S, lp.N, g * 4 + wave, nprod * 4, wave, lane, smem, sc.small);
+        if (lane == 0) __hip_atomic_fetch_add(sc.exited, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return;
+    }
+    if (lp.nbF == 1 && lp.ns == 0)
+        produce_lg<kLgSlots, true>(blob, lp, frame_pos, cap, sc, epoch, g * 4 + wave, nprod * 4, wave, lane, smem);
+    else
+        produce_lg<kLgSlots, false>(blob, lp, frame_pos, cap, sc, epoch, g * 4 + wave, nprod * 4, wave, lane, smem);
+    // Exit count: relaxed after this wave's own vmcnt drain. Everything the
+    // consumer reads after it (first_bad, spec_fail, errslot, unit sums) was
+    // written by device atomics or sc1 stores and is read with sc1 loads, so no
+    // release is needed -- and a release here (buffer_wbl2 per wave, 1020 of
+    // them at the kernel tail) measured +40 us per C2 decode (scripts/lg_micro.hip).
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (lane == 0) __hip_atomic_fetch_add(sc.exited, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 template __global__ void k_decode_uniform<true>(const uint8_t *__restrict__, uint64_t, uint64_t *, uint64_t,

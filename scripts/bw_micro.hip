@@ -5,6 +5,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdio.h>
+#include <stdlib.h>
 
 __global__ void rd_coalesced(const uint4 *__restrict__ p, uint64_t n16, uint64_t *out, int unroll) {
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
@@ -119,13 +120,27 @@ __global__ __launch_bounds__(256, 1) void lds_frames(const uint8_t *__restrict__
     if (x == 0x12345678) out[0] = x;
 }
 
+__global__ void fill_random(uint64_t *p, uint64_t n) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+        uint64_t z = i * 0x9E3779B97F4A7C15ull + 0x1234567;
+        z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+        z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+        p[i] = z ^ (z >> 31);
+    }
+}
+
 int main() {
     const uint64_t N = 1 << 20, S = 1072, L = 256 + N * S;
     uint8_t *d;
     uint64_t *o;
     hipMalloc(&d, L + 4096);
     hipMalloc(&o, 64);
-    hipMemset(d, 0x5a, L + 4096);
+    if (getenv("BW_RANDOM")) {  // random bytes (the product reads random payloads)
+        hipLaunchKernelGGL(fill_random, 4096, 256, 0, 0, (uint64_t *)d, (L + 4096) / 8);
+        hipDeviceSynchronize();
+    } else {
+        hipMemset(d, 0x5a, L + 4096);
+    }
     hipEvent_t e0, e1;
     hipEventCreate(&e0);
     hipEventCreate(&e1);

@@ -1,0 +1,48 @@
+// Diagnostic (not product): time iggy_codec_decode_batch_device from plain C++
+// (no Python/torch in the process) on a C2 record file (argv[1]), to separate
+// the kernel's own rate from anything the Python benchmark environment adds.
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <vector>
+#include "../include/iggy_codec.h"
+
+int main(int argc, char **argv) {
+    if (argc < 2) { fprintf(stderr, "usage: %s record.bin [reps]\n", argv[0]); return 2; }
+    const int reps = argc > 2 ? atoi(argv[2]) : 20;
+    FILE *f = fopen(argv[1], "rb");
+    if (!f) { perror("open"); return 1; }
+    fseek(f, 0, SEEK_END);
+    const long L = ftell(f);
+    fseek(f, 0, SEEK_SET);
+    std::vector<unsigned char> h(L);
+    if (fread(h.data(), 1, L, f) != (size_t)L) { fprintf(stderr, "short read\n"); return 1; }
+    fclose(f);
+    iggy_codec_ctx *cx = nullptr;
+    if (iggy_codec_create(0, &cx)) { fprintf(stderr, "create failed\n"); return 1; }
+    iggy_codec_reserve(cx, L, 0);
+    unsigned char *d = nullptr;
+    uint64_t *pos = nullptr;
+    iggy_decode_result *res = nullptr;
+    const uint64_t n = (uint64_t)L / 48;
+    if (hipMalloc(&d, L) || hipMalloc(&pos, n * 8) || hipMalloc(&res, sizeof(*res))) return 1;
+    if (hipMemcpy(d, h.data(), L, hipMemcpyHostToDevice)) return 1;
+    void *s = iggy_codec_stream(cx);
+    hipEvent_t e0, e1;
+    (void)hipEventCreate(&e0);
+    (void)hipEventCreate(&e1);
+    for (int w = 0; w < 3; ++w) iggy_codec_decode_batch_device(cx, d, L, 0, pos, n, res, s);
+    (void)hipStreamSynchronize((hipStream_t)s);
+    (void)hipEventRecord(e0, (hipStream_t)s);
+    for (int r = 0; r < reps; ++r) iggy_codec_decode_batch_device(cx, d, L, 0, pos, n, res, s);
+    (void)hipEventRecord(e1, (hipStream_t)s);
+    (void)hipEventSynchronize(e1);
+    float ms = 0;
+    (void)hipEventElapsedTime(&ms, e0, e1);
+    iggy_decode_result hr;
+    (void)hipMemcpy(&hr, res, sizeof(hr), hipMemcpyDeviceToHost);
+    printf("decode Verify: %.4f ms/decode  %.1f GB/s  err=%u frames=%lu path=%u\n", ms / reps,
+           L / (ms / reps * 1e-3) / 1e9, hr.error.kind, (unsigned long)hr.frame_count, hr.path);
+    iggy_codec_destroy(cx);
+    return 0;
+}

@@ -1,7 +1,9 @@
 """Diagnostic A/B of the uniform decode kernel's roles (not part of the bench).
 
 IGGY_CODEC_DBG bits (read at context creation): 1 = consumer skips the serial
-batch-checksum chain, 2 = producers skip hashing, 4 = feeder skips loading sums.
+batch-checksum chain, 32 = LDS-staged producers, 64 = lane-group producers stage
+only (no hashing), 128 = lane-group producers publish nothing. DIAG_VARIANTS
+selects the set (default 0,1,65,32).
 All variants run interleaved in one process on the same batch.
 """
 import ctypes
@@ -22,7 +24,7 @@ def main():
     pl = int(sys.argv[2]) if len(sys.argv) > 2 else 1024
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(0)
-    variants = [0, 1, 65, 32]
+    variants = [int(v) for v in os.environ.get("DIAG_VARIANTS", "0,1,65,32").split(",")]
     ctxs = {}
     for v in variants:
         os.environ["IGGY_CODEC_DBG"] = str(v)
@@ -34,6 +36,26 @@ def main():
     assert stream != 0
     batch = bench.make_batch(ctxs[0], n, pl, 0, dev, stream)
     L = batch.numel()
+    if os.environ.get("DIAG_HIPMALLOC"):  # the record in a plain hipMalloc buffer instead of torch's allocator
+        hip = ctypes.CDLL("libamdhip64.so")
+        ptr = ctypes.c_void_p()
+        assert hip.hipMalloc(ctypes.byref(ptr), ctypes.c_size_t(L + 4096)) == 0
+        torch.cuda.synchronize()
+        assert hip.hipMemcpy(ptr, ctypes.c_void_p(batch.data_ptr()), ctypes.c_size_t(L), 3) == 0  # D2D
+
+        class _Rec:
+            def __init__(self, p, n):
+                self.p, self.n = p, n
+
+            def data_ptr(self):
+                return self.p
+
+            def numel(self):
+                return self.n
+
+        del batch
+        batch = _Rec(ptr.value, L)
+        print(f"record at hipMalloc {ptr.value:#x}", flush=True)
     d_pos = torch.empty(n, dtype=torch.int64, device=dev)
     d_res = torch.zeros(ctypes.sizeof(abi.DecodeResult), dtype=torch.uint8, device=dev)
     for v, cx in ctxs.items():
