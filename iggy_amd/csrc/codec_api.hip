@@ -197,9 +197,6 @@ int enqueue_decode(iggy_codec_ctx *c, const uint8_t *d_body, uint64_t len, int i
     const uint32_t grid = (uint32_t)std::max(2, c->ncu);
     const uint32_t au = (uint32_t)c->allow_unaligned;
     prof_begin(c, 0, s);
-    if (verify)  // lane-group grid first: it returns at once unless the record is its shape
-        hipLaunchKernelGGL(k_decode_lg, dim3(grid), dim3(256), kLgLds, s, d_body, len, d_pos, cap, d_res, ds,
-                           c->epoch, au, c->dbg);
     if (verify)
         hipLaunchKernelGGL(k_decode_uniform<true>, dim3(grid), dim3(256), kUniformLds, s, d_body, len, d_pos,
                            cap, d_res, ds, c->epoch, au, c->dbg);
@@ -292,9 +289,7 @@ int iggy_codec_create(int device, iggy_codec_ctx **out) {
     r |= c->dresult.ensure(4096);
     if (hipHostMalloc(&c->h_pinned, 4096, hipHostMallocDefault) != hipSuccess) r = IGGY_ERR_DEVICE;
     if (!r) {
-        if (hipFuncSetAttribute((const void *)k_decode_lg, hipFuncAttributeMaxDynamicSharedMemorySize, kLgLds) !=
-                hipSuccess ||
-            hipFuncSetAttribute((const void *)k_decode_uniform<true>,
+        if (hipFuncSetAttribute((const void *)k_decode_uniform<true>,
                                 hipFuncAttributeMaxDynamicSharedMemorySize, kUniformLds) != hipSuccess ||
             hipFuncSetAttribute((const void *)k_decode_uniform<false>,
                                 hipFuncAttributeMaxDynamicSharedMemorySize, kUniformLds) != hipSuccess)
@@ -815,6 +810,22 @@ int iggy_codec_profile_read(iggy_codec_ctx *c, int which, uint64_t *launches, do
     if (total_ms) *total_ms = c->prof_ms[which];
     c->prof_n[which] = 0;
     c->prof_ms[which] = 0;
+    return 0;
+}
+
+// Diagnostics only (not part of include/iggy_codec.h): copy the context's small
+// sync scratch (768 B; the decode's dbg-512 stamps live at [256..]) to host.
+int iggy_codec_debug_read(iggy_codec_ctx *c, void *out, uint64_t bytes) {
+    if (!c || !out) return IGGY_ERR_INVALID_ARGUMENT;
+    HIP_OK(hipStreamSynchronize(c->stream));
+    HIP_OK(hipDeviceSynchronize());
+    HIP_OK(hipMemcpy(out, c->dsync.as<uint8_t>(kSyncSmall), std::min<uint64_t>(bytes, kSyncBytes - kSyncSmall),
+                     hipMemcpyDeviceToHost));
+    return 0;
+}
+int iggy_codec_debug_clear(iggy_codec_ctx *c) {
+    if (!c) return IGGY_ERR_INVALID_ARGUMENT;
+    HIP_OK(hipMemset(c->dsync.as<uint8_t>(kSyncSmall + 256), 0, 256));
     return 0;
 }
 

@@ -59,14 +59,14 @@ constexpr uint32_t kRing = 8;
 constexpr uint32_t kGatherWaves = 3;  // consumer WG waves 1..3; wave 0 (the chain) has SIMD 0 alone
 constexpr uint32_t kCtlOff = kRing * kBatch * 16 * 8;  // 64 KiB
 struct ChainCtl {
-    uint32_t ready[kRing];  // batch index + 1 staged in the slot
+    uint32_t staged[kRing];  // (batch index + 1) << 7 | leading chunks of the slot staged so far
     uint32_t consumed;      // batches the chain wave has finished
     uint32_t abort;         // a gatherer or the chain wave gave up (spin limit)
 };
 constexpr uint32_t kConsumerLds = kCtlOff + 64;
 // lane-group producers: kLgSlots x 10 KiB per wave (set where kLgSlots is)
 constexpr uint32_t kLgLds = 4 * 4 * 10 * 1024;
-constexpr uint32_t kUniformLds = kLdsBytes;  // dynamic LDS of the LDS-staged grid (kLgLds: lane-group grid)
+constexpr uint32_t kUniformLds = kLgLds > kLdsBytes ? kLgLds : kLdsBytes;  // the grid's dynamic LDS
 static_assert(kConsumerLds <= kLgLds && kConsumerLds <= kLdsBytes, "consumer WG fits either grid's LDS");
 static_assert(kCtlOff + sizeof(ChainCtl) <= kConsumerLds, "consumer LDS");
 static_assert(kLdsBytes <= 160 * 1024, "LDS budget");
@@ -550,7 +550,7 @@ __device__ __forceinline__ uint64_t swz_xor4(uint64_t x) {  // ds_swizzle bit mo
 }
 
 // The lane-group producer's whole view of the record (a small subset of UPlan,
-// so the producer loop of k_decode_lg carries no state of the other forms).
+// so the lane-group producer loop carries no state of the other forms).
 struct LgPlan {
     uint64_t S, N, L, nbF, ns, nchunks, Mreg;
     bool long_cs, nt, nopub;
@@ -824,6 +824,14 @@ __device__ __forceinline__ void produce_lg(const uint8_t *blob, const LgPlan &pl
 }
 
 // ------------------------------------------------------------- consumer
+// diagnostics (dbg bit 512): s_memrealtime stamps (100 MHz) of the consumer's
+// progress in sc.small[256..], read back with iggy_codec_debug_read:
+// [0] consumer start, [1] batch 0 staged, [2 + bi/8] batch bi (bi % 8 == 0),
+// [20] chain done, [21] all producers exited, [22] latest producer exit.
+__device__ __forceinline__ void dbg_stamp(const DecodeScratch &sc, uint32_t dbg, int idx) {
+    if (dbg & 512) ((uint64_t *)(sc.small + 256))[idx] = rt_now();
+}
+
 __device__ __forceinline__ uint64_t chain_batches(const UPlan &pl) {
     return ((pl.nb >> 1) + 1 + kBatch - 1) / kBatch;  // chunks 0 .. nb/2 hold blocks 0 .. nb
 }
@@ -854,35 +862,43 @@ __device__ __forceinline__ void gather(const uint8_t *blob, const UPlan &pl, con
         const bool live = c < need && c < pl.nchunks;
         const bool has_next = live && c + 1 < pl.nchunks;
         auto tag_ok = [&](uint64_t v) { return (uint32_t)(v >> 32) == epoch; };
-        // one round trip when the producers are ahead: 73 coalesced loads (16 sum halves
-        // + 2 boundary halves per unit, and the next chunk's first boundary half), every
-        // tag checked; otherwise poll one tagged word per unit, then reload
-        uint64_t B[16];
-        uint32_t first_lo[5], last_hi[4];
+        // Progressive staging: every pass loads the 73 tagged granules of each chunk
+        // not staged yet (16 sum halves + 2 boundary halves per unit and the next
+        // chunk's first boundary half), stages the chunks whose tags all match, and
+        // publishes how many LEADING chunks of the batch are staged, so the chain
+        // starts on chunk 0 as soon as its 4 producer waves are done (not when the
+        // whole 64-chunk batch is). Between passes it polls one tagged word per unit
+        // of the lowest unstaged chunk.
+        bool staged = !live;
+        uint32_t published = 0;
         for (bool first = true; !abort; first = false) {
             if (!first) {
                 while (!abort) {
                     bool ok = true;
-                    if (live) {
+                    if (!staged) {
 #pragma unroll
                         for (int w = 0; w < 4; ++w)
                             ok &= tag_ok(__hip_atomic_load(unit_row(sc, c, w, 17), __ATOMIC_RELAXED,
                                                            __HIP_MEMORY_SCOPE_AGENT));
                     }
-                    if (__ballot(!ok) == 0) break;
+                    const uint64_t pend = __ballot(!staged);
+                    const uint64_t bad = __ballot(!ok);
+                    if (!(bad & (pend & (~pend + 1)))) break;  // the lowest unstaged chunk is ready
                     __builtin_amdgcn_s_sleep(2);
                     if (give_up()) abort = true;
                 }
                 if (abort) break;
             }
             bool ok = true;
+            uint64_t B[16];
+            uint32_t first_lo[5], last_hi[4];
 #pragma unroll
             for (int t = 0; t < 16; ++t) B[t] = 0;
 #pragma unroll
             for (int w = 0; w < 5; ++w) first_lo[w] = 0;
 #pragma unroll
             for (int w = 0; w < 4; ++w) last_hi[w] = 0;
-            if (live) {
+            if (!staged) {
 #pragma unroll
                 for (int w = 0; w < 4; ++w) {
 #pragma unroll
@@ -903,38 +919,47 @@ __device__ __forceinline__ void gather(const uint8_t *blob, const UPlan &pl, con
                     first_lo[w] = (uint32_t)f;
                     last_hi[w] = (uint32_t)l;
                 }
+                if (has_next) {
+                    const uint64_t f = __hip_atomic_load(unit_row(sc, c + 1, 0, 16), __ATOMIC_RELAXED,
+                                                         __HIP_MEMORY_SCOPE_AGENT);
+                    ok &= tag_ok(f);
+                    first_lo[4] = (uint32_t)f;
+                }
+                if (ok) {
+#pragma unroll
+                    for (int w = 0; w < 4; ++w) {
+                        // unit-boundary word m = 256c + 64w + 63 = hi32(cs of the unit's last frame)
+                        //                                        | lo32(cs of the next unit's first frame) << 32
+                        const uint64_t m = 256 * c + 64 * w + 63;
+                        if (m >= 6 && m < pl.Mreg) {
+                            const uint64_t v = (uint64_t)last_hi[w] | ((uint64_t)first_lo[w + 1] << 32);
+                            // lane j = 7 of stripe (8w + 7) mod 16: acc[6] += v, acc[7] += mul
+                            const int hb = w >> 1;
+                            B[8 * hb + 6] += v;
+                            B[8 * hb + 7] += mul32x32(v ^ kSecretW8[((8 * w + 7) & 15) + 7]);
+                        }
+                    }
+                    uint64_t *dst = ring + ((uint64_t)slot * kBatch + lane) * 16;
+#pragma unroll
+                    for (int t = 0; t < 16; ++t) dst[t] = B[t];
+                    staged = true;
+                }
             }
-            if (has_next) {
-                const uint64_t f = __hip_atomic_load(unit_row(sc, c + 1, 0, 16), __ATOMIC_RELAXED,
-                                                     __HIP_MEMORY_SCOPE_AGENT);
-                ok &= tag_ok(f);
-                first_lo[4] = (uint32_t)f;
+            const uint64_t notyet = __ballot(!staged);
+            const uint32_t k = notyet ? (uint32_t)__builtin_ctzll(notyet) : 64u;
+            if (k > published) {  // the release orders this wave's ring writes before the count
+                if (lane == 0)
+                    __hip_atomic_store(&ctl->staged[slot], (uint32_t)((bi + 1) << 7) | k, __ATOMIC_RELEASE,
+                                       __HIP_MEMORY_SCOPE_WORKGROUP);
+                published = k;
             }
-            if (__ballot(!ok) == 0) break;
+            if (k == 64) break;
             if (give_up()) abort = true;
         }
         if (abort) {
             if (lane == 0) __hip_atomic_store(&ctl->abort, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             return;
         }
-#pragma unroll
-        for (int w = 0; w < 4; ++w) {
-            // unit-boundary word m = 256c + 64w + 63 = hi32(cs of the unit's last frame)
-            //                                        | lo32(cs of the next unit's first frame) << 32
-            const uint64_t m = 256 * c + 64 * w + 63;
-            if (live && m >= 6 && m < pl.Mreg) {
-                const uint64_t v = (uint64_t)last_hi[w] | ((uint64_t)first_lo[w + 1] << 32);
-                // lane j = 7 of stripe (8w + 7) mod 16: acc[6] += v, acc[7] += mul
-                const int hb = w >> 1;
-                B[8 * hb + 6] += v;
-                B[8 * hb + 7] += mul32x32(v ^ kSecretW8[((8 * w + 7) & 15) + 7]);
-            }
-        }
-        uint64_t *dst = ring + ((uint64_t)slot * kBatch + lane) * 16;
-#pragma unroll
-        for (int t = 0; t < 16; ++t) dst[t] = B[t];
-        if (lane == 0)
-            __hip_atomic_store(&ctl->ready[slot], (uint32_t)(bi + 1), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
 }
 
@@ -977,6 +1002,7 @@ __device__ __forceinline__ void consumer(const uint8_t *body, const HeaderInfo &
     }
 
     const uint64_t t_start = rt_now();
+    if (wave == 0 && lane == 0) dbg_stamp(sc, dbg, 0);
     bool timed_out = false;
     uint64_t computed = 0;
     const bool chain = VERIFY && pl.long_cs && !(dbg & 1);
@@ -1013,25 +1039,13 @@ __device__ __forceinline__ void consumer(const uint8_t *body, const HeaderInfo &
         uint64_t y = acc;
         for (uint64_t bi = 0; bi < nbatch && !timed_out; ++bi) {
             const uint32_t slot = (uint32_t)(bi % kRing);
-            while (__hip_atomic_load(&ctl->ready[slot], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) !=
-                   (uint32_t)(bi + 1)) {
-                __builtin_amdgcn_s_sleep(1);
-                if (__hip_atomic_load(&ctl->abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) ||
-                    rt_now() - t_start > kSpinLimitTicks) {
-                    timed_out = true;
-                    break;
-                }
-            }
-            if (timed_out) break;
             const uint64_t b0 = 2 * kBatch * bi;
             uint64_t bend = b0 + 2 * kBatch;
             if (bend > pl.nb + 1) bend = pl.nb + 1;
             // block b of this batch at src[8 * (b - b0)]
             const uint64_t *src = ring + (uint64_t)slot * (kBatch * 16) + j;
-            uint32_t k = 0;
             const uint32_t kend = (uint32_t)(bend - b0);
-            if (bi == 0) { y += src[0]; k = 1; }
-            // groups of 16 blocks, next group's LDS reads in flight during this group
+            uint32_t k = 0;
             uint64_t va[16], vb[16];
             auto ld16 = [&](uint64_t *v, uint32_t k0) {
 #pragma unroll
@@ -1041,20 +1055,45 @@ __device__ __forceinline__ void consumer(const uint8_t *body, const HeaderInfo &
 #pragma unroll
                 for (int x = 0; x < 16; ++x) y = chain_step(y, v[x], klo, khi);
             };
-            if (k + 16 <= kend) ld16(va, k);
-            while (k + 16 <= kend) {
-                const bool more = k + 32 <= kend;
-                if (more) ld16(vb, k + 16);
-                run16(va);
-                k += 16;
-                if (!more) break;
-                const bool more2 = k + 32 <= kend;
-                if (more2) ld16(va, k + 16);
-                run16(vb);
-                k += 16;
-                if (!more2) break;
+            while (k < kend) {
+                // the gatherer stages the batch's chunks progressively (2 blocks each)
+                uint32_t avail = 0;
+                while (true) {
+                    const uint32_t w = __hip_atomic_load(&ctl->staged[slot], __ATOMIC_ACQUIRE,
+                                                         __HIP_MEMORY_SCOPE_WORKGROUP);
+                    avail = (w >> 7) == (uint32_t)(bi + 1) ? 2 * (w & 127u) : 0u;
+                    if (avail > kend) avail = kend;
+                    if (avail > k) break;
+                    __builtin_amdgcn_s_sleep(1);
+                    if (__hip_atomic_load(&ctl->abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) ||
+                        rt_now() - t_start > kSpinLimitTicks) {
+                        timed_out = true;
+                        break;
+                    }
+                }
+                if (timed_out) break;
+                if (k == 0 && (dbg & 512) && lane == 0 && (bi & 7) == 0)
+                    dbg_stamp(sc, dbg, bi == 0 ? 1 : 2 + (int)(bi >> 3));
+                if (bi == 0 && k == 0) { y += src[0]; k = 1; }
+                // groups of 16 blocks, the next group's LDS reads in flight during this group
+                if (k + 16 <= avail) {
+                    ld16(va, k);
+                    while (true) {
+                        const bool more = k + 32 <= avail;
+                        if (more) ld16(vb, k + 16);
+                        run16(va);
+                        k += 16;
+                        if (!more) break;
+                        const bool more2 = k + 32 <= avail;
+                        if (more2) ld16(va, k + 16);
+                        run16(vb);
+                        k += 16;
+                        if (!more2) break;
+                    }
+                }
+                for (; k < avail; ++k) y = chain_step(y, src[8 * k], klo, khi);
             }
-            for (; k < kend; ++k) y = chain_step(y, src[8 * k], klo, khi);
+            if (timed_out) break;
             __hip_atomic_store(&ctl->consumed, (uint32_t)(bi + 1), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
         }
         if (timed_out) {
@@ -1073,6 +1112,7 @@ __device__ __forceinline__ void consumer(const uint8_t *body, const HeaderInfo &
             for (int i = 0; i < 4; ++i)
                 r += fold64(a[2 * i] ^ Secret::w(11 + 16 * i), a[2 * i + 1] ^ Secret::w(19 + 16 * i));
             computed = avalanche(r);
+            if (lane == 0) dbg_stamp(sc, dbg, 20);
         }
     } else if (VERIFY && !pl.long_cs) {
         // short checksum input (N <= 24): hash it directly
@@ -1102,6 +1142,7 @@ __device__ __forceinline__ void consumer(const uint8_t *body, const HeaderInfo &
         if (rt_now() - t_start > kSpinLimitTicks) timed_out = true;
     }
     if (lane != 0) return;
+    dbg_stamp(sc, dbg, 21);
     if (timed_out) {
         write_result(result, hi, IGGY_ERR_TIMEOUT, 0, 0, 0, 0, 0, 0, 1, kStatusDone, 0);
         return;  // scratch left dirty on purpose: the host re-initialises it
@@ -1176,7 +1217,8 @@ __global__ __launch_bounds__(256, 1) void k_decode_uniform(const uint8_t *__rest
     parse_header(body, len, hi);
     UPlan pl;
     make_plan(hi, body + kHdr, len, VERIFY, sc.max_chunks, allow_unaligned != 0, pl);
-    if (uniform_uses_lg<VERIFY>(pl, dbg)) return;  // k_decode_lg decoded this record
+    const bool lg = uniform_uses_lg<VERIFY>(pl, dbg);
+    if (lg) pl.tail_unsafe = false;  // every lane-group load stays inside its frame
     const uint32_t nprod = gridDim.x - 1;
     if (blockIdx.x == 0) {
         consumer<VERIFY>(body, hi, pl, result, sc, epoch, 4 * nprod, wave, smem, dbg);
@@ -1185,113 +1227,30 @@ __global__ __launch_bounds__(256, 1) void k_decode_uniform(const uint8_t *__rest
     if (pl.state != 0) return;
     const uint8_t *blob = body + kHdr;
     const uint32_t g = blockIdx.x - 1;
+    if (VERIFY && lg) {
+        pl.nt = (dbg & 64) != 0;
+        pl.nopub = (dbg & 128) != 0;
+        const LgPlan lp = lg_plan(pl);
+        if (lp.nbF == 1 && lp.ns == 0)
+            produce_lg<kLgSlots, true>(blob, lp, frame_pos, cap, sc, epoch, g * 4 + wave, nprod * 4, wave, lane, smem);
+        else
+            produce_lg<kLgSlots, false>(blob, lp, frame_pos, cap, sc, epoch, g * 4 + wave, nprod * 4, wave, lane, smem);
+        // Exit count: relaxed after this wave's own vmcnt drain. Everything the
+        // consumer reads after it (first_bad, spec_fail, errslot, unit sums) was
+        // written by device atomics or sc1 stores and is read with sc1 loads, so no
+        // release is needed -- and a release here (buffer_wbl2 per wave, 1020 of
+        // them at the kernel tail) measured +40 us per C2 decode (scripts/lg_micro.hip).
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if ((dbg & 512) && lane == 0)
+            atomicMax((unsigned long long *)(sc.small + 256 + 8 * 22), (unsigned long long)rt_now());
+        if (lane == 0) __hip_atomic_fetch_add(sc.exited, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return;
+    }
     pl.nt = (dbg & 16) != 0;
     if (VERIFY && pl.long_frames)
         produce<8, 4, 3, VERIFY>(blob, pl, frame_pos, cap, sc, epoch, g, nprod, wave, lane, smem, dbg);
     else
         produce<16, 2, 1, VERIFY>(blob, pl, frame_pos, cap, sc, epoch, g, nprod, wave, lane, smem, dbg);
-}
-
-// diagnostics (dbg bit 256): scripts/lg_micro.hip's staging loop (unit64, 4 slots,
-// no hashing) verbatim inside this kernel, to separate loop code from environment
-__device__ __attribute__((noinline)) void lg_micro_loop(const uint8_t *blob, uint64_t S, uint64_t N, uint32_t gw,
-                                                        uint32_t nw, uint32_t wave, int lane, uint8_t *smem,
-                                                        uint8_t *sink) {
-    constexpr int SLOTS = 4;
-    const uint32_t ring = wave * SLOTS * 10240;
-    const uint32_t l = lane & 7, fg = lane >> 3, m = l >> 1, par = l & 1;
-    const uint32_t poff = 16 * (m + 4 * par);
-    const uint64_t L = S - 8;
-    const uint64_t ngroups = (N + 7) / 8;
-    auto group_of = [&](uint64_t k) -> uint64_t { return (k / 8) * nw * 8 + (uint64_t)gw * 8 + (k % 8); };
-    uint64_t mine = 0;
-    while (group_of(mine) < ngroups) ++mine;
-    auto issue = [&](uint64_t k) {
-        const uint64_t f = group_of(k) * 8 + fg;
-        const uint8_t *fb = blob + (f < N ? f : 0) * S;
-        const uint32_t slot = ring + (uint32_t)(k % SLOTS) * 10240;
-        for (int q = 0; q < 8; ++q) glds16(fb + 8 + 128 * q + poff, slot + 1024 * q);
-        glds16(fb + 8 + L - 64 + 16 * m, slot + 8192);
-        glds16(fb, slot + 9216);
-    };
-    uint32_t x = 0;
-    for (uint64_t k = 0; k < SLOTS && k < mine; ++k) issue(k);
-    for (uint64_t k = 0; k < mine; ++k) {
-        if (k + SLOTS <= mine) wait_vm_const<30>(); else wait_vm_const<0>();
-        const uint8_t *p = smem + ring + (k % SLOTS) * 10240 + 16 * lane;
-        uint4 v[8];
-        for (int q = 0; q < 8; ++q) v[q] = *(const uint4 *)(p + 1024 * q);
-        const uint4 lastp = *(const uint4 *)(p + 8192);
-        const uint64_t stored = *(const uint64_t *)(p + 9216);
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        if (k + SLOTS < mine) issue(k + SLOTS);
-        for (int q = 0; q < 8; ++q) x ^= v[q].x ^ v[q].w;
-        x ^= lastp.y ^ (uint32_t)stored;
-    }
-    wait_vm_const<0>();
-    if (x == 0x12345678) sink[lane] = 1;
-}
-
-// The lane-group grid's consumer WG as a real call: the chain/gather code's
-// register pressure then stays out of the producer loop's allocation.
-__device__ __attribute__((noinline)) void consumer_lg(const uint8_t *body, const HeaderInfo &hi, const UPlan &pl,
-                                                      iggy_decode_result *result, const DecodeScratch &sc,
-                                                      uint32_t epoch, uint32_t nwaves_prod, uint32_t wave,
-                                                      uint8_t *smem, uint32_t dbg) {
-    consumer<true>(body, hi, pl, result, sc, epoch, nwaves_prod, wave, smem, dbg);
-}
-
-// Lane-group uniform grid (the C2 path: long frames under Verify): one WG per CU
-// (256 threads, 160 KiB LDS), block 0 the consumer WG, blocks 1.. the
-// lane-group producers. Enqueued ahead of k_decode_uniform for every Verify
-// decode; returns at once unless the record takes this form.
-__global__ __launch_bounds__(256, 1) void k_decode_lg(const uint8_t *__restrict__ body, uint64_t len,
-                                                      uint64_t *frame_pos, uint64_t cap, iggy_decode_result *result,
-                                                      DecodeScratch sc, uint32_t epoch, uint32_t allow_unaligned,
-                                                      uint32_t dbg) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    const int lane = threadIdx.x & 63;
-    const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const uint32_t nprod = gridDim.x - 1;
-    if (blockIdx.x == 0) {
-        HeaderInfo hi;
-        parse_header(body, len, hi);
-        UPlan pl;
-        make_plan(hi, body + kHdr, len, true, sc.max_chunks, allow_unaligned != 0, pl);
-        if (!uniform_uses_lg<true>(pl, dbg)) return;
-        pl.tail_unsafe = false;  // every lane-group load stays inside its frame
-        consumer_lg(body, hi, pl, result, sc, epoch, 4 * nprod, wave, smem, dbg);
-        return;
-    }
-    LgPlan lp;
-    {
-        HeaderInfo hi;
-        parse_header(body, len, hi);
-        UPlan pl;
-        make_plan(hi, body + kHdr, len, true, sc.max_chunks, allow_unaligned != 0, pl);
-        if (!uniform_uses_lg<true>(pl, dbg)) return;
-        pl.nt = (dbg & 64) != 0;
-        pl.nopub = (dbg & 128) != 0;
-        lp = lg_plan(pl);
-    }
-    const uint8_t *blob = body + kHdr;
-    const uint32_t g = blockIdx.x - 1;
-    if (dbg & 256) {
-        lg_micro_loop(blob, lp.S, lp.N, g * 4 + wave, nprod * 4, wave, lane, smem, sc.small);
-        if (lane == 0) __hip_atomic_fetch_add(sc.exited, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        return;
-    }
-    if (lp.nbF == 1 && lp.ns == 0)
-        produce_lg<kLgSlots, true>(blob, lp, frame_pos, cap, sc, epoch, g * 4 + wave, nprod * 4, wave, lane, smem);
-    else
-        produce_lg<kLgSlots, false>(blob, lp, frame_pos, cap, sc, epoch, g * 4 + wave, nprod * 4, wave, lane, smem);
-    // Exit count: relaxed after this wave's own vmcnt drain. Everything the
-    // consumer reads after it (first_bad, spec_fail, errslot, unit sums) was
-    // written by device atomics or sc1 stores and is read with sc1 loads, so no
-    // release is needed -- and a release here (buffer_wbl2 per wave, 1020 of
-    // them at the kernel tail) measured +40 us per C2 decode (scripts/lg_micro.hip).
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if (lane == 0) __hip_atomic_fetch_add(sc.exited, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 template __global__ void k_decode_uniform<true>(const uint8_t *__restrict__, uint64_t, uint64_t *, uint64_t,

@@ -6,6 +6,9 @@
 #include <stdlib.h>
 #include <vector>
 #include "../include/iggy_codec.h"
+#include <string.h>
+extern "C" int iggy_codec_debug_read(iggy_codec_ctx *, void *, uint64_t);
+extern "C" int iggy_codec_debug_clear(iggy_codec_ctx *);
 
 int main(int argc, char **argv) {
     if (argc < 2) { fprintf(stderr, "usage: %s record.bin [reps]\n", argv[0]); return 2; }
@@ -43,6 +46,18 @@ int main(int argc, char **argv) {
     (void)hipMemcpy(&hr, res, sizeof(hr), hipMemcpyDeviceToHost);
     printf("decode Verify: %.4f ms/decode  %.1f GB/s  err=%u frames=%lu path=%u\n", ms / reps,
            L / (ms / reps * 1e-3) / 1e9, hr.error.kind, (unsigned long)hr.frame_count, hr.path);
+    if (getenv("IGGY_CODEC_DBG") && (strtoul(getenv("IGGY_CODEC_DBG"), nullptr, 0) & 512)) {
+        // one more decode with fresh stamps (us since consumer start, 100 MHz ticks)
+        iggy_codec_debug_clear(cx);
+        iggy_codec_decode_batch_device(cx, d, L, 0, pos, n, res, s);
+        uint64_t t[64];
+        iggy_codec_debug_read(cx, t, 512);
+        const uint64_t *ts = t + 32;  // small + 256
+        printf("stamps (us from consumer start):");
+        for (int i = 0; i < 23; ++i)
+            if (ts[i]) printf(" [%d]=%.1f", i, (double)(ts[i] - ts[0]) / 100.0);
+        printf("\n");
+    }
     iggy_codec_destroy(cx);
     return 0;
 }
