@@ -7,6 +7,14 @@ step = decode_batch_slice_with(Verify) of that batch
 XXH3-verified, the batch checksum recomputed and compared, the blob-relative
 position of every frame written out (8 B per frame).
 
+Steps alternate over `--streams` (default 2) lanes per GPU: each lane is its own
+codec context + HIP stream + device-resident record (a partition's consecutive
+batches), and every step is one complete single-record decode through
+iggy_codec_decode_batch_device. Two lanes let one batch's serial batch-checksum
+tail overlap the next batch's streaming phase; the
+single-stream rate is reported beside it (`config.single_stream_gib_s`), and
+`roofline` prices one launch at a time.
+
 Multi-GPU (BASELINE configs[4], "C5"): one rank per GPU, each with its own
 independent partition's batch; no data-path collective (weak scaling). The
 barrier + max-over-ranks timing is the only cross-rank traffic.
@@ -148,6 +156,7 @@ def main():
     ap.add_argument("--messages", type=int, default=N_MSG)
     ap.add_argument("--no-cpu", action="store_true", help="skip the cpu_baseline leg")
     ap.add_argument("--cpu-seconds", type=float, default=4.0)
+    ap.add_argument("--streams", type=int, default=2, help="decode lanes (contexts/streams) steps alternate over")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -160,58 +169,78 @@ def main():
         dist.init_process_group("nccl", init_method="env://")
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    cx = Codec(local)
-    # an explicit stream: the library enqueues on it and the timing brackets it
-    ts = torch.cuda.Stream(dev)
-    torch.cuda.set_stream(ts)
-    stream = ts.cuda_stream
-
     n = args.messages
-    batch = make_batch(cx, n, PAYLOAD, rank, dev, stream)
-    L = batch.numel()
-    cx.reserve(L)
-    d_pos = torch.empty(n, dtype=torch.int64, device=dev)
-    d_res = torch.zeros(ctypes.sizeof(abi.DecodeResult), dtype=torch.uint8, device=dev)
+    # Steps alternate over `--streams` lanes, each its own codec context, HIP stream
+    # and device-resident C2 record (a partition's consecutive batches): every step
+    # is one complete decode_batch_slice_with(Verify) of one 1 M x 1 KiB batch,
+    # enqueued through the single-record device API; lanes let one batch's serial
+    # batch-checksum tail overlap the next batch's streaming phase.
+    lanes = []
+    for li in range(args.streams):
+        cx = Codec(local)
+        ts = torch.cuda.Stream(dev)
+        batch = make_batch(cx, n, PAYLOAD, rank * 16 + li, dev, ts.cuda_stream)
+        cx.reserve(batch.numel())
+        lanes.append({
+            "cx": cx, "stream": ts.cuda_stream, "batch": batch,
+            "pos": torch.empty(n, dtype=torch.int64, device=dev),
+            "res": torch.zeros(ctypes.sizeof(abi.DecodeResult), dtype=torch.uint8, device=dev),
+        })
+    L = lanes[0]["batch"].numel()
+    torch.cuda.synchronize(dev)
 
-    def step():
-        rc = cx.decode_device(batch.data_ptr(), L, abi.INTEGRITY_VERIFY, d_pos.data_ptr(), n,
-                              d_res.data_ptr(), stream)
+    def step(i):
+        ln = lanes[i % len(lanes)]
+        rc = ln["cx"].decode_device(ln["batch"].data_ptr(), L, abi.INTEGRITY_VERIFY, ln["pos"].data_ptr(), n,
+                                    ln["res"].data_ptr(), ln["stream"])
         if rc:
             raise RuntimeError(f"decode_device rc={rc}")
 
-    for _ in range(args.warmup):
-        step()
+    for i in range(max(args.warmup, len(lanes))):
+        step(i)
     torch.cuda.synchronize(dev)
-    res = abi.DecodeResult.from_buffer_copy(d_res.cpu().numpy().tobytes())
-    if res.error.kind != 0 or res.frame_count != n or res.path != 1:
-        raise RuntimeError(f"decode check failed: {res.error!r} frames={res.frame_count} path={res.path}")
-    pos = d_pos[:4].cpu().tolist()
-    assert pos == [i * (48 + PAYLOAD) for i in range(4)], pos
+    for ln in lanes:
+        res = abi.DecodeResult.from_buffer_copy(ln["res"].cpu().numpy().tobytes())
+        if res.error.kind != 0 or res.frame_count != n or res.path != 1:
+            raise RuntimeError(f"decode check failed: {res.error!r} frames={res.frame_count} path={res.path}")
+        pos = ln["pos"][:4].cpu().tolist()
+        assert pos == [i * (48 + PAYLOAD) for i in range(4)], pos
 
     if dist:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
+    for i in range(args.steps):
+        step(i)
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
     if dist:
         dist.barrier()
     elapsed = max_over_ranks(elapsed, dist, dev)
+    for ln in lanes:  # every timed decode left a clean result
+        res = abi.DecodeResult.from_buffer_copy(ln["res"].cpu().numpy().tobytes())
+        if res.error.kind != 0 or res.frame_count != n:
+            raise RuntimeError(f"timed decode failed: {res.error!r}")
 
-    # the decode's device phase: the lane-group producer kernel on the launch stream
-    # plus the chain/consumer WG forked onto the context's side stream and joined
-    # back, bracketed by HIP events on the launch stream inside the library
+    # roofline: the decode grid's own duration, one launch at a time on one
+    # stream (HIP events on the launch stream, bracketing k_decode_uniform)
+    cx = lanes[0]["cx"]
     cx.profile_enable(True)
     for _ in range(args.steps):
-        step()
-    torch.cuda.synchronize(dev)
+        step(0)
+        torch.cuda.synchronize(dev)
     launches, total_ms = cx.profile_read(0)
     cx.profile_enable(False)
     k_ms = total_ms / max(launches, 1)
     alg_bytes = L + 8 * n  # read the record once + one 8-B frame position per message
     achieved = alg_bytes / (k_ms * 1e-3) / 1e9
+    # single-stream step rate, for reference (no overlap between batches)
+    torch.cuda.synchronize(dev)
+    t1 = time.perf_counter()
+    for _ in range(args.steps):
+        step(0)
+    torch.cuda.synchronize(dev)
+    single_gib_s = L * args.steps / (time.perf_counter() - t1) / 2**30
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
@@ -242,6 +271,8 @@ def main():
                 "batch_bytes": L,
                 "outputs": "frame positions (8 B/msg) + result struct",
                 "parallelism": f"{world} independent partitions, one per GPU, no collective",
+                "streams_per_gpu": len(lanes),
+                "single_stream_gib_s": round(single_gib_s, 2),
             },
             "roofline": {
                 "bound": "hbm",
@@ -251,14 +282,16 @@ def main():
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": traffic,
                 "traffic_source": traffic_src,
-                "kernel": "k_decode_uniform<true> (one persistent grid: lane-group producers + chain WG)",
+                "kernel": "k_decode_uniform<true> (one persistent grid: lane-group producers + chain WG), "
+                          "one launch at a time",
                 "kernel_ms": round(k_ms, 4),
                 "algorithmic_bytes": alg_bytes,
             },
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)
-    cx.close()
+    for ln in lanes:
+        ln["cx"].close()
     if dist:
         dist.destroy_process_group()
 

@@ -5,6 +5,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <vector>
+#include <chrono>
 #include "../include/iggy_codec.h"
 #include <string.h>
 extern "C" int iggy_codec_debug_read(iggy_codec_ctx *, void *, uint64_t);
@@ -46,6 +47,36 @@ int main(int argc, char **argv) {
     (void)hipMemcpy(&hr, res, sizeof(hr), hipMemcpyDeviceToHost);
     printf("decode Verify: %.4f ms/decode  %.1f GB/s  err=%u frames=%lu path=%u\n", ms / reps,
            L / (ms / reps * 1e-3) / 1e9, hr.error.kind, (unsigned long)hr.frame_count, hr.path);
+    if (getenv("HARNESS_STREAMS")) {  // decodes alternated over S contexts/streams (pipelined batches)
+        const int ns = atoi(getenv("HARNESS_STREAMS"));
+        std::vector<iggy_codec_ctx *> cs(ns, nullptr);
+        std::vector<unsigned char *> recs(ns, nullptr);
+        std::vector<iggy_decode_result *> rs(ns, nullptr);
+        std::vector<uint64_t *> ps(ns, nullptr);
+        for (int i = 0; i < ns; ++i) {
+            if (iggy_codec_create(0, &cs[i])) return 1;
+            iggy_codec_reserve(cs[i], L, 0);
+            if (hipMalloc(&recs[i], L) || hipMalloc(&ps[i], n * 8) || hipMalloc(&rs[i], sizeof(iggy_decode_result)))
+                return 1;
+            (void)hipMemcpy(recs[i], d, L, hipMemcpyDeviceToDevice);
+        }
+        for (int w = 0; w < 2 * ns; ++w)
+            iggy_codec_decode_batch_device(cs[w % ns], recs[w % ns], L, 0, ps[w % ns], n, rs[w % ns], nullptr);
+        (void)hipDeviceSynchronize();
+        auto t0 = std::chrono::steady_clock::now();
+        for (int r = 0; r < reps; ++r)
+            iggy_codec_decode_batch_device(cs[r % ns], recs[r % ns], L, 0, ps[r % ns], n, rs[r % ns], nullptr);
+        (void)hipDeviceSynchronize();
+        const double sec = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+        int bad = 0;
+        for (int i = 0; i < ns; ++i) {
+            iggy_decode_result x;
+            (void)hipMemcpy(&x, rs[i], sizeof(x), hipMemcpyDeviceToHost);
+            bad += x.error.kind != 0 || x.frame_count != 1048576;
+        }
+        printf("%d streams: %.4f ms/decode  %.1f GB/s  results_bad=%d\n", ns, sec * 1e3 / reps, L * reps / sec / 1e9,
+               bad);
+    }
     if (getenv("IGGY_CODEC_DBG") && (strtoul(getenv("IGGY_CODEC_DBG"), nullptr, 0) & 512)) {
         // one more decode with fresh stamps (us since consumer start, 100 MHz ticks)
         iggy_codec_debug_clear(cx);
