@@ -120,6 +120,36 @@ class EncodeResult(ctypes.Structure):
     ]
 
 
+LOOKUP_OFFSET = 0
+LOOKUP_TIMESTAMP = 1
+
+
+class SliceQuery(ctypes.Structure):
+    """MessageLookup (core/partitions/src/journal.rs:68-95) + already-matched count."""
+    _fields_ = [("kind", u32), ("count", u32), ("value", u64), ("ceiling", u64),
+                ("already_matched", u32), ("_pad", u32)]
+
+
+class SliceResult(ctypes.Structure):
+    _fields_ = [
+        ("selected", u32),
+        ("full_body", u32),
+        ("start", u64),
+        ("end", u64),
+        ("matched_messages", u32),
+        ("_pad0", u32),
+        ("last_matching_offset", u64),
+        ("header", BatchHeader),
+        ("_pad1", u64 * 3),
+    ]
+
+    def astuple(self):
+        return (self.selected, self.full_body, self.start, self.end, self.matched_messages,
+                self.last_matching_offset) + self.header.astuple()
+
+
+assert ctypes.sizeof(SliceQuery) == 32
+assert ctypes.sizeof(SliceResult) == 128
 assert ctypes.sizeof(BatchHeader) == 64
 assert ctypes.sizeof(WireError) == 32
 assert ctypes.sizeof(PolledMessage) == 80

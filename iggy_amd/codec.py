@@ -16,7 +16,8 @@ import re
 import numpy as np
 
 from . import abi
-from .abi import BatchHeader, DecodeResult, EncodeResult, PolledMessage, RawMessages, WireError
+from .abi import (BatchHeader, DecodeResult, EncodeResult, PolledMessage, RawMessages, SliceQuery, SliceResult,
+                  WireError)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libiggy_codec.so")
@@ -77,6 +78,9 @@ def lib() -> ctypes.CDLL:
     L.iggy_codec_encode_batch_device.argtypes = [vp, vp, u64, vp, u64, vp, vp]
     L.iggy_codec_batch_checksum_device.argtypes = [vp, vp, vp, vp, u64, vp, vp]
     L.iggy_codec_xxh3_64_ranges_device.argtypes = [vp, vp, vp, vp, u64, vp, vp]
+    L.iggy_codec_select_slice.argtypes = [vp, vp, u64, vp, vp, vp, vp]
+    L.iggy_codec_select_slice_device.argtypes = [vp, vp, vp, u64, vp, vp, vp, vp]
+    L.iggy_codec_stamp_batch_device.argtypes = [vp, vp, vp, u64, u64, u64, vp, vp]
     L.iggy_codec_profile_enable.argtypes = [vp, ci]
     L.iggy_codec_profile_read.argtypes = [vp, ci, vp, vp]
     L.iggy_codec_error_string.argtypes = [u32, u32]
@@ -198,6 +202,29 @@ class Codec:
         rc = self._L.iggy_codec_stamp_batch(self._h, a.ctypes.data, a.size, base_offset,
                                             base_timestamp, ctypes.byref(h), ctypes.byref(e))
         return rc, e, h, a.tobytes()
+
+    def select_slice(self, record, kind: int, value: int, count: int, ceiling: int = 2**64 - 1,
+                     already_matched: int = 0):
+        """select_batch_slice + served header (journal.rs:1025-1137) ->
+        (rc, WireError, SliceResult, header bytes or None)."""
+        a = _np(record)
+        q = SliceQuery(kind, count, value, ceiling, already_matched, 0)
+        out = SliceResult()
+        hdr = np.zeros(256, dtype=np.uint8)
+        e = WireError()
+        rc = self._L.iggy_codec_select_slice(self._h, _addr(a), a.size, ctypes.byref(q), ctypes.byref(out),
+                                             hdr.ctypes.data, ctypes.byref(e))
+        return rc, e, out, (hdr.tobytes() if rc == 0 and out.selected else None)
+
+    def select_slice_device(self, d_record: int, d_frame_pos: int, nframes: int, query: SliceQuery,
+                            d_out: int, d_header: int | None = None, stream: int | None = None) -> int:
+        return self._L.iggy_codec_select_slice_device(self._h, d_record, d_frame_pos, nframes, ctypes.byref(query),
+                                                      d_out, d_header, stream)
+
+    def stamp_device(self, d_record: int, d_frame_pos: int, nframes: int, base_offset: int, base_timestamp: int,
+                     d_header: int | None = None, stream: int | None = None) -> int:
+        return self._L.iggy_codec_stamp_batch_device(self._h, d_record, d_frame_pos, nframes, base_offset,
+                                                     base_timestamp, d_header, stream)
 
     # --------------------------------------------------------- device buffers
     def decode_device(self, d_body: int, length: int, integrity: int, d_frame_pos: int | None,

@@ -18,6 +18,7 @@ struct CsSource {
     const uint64_t *cs;     // dense array (decode general / encode), or
     const uint8_t *blob;    // gathered at blob + fpos[i]
     const uint64_t *fpos;
+    const uint64_t *first = nullptr;  // device-resident index of fpos[0] (a slice), applied per kernel
     __device__ __forceinline__ uint64_t operator()(uint64_t i) const {
         return cs ? cs[i] : ld64_any(blob + fpos[i]);
     }
@@ -63,6 +64,7 @@ __global__ __launch_bounds__(256) void k_bsum_blocks(const iggy_batch_header *hp
     const iggy_batch_header h = *hp;
     const CsPlan pl = cs_plan(*nframes_p);
     if (!pl.long_cs) return;
+    if (src.first) src.fpos += *src.first;
     const int lane = threadIdx.x & 63;
     const uint64_t wid = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     const uint64_t nwaves = ((uint64_t)gridDim.x * blockDim.x) >> 6;
@@ -93,6 +95,7 @@ __global__ __launch_bounds__(64) void k_bsum_chain(const iggy_batch_header *hp,
     if (skip && *skip) return;
     const iggy_batch_header h = *hp;
     const uint64_t N = *nframes_p;
+    if (src.first) src.fpos += *src.first;
     const CsPlan pl = cs_plan(N);
     const int lane = threadIdx.x & 63;
     if (pl.long_cs) {

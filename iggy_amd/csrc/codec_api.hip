@@ -21,6 +21,7 @@
 #include "decode_uniform.hip"
 #include "encode.hip"
 #include "poll.hip"
+#include "slice.hip"
 
 using namespace iggy;
 
@@ -84,6 +85,8 @@ struct iggy_codec_ctx {
     DevBuf hbsums;
     // poll
     DevBuf ppos, pmsgs;
+    // slice / device stamp: [0,512) control words + header + small, then tile counts
+    DevBuf sl, slres;
     // pinned host mirror of results
     void *h_pinned = nullptr;
     // profiling
@@ -334,7 +337,7 @@ void iggy_codec_destroy(iggy_codec_ctx *c) {
                       &c->gtiles_cnt, &c->gtiles_list, &c->gtiles_base, &c->gfpos, &c->gcs,
                       &c->gbsums, &c->dresult, &c->din, &c->dpos, &c->dout, &c->epl, &c->euh,
                       &c->etile, &c->ecs, &c->emisc, &c->eids, &c->eots, &c->epay, &c->eplen,
-                      &c->euhb, &c->euhl, &c->hbsums, &c->ppos, &c->pmsgs};
+                      &c->euhb, &c->euhl, &c->hbsums, &c->ppos, &c->pmsgs, &c->sl, &c->slres};
     for (DevBuf *b : bufs) b->release();
     if (c->h_pinned) (void)hipHostFree(c->h_pinned);
     for (int w = 0; w < 2; ++w) {
@@ -779,6 +782,107 @@ int iggy_codec_xxh3_64_ranges_device(iggy_codec_ctx *c, const uint8_t *d_data, c
     const uint64_t blocks = std::min<uint64_t>((n + 255) / 256, (uint64_t)c->ncu * 16);
     hipLaunchKernelGGL(k_xxh3_ranges, dim3((uint32_t)blocks), dim3(256), 0, pick(c, stream), d_data,
                        d_offsets, d_lengths, n, d_out);
+    HIP_OK(hipGetLastError());
+    return 0;
+}
+
+// ------------------------------------------------- poll-path slicing / stamp
+int iggy_codec_select_slice_device(iggy_codec_ctx *c, const uint8_t *d_record, const uint64_t *d_frame_pos,
+                                   uint64_t nframes, const iggy_slice_query *q, iggy_slice_result *d_out,
+                                   uint8_t *d_header_out, void *stream) {
+    if (!c || !d_record || !q || !d_out || (nframes && !d_frame_pos)) return IGGY_ERR_INVALID_ARGUMENT;
+    if (q->kind != IGGY_LOOKUP_OFFSET && q->kind != IGGY_LOOKUP_TIMESTAMP) return IGGY_ERR_INVALID_ARGUMENT;
+    hipStream_t s = pick(c, stream);
+    const uint64_t ntiles = (nframes + kSliceTile - 1) / kSliceTile;
+    int r = c->sl.ensure(512 + ntiles * 4);
+    r |= c->gbsums.ensure(((44 + 8 * nframes) / 1024 + 2) * 64);
+    if (r) return IGGY_ERR_DEVICE;
+    SliceScratch ss;
+    ss.stop = c->sl.as<uint64_t>(0);
+    ss.nsel = c->sl.as<uint64_t>(8);
+    ss.first = c->sl.as<uint64_t>(16);
+    ss.computed = c->sl.as<uint64_t>(24);
+    ss.skip = c->sl.as<uint32_t>(32);
+    ss.hdr = c->sl.as<iggy_batch_header>(64);
+    ss.tile_cnt = c->sl.as<uint32_t>(512);
+    HIP_OK(hipMemsetAsync(ss.stop, 0xff, 8, s));
+    const iggy_slice_query qq = *q;
+    if (nframes) {
+        const uint32_t g = (uint32_t)std::min<uint64_t>((nframes + 255) / 256, (uint64_t)c->ncu * 8);
+        hipLaunchKernelGGL(k_slice_stop, dim3(g), dim3(256), 0, s, d_record, d_frame_pos, nframes, qq, ss.stop);
+        hipLaunchKernelGGL(k_slice_count, dim3((uint32_t)ntiles), dim3(256), 0, s, d_record, d_frame_pos, nframes, qq,
+                           (const uint64_t *)ss.stop, ss.tile_cnt);
+    }
+    hipLaunchKernelGGL(k_slice_pick, dim3(1), dim3(256), 0, s, d_record, d_frame_pos, nframes, qq,
+                       (const uint32_t *)ss.tile_cnt, ntiles, ss, d_out);
+    CsSource src{nullptr, d_record + kHdr, d_frame_pos, ss.first};
+    hipLaunchKernelGGL(k_bsum_blocks, dim3(c->ncu * 4), dim3(256), 0, s, (const iggy_batch_header *)ss.hdr,
+                       (const uint64_t *)ss.nsel, src, c->gbsums.as<uint64_t>(), (const uint32_t *)ss.skip);
+    hipLaunchKernelGGL(k_bsum_chain, dim3(1), dim3(64), 0, s, (const iggy_batch_header *)ss.hdr,
+                       (const uint64_t *)ss.nsel, src, (const uint64_t *)c->gbsums.as<uint64_t>(),
+                       c->sl.as<uint8_t>(128), ss.computed, (const uint32_t *)ss.skip);
+    hipLaunchKernelGGL(k_slice_finish, dim3(1), dim3(64), 0, s, d_record, ss, d_out, d_header_out);
+    HIP_OK(hipGetLastError());
+    return 0;
+}
+
+int iggy_codec_select_slice(iggy_codec_ctx *c, const uint8_t *record, uint64_t len, const iggy_slice_query *q,
+                            iggy_slice_result *out, uint8_t *header_out, iggy_wire_error *err) {
+    if (!c || !q || !out || (!record && len)) return IGGY_ERR_INVALID_ARGUMENT;
+    HIP_OK(hipSetDevice(c->device));
+    set_err(err, IGGY_OK);
+    const uint64_t cap = len / kFrameHdr + 1;
+    int r = c->din.ensure(len + 16);
+    r |= c->dpos.ensure((cap + 1) * 8);
+    r |= c->slres.ensure(512);
+    if (r) return IGGY_ERR_DEVICE;
+    if (len) HIP_OK(hipMemcpyAsync(c->din.p, record, len, hipMemcpyHostToDevice, c->stream));
+    // the reference selects on a decoded batch: decode it (layout) first
+    iggy_decode_result *d_res = c->dresult.as<iggy_decode_result>();
+    r = enqueue_decode(c, c->din.as<uint8_t>(), len, IGGY_INTEGRITY_LAYOUT_ONLY, c->dpos.as<uint64_t>(), cap, d_res,
+                       c->stream);
+    if (r) return r;
+    iggy_decode_result *h_res = (iggy_decode_result *)c->h_pinned;
+    HIP_OK(hipMemcpyAsync(h_res, d_res, sizeof(*h_res), hipMemcpyDeviceToHost, c->stream));
+    HIP_OK(hipStreamSynchronize(c->stream));
+    const iggy_decode_result res = *h_res;
+    if (res.error.kind == IGGY_ERR_TIMEOUT) reset_after_timeout(c);
+    if (res.error.kind != IGGY_OK) {
+        fill_err(err, res.error);
+        return (int)res.error.kind;
+    }
+    iggy_slice_result *d_out = c->slres.as<iggy_slice_result>(0);
+    uint8_t *d_hdr = c->slres.as<uint8_t>(256);
+    r = iggy_codec_select_slice_device(c, c->din.as<uint8_t>(), c->dpos.as<uint64_t>(), res.frame_count, q, d_out,
+                                       d_hdr, c->stream);
+    if (r) return r;
+    uint8_t *h = (uint8_t *)c->h_pinned + 1024;
+    HIP_OK(hipMemcpyAsync(h, d_out, 512, hipMemcpyDeviceToHost, c->stream));
+    HIP_OK(hipStreamSynchronize(c->stream));
+    memcpy(out, h, sizeof(*out));
+    if (header_out && out->selected) memcpy(header_out, h + 256, 256);
+    return 0;
+}
+
+int iggy_codec_stamp_batch_device(iggy_codec_ctx *c, uint8_t *d_record, const uint64_t *d_frame_pos,
+                                  uint64_t nframes, uint64_t base_offset, uint64_t base_timestamp,
+                                  iggy_batch_header *d_header, void *stream) {
+    if (!c || !d_record || (nframes && !d_frame_pos)) return IGGY_ERR_INVALID_ARGUMENT;
+    hipStream_t s = pick(c, stream);
+    int r = c->sl.ensure(512 + 4);
+    r |= c->gbsums.ensure(((44 + 8 * nframes) / 1024 + 2) * 64);
+    if (r) return IGGY_ERR_DEVICE;
+    iggy_batch_header *dh = c->sl.as<iggy_batch_header>(64);
+    uint64_t *dn = c->sl.as<uint64_t>(8), *dcs = c->sl.as<uint64_t>(24);
+    hipLaunchKernelGGL(k_stamp_prep, dim3(1), dim3(64), 0, s, (const uint8_t *)d_record, base_offset, base_timestamp,
+                       nframes, dh, dn);
+    CsSource src{nullptr, d_record + kHdr, d_frame_pos};
+    hipLaunchKernelGGL(k_bsum_blocks, dim3(c->ncu * 4), dim3(256), 0, s, (const iggy_batch_header *)dh,
+                       (const uint64_t *)dn, src, c->gbsums.as<uint64_t>(), nullptr);
+    hipLaunchKernelGGL(k_bsum_chain, dim3(1), dim3(64), 0, s, (const iggy_batch_header *)dh, (const uint64_t *)dn,
+                       src, (const uint64_t *)c->gbsums.as<uint64_t>(), c->sl.as<uint8_t>(128), dcs, nullptr);
+    hipLaunchKernelGGL(k_stamp_finish, dim3(1), dim3(64), 0, s, d_record, (const iggy_batch_header *)dh,
+                       (const uint64_t *)dcs, d_header);
     HIP_OK(hipGetLastError());
     return 0;
 }

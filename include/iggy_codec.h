@@ -258,6 +258,58 @@ int iggy_codec_xxh3_64_ranges_device(iggy_codec_ctx *ctx, const uint8_t *d_data,
                                      const uint64_t *d_offsets, const uint32_t *d_lengths,
                                      uint64_t n, uint64_t *d_out, void *stream);
 
+/* ------------------------------------------------- poll-path slicing (a17+) */
+/* MessageLookup (core/partitions/src/journal.rs:68-95). */
+#define IGGY_LOOKUP_OFFSET 0
+#define IGGY_LOOKUP_TIMESTAMP 1
+typedef struct iggy_slice_query {
+    uint32_t kind;             /* IGGY_LOOKUP_* */
+    uint32_t count;            /* query.count() */
+    uint64_t value;            /* offset (>=) or timestamp (base_timestamp >=) */
+    uint64_t ceiling;          /* inclusive commit frontier: no offset above it is served */
+    uint32_t already_matched;  /* messages matched by earlier batches of this poll */
+    uint32_t _pad;
+} iggy_slice_query;
+
+/* select_batch_slice (journal.rs:1025-1086) plus the header that
+ * push_selected_batch_fragments (journal.rs:1096-1137) serves it with. 128 B. */
+typedef struct iggy_slice_result {
+    uint32_t selected;             /* 0 = None: nothing of this batch is served */
+    uint32_t full_body;            /* 1 = the whole record is forwarded by reference */
+    uint64_t start, end;           /* blob-relative byte range of the selection */
+    uint32_t matched_messages;
+    uint32_t _pad0;
+    uint64_t last_matching_offset;
+    iggy_batch_header header;      /* rewritten (length, count, checksum) when partial,
+                                      the record's own header when full_body */
+    uint64_t _pad1[3];
+} iggy_slice_result;
+
+/* Select a poll's messages from one decoded record (host buffers): the record is
+ * decoded LayoutOnly first (its error is returned if it does not decode), then
+ * selected; header_out (nullable, 256 B) receives the header bytes to serve. */
+int iggy_codec_select_slice(iggy_codec_ctx *ctx, const uint8_t *record, uint64_t len,
+                            const iggy_slice_query *query, iggy_slice_result *out,
+                            uint8_t *header_out, iggy_wire_error *err);
+
+/* Device-resident form on a record already decoded by iggy_codec_decode_batch_device
+ * (d_frame_pos / nframes are its output): selection, rewritten header and its batch
+ * checksum (recomputed over the selected frames, batch.rs:439-450 via
+ * BatchHeader::checksum_for_blob, batch.rs:174-176) are enqueued on `stream`;
+ * *d_out and d_header_out (nullable, 256 B) are device memory. */
+int iggy_codec_select_slice_device(iggy_codec_ctx *ctx, const uint8_t *d_record,
+                                   const uint64_t *d_frame_pos, uint64_t nframes,
+                                   const iggy_slice_query *query, iggy_slice_result *d_out,
+                                   uint8_t *d_header_out, void *stream);
+
+/* stamp_prepare_for_persistence core (server_common/src/send_messages.rs:642-663) on a
+ * device-resident record whose frames were walked by a decode (d_frame_pos/nframes):
+ * base_offset and base_timestamp written, batch checksum recomputed, header rewritten
+ * in place; the new header also lands in *d_header (nullable, device memory). */
+int iggy_codec_stamp_batch_device(iggy_codec_ctx *ctx, uint8_t *d_record, const uint64_t *d_frame_pos,
+                                  uint64_t nframes, uint64_t base_offset, uint64_t base_timestamp,
+                                  iggy_batch_header *d_header, void *stream);
+
 /* ------------------------------------------------------------- profiling */
 /* When enabled, the context brackets the dominant kernel of every decode /
  * encode with hipEvents on the launch stream and accumulates its duration. */

@@ -394,6 +394,61 @@ int oracle_stamp_batch(uint8_t *batch, uint64_t len, uint64_t base_offset,
     return 0;
 }
 
+/* select_batch_slice — core/partitions/src/journal.rs:1025-1086, then the header
+ * push_selected_batch_fragments serves (journal.rs:1096-1137): a partial selection
+ * gets batch_length = 256 + (end - start), message_count = matched and the batch
+ * checksum of the byte range (BatchHeader::checksum_for_blob, batch.rs:174-176 ->
+ * calculate_batch_checksum's infallible walk over the slice). */
+int oracle_select_batch_slice(const uint8_t *record, uint64_t len, const iggy_slice_query *q,
+                              iggy_slice_result *out, uint8_t *header_out) {
+    iggy_batch_header h;
+    iggy_wire_error e;
+    memset(out, 0, sizeof(*out));
+    int rc = oracle_batch_header_decode(record, len, &h, &e);
+    if (rc) return rc;
+    if (len < h.batch_length) return IGGY_ERR_UNEXPECTED_EOF;
+    out->header = h;
+    uint32_t remaining = q->count > q->already_matched ? q->count - q->already_matched : 0; /* :1030 */
+    if (remaining == 0 || h.message_count == 0) return 0;                                   /* :1032 */
+    const uint8_t *blob = record + HDR;
+    uint64_t blob_len = h.batch_length - HDR, pos = 0, end, start = 0, sel_end = 0, last = 0;
+    uint32_t pl, uh, matched = 0;
+    int have = 0;
+    while (walk_next(blob, blob_len, pos, &end, &pl, &uh)) {                /* iter_with_offsets */
+        uint64_t offset = h.base_offset + rd32(blob + pos + 24);          /* :1043, wrapping */
+        if (offset > q->ceiling) break;                                   /* :1048 */
+        int selected = q->kind == IGGY_LOOKUP_OFFSET ? offset >= q->value  /* :1052-1065 */
+                                                     : h.base_timestamp >= q->value;
+        if (selected) {
+            if (!have) { start = pos; have = 1; }                          /* :1070 */
+            sel_end = end;
+            matched++;
+            last = offset;
+            if (matched == remaining) break;                              /* :1075 */
+        }
+        pos = end;
+    }
+    if (!have) return 0;                                                  /* `start?` */
+    out->selected = 1;
+    out->start = start;
+    out->end = sel_end;
+    out->matched_messages = matched;
+    out->last_matching_offset = last;
+    out->full_body = start == 0 && sel_end == blob_len;                   /* :1105 */
+    iggy_batch_header r = h;
+    if (!out->full_body) {                                                /* :1114-1124 */
+        r.batch_length = HDR + (sel_end - start);
+        r.message_count = matched;
+        r.batch_checksum = oracle_calculate_batch_checksum(&r, blob + start, sel_end - start);
+    }
+    out->header = r;
+    if (header_out) {
+        if (out->full_body) memcpy(header_out, record, HDR);
+        else oracle_batch_header_encode(&r, header_out);
+    }
+    return 0;
+}
+
 /* ---------------------------------------------------- synthetic inputs */
 static inline uint64_t splitmix64(uint64_t *s) {
     uint64_t z = (*s += 0x9E3779B97F4A7C15ull);

@@ -54,6 +54,11 @@ int oracle_poll_decode(const uint8_t *records, uint64_t len, int mode,
 int oracle_stamp_batch(uint8_t *batch, uint64_t len, uint64_t base_offset,
                        uint64_t base_timestamp, iggy_batch_header *out, iggy_wire_error *e);
 
+/* select_batch_slice + push_selected_batch_fragments header rewrite
+ * (core/partitions/src/journal.rs:1025-1137) on a record that decodes. */
+int oracle_select_batch_slice(const uint8_t *record, uint64_t len, const iggy_slice_query *q,
+                              iggy_slice_result *out, uint8_t *header_out);
+
 /* synthetic input generator shared by tests and bench (BASELINE.md:
  * splitmix64, seed 0x16619E3779B97F4A ^ partition). Builds a stamped,
  * checksummed record of n frames; payload length of frame i =

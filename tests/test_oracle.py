@@ -102,3 +102,63 @@ def test_synth_batches_verify():
         rc, e, h, frames = O.decode_batch_slice_with(rec, 0)
         assert rc == 0, (n, lo, hi, e)
         assert len(frames) == n
+
+
+# ---- poll-path slicing (core/partitions/src/journal.rs:1025-1137)
+def _stamped(n, lo, hi, base_offset, base_ts, seed=7):
+    rec = O.synth_batch(n, lo, hi, 0, seed=seed)
+    rc, e, h, out = O.stamp_batch(rec.copy(), base_offset, base_ts)
+    assert rc == 0, e
+    return np.frombuffer(out, dtype=np.uint8).copy()
+
+
+def test_select_slice_timestamp_at_exact_broker_time():
+    """journal.rs:1496-1533: three 8-byte messages, producer clock 900+i, broker
+    base_timestamp 1000; a poll at 1000 takes the whole batch, at 1001 nothing."""
+    ids = np.array([1, 0, 2, 0, 3, 0], dtype=np.uint64)
+    ots = np.array([900, 901, 902], dtype=np.uint64)
+    pay = np.frombuffer(b"abcdefgh" * 3, dtype=np.uint8).copy()
+    pls = np.full(3, 8, dtype=np.uint32)
+    raw = abi.RawMessages(3, ids.ctypes.data, ots.ctypes.data, pay.ctypes.data, pls.ctypes.data, None, None)
+    rc, e, enc = O.encode_batch(raw, 1)
+    assert rc == 0, e
+    rc, e, h, rec = O.stamp_batch(np.frombuffer(enc, dtype=np.uint8).copy(), 0, 1000)
+    rec = np.frombuffer(rec, dtype=np.uint8)
+    rc, r, hdr = O.select_slice(rec, abi.LOOKUP_TIMESTAMP, 1000, 10)
+    assert rc == 0 and r.selected and r.matched_messages == 3 and r.full_body
+    assert hdr == bytes(rec[:256])
+    rc, r, hdr = O.select_slice(rec, abi.LOOKUP_TIMESTAMP, 1001, 10)
+    assert rc == 0 and not r.selected and hdr is None
+
+
+def test_selected_slices_are_valid_batches():
+    """A partial selection is served as [rewritten header][blob slice]: it must decode
+    (Verify) on its own, with the clamped count and recomputed checksum."""
+    rec = _stamped(400, 10, 700, 5000, 77)
+    n_ok = 0
+    for value, count, ceiling in [(5000, 10, 2**64 - 1), (5123, 57, 2**64 - 1), (5390, 100, 2**64 - 1),
+                                  (5100, 1000, 5200), (4000, 3, 2**64 - 1), (5399, 1, 2**64 - 1)]:
+        rc, r, hdr = O.select_slice(rec, abi.LOOKUP_OFFSET, value, count, ceiling)
+        assert rc == 0 and r.selected
+        if r.full_body:
+            continue
+        sliced = np.frombuffer(hdr + bytes(rec[256 + r.start: 256 + r.end]), dtype=np.uint8)
+        rc2, e2, h2, frames = O.decode_batch_slice_with(sliced, abi.INTEGRITY_VERIFY)
+        assert rc2 == 0, (value, count, ceiling, e2)
+        assert h2.message_count == r.matched_messages and h2.base_offset == 5000
+        assert h2.batch_checksum == r.header.batch_checksum
+        n_ok += 1
+    assert n_ok >= 4
+
+
+def test_select_slice_non_monotone_offsets_keep_unselected_inside():
+    """A frame whose offset is below the query between two selected ones stays in the
+    byte range (and in the checksum walk) but not in matched_messages."""
+    rec = _stamped(6, 100, 100, 0, 1)
+    S = 48 + 100
+    for i, d in enumerate([0, 9, 3, 9, 9, 1]):  # offset_delta rewrite (layout stays valid)
+        struct.pack_into("<I", rec, 256 + i * S + 24, d)
+    rc, r, hdr = O.select_slice(rec, abi.LOOKUP_OFFSET, 5, 3)
+    assert rc == 0 and r.selected
+    assert (r.start, r.end, r.matched_messages, r.last_matching_offset) == (1 * S, 5 * S, 3, 9)
+    assert r.header.message_count == 3 and r.header.batch_length == 256 + 4 * S

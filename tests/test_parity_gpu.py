@@ -266,3 +266,81 @@ def _check_decode_integrity(cx, rec, integrity):
     if rc == 0:
         assert h.astuple() == oh.astuple()
         assert np.array_equal(frames, of)
+
+
+# ---- poll-path slicing and device stamp
+def _stamped_rec(n, lo, hi, base_offset, base_ts, seed):
+    rec = O.synth_batch(n, lo, hi, 0, seed=seed)
+    rc, e, h, out = O.stamp_batch(rec.copy(), base_offset, base_ts)
+    assert rc == 0
+    return np.frombuffer(out, dtype=np.uint8).copy()
+
+
+_SLICE_QUERIES = [
+    (abi.LOOKUP_OFFSET, 0, 10**9, 2**64 - 1), (abi.LOOKUP_OFFSET, 7000, 25, 2**64 - 1),
+    (abi.LOOKUP_OFFSET, 7000, 10**6, 2**64 - 1), (abi.LOOKUP_OFFSET, 9000, 5000, 12000),
+    (abi.LOOKUP_OFFSET, 5000, 1, 2**64 - 1), (abi.LOOKUP_OFFSET, 10**9, 5, 2**64 - 1),
+    (abi.LOOKUP_OFFSET, 6000, 3000, 5500), (abi.LOOKUP_OFFSET, 6024, 1024, 2**64 - 1),
+    (abi.LOOKUP_TIMESTAMP, 4242, 10, 2**64 - 1), (abi.LOOKUP_TIMESTAMP, 4243, 10, 2**64 - 1),
+    (abi.LOOKUP_TIMESTAMP, 0, 10**9, 6100),
+]
+
+
+@pytest.mark.parametrize("shape", [(3000, 1024, 1024), (2500, 10, 900), (40, 300, 300)])
+@pytest.mark.parametrize("q", _SLICE_QUERIES)
+def test_select_slice_matches_oracle(cx, shape, q):
+    n, lo, hi = shape
+    rec = _stamped_rec(n, lo, hi, 5000, 4242, seed=n)
+    kind, value, count, ceiling = q
+    for already in (0, 3):
+        rc, e, r, hdr = cx.select_slice(rec, kind, value, count, ceiling, already)
+        orc, orr, ohdr = O.select_slice(rec, kind, value, count, ceiling, already)
+        assert rc == orc == 0, e
+        assert r.astuple() == orr.astuple()
+        assert hdr == ohdr
+
+
+def test_select_slice_non_monotone_and_errors(cx):
+    rec = _stamped_rec(5000, 100, 100, 0, 1, seed=9)
+    S = 148
+    rng = np.random.default_rng(4)
+    for i in range(5000):  # scrambled offset deltas: unselected frames inside selections
+        struct.pack_into("<I", rec, 256 + i * S + 24, int(rng.integers(0, 6000)))
+    for value, count, ceiling in [(3000, 7, 2**64 - 1), (100, 2000, 5000), (5990, 4, 2**64 - 1), (0, 1, 10)]:
+        rc, e, r, hdr = cx.select_slice(rec, abi.LOOKUP_OFFSET, value, count, ceiling)
+        orc, orr, ohdr = O.select_slice(rec, abi.LOOKUP_OFFSET, value, count, ceiling)
+        assert rc == orc == 0 and r.astuple() == orr.astuple() and hdr == ohdr
+    bad = rec.copy()
+    bad[256 + 40] = 1  # frame 0 reserved: the batch does not decode -> its error, nothing selected
+    rc, e, r, hdr = cx.select_slice(bad, abi.LOOKUP_OFFSET, 0, 10)
+    orc, oe, _, _ = O.decode_batch_slice_with(bad, abi.INTEGRITY_LAYOUT_ONLY)
+    assert rc == orc != 0 and e.astuple() == oe.astuple()
+
+
+def test_device_select_and_stamp(cx):
+    import torch
+    rec = _stamped_rec(20000, 64, 2000, 100, 200, seed=11)
+    n = 20000
+    d_rec = torch.from_numpy(rec).to("cuda:0")
+    d_pos = torch.zeros(n, dtype=torch.int64, device="cuda:0")
+    d_res = torch.zeros(ctypes.sizeof(abi.DecodeResult), dtype=torch.uint8, device="cuda:0")
+    s = torch.cuda.current_stream().cuda_stream
+    assert cx.decode_device(d_rec.data_ptr(), rec.size, 0, d_pos.data_ptr(), n, d_res.data_ptr(), s) == 0
+    d_sr = torch.zeros(ctypes.sizeof(abi.SliceResult), dtype=torch.uint8, device="cuda:0")
+    d_hdr = torch.zeros(256, dtype=torch.uint8, device="cuda:0")
+    q = abi.SliceQuery(abi.LOOKUP_OFFSET, 777, 5100, 2**64 - 1, 0, 0)
+    assert cx.select_slice_device(d_rec.data_ptr(), d_pos.data_ptr(), n, q, d_sr.data_ptr(), d_hdr.data_ptr(), s) == 0
+    # stamp the same record in place (new base values), then re-verify it
+    d_h = torch.zeros(64, dtype=torch.uint8, device="cuda:0")
+    assert cx.stamp_device(d_rec.data_ptr(), d_pos.data_ptr(), n, 424242, 999, d_h.data_ptr(), s) == 0
+    torch.cuda.synchronize()
+    sr = abi.SliceResult.from_buffer_copy(d_sr.cpu().numpy().tobytes())
+    orc, orr, ohdr = O.select_slice(rec, abi.LOOKUP_OFFSET, 5100, 777)
+    assert sr.astuple() == orr.astuple() and d_hdr.cpu().numpy().tobytes() == ohdr
+    stamped = d_rec.cpu().numpy()
+    orc, oe, oh, oout = O.stamp_batch(rec.copy(), 424242, 999)
+    assert stamped.tobytes() == oout
+    h = abi.BatchHeader.from_buffer_copy(d_h.cpu().numpy().tobytes())
+    assert h.astuple() == oh.astuple()
+    rc, e, hh, _ = cx.decode_batch_slice_with(stamped, abi.INTEGRITY_VERIFY)
+    assert rc == 0, e
