@@ -74,7 +74,8 @@ struct iggy_codec_ctx {
     uint64_t dec_cap_len = 0;
     DevBuf dsync;    // exited | first_bad | spec_fail | bar[4] | misc[16] | small[512]
     DevBuf dsums, derr;
-    DevBuf gtiles_s, gtiles_x, gtiles_cnt, gtiles_list, gtiles_base, gfpos, gcs, gbsums;
+    DevBuf gtiles_s, gtiles_x, gtiles_cnt, gtiles_e, gtiles_base, ggrp, gfpos, gcs, gbsums;
+    int gen_grid = 0;  // co-resident WGs of k_decode_general
     DevBuf dresult;  // iggy_decode_result + iggy_encode_result + u64 scratch
     // sync-API staging
     DevBuf din, dpos, dout;
@@ -107,7 +108,8 @@ int ensure_decode_scratch(iggy_codec_ctx *c, uint64_t len) {
     const uint64_t L = std::max<uint64_t>(len, 1 << 20);
     const uint64_t max_frames = L / 48 + 2;
     const uint64_t max_chunks = (max_frames + 6) / 256 + 2;
-    const uint64_t ntiles = L / kTile + 2;
+    const uint64_t ntiles = L / kTileMin + 2;
+    const uint64_t ngroups = ntiles / 64 + 2;
     const uint64_t max_blocks = (44 + 8 * max_frames) / 1024 + 2;
     int r = 0;
     if (!c->dsync.p) {
@@ -123,7 +125,8 @@ int ensure_decode_scratch(iggy_codec_ctx *c, uint64_t len) {
     r |= c->gtiles_s.ensure(ntiles * 8);
     r |= c->gtiles_x.ensure(ntiles * 8);
     r |= c->gtiles_cnt.ensure(ntiles * 4);
-    r |= c->gtiles_list.ensure(ntiles * kTileCap * 2);
+    r |= c->gtiles_e.ensure(ntiles * 8);
+    r |= c->ggrp.ensure(ngroups * kGrpWords * 8);
     r |= c->gtiles_base.ensure(ntiles * 8);
     r |= c->gfpos.ensure(max_frames * 8);
     r |= c->gcs.ensure(max_frames * 8);
@@ -150,7 +153,8 @@ GeneralScratch gscratch(iggy_codec_ctx *c) {
     g.tile_s = c->gtiles_s.as<uint64_t>();
     g.tile_x = c->gtiles_x.as<uint64_t>();
     g.tile_cnt = c->gtiles_cnt.as<uint32_t>();
-    g.tile_list = c->gtiles_list.as<uint16_t>();
+    g.tile_e = c->gtiles_e.as<uint64_t>();
+    g.grp = c->ggrp.as<uint64_t>();
     g.tile_base = c->gtiles_base.as<uint64_t>();
     g.fpos = c->gfpos.as<uint64_t>();
     g.cs = c->gcs.as<uint64_t>();
@@ -209,10 +213,10 @@ int enqueue_decode(iggy_codec_ctx *c, const uint8_t *d_body, uint64_t len, int i
     prof_end(c, 0, s);
     HIP_OK(hipGetLastError());
     if (verify)
-        hipLaunchKernelGGL(k_decode_general<true>, dim3(c->ncu), dim3(256), 0, s, d_body, len, d_pos,
+        hipLaunchKernelGGL(k_decode_general<true>, dim3(c->gen_grid), dim3(256), 0, s, d_body, len, d_pos,
                            cap, d_res, gs);
     else
-        hipLaunchKernelGGL(k_decode_general<false>, dim3(c->ncu), dim3(256), 0, s, d_body, len,
+        hipLaunchKernelGGL(k_decode_general<false>, dim3(c->gen_grid), dim3(256), 0, s, d_body, len,
                            d_pos, cap, d_res, gs);
     HIP_OK(hipGetLastError());
     return 0;
@@ -298,6 +302,14 @@ int iggy_codec_create(int device, iggy_codec_ctx **out) {
                                 hipFuncAttributeMaxDynamicSharedMemorySize, kUniformLds) != hipSuccess)
             r = IGGY_ERR_DEVICE;
     }
+    if (!r) {
+        // the general decode's grid barriers need every WG co-resident
+        int occ_t = 0, occ_f = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ_t, k_decode_general<true>, 256, 0) != hipSuccess ||
+            hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ_f, k_decode_general<false>, 256, 0) != hipSuccess)
+            r = IGGY_ERR_DEVICE;
+        c->gen_grid = c->ncu * std::max(1, std::min(4, std::min(occ_t, occ_f)));
+    }
     for (int w = 0; w < 2 && !r; ++w)
         if (hipEventCreate(&c->ev0[w]) != hipSuccess || hipEventCreate(&c->ev1[w]) != hipSuccess)
             r = IGGY_ERR_DEVICE;
@@ -334,7 +346,7 @@ void iggy_codec_destroy(iggy_codec_ctx *c) {
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     DevBuf *bufs[] = {&c->dsync, &c->dsums, &c->derr, &c->gtiles_s, &c->gtiles_x,
-                      &c->gtiles_cnt, &c->gtiles_list, &c->gtiles_base, &c->gfpos, &c->gcs,
+                      &c->gtiles_cnt, &c->gtiles_e, &c->gtiles_base, &c->ggrp, &c->gfpos, &c->gcs,
                       &c->gbsums, &c->dresult, &c->din, &c->dpos, &c->dout, &c->epl, &c->euh,
                       &c->etile, &c->ecs, &c->emisc, &c->eids, &c->eots, &c->epay, &c->eplen,
                       &c->euhb, &c->euhl, &c->hbsums, &c->ppos, &c->pmsgs, &c->sl, &c->slres};
