@@ -74,7 +74,7 @@ struct iggy_codec_ctx {
     uint64_t dec_cap_len = 0;
     DevBuf dsync;    // exited | first_bad | spec_fail | bar[4] | misc[16] | small[512]
     DevBuf dsums, derr;
-    DevBuf gtiles_s, gtiles_x, gtiles_cnt, gtiles_e, gtiles_base, ggrp, gfpos, gcs, gbsums;
+    DevBuf gtiles_s, gtiles_x, gtiles_cnt, gtiles_pre, gtiles_list, gtiles_e, gtiles_base, ggrp, gfpos, gcs, gflen, gbsums;
     int gen_grid = 0;  // co-resident WGs of k_decode_general
     DevBuf dresult;  // iggy_decode_result + iggy_encode_result + u64 scratch
     // sync-API staging
@@ -109,7 +109,7 @@ int ensure_decode_scratch(iggy_codec_ctx *c, uint64_t len) {
     const uint64_t max_frames = L / 48 + 2;
     const uint64_t max_chunks = (max_frames + 6) / 256 + 2;
     const uint64_t ntiles = L / kTileMin + 2;
-    const uint64_t ngroups = ntiles / 64 + 2;
+    const uint64_t ngroups = ntiles / kGrpTiles + 2;
     const uint64_t max_blocks = (44 + 8 * max_frames) / 1024 + 2;
     int r = 0;
     if (!c->dsync.p) {
@@ -126,10 +126,13 @@ int ensure_decode_scratch(iggy_codec_ctx *c, uint64_t len) {
     r |= c->gtiles_x.ensure(ntiles * 8);
     r |= c->gtiles_cnt.ensure(ntiles * 4);
     r |= c->gtiles_e.ensure(ntiles * 8);
+    r |= c->gtiles_pre.ensure(ntiles * 4);
+    r |= c->gtiles_list.ensure(tile_list_words(L) * 4);
     r |= c->ggrp.ensure(ngroups * kGrpWords * 8);
     r |= c->gtiles_base.ensure(ntiles * 8);
     r |= c->gfpos.ensure(max_frames * 8);
     r |= c->gcs.ensure(max_frames * 8);
+    r |= c->gflen.ensure(max_frames * 8);
     r |= c->gbsums.ensure(max_blocks * 64);
     if (r) return IGGY_ERR_DEVICE;
     c->dec_cap_len = L;
@@ -154,10 +157,13 @@ GeneralScratch gscratch(iggy_codec_ctx *c) {
     g.tile_x = c->gtiles_x.as<uint64_t>();
     g.tile_cnt = c->gtiles_cnt.as<uint32_t>();
     g.tile_e = c->gtiles_e.as<uint64_t>();
+    g.tile_pre = c->gtiles_pre.as<uint32_t>();
+    g.tile_list = c->gtiles_list.as<uint32_t>();
     g.grp = c->ggrp.as<uint64_t>();
     g.tile_base = c->gtiles_base.as<uint64_t>();
     g.fpos = c->gfpos.as<uint64_t>();
     g.cs = c->gcs.as<uint64_t>();
+    g.flen = c->gflen.as<uint64_t>();
     g.bsums = c->gbsums.as<uint64_t>();
     g.misc = c->dsync.as<uint64_t>(kSyncMisc);
     g.bar = c->dsync.as<uint32_t>(kSyncBar);
@@ -213,10 +219,10 @@ int enqueue_decode(iggy_codec_ctx *c, const uint8_t *d_body, uint64_t len, int i
     prof_end(c, 0, s);
     HIP_OK(hipGetLastError());
     if (verify)
-        hipLaunchKernelGGL(k_decode_general<true>, dim3(c->gen_grid), dim3(256), 0, s, d_body, len, d_pos,
+        hipLaunchKernelGGL(k_decode_general<true>, dim3(c->gen_grid), dim3(kGenThreads), 0, s, d_body, len, d_pos,
                            cap, d_res, gs);
     else
-        hipLaunchKernelGGL(k_decode_general<false>, dim3(c->gen_grid), dim3(256), 0, s, d_body, len,
+        hipLaunchKernelGGL(k_decode_general<false>, dim3(c->gen_grid), dim3(kGenThreads), 0, s, d_body, len,
                            d_pos, cap, d_res, gs);
     HIP_OK(hipGetLastError());
     return 0;
@@ -305,10 +311,10 @@ int iggy_codec_create(int device, iggy_codec_ctx **out) {
     if (!r) {
         // the general decode's grid barriers need every WG co-resident
         int occ_t = 0, occ_f = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ_t, k_decode_general<true>, 256, 0) != hipSuccess ||
-            hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ_f, k_decode_general<false>, 256, 0) != hipSuccess)
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ_t, k_decode_general<true>, kGenThreads, 0) != hipSuccess ||
+            hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ_f, k_decode_general<false>, kGenThreads, 0) != hipSuccess)
             r = IGGY_ERR_DEVICE;
-        c->gen_grid = c->ncu * std::max(1, std::min(4, std::min(occ_t, occ_f)));
+        c->gen_grid = c->ncu * std::max(1, std::min(2, std::min(occ_t, occ_f)));
     }
     for (int w = 0; w < 2 && !r; ++w)
         if (hipEventCreate(&c->ev0[w]) != hipSuccess || hipEventCreate(&c->ev1[w]) != hipSuccess)
@@ -346,7 +352,7 @@ void iggy_codec_destroy(iggy_codec_ctx *c) {
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     DevBuf *bufs[] = {&c->dsync, &c->dsums, &c->derr, &c->gtiles_s, &c->gtiles_x,
-                      &c->gtiles_cnt, &c->gtiles_e, &c->gtiles_base, &c->ggrp, &c->gfpos, &c->gcs,
+                      &c->gtiles_cnt, &c->gtiles_pre, &c->gtiles_list, &c->gtiles_e, &c->gtiles_base, &c->ggrp, &c->gfpos, &c->gcs, &c->gflen,
                       &c->gbsums, &c->dresult, &c->din, &c->dpos, &c->dout, &c->epl, &c->euh,
                       &c->etile, &c->ecs, &c->emisc, &c->eids, &c->eots, &c->epay, &c->eplen,
                       &c->euhb, &c->euhl, &c->hbsums, &c->ppos, &c->pmsgs, &c->sl, &c->slres};

@@ -5,26 +5,29 @@
 // One persistent launch (grid = every co-resident WG, bounded grid barriers)
 // that returns immediately unless the uniform-stride kernel left
 // result->status == kStatusNeedGeneral. The blob is cut into tiles of
-// T = 2^sh bytes, sized from the header's message count to hold ~8 frames
-// (4 KiB <= T <= 1 MiB); tiles form groups of 64. Phases:
-//   A  locate : one lane per tile finds the first candidate frame start (8 zero
-//               reserved bytes at +40 and lengths inside the blob; 256-B vector
-//               scan for a zero dword) and walks the candidate chain from it
-//               until it leaves the tile: start s_t, exit x_t, count cnt_t.
+// T = 2^sh bytes, sized from the header's message count to hold 8-16 frames
+// (4 KiB <= T <= 1 MiB); a group is 256 tiles, 4 per lane of one wave. Phases:
+//   A  locate : one lane per tile picks a speculative entry (a confirmed
+//               candidate frame start: 8 zero reserved bytes at +40, lengths
+//               inside the blob; 256-B vector scan for zero dwords) and walks
+//               the candidate chain from it until it leaves the tile, listing
+//               the frame offsets: start s_t, exit x_t, count cnt_t, list.
 //   B1 groups : one wave per group: is the group self-consistent when entered at
 //               its first start (every later tile entered at its own start, or
-//               spanned by one frame when it has none)? -> (S, X, CNT, ok, term).
-//   B2 link   : one wave chains groups from offset 0, 64 per ballot step; a
-//               group that is not entered at S or is not self-consistent is
-//               linked tile by tile (spans skipped, entries re-walked). The
-//               result is exactly the reference walk: true frame starts are
-//               always candidates and the first non-candidate ends the walk.
-//   C  scatter: one lane per accepted tile re-walks from its true entry: frame
-//               positions and stored checksums in walk order.
+//               spanned by one frame when it has none)? -> (S, X, CNT, ok, term)
+//               and each tile's frame prefix inside the group.
+//   B2 link   : one wave chains groups from offset 0, up to 64 per ballot step,
+//               advancing to the first group that is not entered at S or not
+//               self-consistent; that group is linked tile by tile (spans
+//               skipped, entries re-walked and re-listed). The result is exactly
+//               the reference walk: true frame starts are always candidates and
+//               the first non-candidate ends the walk.
+//   C  scatter: one lane per accepted tile copies its list to walk order:
+//               frame positions, stored checksums, hashed lengths.
 //   E  sums   : XXH3 stripe sums of the batch-checksum input, one wave / block.
 //   D + F     : wave 0 of WG 0 runs the serial scramble chain over the block
-//               sums while every other wave verifies frames, eight per wave
-//               (8 lanes per frame, 16 B per lane per stripe pair); then
+//               sums while every other wave verifies frames (8 lanes per frame,
+//               one 1024-B block per step, the next block in flight); then
 //               precedence resolution and the result.
 #include "codec_common.hpp"
 
@@ -34,18 +37,31 @@ constexpr uint32_t kTileShiftMin = 12, kTileShiftMax = 20;
 constexpr uint64_t kTileMin = 1ull << kTileShiftMin;  // host sizing unit
 constexpr uint64_t kNoStart = ~0ull;
 constexpr uint64_t kStopBit = 1ull << 63;
-constexpr uint32_t kGrpWords = 6;  // S, X, CNT, flags | base, mode
+constexpr uint32_t kGrpTiles = 256;  // 4 tiles per lane
+constexpr uint32_t kGrpWords = 6;    // S, X, CNT, flags | base, mode
 constexpr uint64_t kGrpOk = 1, kGrpTerm = 2;
+constexpr uint32_t kNotLive = ~0u;
+constexpr uint32_t kGenThreads = 512;  // one WG per CU: half the barrier arrivals of 2 x 256
+
+// list entries (u32 offsets from the tile start) per tile of 2^sh bytes
+__host__ __device__ __forceinline__ uint64_t tile_list_cap(uint32_t sh) { return ((1ull << sh) / 48) + 1; }
+// host sizing of the list area for a blob of up to L bytes (any tile size)
+__host__ __device__ __forceinline__ uint64_t tile_list_words(uint64_t L) {
+    return L / 48 + L / kTileMin + (1ull << kTileShiftMax) / 48 + 64;
+}
 
 struct GeneralScratch {
-    uint64_t *tile_s;    // [ntiles] first candidate start (blob offset) or kNoStart
+    uint64_t *tile_s;    // [ntiles] speculative entry (blob offset) or kNoStart
     uint64_t *tile_x;    // [ntiles] exit position (| kStopBit when the walk stopped inside)
-    uint32_t *tile_cnt;  // [ntiles] frames on the candidate chain inside the tile
+    uint32_t *tile_cnt;  // [ntiles] frames listed for the tile
+    uint32_t *tile_pre;  // [ntiles] frames before the tile inside its group (kNotLive: none)
+    uint32_t *tile_list; // [ntiles * tile_list_cap(sh)] frame offsets from the tile start
     uint64_t *tile_e;    // [ntiles] repaired groups: true entry (~0: no frame starts here)
     uint64_t *tile_base; // [ntiles] repaired groups: frames before the tile
     uint64_t *grp;       // [ngroups * kGrpWords]
     uint64_t *fpos;      // [max_frames] frame starts in walk order
     uint64_t *cs;        // [max_frames] stored checksums in walk order
+    uint64_t *flen;      // [max_frames] hashed lengths (frame size - 8) in walk order
     uint64_t *bsums;     // [max_blocks * 8]
     uint64_t *misc;      // [16]: 0 nwalk, 1 end (with stop bit), 2 first_bad enc
     uint32_t *bar;       // [4]: arrive counter, exit counter
@@ -90,7 +106,7 @@ __device__ __forceinline__ void gstamp(const GeneralScratch &gs, int idx, uint64
     if (blockIdx.x == 0 && threadIdx.x == 0) ((uint64_t *)(gs.small + 512))[idx] = v;
 }
 
-// tile size: ~8 frames of the header's average size, a power of two in range
+// tile size: 8-16 frames of the header's average size, a power of two in range
 __device__ __forceinline__ uint32_t tile_shift(uint64_t bl, uint32_t message_count) {
     const uint64_t want = 8 * (message_count ? bl / message_count : bl);
     uint32_t sh = kTileShiftMin;
@@ -98,13 +114,10 @@ __device__ __forceinline__ uint32_t tile_shift(uint64_t bl, uint32_t message_cou
     return sh;
 }
 
-// walk the candidate chain from p while p < hi (hi <= bl); EMIT writes every
-// frame's position (and stored checksum) at index base + k
-template <bool EMIT, bool CS>
+// walk the candidate chain from p while p < hi (hi <= bl); with a list, every
+// frame's offset from lo is recorded
 __device__ inline uint32_t walk(const uint8_t *blob, uint64_t bl, uint64_t p, uint64_t hi,
-                                uint64_t *x_out, uint64_t base = 0, uint64_t *fpos = nullptr,
-                                uint64_t *cs = nullptr, uint64_t *frame_pos = nullptr,
-                                uint64_t cap = 0) {
+                                uint64_t *x_out, uint32_t *list = nullptr, uint64_t lo = 0) {
     uint32_t cnt = 0;
     while (p < hi) {
         uint64_t e;
@@ -112,12 +125,7 @@ __device__ inline uint32_t walk(const uint8_t *blob, uint64_t bl, uint64_t p, ui
             *x_out = p | kStopBit;
             return cnt;
         }
-        if (EMIT) {
-            const uint64_t i = base + cnt;
-            fpos[i] = p;
-            if (CS) cs[i] = ld64_any(blob + p);
-            if (frame_pos && i < cap) frame_pos[i] = p;
-        }
+        if (list) list[cnt] = (uint32_t)(p - lo);
         ++cnt;
         p = e;
     }
@@ -190,8 +198,8 @@ __device__ inline uint64_t first_candidate(const uint8_t *blob, uint64_t bl, uin
 // whose pick disagrees with the true entry.
 constexpr int kPickTries = 8;
 __device__ inline void pick_start(const uint8_t *blob, uint64_t bl, uint64_t lo, uint64_t hi,
-                                  uint64_t *s_out, uint64_t *x_out, uint32_t *cnt_out) {
-    uint64_t bs = kNoStart, bx = kNoStart;
+                                  uint32_t *list, uint64_t *s_out, uint64_t *x_out, uint32_t *cnt_out) {
+    uint64_t bs = kNoStart, bx = kNoStart, listed = kNoStart;
     uint32_t bc = 0;
     bool bclean = false;
     uint64_t from = lo;
@@ -199,7 +207,8 @@ __device__ inline void pick_start(const uint8_t *blob, uint64_t bl, uint64_t lo,
         const uint64_t c = first_candidate(blob, bl, from, hi);
         if (c == kNoStart) break;
         uint64_t x;
-        const uint32_t n = walk<false, false>(blob, bl, c, hi, &x);
+        const uint32_t n = walk(blob, bl, c, hi, &x, list, lo);
+        listed = c;
         const bool clean = !(x & kStopBit);
         if (clean && n >= 2) {
             bs = c; bx = x; bc = n;
@@ -209,6 +218,10 @@ __device__ inline void pick_start(const uint8_t *blob, uint64_t bl, uint64_t lo,
             bs = c; bx = x; bc = n; bclean = clean;
         }
         from = c + 1;
+    }
+    if (bs != kNoStart && bs != listed) {
+        uint64_t x;
+        walk(blob, bl, bs, hi, &x, list, lo);
     }
     *s_out = bs;
     *x_out = bx;
@@ -241,12 +254,41 @@ __device__ __forceinline__ void piece(uint64_t &a0, uint64_t &a1, uint4 p, uint6
     a1 += mul32x32(w1 ^ s1) + w0;
 }
 
-// Frame verification, 8 frames per wave step: lane group fg (8 lanes) hashes
-// frame 8k+fg of the walk. Lane l = (m, par) owns accumulators 2m, 2m+1 for the
-// stripes of parity par: in every 1024-B block it reads the 16 B at
-// 128q + 16(m + 4 par), q = 0..7 (stripe 2q+par, words 2m, 2m+1). The pair of
+// Frame verification. Lane group fg (8 lanes) of verify wave vw hashes frames
+// f = 8 vw + fg + j * 8 nvw, j = 0, 1, ... at its own pace: every wave step
+// each group hashes one 1024-B block of its current frame while the next block
+// (or the next frame's first block and last stripe) is already loading, so a
+// group never waits on a frame boundary and never on the other groups' frame
+// sizes. Positions, lengths and stored checksums come from the scatter phase's
+// arrays (prefetched one frame ahead). Lane l = (m, par) owns accumulators
+// 2m, 2m+1 for the stripes of parity par: in every block it reads the 16 B at
+// 128q + 16(m + 4 par), q = 0..7 (stripe 2q+par, words 2m, 2m+1); the pair of
 // parity lanes is folded before each scramble; the last stripe and merge follow
 // the XXH3 long form (> 240 B). Shorter frames are hashed by one lane.
+struct VFrame {
+    uint64_t f, p, stored, L;
+};
+__device__ __forceinline__ VFrame vframe(const GeneralScratch &gs, uint64_t f, uint64_t nwalk) {
+    VFrame v;
+    v.f = f;
+    if (f < nwalk) {
+        v.p = gs.fpos[f];
+        v.stored = gs.cs[f];
+        v.L = gs.flen[f];
+    } else {
+        v.p = 0; v.stored = 0; v.L = 0;
+    }
+    return v;
+}
+__device__ __forceinline__ void vblock(const uint8_t *blob, const VFrame &v, uint32_t b, uint32_t par,
+                                       uint32_t poff, uint4 (&dst)[8]) {
+    const uint64_t nbF = (v.L - 1) / 1024, ns = ((v.L - 1) - 1024 * nbF) / 64;
+    const uint8_t *hb = blob + v.p + 8 + 1024ull * b + poff;
+#pragma unroll
+    for (int q = 0; q < 8; ++q)
+        dst[q] = (b < nbF || 2 * q + par < ns) ? ld128_any(hb + 128 * q) : make_uint4(0, 0, 0, 0);
+}
+
 __device__ inline void verify_frames(const uint8_t *blob, const GeneralScratch &gs, uint64_t nwalk,
                                      uint32_t vw, uint32_t nvw, int lane) {
     const uint32_t l = lane & 7, m = l >> 1, par = l & 1, fg = (uint32_t)lane >> 3;
@@ -261,43 +303,38 @@ __device__ inline void verify_frames(const uint8_t *blob, const GeneralScratch &
     const uint64_t init0 = par ? 0 : kAccInit[2 * m], init1 = par ? 0 : kAccInit[2 * m + 1];
     const uint64_t last0 = kSecretLast[2 * m], last1 = kSecretLast[2 * m + 1];
     const uint64_t mrg0 = kSecretMerge[2 * m], mrg1 = kSecretMerge[2 * m + 1];
-    for (uint64_t k = vw; 8 * k < nwalk; k += nvw) {
-        const uint64_t f = 8 * k + fg;
-        const bool valid = f < nwalk;
-        const uint64_t p = valid ? gs.fpos[f] : 0;
-        const uint64_t stored = valid ? gs.cs[f] : 0;
-        const uint64_t lens = ld64_any(blob + p + 32);
-        const uint64_t L = 40 + (uint64_t)(uint32_t)lens + (lens >> 32);
-        const bool lng = valid && L > 240;
-        const uint64_t nbF = lng ? (L - 1) / 1024 : 0;
-        const uint64_t ns = lng ? ((L - 1) - 1024 * nbF) / 64 : 0;
-        const uint32_t nsteps = (uint32_t)(nbF + (ns > 0));
-        uint32_t maxs = nsteps;
-        maxs = max(maxs, (uint32_t)__shfl_xor((int)maxs, 8));
-        maxs = max(maxs, (uint32_t)__shfl_xor((int)maxs, 16));
-        maxs = max(maxs, (uint32_t)__shfl_xor((int)maxs, 32));
-        const uint8_t *hb = blob + p + 8 + poff;
-        uint64_t a0 = init0, a1 = init1;
-        uint4 cur[8];
-        if (nsteps > 0) {
-#pragma unroll
-            for (int q = 0; q < 8; ++q)
-                cur[q] = (nbF > 0 || 2 * q + par < ns) ? ld128_any(hb + 128 * q) : make_uint4(0, 0, 0, 0);
-        }
-        for (uint32_t b = 0; b < maxs; ++b) {
-            if (b < nsteps) {
-                uint4 nxt[8];
-                const uint32_t b1 = b + 1;
-                if (b1 < nsteps) {
-                    const uint8_t *nb = hb + 1024ull * b1;
-#pragma unroll
-                    for (int q = 0; q < 8; ++q)
-                        nxt[q] = (b1 < nbF || 2 * q + par < ns) ? ld128_any(nb + 128 * q) : make_uint4(0, 0, 0, 0);
-                }
+    const uint64_t stride = 8ull * nvw;
+
+    VFrame cur = vframe(gs, 8ull * vw + fg, nwalk);
+    VFrame nxt = vframe(gs, cur.f + stride, nwalk);
+    uint4 blk[8], lastp = make_uint4(0, 0, 0, 0);
+    if (cur.f < nwalk && cur.L > 240) {
+        vblock(blob, cur, 0, par, poff, blk);
+        lastp = ld128_any(blob + cur.p + 8 + cur.L - 64 + 16 * m);
+    }
+    uint32_t b = 0;
+    uint64_t a0 = init0, a1 = init1;
+    while (__ballot(cur.f < nwalk)) {
+        if (cur.f < nwalk) {
+            const bool lng = cur.L > 240;
+            const uint64_t nbF = lng ? (cur.L - 1) / 1024 : 0;
+            const uint64_t ns = lng ? ((cur.L - 1) - 1024 * nbF) / 64 : 0;
+            const uint32_t nsteps = lng ? (uint32_t)(nbF + (ns > 0)) : 1u;
+            const bool fin = b + 1 == nsteps;
+            // prefetch: this frame's next block, or the next frame's first block + last stripe
+            uint4 nb[8], nlast = lastp;
+            if (!fin) {
+                vblock(blob, cur, b + 1, par, poff, nb);
+            } else if (nxt.f < nwalk && nxt.L > 240) {
+                vblock(blob, nxt, 0, par, poff, nb);
+                nlast = ld128_any(blob + nxt.p + 8 + nxt.L - 64 + 16 * m);
+            }
+            uint64_t h = 0;
+            if (lng) {
                 if (b < nbF) {
                     uint64_t p0[4] = {0, 0, 0, 0}, p1[4] = {0, 0, 0, 0};
 #pragma unroll
-                    for (int q = 0; q < 8; ++q) piece(p0[q & 3], p1[q & 3], cur[q], s0[q], s1[q]);
+                    for (int q = 0; q < 8; ++q) piece(p0[q & 3], p1[q & 3], blk[q], s0[q], s1[q]);
                     a0 += (p0[0] + p0[1]) + (p0[2] + p0[3]);
                     a1 += (p1[0] + p1[1]) + (p1[2] + p1[3]);
                     a0 += gdpp64<0xB1>(a0);
@@ -308,34 +345,41 @@ __device__ inline void verify_frames(const uint8_t *blob, const GeneralScratch &
                 } else {
 #pragma unroll
                     for (int q = 0; q < 8; ++q)
-                        if (2 * q + par < ns) piece(a0, a1, cur[q], s0[q], s1[q]);
+                        if (2 * q + par < ns) piece(a0, a1, blk[q], s0[q], s1[q]);
                 }
-                if (b1 < nsteps) {
-#pragma unroll
-                    for (int q = 0; q < 8; ++q) cur[q] = nxt[q];
+                if (fin) {
+                    a0 += gdpp64<0xB1>(a0);
+                    a1 += gdpp64<0xB1>(a1);
+                    piece(a0, a1, lastp, last0, last1);
+                    uint64_t t = fold64(a0 ^ mrg0, a1 ^ mrg1);
+                    t += gdpp64<0x4E>(t);
+                    t += gswz_xor4(t);
+                    h = avalanche(cur.L * P64_1 + t);
                 }
+            } else if (l == 0) {
+                h = xxh3_64_lane(blob + cur.p + 8, cur.L);
             }
+            if (fin) {
+                if (l == 0 && h != cur.stored)
+                    atomicMax((unsigned long long *)&gs.misc[2], (unsigned long long)~cur.f);
+                cur = nxt;
+                nxt = vframe(gs, cur.f + stride, nwalk);
+                b = 0;
+                a0 = init0;
+                a1 = init1;
+            } else {
+                ++b;
+            }
+#pragma unroll
+            for (int q = 0; q < 8; ++q) blk[q] = nb[q];
+            lastp = nlast;
         }
-        uint64_t h = 0;
-        if (lng) {
-            a0 += gdpp64<0xB1>(a0);
-            a1 += gdpp64<0xB1>(a1);
-            piece(a0, a1, ld128_any(blob + p + 8 + L - 64 + 16 * m), last0, last1);
-            uint64_t t = fold64(a0 ^ mrg0, a1 ^ mrg1);
-            t += gdpp64<0x4E>(t);
-            t += gswz_xor4(t);
-            h = avalanche(L * P64_1 + t);
-        } else if (valid && l == 0) {
-            h = xxh3_64_lane(blob + p + 8, L);
-        }
-        if (valid && l == 0 && h != stored)
-            atomicMax((unsigned long long *)&gs.misc[2], (unsigned long long)~f);
     }
 }
 
 // ------------------------------------------------------------------ kernel
 template <bool VERIFY>
-__global__ __launch_bounds__(256) void k_decode_general(const uint8_t *__restrict__ body,
+__global__ __launch_bounds__(kGenThreads) void k_decode_general(const uint8_t *__restrict__ body,
                                                         uint64_t len, uint64_t *frame_pos,
                                                         uint64_t cap, iggy_decode_result *result,
                                                         GeneralScratch gs) {
@@ -349,7 +393,8 @@ __global__ __launch_bounds__(256) void k_decode_general(const uint8_t *__restric
     const uint32_t sh = tile_shift(bl, h.message_count);
     const uint64_t T = 1ull << sh;
     const uint64_t ntiles = (bl + T - 1) >> sh;
-    const uint64_t ngroups = (ntiles + 63) / 64;
+    const uint64_t ngroups = (ntiles + kGrpTiles - 1) / kGrpTiles;
+    const uint64_t lcap = tile_list_cap(sh);
     const uint32_t nwg = gridDim.x;
     const uint64_t gtid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const uint64_t gthreads = (uint64_t)nwg * blockDim.x;
@@ -362,13 +407,14 @@ __global__ __launch_bounds__(256) void k_decode_general(const uint8_t *__restric
     // ---------------- A: locate
     for (uint64_t t = gtid; t < ntiles; t += gthreads) {
         const uint64_t lo = t << sh, hi = min(lo + T, bl);
+        uint32_t *list = gs.tile_list + t * lcap;
         uint64_t s = kNoStart, x = kNoStart;
         uint32_t cnt = 0;
         if (t == 0) {
             s = 0;
-            cnt = walk<false, false>(blob, bl, 0, hi, &x);
+            cnt = walk(blob, bl, 0, hi, &x, list, 0);
         } else {
-            pick_start(blob, bl, lo, hi, &s, &x, &cnt);
+            pick_start(blob, bl, lo, hi, list, &s, &x, &cnt);
         }
         gs.tile_s[t] = s;
         gs.tile_cnt[t] = cnt;
@@ -377,39 +423,70 @@ __global__ __launch_bounds__(256) void k_decode_general(const uint8_t *__restric
     ok &= grid_barrier(gs.bar, nwg * ++phase, t0);
     gstamp(gs, 1, rt_now() - t0);
 
-    // ---------------- B1: group summaries (one wave per 64 tiles)
+    // ---------------- B1: group summaries (one wave per 256 tiles, 4 per lane)
     for (uint64_t g = wid; g < ngroups; g += nwaves) {
-        const uint64_t t = 64 * g + lane;
-        const bool in = t < ntiles;
-        const uint64_t s = in ? gs.tile_s[t] : kNoStart;
-        const uint64_t x = in ? gs.tile_x[t] : 0;
-        const uint32_t cnt = in ? gs.tile_cnt[t] : 0;
-        const bool has = s != kNoStart;
-        const uint64_t termmask = __ballot(has && ((x & kStopBit) || x >= bl));
+        // lane-local fold over its 4 tiles, assuming the lane is entered at its first start
+        const uint64_t tb = (uint64_t)kGrpTiles * g + 4 * lane;
+        bool lhas = false, lok = true, lterm = false;
+        uint64_t ls = kNoStart, lx = 0, lhi = 0;
+        uint32_t lc = 0, pre[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const uint64_t t = tb + i;
+            pre[i] = kNotLive;
+            if (t >= ntiles || lterm) continue;
+            const uint64_t s = gs.tile_s[t], x = gs.tile_x[t];
+            const uint32_t c = gs.tile_cnt[t];
+            const uint64_t hi_t = min((t + 1) << sh, bl);
+            lhi = hi_t;
+            if (s != kNoStart && !(lhas && lx >= hi_t)) {  // else spanned by the running frame
+                if (lhas) lok &= s == lx;
+                else ls = s;
+                lhas = true;
+                pre[i] = lc;
+                lc += c;
+                lx = x;
+                lterm = (x & kStopBit) || x >= bl;
+            } else if (lhas) {
+                lok &= lx >= hi_t;  // must be spanned by the frame that entered it
+            }
+        }
+        const uint64_t termmask = __ballot(lhas && lterm);
         const int last = termmask ? __builtin_ctzll(termmask) : 63;
-        const uint64_t hasmask = __ballot(has && lane <= last);
+        const bool live = lhas && lane <= last;
+        const uint64_t hasmask = __ballot(live);
         uint64_t S = kNoStart, X = 0, CNT = 0, flags = kGrpOk;
+        uint32_t lpre = 0;
         if (hasmask) {
             const int f0 = __builtin_ctzll(hasmask);
             const int lh = 63 - __builtin_clzll(hasmask);
-            // predecessor exit of lane l: max exit over the group's live starts before l
-            uint64_t pm = (has && lane <= last) ? x : 0;
+            uint64_t pm = live ? lx : 0;  // max exit over live lanes up to this one
 #pragma unroll
             for (int d = 1; d < 64; d <<= 1) {
                 const uint64_t o = __shfl_up(pm, d);
                 if (lane >= d) pm = max(pm, o);
             }
-            uint64_t pred = __shfl_up(pm, 1);
-            const uint64_t hi_t = min((t + 1) << sh, bl);
-            const bool okl = !in || lane <= f0 || lane > last || (has ? s == pred : pred >= hi_t);
+            const uint64_t pred = __shfl_up(pm, 1);
+            const bool okl = lane < f0 || lane > last || lhi == 0 ||
+                             (lok && (lane == f0 || (lhas ? ls == pred : pred >= lhi)));
             if (__ballot(!okl)) flags = 0;
-            uint64_t c = (has && lane <= last) ? cnt : 0;
+            const uint64_t c = live ? lc : 0;
+            uint64_t inc = c;
 #pragma unroll
-            for (int d = 32; d >= 1; d >>= 1) c += __shfl_xor(c, d);
-            S = __shfl(s, f0);
-            X = __shfl(x, lh);
-            CNT = c;
+            for (int d = 1; d < 64; d <<= 1) {
+                const uint64_t o = __shfl_up(inc, d);
+                if (lane >= d) inc += o;
+            }
+            lpre = (uint32_t)(inc - c);
+            S = __shfl(ls, f0);
+            X = __shfl(lx, lh);
+            CNT = __shfl(inc, 63);
             if (termmask) flags |= kGrpTerm;
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const uint64_t t = tb + i;
+            if (t < ntiles) gs.tile_pre[t] = (live && pre[i] != kNotLive) ? lpre + pre[i] : kNotLive;
         }
         if (lane == 0) {
             uint64_t *q = gs.grp + kGrpWords * g;
@@ -425,17 +502,20 @@ __global__ __launch_bounds__(256) void k_decode_general(const uint8_t *__restric
         uint64_t total = 0;  // frames accepted so far
         bool ended = false;  // the walk stopped (stop bit) or reached the blob end
         uint64_t nfast = 0, nsum = 0, nspan = 0, nrep = 0;  // diagnostics
-        for (uint64_t G0 = 0; G0 < ngroups; G0 += 64) {
+        uint64_t G0 = 0;
+        while (G0 < ngroups) {
             const uint64_t g = G0 + lane;
             const bool in = g < ngroups;
             uint64_t *q = gs.grp + kGrpWords * g;
             if (ended) {
                 if (in) q[5] = 0;
+                G0 += 64;
                 continue;
             }
             const uint64_t S = in ? q[0] : kNoStart, X = in ? q[1] : 0, CNT = in ? q[2] : 0;
             const uint64_t flags = in ? q[3] : 0;
             const bool has = S != kNoStart;
+            const uint64_t ghi = min(min((uint64_t)kGrpTiles * (g + 1), ntiles) << sh, bl);
             const uint64_t termmask = __ballot(in && has && (flags & kGrpTerm));
             const int last = termmask ? __builtin_ctzll(termmask) : 63;
             uint64_t pm = (in && has && lane <= last) ? X : 0;
@@ -447,90 +527,204 @@ __global__ __launch_bounds__(256) void k_decode_general(const uint8_t *__restric
             uint64_t pred = __shfl_up(pm, 1);
             if (lane == 0) pred = 0;
             pred = max(pred, e);
-            const uint64_t ghi = min(min(64 * (g + 1), ntiles) << sh, bl);
             const bool okl = !in || lane > last || ((flags & kGrpOk) && (has ? S == pred : pred >= ghi));
-            if (__ballot(!okl) == 0) {
-                const uint64_t c = (in && has && lane <= last) ? CNT : 0;
+            const uint64_t badmask = __ballot(!okl);
+            // lanes before the first failing one are accepted as summarised
+            const int nacc = badmask ? __builtin_ctzll(badmask) : 64;
+            if (nacc > 0) {
+                const bool acc = in && lane < nacc;
+                const uint64_t c = (acc && has && lane <= last) ? CNT : 0;
                 uint64_t inc = c;
 #pragma unroll
                 for (int d = 1; d < 64; d <<= 1) {
                     const uint64_t o = __shfl_up(inc, d);
                     if (lane >= d) inc += o;
                 }
-                if (in) {
+                if (acc) {
                     q[4] = total + inc - c;
                     q[5] = (has && lane <= last) ? 1 : 0;
                 }
                 total += __shfl(inc, 63);
                 ++nfast;
-                if (termmask) {
+                if (termmask && last < nacc) {
                     e = __shfl(X, last);
                     ended = true;
                 } else {
-                    e = max(e, __shfl(pm, 63));
+                    e = max(e, __shfl(pm, nacc - 1));
                 }
+            }
+            if (nacc == 64 || ended) {
+                G0 += 64;
                 continue;
             }
-            // exact sequential rule, group by group
-            for (int l = 0; l < 64; ++l) {
-                const uint64_t gg = G0 + l;
-                if (gg >= ngroups) break;
-                const uint64_t Sl = __shfl(S, l), Xl = __shfl(X, l), Cl = __shfl(CNT, l);
-                const uint64_t Fl = __shfl(flags, l);
-                const uint64_t ghl = __shfl(ghi, l);
-                uint64_t *ql = gs.grp + kGrpWords * gg;
-                if (ended) {
-                    if (lane == 0) ql[5] = 0;
-                    continue;
-                }
-                if ((Fl & kGrpOk) && Sl != kNoStart && Sl == e) {
-                    if (lane == 0) { ql[4] = total; ql[5] = 1; }
-                    total += Cl;
-                    ++nsum;
-                    e = Xl;
-                    if (Fl & kGrpTerm) ended = true;
-                    continue;
-                }
-                if ((Fl & kGrpOk) && Sl == kNoStart && e >= ghl) {
-                    if (lane == 0) ql[5] = 0;  // one frame spans the whole group
-                    ++nspan;
-                    continue;
-                }
-                // tile by tile
-                const uint64_t t = 64 * gg + lane;
-                const bool tin = t < ntiles;
-                const uint64_t ts = tin ? gs.tile_s[t] : kNoStart, tx = tin ? gs.tile_x[t] : 0;
-                const uint32_t tc = tin ? gs.tile_cnt[t] : 0;
-                for (int u = 0; u < 64; ++u) {
-                    const uint64_t tt = 64 * gg + u;
-                    if (tt >= ntiles) break;
-                    const uint64_t su = __shfl(ts, u), xu = __shfl(tx, u);
-                    const uint32_t cu = __shfl(tc, u);
-                    if (lane == 0) {
-                        const uint64_t hi = min((tt + 1) << sh, bl);
-                        uint64_t te = ~0ull;
-                        if (!ended && e < hi) {
-                            te = e;
-                            gs.tile_base[tt] = total;
-                            if (e == su) {
-                                total += cu;
-                                e = xu;
-                            } else {
-                                uint64_t x2;
-                                total += walk<false, false>(blob, bl, e, hi, &x2);
-                                e = x2;
-                            }
-                            if ((e & kStopBit) || e >= bl) ended = true;
-                        }
-                        gs.tile_e[tt] = te;
-                    }
-                    e = __shfl(e, 0);
-                    total = __shfl(total, 0);
-                    ended = __shfl((int)ended, 0) != 0;
-                }
-                if (lane == 0) ql[5] = 2;
-                ++nrep;
+            // group G0 + nacc, exactly
+            const uint64_t gg = G0 + nacc;
+            if (gg >= ngroups) break;
+            const uint64_t Sl = __shfl(S, nacc), Xl = __shfl(X, nacc), Cl = __shfl(CNT, nacc);
+            const uint64_t Fl = __shfl(flags, nacc), ghl = __shfl(ghi, nacc);
+            uint64_t *ql = gs.grp + kGrpWords * gg;
+            G0 = gg + 1;
+            if ((Fl & kGrpOk) && Sl != kNoStart && Sl == e) {
+                if (lane == 0) { ql[4] = total; ql[5] = 1; }
+                total += Cl;
+                ++nsum;
+                e = Xl;
+                if (Fl & kGrpTerm) ended = true;
+                continue;
             }
+            if ((Fl & kGrpOk) && Sl == kNoStart && e >= ghl) {
+                if (lane == 0) ql[5] = 0;  // one frame spans the whole group
+                ++nspan;
+                continue;
+            }
+            // tile by tile: lane l holds tiles 4l..4l+3 of the group
+            uint64_t ts[4], tx[4];
+            uint32_t tc[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const uint64_t t = (uint64_t)kGrpTiles * gg + 4 * lane + i;
+                const bool tin = t < ntiles;
+                ts[i] = tin ? gs.tile_s[t] : kNoStart;
+                tx[i] = tin ? gs.tile_x[t] : 0;
+                tc[i] = tin ? gs.tile_cnt[t] : 0;
+            }
+            // Parallel repair. From tile k0 (true entry e), every lane folds its 4
+            // tiles twice: as B1 assumed (its first start entered, later tiles entered
+            // at their start unless the running exit spans them) and as the true walk
+            // does given the exits of the lanes before it. The first tile where the
+            // two disagree (or the true walk finds no start at its entry) is the first
+            // break in sequential order: every tile before it is accepted as listed,
+            // that tile is re-walked from its true entry, and the next pass starts
+            // after it. One scan + one walk per break.
+            const uint64_t gt0 = (uint64_t)kGrpTiles * gg;
+            uint32_t k0 = 0;
+            while (!ended && k0 < kGrpTiles && gt0 + k0 < ntiles) {
+                // pass 1: the lane's exit as B1 assumed it
+                bool seen = false, lterm = false;
+                uint64_t lx = 0;
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const uint32_t k = 4 * lane + i;
+                    const uint64_t t = gt0 + k;
+                    if (k < k0 || t >= ntiles || lterm || ts[i] == kNoStart) continue;
+                    const uint64_t hi = min((t + 1) << sh, bl);
+                    if (seen && lx >= hi) continue;  // spanned
+                    seen = true;
+                    lx = tx[i];
+                    lterm = (lx & kStopBit) || lx >= bl;
+                }
+                const uint64_t tm = __ballot(seen && lterm);
+                const int tl = tm ? __builtin_ctzll(tm) : 63;
+                uint64_t pm = (seen && lane <= tl) ? lx : 0;
+#pragma unroll
+                for (int d = 1; d < 64; d <<= 1) {
+                    const uint64_t o = __shfl_up(pm, d);
+                    if (lane >= d) pm = max(pm, o);
+                }
+                uint64_t r = __shfl_up(pm, 1);
+                if (lane == 0) r = 0;
+                r = max(r, e);
+                // pass 2: the true walk through the lane vs the assumption
+                uint32_t kbad = kGrpTiles;
+                uint64_t ebad = 0;
+                bool aseen = false, stop = false;
+                uint64_t ax = 0;
+                uint32_t live = 0;  // bit i: tile i entered at its start by the true walk
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const uint32_t k = 4 * lane + i;
+                    const uint64_t t = gt0 + k;
+                    if (k < k0 || t >= ntiles || stop || kbad != kGrpTiles || lane > tl) continue;
+                    const uint64_t hi = min((t + 1) << sh, bl);
+                    const bool has = ts[i] != kNoStart;
+                    const bool assumed = has && (!aseen || ax < hi);
+                    bool fail;
+                    if (r >= hi) {
+                        fail = assumed;  // truly spanned
+                    } else {
+                        fail = !has || ts[i] != r || !assumed;
+                    }
+                    if (fail) {
+                        kbad = k;
+                        ebad = r;
+                        continue;
+                    }
+                    if (assumed) {
+                        aseen = true;
+                        ax = tx[i];
+                        live |= 1u << i;
+                        r = tx[i];
+                        stop = (r & kStopBit) || r >= bl;
+                    }
+                }
+                uint32_t kb = kbad;
+#pragma unroll
+                for (int d = 32; d >= 1; d >>= 1) kb = min(kb, (uint32_t)__shfl_xor((int)kb, d));
+                // accept tiles [k0, kb)
+                uint64_t c = 0;
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+                    if (((live >> i) & 1) && 4 * (uint32_t)lane + i < kb) c += tc[i];
+                uint64_t inc = c;
+#pragma unroll
+                for (int d = 1; d < 64; d <<= 1) {
+                    const uint64_t o = __shfl_up(inc, d);
+                    if (lane >= d) inc += o;
+                }
+                uint64_t run = total + inc - c;
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const uint32_t k = 4 * lane + i;
+                    const uint64_t t = gt0 + k;
+                    if (k < k0 || k >= kb || t >= ntiles) continue;
+                    const bool lv = (live >> i) & 1;
+                    gs.tile_e[t] = lv ? ts[i] : ~0ull;
+                    if (lv) {
+                        gs.tile_base[t] = run;
+                        run += tc[i];
+                    }
+                }
+                total += __shfl(inc, 63);
+                if (kb == kGrpTiles) {  // the rest of the group agreed
+                    if (tm) {
+                        e = __shfl(lx, tl);
+                        ended = true;
+                    } else {
+                        e = max(e, __shfl(pm, 63));
+                    }
+                    k0 = kGrpTiles;
+                    break;
+                }
+                // re-walk tile kb from its true entry (no frames when the entry spans it)
+                const uint32_t owner = kb >> 2;
+                const uint64_t eb = __shfl(ebad, (int)owner);
+                const uint64_t t = gt0 + kb;
+                const uint64_t lo = t << sh, hi = min(lo + T, bl);
+                uint64_t x2 = 0;
+                uint32_t c2 = 0;
+                if (lane == 0) {
+                    c2 = walk(blob, bl, eb, hi, &x2, gs.tile_list + t * lcap, lo);
+                    gs.tile_cnt[t] = c2;
+                    gs.tile_e[t] = eb;
+                    gs.tile_base[t] = total;
+                }
+                x2 = __shfl(x2, 0);
+                c2 = (uint32_t)__shfl((int)c2, 0);
+                total += c2;
+                e = x2;
+                if ((e & kStopBit) || e >= bl) ended = true;
+                k0 = kb + 1;
+            }
+            // the walk ended inside the group: later tiles start no frames
+            if (ended) {
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const uint32_t k = 4 * lane + i;
+                    if (k >= k0 && gt0 + k < ntiles) gs.tile_e[gt0 + k] = ~0ull;
+                }
+            }
+            if (lane == 0) ql[5] = 2;
+            ++nrep;
         }
         if (lane == 0) {
             uint64_t *st = (uint64_t *)(gs.small + 512);
@@ -543,38 +737,54 @@ __global__ __launch_bounds__(256) void k_decode_general(const uint8_t *__restric
     gstamp(gs, 3, rt_now() - t0);
 
     const uint64_t nwalk = __hip_atomic_load(&gs.misc[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    // ---------------- C: scatter frame positions (walk order), one wave per group
-    for (uint64_t g = wid; g < ngroups; g += nwaves) {
-        const uint64_t *q = gs.grp + kGrpWords * g;
+    // ---------------- C: scatter the accepted tiles' lists (walk order), one lane per tile
+    for (uint64_t t = gtid; t < ntiles; t += gthreads) {
+        const uint64_t *q = gs.grp + kGrpWords * (t / kGrpTiles);
         const uint64_t mode = q[5];
-        if (mode == 0) continue;
-        const uint64_t t = 64 * g + lane;
-        const bool in = t < ntiles;
-        uint64_t entry = ~0ull, base = 0;
+        uint64_t base;
         if (mode == 1) {
-            const uint64_t s = in ? gs.tile_s[t] : kNoStart;
-            const uint64_t x = in ? gs.tile_x[t] : 0;
-            const uint32_t cnt = in ? gs.tile_cnt[t] : 0;
-            const bool has = s != kNoStart;
-            const uint64_t termmask = __ballot(has && ((x & kStopBit) || x >= bl));
-            const int last = termmask ? __builtin_ctzll(termmask) : 63;
-            const bool live = has && lane <= last;
-            const uint64_t c = live ? cnt : 0;
-            uint64_t inc = c;
-#pragma unroll
-            for (int d = 1; d < 64; d <<= 1) {
-                const uint64_t o = __shfl_up(inc, d);
-                if (lane >= d) inc += o;
-            }
-            if (live) { entry = s; base = q[4] + inc - c; }
-        } else if (in) {
-            entry = gs.tile_e[t];
-            if (entry != ~0ull) base = gs.tile_base[t];
+            const uint32_t pre = gs.tile_pre[t];
+            if (pre == kNotLive) continue;
+            base = q[4] + pre;
+        } else if (mode == 2) {
+            if (gs.tile_e[t] == ~0ull) continue;
+            base = gs.tile_base[t];
+        } else {
+            continue;
         }
-        if (entry != ~0ull) {
-            uint64_t x;
-            walk<true, VERIFY>(blob, bl, entry, min((t + 1) << sh, bl), &x, base, gs.fpos, gs.cs,
-                               frame_pos, cap);
+        const uint32_t cnt = gs.tile_cnt[t];
+        const uint32_t *list = gs.tile_list + t * lcap;
+        const uint64_t lo = t << sh;
+        uint32_t k = 0;
+        for (; k + 4 <= cnt; k += 4) {
+            uint64_t p[4], c[4], ln[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) p[j] = lo + list[k + j];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                if (VERIFY) c[j] = ld64_any(blob + p[j]);
+                ln[j] = ld64_any(blob + p[j] + 32);
+            }
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const uint64_t i = base + k + j;
+                gs.fpos[i] = p[j];
+                if (VERIFY) {
+                    gs.cs[i] = c[j];
+                    gs.flen[i] = 40 + (uint64_t)(uint32_t)ln[j] + (ln[j] >> 32);
+                }
+                if (frame_pos && i < cap) frame_pos[i] = p[j];
+            }
+        }
+        for (; k < cnt; ++k) {
+            const uint64_t p = lo + list[k], i = base + k;
+            gs.fpos[i] = p;
+            if (VERIFY) {
+                gs.cs[i] = ld64_any(blob + p);
+                const uint64_t ln = ld64_any(blob + p + 32);
+                gs.flen[i] = 40 + (uint64_t)(uint32_t)ln + (ln >> 32);
+            }
+            if (frame_pos && i < cap) frame_pos[i] = p;
         }
     }
     ok &= grid_barrier(gs.bar, nwg * ++phase, t0);

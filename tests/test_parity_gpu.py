@@ -123,6 +123,46 @@ def test_count_and_stride_breaks(cx):
     _check_decode(cx, np.concatenate([base, np.full(77, 9, dtype=np.uint8)]))
 
 
+def _crafted_record(n, lo, hi, fill, seed):
+    """A stamped record whose payloads defeat the tile speculation: "zero" payloads
+    (every offset inside them is a candidate frame start) or "fake" payloads that
+    carry chains of well-formed fake frame headers every 100 B (confirmed false
+    starts), so the link phase must repair groups exactly."""
+    from iggy_amd.codec import raw_messages
+    rng = np.random.default_rng(seed)
+    pls = rng.integers(lo, hi + 1, size=n).astype(np.uint32)
+    ids = rng.integers(0, 2**63, size=2 * n, dtype=np.uint64)
+    ots = (1_700_000_000_000_000 + np.arange(n)).astype(np.uint64)
+    if fill == "zero":
+        pay = np.zeros(int(pls.sum()), dtype=np.uint8)
+    else:
+        pay = rng.integers(0, 256, size=int(pls.sum()), dtype=np.uint8)
+        fake = np.zeros(48, dtype=np.uint8)
+        struct.pack_into("<II", fake, 32, 0, 52)  # user headers 0, payload 52: a 100-B frame
+        starts = np.concatenate([[0], np.cumsum(pls)[:-1]]).astype(np.int64)
+        for st, ln in zip(starts, pls):
+            for o in range(int(rng.integers(0, 100)), int(ln) - 48, 100):
+                pay[st + o: st + o + 48] = fake
+    raw = raw_messages(ids, ots, pay, pls)
+    rc, e, out = O.encode_batch(raw, 1)
+    assert rc == 0, e
+    return np.frombuffer(out, dtype=np.uint8).copy()
+
+
+@pytest.mark.parametrize("n,lo,hi,fill", [(3000, 64, 4096, "zero"), (20000, 0, 600, "zero"),
+                                          (3000, 64, 4096, "fake"), (20000, 100, 700, "fake"),
+                                          (60, 50000, 300000, "fake"), (40, 100000, 200000, "zero")])
+def test_adversarial_variable_batches(cx, n, lo, hi, fill):
+    rec = _crafted_record(n, lo, hi, fill, seed=n ^ lo)
+    _check_decode(cx, rec)
+    # and with a break in the middle: a frame's reserved bytes set
+    rc, e, h, frames = O.decode_batch_slice_with(rec, 0)
+    assert rc == 0, e
+    r = rec.copy()
+    r[256 + int(frames[len(frames) // 2]) + 41] = 7
+    _check_decode(cx, r)
+
+
 def _raw_from_arrays(n, pls, uhl, rng):
     ids = rng.integers(0, 2**63, size=2 * n, dtype=np.uint64)
     ots = (1_700_000_000_000_000 + rng.integers(0, 10**6, size=n)).astype(np.uint64)
