@@ -848,12 +848,16 @@ __global__ __launch_bounds__(kGenThreads) void k_decode_general(const uint8_t *_
                     const uint64_t ix = 8 * (B0 + 64) + 64 * r + lane;
                     nxt[r] = ix < 8 * nb ? gs.bsums[ix] : 0;
                 }
-                const uint64_t left = nb - B0;  // scalar: the tail group stops early
+                // straight-line (the tail group keeps acc by select, not by branch), so the
+                // compiler waits once for this group's sums, not for every load in flight
+                const uint64_t left = nb - B0;
 #pragma unroll
                 for (int r = 0; r < 8; ++r)
 #pragma unroll
-                    for (int c = 0; c < 8; ++c)
-                        if ((uint64_t)(8 * r + c) < left) acc = scramble1(acc + __shfl(cur[r], 8 * c + j), key);
+                    for (int c = 0; c < 8; ++c) {
+                        const uint64_t na = scramble1(acc + __shfl(cur[r], 8 * c + j), key);
+                        acc = (uint64_t)(8 * r + c) < left ? na : acc;
+                    }
 #pragma unroll
                 for (int r = 0; r < 8; ++r) cur[r] = nxt[r];
             }
