@@ -55,6 +55,62 @@ __device__ __forceinline__ uint64_t cs_word(uint64_t m, const iggy_batch_header 
     }
 }
 
+// One XXH3 scramble of accumulator lane j (key = secret word 16 + j) in the
+// 32-bit-piece form measured fastest on gfx950 (scripts/chain_micro.hip); the
+// empty asm keeps the next block sum out of the multiply-add's addend.
+__device__ __forceinline__ uint64_t scramble_fast(uint64_t y, uint32_t klo, uint32_t khi) {
+    const uint32_t hi = (uint32_t)(y >> 32);
+    const uint32_t lo = (uint32_t)y ^ (hi >> 15) ^ klo;
+    const uint32_t h2 = hi ^ khi;
+    uint64_t t = (uint64_t)lo * P32_1 + ((uint64_t)(h2 * P32_1) << 32);
+    asm volatile("" : "+v"(t));
+    return t;
+}
+
+// The serial part of a long XXH3 input: acc_j over nb full blocks whose stripe
+// sums are bsums[8b + j] (one wave, lane j & 7 carries accumulator j). Groups of
+// 16 sums rotate through three register sets (no copies of in-flight loads), so
+// every group's loads were issued two groups (~32 steps) before it is chained.
+__device__ __forceinline__ void chain_load16(const uint64_t *bsums, uint64_t nb, uint64_t g, int j,
+                                             uint64_t (&v)[16]) {
+    const uint64_t last = 8 * nb - 8 + j;  // clamp: past-the-end groups re-read a valid sum
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        const uint64_t ix = 8 * (16 * g + k) + j;
+        v[k] = bsums[ix < 8 * nb ? ix : last];
+    }
+}
+__device__ __forceinline__ uint64_t chain_run16(uint64_t acc, const uint64_t (&v)[16], uint32_t klo, uint32_t khi) {
+#pragma unroll
+    for (int k = 0; k < 16; ++k) acc = scramble_fast(acc + v[k], klo, khi);
+    return acc;
+}
+__device__ inline uint64_t chain_blocks(const uint64_t *bsums, uint64_t nb, int lane) {
+    const int j = lane & 7;
+    uint64_t acc = kAccInit[j];
+    const uint64_t key = kSecretW8[16 + j];
+    const uint32_t klo = (uint32_t)key, khi = (uint32_t)(key >> 32);
+    if (nb == 0) return acc;
+    const uint64_t ng = nb / 16;  // full groups
+    uint64_t A[16], B[16], C[16];
+    chain_load16(bsums, nb, 0, j, A);
+    chain_load16(bsums, nb, 1, j, B);
+    chain_load16(bsums, nb, 2, j, C);
+    uint64_t g = 0;
+    for (; g + 3 <= ng; g += 3) {
+        acc = chain_run16(acc, A, klo, khi);
+        chain_load16(bsums, nb, g + 3, j, A);
+        acc = chain_run16(acc, B, klo, khi);
+        chain_load16(bsums, nb, g + 4, j, B);
+        acc = chain_run16(acc, C, klo, khi);
+        chain_load16(bsums, nb, g + 5, j, C);
+    }
+    if (g < ng) { acc = chain_run16(acc, A, klo, khi); ++g; }
+    if (g < ng) { acc = chain_run16(acc, B, klo, khi); ++g; }
+    for (uint64_t b = 16 * ng; b < nb; ++b) acc = scramble_fast(acc + bsums[8 * b + j], klo, khi);
+    return acc;
+}
+
 // header and frame count come from device memory (written by an earlier kernel
 // on the stream) so nothing has to travel back to the host in between.
 __global__ __launch_bounds__(256) void k_bsum_blocks(const iggy_batch_header *hp,
@@ -100,18 +156,7 @@ __global__ __launch_bounds__(64) void k_bsum_chain(const iggy_batch_header *hp,
     const int lane = threadIdx.x & 63;
     if (pl.long_cs) {
         const int j = lane & 7;
-        uint64_t acc = kAccInit[j];
-        const uint64_t key = kSecretW8[16 + j];
-        uint64_t b = 0;
-        // batches of 8 blocks: loads issued ahead of the dependent scrambles
-        for (; b + 8 <= pl.nb; b += 8) {
-            uint64_t v[8];
-#pragma unroll
-            for (int k = 0; k < 8; ++k) v[k] = bsums[(b + k) * 8 + j];
-#pragma unroll
-            for (int k = 0; k < 8; ++k) acc = scramble1(acc + v[k], key);
-        }
-        for (; b < pl.nb; ++b) acc = scramble1(acc + bsums[b * 8 + j], key);
+        uint64_t acc = chain_blocks(bsums, pl.nb, lane);
         acc += bsums[pl.nb * 8 + j];
         const uint64_t v = src(N - 8 + j);
         acc += __shfl_xor(v, 1);
@@ -180,17 +225,7 @@ __global__ __launch_bounds__(64) void k_xxh3_big_chain(const uint8_t *p, uint64_
     }
     const uint64_t nb = (len - 1) / 1024;
     const int j = lane & 7;
-    uint64_t acc = kAccInit[j];
-    const uint64_t key = kSecretW8[16 + j];
-    uint64_t b = 0;
-    for (; b + 8 <= nb; b += 8) {
-        uint64_t v[8];
-#pragma unroll
-        for (int k = 0; k < 8; ++k) v[k] = bsums[(b + k) * 8 + j];
-#pragma unroll
-        for (int k = 0; k < 8; ++k) acc = scramble1(acc + v[k], key);
-    }
-    for (; b < nb; ++b) acc = scramble1(acc + bsums[b * 8 + j], key);
+    uint64_t acc = chain_blocks(bsums, nb, lane);
     acc += bsums[nb * 8 + j];
     const uint64_t v = ld64_any(p + len - 64 + 8 * j);
     acc += __shfl_xor(v, 1);

@@ -596,7 +596,16 @@ static int enqueue_encode(iggy_codec_ctx *c, const iggy_raw_messages *dm, uint64
     hipLaunchKernelGGL(k_enc_prep, dim3(ntiles), dim3(256), 0, s, m, es);
     hipLaunchKernelGGL(k_enc_scan, dim3(1), dim3(256), 0, s, ntiles, n, partition_id, es);
     const uint64_t waves = std::min<uint64_t>(n, (uint64_t)c->ncu * 32);
-    hipLaunchKernelGGL(k_enc_frames, dim3((waves + 3) / 4), dim3(256), 0, s, m, es, d_out);
+    if (!m.user_headers_lengths) {
+        // no user headers: lane-group kernel (k_enc_frames only covers a < 16-B payload area)
+        const uint64_t lwg = std::min<uint64_t>((n + 31) / 32, (uint64_t)c->ncu * 8);
+        hipLaunchKernelGGL(k_enc_lanes, dim3(lwg), dim3(256), 0, s, m, es, d_out);
+        hipLaunchKernelGGL(k_enc_short, dim3(std::min<uint64_t>((n + 255) / 256, (uint64_t)c->ncu * 4)), dim3(256),
+                           0, s, m, es, d_out);
+        hipLaunchKernelGGL(k_enc_frames, dim3((waves + 3) / 4), dim3(256), 0, s, m, es, d_out, 1u);
+    } else {
+        hipLaunchKernelGGL(k_enc_frames, dim3((waves + 3) / 4), dim3(256), 0, s, m, es, d_out, 0u);
+    }
     prof_end(c, 1, s);
     CsSource src{es.cs, nullptr, nullptr};
     hipLaunchKernelGGL(k_bsum_blocks, dim3(c->ncu * 4), dim3(256), 0, s, (const iggy_batch_header *)es.hdr,

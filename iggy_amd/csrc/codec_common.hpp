@@ -101,4 +101,24 @@ __device__ __forceinline__ uint64_t sat_add(uint64_t a, uint64_t b) {
 __device__ __forceinline__ uint64_t rt_now() { return __builtin_amdgcn_s_memrealtime(); }
 constexpr uint64_t kSpinLimitTicks = 100000000ull * 4;  // 4 s: a bug guard, never a timing knob
 
+// lane-group XXH3 helpers (decode_uniform / decode_general / encode): DPP quad_perm
+// and ds_swizzle moves of a 64-bit value, and one 16-B stripe-pair piece
+template <int CTRL>
+__device__ __forceinline__ uint64_t gdpp64(uint64_t x) {
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_mov_dpp((int)(uint32_t)x, CTRL, 0xF, 0xF, false);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_mov_dpp((int)(uint32_t)(x >> 32), CTRL, 0xF, 0xF, false);
+    return (uint64_t)lo | ((uint64_t)hi << 32);
+}
+__device__ __forceinline__ uint64_t gswz_xor4(uint64_t x) {
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_ds_swizzle((int)(uint32_t)x, 0x101F);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_ds_swizzle((int)(uint32_t)(x >> 32), 0x101F);
+    return (uint64_t)lo | ((uint64_t)hi << 32);
+}
+__device__ __forceinline__ void piece(uint64_t &a0, uint64_t &a1, uint4 p, uint64_t s0, uint64_t s1) {
+    const uint64_t w0 = (uint64_t)p.x | ((uint64_t)p.y << 32);
+    const uint64_t w1 = (uint64_t)p.z | ((uint64_t)p.w << 32);
+    a0 += mul32x32(w0 ^ s0) + w1;
+    a1 += mul32x32(w1 ^ s1) + w0;
+}
+
 }  // namespace iggy

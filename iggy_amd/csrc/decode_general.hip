@@ -236,24 +236,6 @@ __device__ __forceinline__ void word_contrib(uint64_t m, uint64_t v, uint64_t &x
     x = mul32x32(v ^ kSecretW8[sib + j]);
 }
 
-template <int CTRL>
-__device__ __forceinline__ uint64_t gdpp64(uint64_t x) {
-    const uint32_t lo = (uint32_t)__builtin_amdgcn_mov_dpp((int)(uint32_t)x, CTRL, 0xF, 0xF, false);
-    const uint32_t hi = (uint32_t)__builtin_amdgcn_mov_dpp((int)(uint32_t)(x >> 32), CTRL, 0xF, 0xF, false);
-    return (uint64_t)lo | ((uint64_t)hi << 32);
-}
-__device__ __forceinline__ uint64_t gswz_xor4(uint64_t x) {
-    const uint32_t lo = (uint32_t)__builtin_amdgcn_ds_swizzle((int)(uint32_t)x, 0x101F);
-    const uint32_t hi = (uint32_t)__builtin_amdgcn_ds_swizzle((int)(uint32_t)(x >> 32), 0x101F);
-    return (uint64_t)lo | ((uint64_t)hi << 32);
-}
-__device__ __forceinline__ void piece(uint64_t &a0, uint64_t &a1, uint4 p, uint64_t s0, uint64_t s1) {
-    const uint64_t w0 = (uint64_t)p.x | ((uint64_t)p.y << 32);
-    const uint64_t w1 = (uint64_t)p.z | ((uint64_t)p.w << 32);
-    a0 += mul32x32(w0 ^ s0) + w1;
-    a1 += mul32x32(w1 ^ s1) + w0;
-}
-
 // Frame verification. Lane group fg (8 lanes) of verify wave vw hashes frames
 // f = 8 vw + fg + j * 8 nvw, j = 0, 1, ... at its own pace: every wave step
 // each group hashes one 1024-B block of its current frame while the next block
@@ -833,34 +815,7 @@ __global__ __launch_bounds__(kGenThreads) void k_decode_general(const uint8_t *_
     if (blockIdx.x == 0 && wave == 0) {
         if (long_cs) {
             const int j = lane & 7;
-            uint64_t acc = kAccInit[j];
-            const uint64_t key = kSecretW8[16 + j];
-            // block sums arrive 8 blocks per 64-lane load, 64 blocks ahead of the chain
-            uint64_t cur[8], nxt[8];
-#pragma unroll
-            for (int r = 0; r < 8; ++r) {
-                const uint64_t ix = 64 * r + lane;
-                cur[r] = ix < 8 * nb ? gs.bsums[ix] : 0;
-            }
-            for (uint64_t B0 = 0; B0 < nb; B0 += 64) {
-#pragma unroll
-                for (int r = 0; r < 8; ++r) {
-                    const uint64_t ix = 8 * (B0 + 64) + 64 * r + lane;
-                    nxt[r] = ix < 8 * nb ? gs.bsums[ix] : 0;
-                }
-                // straight-line (the tail group keeps acc by select, not by branch), so the
-                // compiler waits once for this group's sums, not for every load in flight
-                const uint64_t left = nb - B0;
-#pragma unroll
-                for (int r = 0; r < 8; ++r)
-#pragma unroll
-                    for (int c = 0; c < 8; ++c) {
-                        const uint64_t na = scramble1(acc + __shfl(cur[r], 8 * c + j), key);
-                        acc = (uint64_t)(8 * r + c) < left ? na : acc;
-                    }
-#pragma unroll
-                for (int r = 0; r < 8; ++r) cur[r] = nxt[r];
-            }
+            uint64_t acc = chain_blocks(gs.bsums, nb, lane);
             acc += gs.bsums[nb * 8 + j];
             const uint64_t v = gs.cs[nwalk - 8 + j];
             const uint64_t vx = __shfl_xor(v, 1);

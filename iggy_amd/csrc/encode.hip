@@ -28,7 +28,7 @@ struct EncScratch {
     uint64_t *tile_uh;    // [ntiles]
     uint64_t *tile_min;   // [ntiles] minimum origin timestamp
     uint64_t *cs;         // [n] frame checksums
-    uint64_t *misc;       // [8]: 0 min origin, 1 blob bytes, 2 ts-error (~index, max), 3 n
+    uint64_t *misc;       // [8]: 0 min origin, 1 blob bytes, 2 ts-error (~index, max), 3 n, 4 payload bytes
     iggy_batch_header *hdr;  // header being built
 };
 
@@ -127,6 +127,7 @@ __global__ __launch_bounds__(256) void k_enc_scan(uint64_t ntiles, uint64_t n, u
         es.misc[1] = 48 * n + carry_pl + carry_uh;
         es.misc[2] = 0;
         es.misc[3] = n;
+        es.misc[4] = carry_pl;  // total payload bytes (bounds the lane-group kernel's loads)
         iggy_batch_header h{};
         h.partition_id = partition_id;
         h.base_offset = 0;
@@ -198,7 +199,9 @@ __device__ inline uint64_t xxh3_short_stream(const FrameStream &fs) {
 }
 
 __global__ __launch_bounds__(256) void k_enc_frames(iggy_raw_messages m, EncScratch es,
-                                                    uint8_t *out) {
+                                                    uint8_t *out, uint32_t fallback_only) {
+    // fallback_only: the lane-group kernel ran unless the payload area is < 16 B
+    if (fallback_only && es.misc[4] >= 16) return;
     const int lane = threadIdx.x & 63;
     const uint64_t n = m.count;
     const uint64_t origin = es.misc[0];
@@ -299,6 +302,235 @@ __global__ __launch_bounds__(256) void k_enc_frames(iggy_raw_messages m, EncScra
             st64_any(dst, hsh);
             es.cs[i] = hsh;
         }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// k_enc_lanes: the frames step for batches without user headers (every SDK
+// producer batch without headers; C3), in the decode's lane-group shape.
+// Lane group fg (8 lanes) of wave vw encodes frames i = 8 vw + fg + j * 8 nvw at
+// its own pace, one 1024-B block of the hashed stream H(40) || P(pl) per wave
+// step, the next block (or the next frame's first block) already loading. Lane
+// l = (m, par) carries stream pieces 1024b + 128q + 16(m + 4 par), q = 0..7: it
+// loads them once (16 B from the payload), stores them to the frame and
+// accumulates them into XXH3 accumulators 2m, 2m+1 for stripe parity par (the
+// pair is folded before each scramble). Pieces below stream byte 40 are the
+// synthesised header (ids, offset/timestamp deltas, lengths, reserved). The
+// payload of frame i is followed by frame i+1's in the SoA buffer, so a piece
+// that runs past its payload reads (and discards) the next one's bytes; only
+// the buffer's last 15 bytes need a clamped, realigned load.
+struct EFrame {
+    uint64_t i, po, pl;  // i >= count: none
+};
+__device__ __forceinline__ EFrame eframe(const iggy_raw_messages &m, const EncScratch &es, uint64_t i) {
+    EFrame f;
+    f.i = i;
+    if (i < m.count) {
+        f.po = es.tile_pl[i / kEncTile] + es.pl_local[i];
+        f.pl = m.payload_lengths[i];
+    } else {
+        f.po = 0;
+        f.pl = 0;
+    }
+    return f;
+}
+// 128-bit little-endian value (lo, hi) moved down by d bytes (0 <= d < 16)
+__device__ __forceinline__ void shr_bytes(uint64_t &lo, uint64_t &hi, uint32_t d) {
+    const uint32_t n = 8 * d;
+    if (n == 0) return;
+    if (n < 64) {
+        lo = (lo >> n) | (hi << (64 - n));
+        hi >>= n;
+    } else {
+        lo = hi >> (n - 64);
+        hi = 0;
+    }
+}
+struct EStep {
+    uint4 v[8];    // raw 16-B payload loads of the 8 pieces
+    uint4 last;    // last-stripe piece (long frames, first step only)
+    uint64_t id0, id1, ots;  // header inputs (first step only)
+};
+// the loads of frame f's block b (fixed count: unneeded ones read the buffer start)
+__device__ __forceinline__ void eissue(const iggy_raw_messages &m, const EFrame &f, uint32_t b, uint32_t poff,
+                                       uint32_t mm, uint64_t ptot, EStep &st) {
+    const bool live = f.i < m.count;
+    const uint64_t L = 40 + f.pl;
+    const uint8_t *P = m.payloads;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+        const uint64_t sp = 1024ull * b + 128 * q + poff;  // stream position of the piece
+        // payload index of the piece's first byte (the s == 32 piece starts 8 B early)
+        const uint64_t px = f.po + (sp >= 40 ? sp - 40 : 0);
+        const bool need = live && sp + 16 > 32 && sp < L;
+        const uint64_t a = (px + 16 <= ptot) ? px : ptot - 16;  // clamp: realigned at use
+        st.v[q] = ld128_any(P + (need ? a : 0));
+    }
+    const bool lng = live && L > 240 && b == 0;
+    st.last = ld128_any(P + (lng ? f.po + (L - 64 + 16 * mm) - 40 : 0));
+    const uint64_t i = live && b == 0 ? f.i : 0;
+    st.id0 = m.ids[2 * i];
+    st.id1 = m.ids[2 * i + 1];
+    st.ots = m.origin_timestamps[i];
+}
+
+__global__ __launch_bounds__(256, 2) void k_enc_lanes(iggy_raw_messages m, EncScratch es, uint8_t *out) {
+    const uint64_t ptot = es.misc[4];
+    if (ptot < 16) return;  // tiny payload area: k_enc_frames (fallback) encodes it
+    const uint64_t n = m.count;
+    const uint64_t origin = es.misc[0];
+    const int lane = threadIdx.x & 63;
+    const uint32_t l = lane & 7, mm = l >> 1, par = l & 1, fg = (uint32_t)lane >> 3;
+    const uint32_t poff = 16 * (mm + 4 * par);
+    const uint32_t vw = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const uint32_t nvw = (gridDim.x * blockDim.x) >> 6;
+    // stripe secrets live in LDS (one ds_read_b128 per piece) to keep the two
+    // in-flight load sets and the accumulators in registers
+    __shared__ uint64_t s_sec[24];
+    if (threadIdx.x < 24) s_sec[threadIdx.x] = kSecretW8[threadIdx.x];
+    __syncthreads();
+    const uint64_t key0 = kSecretW8[16 + 2 * mm], key1 = kSecretW8[17 + 2 * mm];
+    const uint64_t init0 = par ? 0 : kAccInit[2 * mm], init1 = par ? 0 : kAccInit[2 * mm + 1];
+    const uint64_t last0 = kSecretLast[2 * mm], last1 = kSecretLast[2 * mm + 1];
+    const uint64_t mrg0 = kSecretMerge[2 * mm], mrg1 = kSecretMerge[2 * mm + 1];
+    const uint64_t stride = 8ull * nvw;
+    const uint32_t sbase = par + 2 * mm;  // secret word of piece q: sbase + 2q (and + 1)
+
+    EFrame cur = eframe(m, es, 8ull * vw + fg);
+    EFrame nxt = eframe(m, es, cur.i + stride);
+    uint32_t b = 0;
+    uint64_t a0 = init0, a1 = init1;
+    uint64_t h0 = 0, h1 = 0, h2 = 0, h3 = 0;  // header words of the current frame
+    uint4 lastp = make_uint4(0, 0, 0, 0);      // the current frame's last-stripe piece
+    // process the step whose loads are in X, issue the next step's into Y
+    auto step = [&](EStep &X, EStep &Y) {
+        if (cur.i >= n) return;
+        const uint64_t L = 40 + cur.pl;
+        const bool lng = L > 240;
+        const uint64_t nbF = lng ? (L - 1) / 1024 : 0;
+        const uint64_t ns = lng ? ((L - 1) - 1024 * nbF) / 64 : 0;
+        const uint32_t nblk = (uint32_t)((L + 1023) / 1024);
+        const bool fin = b + 1 == nblk;
+        if (!fin) eissue(m, cur, b + 1, poff, mm, ptot, Y);
+        else eissue(m, nxt, 0, poff, mm, ptot, Y);
+        if (b == 0) {
+            const uint64_t delta = X.ots - origin;
+            if (delta > IGGY_MAX_TIMESTAMP_DELTA_MICROS && l == 0)
+                atomicMax((unsigned long long *)&es.misc[2], (unsigned long long)~cur.i);
+            h0 = X.id0;
+            h1 = X.id1;
+            h2 = (cur.i & 0xFFFFFFFFull) | ((delta & 0xFFFFFFFFull) << 32);
+            h3 = cur.pl << 32;  // user_headers_len 0 | payload_len
+            lastp = X.last;
+        }
+        uint8_t *F = out + 256 + 48 * cur.i + cur.po;  // frame start
+        uint64_t p0[4] = {0, 0, 0, 0}, p1[4] = {0, 0, 0, 0};
+        uint64_t tw0 = 0, tw1 = 0, tsp = ~0ull;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            const uint64_t sp = 1024ull * b + 128 * q + poff;
+            uint64_t w0 = (uint64_t)X.v[q].x | ((uint64_t)X.v[q].y << 32);
+            uint64_t w1 = (uint64_t)X.v[q].z | ((uint64_t)X.v[q].w << 32);
+            if (sp < 40) {
+                if (sp == 0) { w0 = h0; w1 = h1; }
+                else if (sp == 16) { w0 = h2; w1 = h3; }
+                else { w1 = w0; w0 = 0; }  // reserved | payload[0..8)
+            } else {
+                const uint64_t px = cur.po + sp - 40;
+                if (px + 16 > ptot) shr_bytes(w0, w1, (uint32_t)(px + 16 - ptot));
+            }
+            if (sp + 16 <= L) {
+                st128_any(F + 8 + sp, make_uint4((uint32_t)w0, (uint32_t)(w0 >> 32), (uint32_t)w1, (uint32_t)(w1 >> 32)));
+            } else if (sp < L) {  // the frame's partial last piece (at most one per lane)
+                tw0 = w0; tw1 = w1; tsp = sp;
+            }
+            if (lng) {
+                const uint64_t sa = s_sec[sbase + 2 * q], sb = s_sec[sbase + 2 * q + 1];
+                if (b < nbF) {
+                    p0[q & 3] += mul32x32(w0 ^ sa) + w1;
+                    p1[q & 3] += mul32x32(w1 ^ sb) + w0;
+                } else if (2 * q + par < ns) {
+                    a0 += mul32x32(w0 ^ sa) + w1;
+                    a1 += mul32x32(w1 ^ sb) + w0;
+                }
+            }
+        }
+        if (tsp != ~0ull) {
+            uint8_t *d = F + 8 + tsp;
+            const uint32_t rem = (uint32_t)(L - tsp);
+            for (uint32_t k = 0; k < rem; ++k) d[k] = (uint8_t)((k < 8 ? tw0 : tw1) >> (8 * (k & 7)));
+        }
+        uint64_t hsh = 0;
+        if (lng) {
+            if (b < nbF) {
+                a0 += (p0[0] + p0[1]) + (p0[2] + p0[3]);
+                a1 += (p1[0] + p1[1]) + (p1[2] + p1[3]);
+                a0 += gdpp64<0xB1>(a0);
+                a1 += gdpp64<0xB1>(a1);
+                a0 = scramble1(a0, key0);
+                a1 = scramble1(a1, key1);
+                if (par) { a0 = 0; a1 = 0; }
+            }
+            if (fin) {
+                a0 += gdpp64<0xB1>(a0);
+                a1 += gdpp64<0xB1>(a1);
+                piece(a0, a1, lastp, last0, last1);
+                uint64_t t = fold64(a0 ^ mrg0, a1 ^ mrg1);
+                t += gdpp64<0x4E>(t);
+                t += gswz_xor4(t);
+                hsh = avalanche(L * P64_1 + t);
+            }
+        }
+        if (fin) {
+            if (l == 0 && lng) {  // frames of <= 240 hashed bytes: k_enc_short
+                st64_any(F, hsh);
+                es.cs[cur.i] = hsh;
+            }
+            cur = nxt;
+            nxt = eframe(m, es, cur.i + stride);
+            b = 0;
+            a0 = init0;
+            a1 = init1;
+        } else {
+            ++b;
+        }
+    };
+    // ping-pong over two load sets (no register copy of in-flight loads)
+    EStep A, B;
+    eissue(m, cur, 0, poff, mm, ptot, A);
+    while (__ballot(cur.i < n)) {
+        step(A, B);
+        if (!__ballot(cur.i < n)) break;
+        step(B, A);
+    }
+}
+
+// Frames of <= 240 hashed bytes of a lane-group encode: one lane each hashes the
+// stream (XXH3 17-128 / 129-240 paths) from the SoA input and backpatches.
+__global__ __launch_bounds__(256) void k_enc_short(iggy_raw_messages m, EncScratch es, uint8_t *out) {
+    if (es.misc[4] < 16) return;  // the fallback kernel encoded everything
+    const uint64_t n = m.count;
+    const uint64_t origin = es.misc[0];
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+         i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t pl = m.payload_lengths[i];
+        if (40 + pl > 240) continue;
+        const uint64_t po = es.tile_pl[i / kEncTile] + es.pl_local[i];
+        FrameStream fs;
+        fs.pl = pl;
+        fs.uh = 0;
+        fs.L = 40 + pl;
+        fs.P = m.payloads + po;
+        fs.U = m.payloads;
+        const uint64_t delta = m.origin_timestamps[i] - origin;
+        fs.h[0] = m.ids[2 * i];
+        fs.h[1] = m.ids[2 * i + 1];
+        fs.h[2] = (i & 0xFFFFFFFFull) | ((delta & 0xFFFFFFFFull) << 32);
+        fs.h[3] = pl << 32;
+        fs.h[4] = 0;
+        const uint64_t hsh = xxh3_short_stream(fs);
+        st64_any(out + 256 + 48 * i + po, hsh);
+        es.cs[i] = hsh;
     }
 }
 
