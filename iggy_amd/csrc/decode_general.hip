@@ -239,14 +239,15 @@ __device__ __forceinline__ void word_contrib(uint64_t m, uint64_t v, uint64_t &x
 // Frame verification. Lane group fg (8 lanes) of verify wave vw hashes frames
 // f = 8 vw + fg + j * 8 nvw, j = 0, 1, ... at its own pace: every wave step
 // each group hashes one 1024-B block of its current frame while the next block
-// (or the next frame's first block and last stripe) is already loading, so a
-// group never waits on a frame boundary and never on the other groups' frame
-// sizes. Positions, lengths and stored checksums come from the scatter phase's
-// arrays (prefetched one frame ahead). Lane l = (m, par) owns accumulators
-// 2m, 2m+1 for the stripes of parity par: in every block it reads the 16 B at
-// 128q + 16(m + 4 par), q = 0..7 (stripe 2q+par, words 2m, 2m+1); the pair of
-// parity lanes is folded before each scramble; the last stripe and merge follow
-// the XXH3 long form (> 240 B). Shorter frames are hashed by one lane.
+// (or the next frame's first block and last stripe) is loading into the other
+// of two register sets (ping-pong: in-flight loads are never copied, which
+// would make the wave wait for them). Positions, lengths and stored checksums
+// come from the scatter phase's arrays, one frame ahead. Lane l = (m, par) owns
+// accumulators 2m, 2m+1 for the stripes of parity par: in every block it reads
+// the 16 B at 128q + 16(m + 4 par), q = 0..7 (stripe 2q+par, words 2m, 2m+1);
+// the pair of parity lanes is folded before each scramble; the last stripe and
+// merge follow the XXH3 long form (> 240 B). Frames of <= 240 hashed bytes are
+// checked after the loop, one lane each.
 struct VFrame {
     uint64_t f, p, stored, L;
 };
@@ -262,13 +263,22 @@ __device__ __forceinline__ VFrame vframe(const GeneralScratch &gs, uint64_t f, u
     }
     return v;
 }
-__device__ __forceinline__ void vblock(const uint8_t *blob, const VFrame &v, uint32_t b, uint32_t par,
-                                       uint32_t poff, uint4 (&dst)[8]) {
-    const uint64_t nbF = (v.L - 1) / 1024, ns = ((v.L - 1) - 1024 * nbF) / 64;
+struct VStep {
+    uint4 v[8];  // the 8 pieces of one block
+    uint4 last;  // the frame's last-stripe piece (first block only)
+};
+// the loads of frame v's block b: always 9 (unneeded pieces read the blob start)
+__device__ __forceinline__ void vissue(const uint8_t *blob, const VFrame &v, uint64_t nwalk, uint32_t b,
+                                       uint32_t par, uint32_t poff, uint32_t m, VStep &st) {
+    const bool lng = v.f < nwalk && v.L > 240;
+    const uint64_t nbF = lng ? (v.L - 1) / 1024 : 0, ns = lng ? ((v.L - 1) - 1024 * nbF) / 64 : 0;
     const uint8_t *hb = blob + v.p + 8 + 1024ull * b + poff;
 #pragma unroll
-    for (int q = 0; q < 8; ++q)
-        dst[q] = (b < nbF || 2 * q + par < ns) ? ld128_any(hb + 128 * q) : make_uint4(0, 0, 0, 0);
+    for (int q = 0; q < 8; ++q) {
+        const bool use = lng && (b < nbF || 2 * q + par < ns);
+        st.v[q] = ld128_any(use ? hb + 128 * q : blob);
+    }
+    st.last = ld128_any((lng && b == 0) ? blob + v.p + 8 + v.L - 64 + 16 * m : blob);
 }
 
 __device__ inline void verify_frames(const uint8_t *blob, const GeneralScratch &gs, uint64_t nwalk,
@@ -289,73 +299,74 @@ __device__ inline void verify_frames(const uint8_t *blob, const GeneralScratch &
 
     VFrame cur = vframe(gs, 8ull * vw + fg, nwalk);
     VFrame nxt = vframe(gs, cur.f + stride, nwalk);
-    uint4 blk[8], lastp = make_uint4(0, 0, 0, 0);
-    if (cur.f < nwalk && cur.L > 240) {
-        vblock(blob, cur, 0, par, poff, blk);
-        lastp = ld128_any(blob + cur.p + 8 + cur.L - 64 + 16 * m);
-    }
     uint32_t b = 0;
     uint64_t a0 = init0, a1 = init1;
-    while (__ballot(cur.f < nwalk)) {
-        if (cur.f < nwalk) {
-            const bool lng = cur.L > 240;
-            const uint64_t nbF = lng ? (cur.L - 1) / 1024 : 0;
-            const uint64_t ns = lng ? ((cur.L - 1) - 1024 * nbF) / 64 : 0;
-            const uint32_t nsteps = lng ? (uint32_t)(nbF + (ns > 0)) : 1u;
-            const bool fin = b + 1 == nsteps;
-            // prefetch: this frame's next block, or the next frame's first block + last stripe
-            uint4 nb[8], nlast = lastp;
-            if (!fin) {
-                vblock(blob, cur, b + 1, par, poff, nb);
-            } else if (nxt.f < nwalk && nxt.L > 240) {
-                vblock(blob, nxt, 0, par, poff, nb);
-                nlast = ld128_any(blob + nxt.p + 8 + nxt.L - 64 + 16 * m);
-            }
-            uint64_t h = 0;
-            if (lng) {
-                if (b < nbF) {
-                    uint64_t p0[4] = {0, 0, 0, 0}, p1[4] = {0, 0, 0, 0};
+    uint4 lastp = make_uint4(0, 0, 0, 0);
+    uint64_t bad = ~0ull;  // first mismatching frame of this group
+    // hash the step whose loads are in X, issue the next step's into Y
+    auto step = [&](VStep &X, VStep &Y) {
+        if (cur.f >= nwalk) return;
+        const uint64_t L = cur.L;
+        const bool lng = L > 240;
+        const uint64_t nbF = lng ? (L - 1) / 1024 : 0;
+        const uint64_t ns = lng ? ((L - 1) - 1024 * nbF) / 64 : 0;
+        const uint32_t nsteps = lng ? (uint32_t)(nbF + (ns > 0)) : 1u;
+        const bool fin = b + 1 == nsteps;
+        if (!fin) vissue(blob, cur, nwalk, b + 1, par, poff, m, Y);
+        else vissue(blob, nxt, nwalk, 0, par, poff, m, Y);
+        if (b == 0) lastp = X.last;
+        if (lng) {
+            if (b < nbF) {
+                uint64_t p0[4] = {0, 0, 0, 0}, p1[4] = {0, 0, 0, 0};
 #pragma unroll
-                    for (int q = 0; q < 8; ++q) piece(p0[q & 3], p1[q & 3], blk[q], s0[q], s1[q]);
-                    a0 += (p0[0] + p0[1]) + (p0[2] + p0[3]);
-                    a1 += (p1[0] + p1[1]) + (p1[2] + p1[3]);
-                    a0 += gdpp64<0xB1>(a0);
-                    a1 += gdpp64<0xB1>(a1);
-                    a0 = scramble1(a0, key0);
-                    a1 = scramble1(a1, key1);
-                    if (par) { a0 = 0; a1 = 0; }
-                } else {
+                for (int q = 0; q < 8; ++q) piece(p0[q & 3], p1[q & 3], X.v[q], s0[q], s1[q]);
+                a0 += (p0[0] + p0[1]) + (p0[2] + p0[3]);
+                a1 += (p1[0] + p1[1]) + (p1[2] + p1[3]);
+                a0 += gdpp64<0xB1>(a0);
+                a1 += gdpp64<0xB1>(a1);
+                a0 = scramble1(a0, key0);
+                a1 = scramble1(a1, key1);
+                if (par) { a0 = 0; a1 = 0; }
+            } else {
 #pragma unroll
-                    for (int q = 0; q < 8; ++q)
-                        if (2 * q + par < ns) piece(a0, a1, blk[q], s0[q], s1[q]);
-                }
-                if (fin) {
-                    a0 += gdpp64<0xB1>(a0);
-                    a1 += gdpp64<0xB1>(a1);
-                    piece(a0, a1, lastp, last0, last1);
-                    uint64_t t = fold64(a0 ^ mrg0, a1 ^ mrg1);
-                    t += gdpp64<0x4E>(t);
-                    t += gswz_xor4(t);
-                    h = avalanche(cur.L * P64_1 + t);
-                }
-            } else if (l == 0) {
-                h = xxh3_64_lane(blob + cur.p + 8, cur.L);
+                for (int q = 0; q < 8; ++q)
+                    if (2 * q + par < ns) piece(a0, a1, X.v[q], s0[q], s1[q]);
             }
             if (fin) {
-                if (l == 0 && h != cur.stored)
-                    atomicMax((unsigned long long *)&gs.misc[2], (unsigned long long)~cur.f);
-                cur = nxt;
-                nxt = vframe(gs, cur.f + stride, nwalk);
-                b = 0;
-                a0 = init0;
-                a1 = init1;
-            } else {
-                ++b;
+                a0 += gdpp64<0xB1>(a0);
+                a1 += gdpp64<0xB1>(a1);
+                piece(a0, a1, lastp, last0, last1);
+                uint64_t t = fold64(a0 ^ mrg0, a1 ^ mrg1);
+                t += gdpp64<0x4E>(t);
+                t += gswz_xor4(t);
+                const uint64_t h = avalanche(L * P64_1 + t);
+                if (h != cur.stored && bad == ~0ull) bad = cur.f;
             }
-#pragma unroll
-            for (int q = 0; q < 8; ++q) blk[q] = nb[q];
-            lastp = nlast;
         }
+        if (fin) {
+            cur = nxt;
+            nxt = vframe(gs, cur.f + stride, nwalk);
+            b = 0;
+            a0 = init0;
+            a1 = init1;
+        } else {
+            ++b;
+        }
+    };
+    VStep A, B;
+    vissue(blob, cur, nwalk, 0, par, poff, m, A);
+    while (__ballot(cur.f < nwalk)) {
+        step(A, B);
+        if (!__ballot(cur.f < nwalk)) break;
+        step(B, A);
+    }
+    if (l == 0 && bad != ~0ull) atomicMax((unsigned long long *)&gs.misc[2], (unsigned long long)~bad);
+    // frames of <= 240 hashed bytes: one lane each, after the streaming loop
+    const uint64_t tid = 64ull * vw + lane, nth = 64ull * nvw;
+    for (uint64_t f = tid; f < nwalk; f += nth) {
+        const uint64_t L = gs.flen[f];
+        if (L <= 240 && xxh3_64_lane(blob + gs.fpos[f] + 8, L) != gs.cs[f])
+            atomicMax((unsigned long long *)&gs.misc[2], (unsigned long long)~f);
     }
 }
 
