@@ -431,13 +431,14 @@ __global__ __launch_bounds__(256, 2) void k_enc_lanes(iggy_raw_messages m, EncSc
             const uint64_t sp = 1024ull * b + 128 * q + poff;
             uint64_t w0 = (uint64_t)X.v[q].x | ((uint64_t)X.v[q].y << 32);
             uint64_t w1 = (uint64_t)X.v[q].z | ((uint64_t)X.v[q].w << 32);
+            {  // a load clamped to the payload area's last 16 B: realign it
+                const uint64_t px = cur.po + (sp >= 40 ? sp - 40 : 0);
+                if (px + 16 > ptot) shr_bytes(w0, w1, (uint32_t)(px + 16 - ptot));
+            }
             if (sp < 40) {
                 if (sp == 0) { w0 = h0; w1 = h1; }
                 else if (sp == 16) { w0 = h2; w1 = h3; }
                 else { w1 = w0; w0 = 0; }  // reserved | payload[0..8)
-            } else {
-                const uint64_t px = cur.po + sp - 40;
-                if (px + 16 > ptot) shr_bytes(w0, w1, (uint32_t)(px + 16 - ptot));
             }
             if (sp + 16 <= L) {
                 st128_any(F + 8 + sp, make_uint4((uint32_t)w0, (uint32_t)(w0 >> 32), (uint32_t)w1, (uint32_t)(w1 >> 32)));

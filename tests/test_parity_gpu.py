@@ -173,7 +173,12 @@ def _raw_from_arrays(n, pls, uhl, rng):
 
 @pytest.mark.parametrize("n,lo,hi,with_uh", [(1, 0, 0, False), (2, 5, 6, True), (100, 64, 4096, False),
                                              (3000, 64, 4096, True), (500, 0, 250, True),
-                                             (2049, 1024, 1024, False), (40, 5000, 9000, False)])
+                                             (2049, 1024, 1024, False), (40, 5000, 9000, False),
+                                             # lane-group encode edges: tiny payloads (the s = 32 piece and the
+                                             # clamped, realigned last piece), the 240-B short/long boundary,
+                                             # a payload area under 16 B (fallback kernel)
+                                             (300, 0, 20, False), (64, 0, 3, False), (5, 1, 2, False),
+                                             (1000, 195, 206, False), (777, 1015, 1033, False)])
 @pytest.mark.parametrize("partition_id", [0, 3])
 def test_encode_matches_oracle(cx, n, lo, hi, with_uh, partition_id):
     from iggy_amd.codec import raw_messages
