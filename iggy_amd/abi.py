@@ -16,6 +16,7 @@ ERR_INVALID_TIMESTAMP_DELTA = 5
 ERR_PAYLOAD_TOO_LARGE = 6
 ERR_INVALID_NUMBER_ENCODING = 20
 ERR_INVALID_MESSAGE_PAYLOAD_LENGTH = 21
+ERR_INVALID_COMMAND = 22  # IggyError::InvalidCommand (server_common batch_error)
 ERR_DEVICE = 100
 ERR_INVALID_ARGUMENT = 101
 ERR_CAPACITY = 102
@@ -122,6 +123,12 @@ class EncodeResult(ctypes.Structure):
 
 LOOKUP_OFFSET = 0
 LOOKUP_TIMESTAMP = 1
+
+# ChecksumMode (server_common/src/send_messages.rs:416-432); prepare frame layout
+CHECKSUM_COMPUTE = 0
+CHECKSUM_SKIP = 1
+PREPARE_HEADER_SIZE = 256
+PREPARE_SIZE_OFFSET = 48
 
 
 class SliceQuery(ctypes.Structure):

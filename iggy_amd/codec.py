@@ -81,6 +81,8 @@ def lib() -> ctypes.CDLL:
     L.iggy_codec_select_slice.argtypes = [vp, vp, u64, vp, vp, vp, vp]
     L.iggy_codec_select_slice_device.argtypes = [vp, vp, vp, u64, vp, vp, vp, vp]
     L.iggy_codec_stamp_batch_device.argtypes = [vp, vp, vp, u64, u64, u64, vp, vp]
+    L.iggy_codec_decode_prepare.argtypes = [vp, vp, u64, ci, vp, vp]
+    L.iggy_codec_admit_batch.argtypes = [vp, vp, u64, u32, u64, ci, vp, u64, vp, vp]
     L.iggy_codec_profile_enable.argtypes = [vp, ci]
     L.iggy_codec_profile_read.argtypes = [vp, ci, vp, vp]
     L.iggy_codec_error_string.argtypes = [u32, u32]
@@ -215,6 +217,29 @@ class Codec:
         rc = self._L.iggy_codec_select_slice(self._h, _addr(a), a.size, ctypes.byref(q), ctypes.byref(out),
                                              hdr.ctypes.data, ctypes.byref(e))
         return rc, e, out, (hdr.tobytes() if rc == 0 and out.selected else None)
+
+    def decode_prepare(self, frame, validate: bool = True):
+        """decode_prepare_slice / _trusted (server_common/src/send_messages.rs:542-622)
+        -> (rc, WireError, BatchHeader)."""
+        a = _np(frame)
+        h = BatchHeader()
+        e = WireError()
+        rc = self._L.iggy_codec_decode_prepare(self._h, _addr(a), a.size, 1 if validate else 0,
+                                               ctypes.byref(h), ctypes.byref(e))
+        return rc, e, h
+
+    def admit_batch(self, batch, metadata_messages_count: int, partition_id: int,
+                    checksum_mode: int = abi.CHECKSUM_COMPUTE):
+        """admit_wire_request's batch half (server_common/src/send_messages.rs:480-540)
+        -> (rc, WireError, BatchHeader, admitted bytes or None)."""
+        a = _np(batch)
+        out = np.zeros(max(a.size, 1), dtype=np.uint8)
+        h = BatchHeader()
+        e = WireError()
+        rc = self._L.iggy_codec_admit_batch(self._h, _addr(a), a.size, metadata_messages_count, partition_id,
+                                            checksum_mode, out.ctypes.data, out.size, ctypes.byref(h),
+                                            ctypes.byref(e))
+        return rc, e, h, (out[:a.size].tobytes() if rc == 0 else None)
 
     def select_slice_device(self, d_record: int, d_frame_pos: int, nframes: int, query: SliceQuery,
                             d_out: int, d_header: int | None = None, stream: int | None = None) -> int:

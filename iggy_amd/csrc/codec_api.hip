@@ -548,6 +548,72 @@ int iggy_codec_stamp_batch(iggy_codec_ctx *c, uint8_t *batch, uint64_t len, uint
     return 0;
 }
 
+// batch_error (server_common/src/send_messages.rs:52-66): integrity errors keep
+// their payloads, every other wire error becomes InvalidCommand
+static int server_error(int rc, iggy_wire_error *err) {
+    if (rc == IGGY_OK || rc == IGGY_ERR_INVALID_BATCH_CHECKSUM || rc == IGGY_ERR_INVALID_MESSAGE_CHECKSUM ||
+        rc >= IGGY_ERR_DEVICE)
+        return rc;
+    set_err(err, IGGY_ERR_INVALID_COMMAND);
+    return IGGY_ERR_INVALID_COMMAND;
+}
+
+// decode_prepare_slice_inner (server_common/src/send_messages.rs:581-622): the
+// structural checks on the host, the per-message + batch checksum pass on the GPU
+int iggy_codec_decode_prepare(iggy_codec_ctx *c, const uint8_t *frame, uint64_t len, int validate,
+                              iggy_batch_header *hdr_out, iggy_wire_error *err) {
+    if (!c || (!frame && len)) return IGGY_ERR_INVALID_ARGUMENT;
+    set_err(err, IGGY_OK);
+    const uint64_t hs = IGGY_PREPARE_HEADER_SIZE;
+    if (len < hs) return server_error(IGGY_ERR_VALIDATION, err);
+    uint32_t total = 0;
+    memcpy(&total, frame + IGGY_PREPARE_SIZE_OFFSET, 4);
+    if (total < hs || len < total) return server_error(IGGY_ERR_VALIDATION, err);
+    const uint8_t *body = frame + hs;
+    const uint64_t body_len = total - hs;
+    if (body_len < 256) return server_error(IGGY_ERR_VALIDATION, err);
+    iggy_batch_header h;
+    int r = iggy_batch_header_decode(body, 256, &h, err);
+    if (r) return server_error(r, err);
+    if (body_len != h.batch_length) return server_error(IGGY_ERR_VALIDATION, err);
+    if (hdr_out) *hdr_out = h;
+    if (!validate) return 0;
+    r = iggy_codec_decode_batch(c, body, body_len, IGGY_INTEGRITY_VERIFY, nullptr, nullptr, 0, nullptr, err);
+    return server_error(r, err);
+}
+
+// admit_wire_request after SendMessagesMetadata::decode
+// (server_common/src/send_messages.rs:505-540)
+int iggy_codec_admit_batch(iggy_codec_ctx *c, const uint8_t *batch, uint64_t len,
+                           uint32_t metadata_messages_count, uint64_t partition_id, int checksum_mode,
+                           uint8_t *out, uint64_t cap, iggy_batch_header *hdr_out, iggy_wire_error *err) {
+    if (!c || (!batch && len) || !out) return IGGY_ERR_INVALID_ARGUMENT;
+    iggy_batch_header h;
+    int r = iggy_codec_decode_batch(c, batch, len, IGGY_INTEGRITY_VERIFY, &h, nullptr, 0, nullptr, err);
+    if (r) return server_error(r, err);
+    if (h.message_count == 0 || h.message_count != metadata_messages_count || len != h.batch_length) {
+        set_err(err, IGGY_ERR_INVALID_COMMAND);
+        return IGGY_ERR_INVALID_COMMAND;
+    }
+    if (cap < len) {
+        set_err(err, IGGY_ERR_CAPACITY, 0, len);
+        return IGGY_ERR_CAPACITY;
+    }
+    memcpy(out, batch, len);
+    h.partition_id = partition_id;
+    h.batch_checksum = 0;
+    if (checksum_mode == IGGY_CHECKSUM_COMPUTE) {
+        r = iggy_codec_calculate_batch_checksum(c, &h, out + 256, len - 256, &h.batch_checksum);
+        if (r) return r;
+    }
+    uint8_t hb[256];
+    iggy_batch_header_encode(&h, hb);
+    memcpy(out, hb, 256);
+    if (hdr_out) *hdr_out = h;
+    set_err(err, IGGY_OK);
+    return 0;
+}
+
 int iggy_codec_xxh3_64(iggy_codec_ctx *c, const void *data, uint64_t len, uint64_t *out) {
     if (!c || !out || (!data && len)) return IGGY_ERR_INVALID_ARGUMENT;
     HIP_OK(hipSetDevice(c->device));

@@ -66,6 +66,9 @@ typedef enum iggy_error_kind {
     /* IggyError mapping used by the SDK poll decode (polled_messages.rs:59-60) */
     IGGY_ERR_INVALID_NUMBER_ENCODING = 20,
     IGGY_ERR_INVALID_MESSAGE_PAYLOAD_LENGTH = 21,
+    /* IggyError::InvalidCommand: batch_error's mapping of every structural WireError
+     * on the server paths (server_common/src/send_messages.rs:52-66) */
+    IGGY_ERR_INVALID_COMMAND = 22,
     /* library-level failures (not wire errors) */
     IGGY_ERR_DEVICE = 100,
     IGGY_ERR_INVALID_ARGUMENT = 101,
@@ -309,6 +312,40 @@ int iggy_codec_select_slice_device(iggy_codec_ctx *ctx, const uint8_t *d_record,
 int iggy_codec_stamp_batch_device(iggy_codec_ctx *ctx, uint8_t *d_record, const uint64_t *d_frame_pos,
                                   uint64_t nframes, uint64_t base_offset, uint64_t base_timestamp,
                                   iggy_batch_header *d_header, void *stream);
+
+/* ------------------------------------------------- server admission / prepare */
+/* PrepareHeader.size (u32) sits at byte 48 of the 256-B consensus header
+ * (binary_protocol/src/consensus/header.rs:901-932); the batch header follows it. */
+#define IGGY_PREPARE_HEADER_SIZE 256u
+#define IGGY_PREPARE_SIZE_OFFSET 48u
+
+/* ChecksumMode (server_common/src/send_messages.rs:416-432) */
+typedef enum iggy_checksum_mode {
+    IGGY_CHECKSUM_COMPUTE = 0,
+    IGGY_CHECKSUM_SKIP = 1
+} iggy_checksum_mode;
+
+/* decode_prepare_slice (validate = 1) / decode_prepare_slice_trusted (validate = 0)
+ * (server_common/src/send_messages.rs:542-622) on one prepare frame
+ * [PrepareHeader 256 B][batch header 256 B][blob] of len bytes. Structural
+ * failures (short frame, size outside [256, len], a body that is not exactly
+ * batch_length long, a batch header that does not decode, frames that do not
+ * tile) return IGGY_ERR_INVALID_COMMAND; validate = 1 also verifies every
+ * message checksum and the batch checksum on the GPU (those two errors keep
+ * their payloads, as batch_error does); validate = 0 reads the header only. */
+int iggy_codec_decode_prepare(iggy_codec_ctx *ctx, const uint8_t *frame, uint64_t len, int validate,
+                              iggy_batch_header *hdr_out, iggy_wire_error *err);
+
+/* admit_wire_request's batch half (server_common/src/send_messages.rs:480-540):
+ * batch = the wire batch after the metadata section (the caller decoded the
+ * metadata and passes its messages_count). Verified as the producer hashed it;
+ * an empty batch, a count unlike the metadata's, or a batch that does not fill
+ * len exactly is IGGY_ERR_INVALID_COMMAND. On success out (>= len bytes)
+ * receives the batch with partition_id stamped and the batch checksum
+ * recomputed (IGGY_CHECKSUM_COMPUTE) or zeroed (IGGY_CHECKSUM_SKIP). */
+int iggy_codec_admit_batch(iggy_codec_ctx *ctx, const uint8_t *batch, uint64_t len,
+                           uint32_t metadata_messages_count, uint64_t partition_id, int checksum_mode,
+                           uint8_t *out, uint64_t cap, iggy_batch_header *hdr_out, iggy_wire_error *err);
 
 /* ------------------------------------------------------------- profiling */
 /* When enabled, the context brackets the dominant kernel of every decode /

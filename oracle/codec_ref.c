@@ -394,6 +394,65 @@ int oracle_stamp_batch(uint8_t *batch, uint64_t len, uint64_t base_offset,
     return 0;
 }
 
+/* batch_error (core/server_common/src/send_messages.rs:52-66): the two integrity
+ * errors keep their payloads, every other wire error is InvalidCommand. */
+static int server_error(int rc, iggy_wire_error *e) {
+    if (rc == 0 || rc == IGGY_ERR_INVALID_BATCH_CHECKSUM || rc == IGGY_ERR_INVALID_MESSAGE_CHECKSUM) return rc;
+    set_err(e, IGGY_ERR_INVALID_COMMAND, 0, 0, 0, 0);
+    return IGGY_ERR_INVALID_COMMAND;
+}
+
+/* decode_prepare_slice_inner — core/server_common/src/send_messages.rs:581-622 */
+int oracle_decode_prepare(const uint8_t *frame, uint64_t len, int validate, iggy_batch_header *h,
+                          iggy_wire_error *e) {
+    set_err(e, IGGY_OK, 0, 0, 0, 0);
+    const uint64_t hs = IGGY_PREPARE_HEADER_SIZE;
+    if (len < hs) return server_error(IGGY_ERR_VALIDATION, e);                     /* :586-588 */
+    uint32_t total = 0;
+    memcpy(&total, frame + IGGY_PREPARE_SIZE_OFFSET, 4);
+    if (total < hs || len < total) return server_error(IGGY_ERR_VALIDATION, e);   /* :603-605 */
+    const uint8_t *body = frame + hs;
+    const uint64_t body_len = total - hs;
+    if (body_len < HDR) return server_error(IGGY_ERR_VALIDATION, e);              /* :608-610 */
+    int rc = oracle_batch_header_decode(body, HDR, h, e);                         /* :612-613 */
+    if (rc) return server_error(rc, e);
+    if (body_len != h->batch_length) return server_error(IGGY_ERR_VALIDATION, e); /* :619-621 */
+    if (validate) {                                                               /* :625-635 */
+        uint64_t computed = 0, n = 0;
+        rc = oracle_verify_and_recompute(h, body + HDR, h->batch_length - HDR, &computed, NULL, 0, &n, e);
+        if (rc) return server_error(rc, e);
+        if (h->batch_checksum != computed) {
+            set_err(e, IGGY_ERR_INVALID_BATCH_CHECKSUM, 0, h->batch_checksum, computed, h->base_offset);
+            return IGGY_ERR_INVALID_BATCH_CHECKSUM;
+        }
+    }
+    return 0;
+}
+
+/* admit_wire_request after the metadata decode — core/server_common/src/send_messages.rs:505-540 */
+int oracle_admit_batch(const uint8_t *batch, uint64_t len, uint32_t meta_count, uint64_t partition_id,
+                       int checksum_mode, uint8_t *out, uint64_t cap, iggy_batch_header *h,
+                       iggy_wire_error *e) {
+    uint64_t n = 0;
+    int rc = oracle_decode_batch_slice_with(batch, len, IGGY_INTEGRITY_VERIFY, h, NULL, 0, &n, e); /* :505 */
+    if (rc) return server_error(rc, e);
+    if (h->message_count == 0 || h->message_count != meta_count || len != h->batch_length) {   /* :506-511 */
+        set_err(e, IGGY_ERR_INVALID_COMMAND, 0, 0, 0, 0);
+        return IGGY_ERR_INVALID_COMMAND;
+    }
+    if (cap < len) {
+        set_err(e, IGGY_ERR_CAPACITY, 0, len, 0, 0);
+        return IGGY_ERR_CAPACITY;
+    }
+    memcpy(out, batch, len);                                                      /* :518-520 */
+    h->partition_id = partition_id;                                               /* :524-530 */
+    h->batch_checksum = checksum_mode == IGGY_CHECKSUM_COMPUTE
+                            ? oracle_calculate_batch_checksum(h, out + HDR, len - HDR)
+                            : 0;
+    oracle_batch_header_encode(h, out);
+    return 0;
+}
+
 /* select_batch_slice — core/partitions/src/journal.rs:1025-1086, then the header
  * push_selected_batch_fragments serves (journal.rs:1096-1137): a partial selection
  * gets batch_length = 256 + (end - start), message_count = matched and the batch

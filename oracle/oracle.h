@@ -59,6 +59,14 @@ int oracle_stamp_batch(uint8_t *batch, uint64_t len, uint64_t base_offset,
 int oracle_select_batch_slice(const uint8_t *record, uint64_t len, const iggy_slice_query *q,
                               iggy_slice_result *out, uint8_t *header_out);
 
+/* decode_prepare_slice(_trusted) and admit_wire_request's batch half
+ * (core/server_common/src/send_messages.rs:480-622), errors mapped by batch_error. */
+int oracle_decode_prepare(const uint8_t *frame, uint64_t len, int validate, iggy_batch_header *h,
+                          iggy_wire_error *e);
+int oracle_admit_batch(const uint8_t *batch, uint64_t len, uint32_t meta_count, uint64_t partition_id,
+                       int checksum_mode, uint8_t *out, uint64_t cap, iggy_batch_header *h,
+                       iggy_wire_error *e);
+
 /* synthetic input generator shared by tests and bench (BASELINE.md:
  * splitmix64, seed 0x16619E3779B97F4A ^ partition). Builds a stamped,
  * checksummed record of n frames; payload length of frame i =

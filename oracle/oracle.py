@@ -61,6 +61,8 @@ def lib() -> ctypes.CDLL:
         L.oracle_cpu_decode_bench.argtypes = [vp, u64, ctypes.c_int, ctypes.c_int, vp]
         L.oracle_has_avx2.restype = ctypes.c_int
         L.oracle_select_batch_slice.argtypes = [vp, u64, vp, vp, vp]
+        L.oracle_decode_prepare.argtypes = [vp, u64, ctypes.c_int, vp, vp]
+        L.oracle_admit_batch.argtypes = [vp, u64, u32, u64, ctypes.c_int, vp, u64, vp, vp]
         _lib = L
     return _lib
 
@@ -148,6 +150,30 @@ def stamp_batch(batch, base_offset: int, base_timestamp: int):
     rc = lib().oracle_stamp_batch(a.ctypes.data, a.size, base_offset, base_timestamp,
                                   ctypes.byref(h), ctypes.byref(e))
     return rc, e, h, a.tobytes()
+
+
+def decode_prepare(frame, validate: bool = True):
+    """decode_prepare_slice / _trusted -> (rc, WireError, BatchHeader)"""
+    a = _as_np(frame)
+    h = BatchHeader()
+    e = WireError()
+    rc = lib().oracle_decode_prepare(a.ctypes.data if a.size else None, a.size, 1 if validate else 0,
+                                     ctypes.byref(h), ctypes.byref(e))
+    return rc, e, h
+
+
+def admit_batch(batch, metadata_messages_count: int, partition_id: int, checksum_mode: int = 0):
+    """admit_wire_request's batch half -> (rc, WireError, BatchHeader, admitted bytes or None)"""
+    import numpy as np
+
+    a = _as_np(batch)
+    out = np.zeros(max(a.size, 1), dtype=np.uint8)
+    h = BatchHeader()
+    e = WireError()
+    rc = lib().oracle_admit_batch(a.ctypes.data if a.size else None, a.size, metadata_messages_count,
+                                  partition_id, checksum_mode, out.ctypes.data, out.size, ctypes.byref(h),
+                                  ctypes.byref(e))
+    return rc, e, h, (out[:a.size].tobytes() if rc == 0 else None)
 
 
 def select_slice(record, kind: int, value: int, count: int, ceiling: int = 2**64 - 1, already_matched: int = 0):

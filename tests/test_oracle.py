@@ -10,6 +10,88 @@ from iggy_amd import abi
 from oracle import oracle as O
 
 
+def _prepare_frame(batch, size=None, trailing=b""):
+    """[PrepareHeader 256 B (size at 48)][batch][trailing], as server_common's
+    prepare_from_owned builds it (send_messages.rs:690-705)."""
+    body = bytes(batch) + trailing
+    hdr = bytearray(256)
+    struct.pack_into("<I", hdr, 48, 256 + len(body) if size is None else size)
+    return np.frombuffer(bytes(hdr) + body, dtype=np.uint8).copy()
+
+
+def _wire_batch(n=7, seed=3):
+    from iggy_amd.codec import raw_messages
+    rng = np.random.default_rng(seed)
+    pls = rng.integers(1, 300, size=n).astype(np.uint32)
+    ids = rng.integers(1, 2**63, size=2 * n, dtype=np.uint64)
+    ots = (1_700_000_000_000_000 + np.arange(n)).astype(np.uint64)
+    pay = rng.integers(0, 256, size=int(pls.sum()), dtype=np.uint8)
+    rc, e, out = O.encode_batch(raw_messages(ids, ots, pay, pls), 0)
+    assert rc == 0, e
+    return np.frombuffer(out, dtype=np.uint8).copy()
+
+
+def test_decode_prepare_mirrors_server_common_tests():
+    # send_messages.rs:721-745: trusted and validating agree on a stamped batch
+    rec = O.synth_batch(40, 10, 500, 0)
+    fr = _prepare_frame(rec)
+    rc, e, h = O.decode_prepare(fr, True)
+    rc2, e2, h2 = O.decode_prepare(fr, False)
+    assert rc == 0 and rc2 == 0, (e, e2)
+    assert h.astuple() == h2.astuple() and h.message_count == 40
+    # :747-766: a mutated stored batch checksum fails only the validating decode
+    bad = fr.copy()
+    bad[256 + 40] ^= 0xFF
+    assert O.decode_prepare(bad, True)[0] == abi.ERR_INVALID_BATCH_CHECKSUM
+    assert O.decode_prepare(bad, False)[0] == 0
+    # :769-782: size below the header size
+    for size in (0, 255):
+        assert O.decode_prepare(_prepare_frame(rec, size=size), True)[0] == abi.ERR_INVALID_COMMAND
+    # :947-966: payload corruption under an intact checksum field
+    bad = fr.copy()
+    bad[512 + 48] ^= 0xFF
+    assert O.decode_prepare(bad, True)[0] == abi.ERR_INVALID_MESSAGE_CHECKSUM
+    assert O.decode_prepare(bad, False)[0] == 0
+    # :1292-1307: trailing bytes past batch_length (size covers them)
+    for junk in (b"\x00", b"\x01" * 7, b"\x00" * 64):
+        assert O.decode_prepare(_prepare_frame(rec, trailing=junk), True)[0] == abi.ERR_INVALID_COMMAND
+    # a size that overruns the buffer, and a tiling break (structural -> InvalidCommand)
+    assert O.decode_prepare(_prepare_frame(rec, size=256 + rec.size + 1), True)[0] == abi.ERR_INVALID_COMMAND
+    brk = fr.copy()
+    brk[512 + 44] = 1  # first frame's reserved bytes
+    assert O.decode_prepare(brk, True)[0] == abi.ERR_INVALID_COMMAND
+
+
+def test_admit_batch_mirrors_server_common_tests():
+    wire = _wire_batch()
+    # :1053-1090: admitted, partition stamped, checksum recomputed over the stamped header
+    rc, e, h, out = O.admit_batch(wire, 7, 5, abi.CHECKSUM_COMPUTE)
+    assert rc == 0, e
+    assert h.partition_id == 5
+    stamped = O.decode_batch_slice_with(np.frombuffer(out, dtype=np.uint8), abi.INTEGRITY_VERIFY)
+    assert stamped[0] == 0 and stamped[2].partition_id == 5
+    assert out[256:] == wire[256:].tobytes()
+    # :1121-1150: Skip leaves the checksum zero until stamp
+    rc, e, h, out = O.admit_batch(wire, 7, 5, abi.CHECKSUM_SKIP)
+    assert rc == 0 and h.batch_checksum == 0 and struct.unpack_from("<Q", out, 40)[0] == 0
+    # :1093-1104: a tampered body keeps its integrity error
+    bad = wire.copy()
+    bad[256 + 48 + 3] ^= 0x10
+    assert O.admit_batch(bad, 7, 5)[0] == abi.ERR_INVALID_MESSAGE_CHECKSUM
+    # :1106-1119: metadata count mismatch
+    assert O.admit_batch(wire, 6, 5)[0] == abi.ERR_INVALID_COMMAND
+    # trailing bytes past batch_length (:1260-1278 at the wire form)
+    assert O.admit_batch(np.concatenate([wire, np.zeros(3, dtype=np.uint8)]), 7, 5)[0] == abi.ERR_INVALID_COMMAND
+    # :1015-1050: an empty batch (header only, valid checksum) is rejected
+    empty = np.zeros(256, dtype=np.uint8)
+    struct.pack_into("<Q", empty, 32, 256)
+    hdr = abi.BatchHeader()
+    hdr.batch_length = 256
+    struct.pack_into("<Q", empty, 40, O.calculate_batch_checksum(hdr, b""))
+    assert O.decode_batch_slice_with(empty, abi.INTEGRITY_VERIFY)[0] == 0
+    assert O.admit_batch(empty, 0, 5)[0] == abi.ERR_INVALID_COMMAND
+
+
 def test_xxh3_matches_libxxhash_fixtures():
     blob, vecs = xxh3_vectors()
     for v in vecs:

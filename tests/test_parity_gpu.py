@@ -123,6 +123,54 @@ def test_count_and_stride_breaks(cx):
     _check_decode(cx, np.concatenate([base, np.full(77, 9, dtype=np.uint8)]))
 
 
+def _prepare_frame(batch, size=None, trailing=b""):
+    body = bytes(batch) + trailing
+    hdr = bytearray(256)
+    struct.pack_into("<I", hdr, 48, 256 + len(body) if size is None else size)
+    return np.frombuffer(bytes(hdr) + body, dtype=np.uint8).copy()
+
+
+def test_decode_prepare_matches_oracle(cx):
+    recs = [O.synth_batch(40, 10, 500, 0), O.synth_batch(3000, 1024, 1024, 0), O.synth_batch(500, 0, 5000, 3)]
+    for rec in recs:
+        fr = _prepare_frame(rec)
+        cases = [fr, _prepare_frame(rec, size=0), _prepare_frame(rec, size=255),
+                 _prepare_frame(rec, size=256 + rec.size + 1), _prepare_frame(rec, trailing=b"\x00" * 9)]
+        for off in (256 + 40, 512 + 48, 512 + 44, 256 + 32, 256 + 60):
+            b = fr.copy()
+            b[off] ^= 0x5A
+            cases.append(b)
+        for c in cases:
+            for validate in (True, False):
+                rc, e, h = cx.decode_prepare(c, validate)
+                orc, oe, oh = O.decode_prepare(c, validate)
+                _same(rc, e, orc, oe)
+                if rc == 0:
+                    assert h.astuple() == oh.astuple()
+
+
+def test_admit_batch_matches_oracle(cx):
+    from iggy_amd.codec import raw_messages
+    rng = np.random.default_rng(11)
+    for n, lo, hi in ((7, 1, 300), (2000, 1024, 1024), (900, 0, 3000)):
+        pls = rng.integers(lo, hi + 1, size=n).astype(np.uint32)
+        ids = rng.integers(1, 2**63, size=2 * n, dtype=np.uint64)
+        ots = (1_700_000_000_000_000 + np.arange(n)).astype(np.uint64)
+        pay = rng.integers(0, 256, size=int(pls.sum()), dtype=np.uint8)
+        rc, e, out = O.encode_batch(raw_messages(ids, ots, pay, pls), 0)
+        wire = np.frombuffer(out, dtype=np.uint8).copy()
+        bad = wire.copy()
+        bad[256 + 48 + 3] ^= 0x10
+        for batch, count in ((wire, n), (wire, n - 1), (bad, n), (np.concatenate([wire, np.zeros(3, np.uint8)]), n)):
+            for mode in (abi.CHECKSUM_COMPUTE, abi.CHECKSUM_SKIP):
+                got = cx.admit_batch(batch, count, 9, mode)
+                exp = O.admit_batch(batch, count, 9, mode)
+                _same(got[0], got[1], exp[0], exp[1])
+                if got[0] == 0:
+                    assert got[2].astuple() == exp[2].astuple()
+                    assert got[3] == exp[3]
+
+
 def _crafted_record(n, lo, hi, fill, seed):
     """A stamped record whose payloads defeat the tile speculation: "zero" payloads
     (every offset inside them is a candidate frame start) or "fake" payloads that
