@@ -85,9 +85,10 @@ __device__ __forceinline__ uint64_t chain_run16(uint64_t acc, const uint64_t (&v
     for (int k = 0; k < 16; ++k) acc = scramble_fast(acc + v[k], klo, khi);
     return acc;
 }
-__device__ inline uint64_t chain_blocks(const uint64_t *bsums, uint64_t nb, int lane) {
+__device__ inline uint64_t chain_blocks(const uint64_t *bsums, uint64_t nb, int lane,
+                                       const uint64_t *acc_in = nullptr) {
     const int j = lane & 7;
-    uint64_t acc = kAccInit[j];
+    uint64_t acc = acc_in ? acc_in[j] : kAccInit[j];
     const uint64_t key = kSecretW8[16 + j];
     const uint32_t klo = (uint32_t)key, khi = (uint32_t)(key >> 32);
     if (nb == 0) return acc;
@@ -157,6 +158,83 @@ __global__ __launch_bounds__(64) void k_bsum_chain(const iggy_batch_header *hp,
     if (pl.long_cs) {
         const int j = lane & 7;
         uint64_t acc = chain_blocks(bsums, pl.nb, lane);
+        acc += bsums[pl.nb * 8 + j];
+        const uint64_t v = src(N - 8 + j);
+        acc += __shfl_xor(v, 1);
+        acc += mul32x32(v ^ kSecretLast[j]);
+        uint64_t a[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) a[i] = __shfl(acc, i);
+        uint64_t r = pl.n * P64_1;
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+            r += fold64(a[2 * i] ^ Secret::w(11 + 16 * i), a[2 * i + 1] ^ Secret::w(19 + 16 * i));
+        if (lane == 0) *out = avalanche(r);
+    } else if (lane == 0) {
+        for (uint64_t m = 0; m < 5; ++m) st64_any(small + 8 * m, cs_word(m, h, src));
+        *(uint32_t *)(small + 40) = h.message_count;
+        for (uint64_t i = 0; i < N; ++i) st64_any(small + 44 + 8 * i, src(i));
+        *out = xxh3_64_lane(small, pl.n);
+    }
+}
+
+// ---- the same checksum in segments, so its serial chain can run beside the
+// kernels still producing later frame checksums (encode: k_enc_lanes by frame
+// range). Blocks [b_lo, b_hi) of the nb full blocks + the last partial block.
+__global__ __launch_bounds__(256) void k_bsum_blocks_range(const iggy_batch_header *hp,
+                                                           const uint64_t *nframes_p, CsSource src,
+                                                           uint64_t *bsums, uint64_t b_lo, uint64_t b_hi) {
+    const iggy_batch_header h = *hp;
+    const CsPlan pl = cs_plan(*nframes_p);
+    if (!pl.long_cs) return;
+    const int lane = threadIdx.x & 63;
+    const uint64_t wid = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const uint64_t nwaves = ((uint64_t)gridDim.x * blockDim.x) >> 6;
+    const uint64_t hi = b_hi < pl.nb + 1 ? b_hi : pl.nb + 1;
+    for (uint64_t b = b_lo + wid; b < hi; b += nwaves) {
+        uint64_t x = 0, y = 0;
+#pragma unroll
+        for (int half = 0; half < 2; ++half) {
+            const uint64_t m = 128 * b + 64 * half + lane;
+            if (m < pl.Mreg) {
+                const uint64_t v = cs_word(m, h, src);
+                y += v;
+                x += mul32x32(v ^ kSecretW8[((m >> 3) & 15) + (m & 7)]);
+            }
+        }
+        x += __shfl_xor(x, 8); y += __shfl_xor(y, 8);
+        x += __shfl_xor(x, 16); y += __shfl_xor(y, 16);
+        x += __shfl_xor(x, 32); y += __shfl_xor(y, 32);
+        const uint64_t t8 = x + __shfl_xor(y, 1);
+        if (lane < 8) bsums[b * 8 + lane] = t8;
+    }
+}
+
+// full blocks [b_lo, min(b_hi, nb)) of the chain; state[8] carries the
+// accumulators between segments (b_lo == 0 starts from the XXH3 init)
+__global__ __launch_bounds__(64) void k_chain_partial(const uint64_t *nframes_p, const uint64_t *bsums,
+                                                      uint64_t *state, uint64_t b_lo, uint64_t b_hi) {
+    const CsPlan pl = cs_plan(*nframes_p);
+    if (!pl.long_cs) return;
+    const int lane = threadIdx.x & 63;
+    const uint64_t hi = b_hi < pl.nb ? b_hi : pl.nb;
+    if (b_lo >= hi) return;
+    const uint64_t acc = chain_blocks(bsums + 8 * b_lo, hi - b_lo, lane, b_lo ? state : nullptr);
+    if (lane < 8) state[lane] = acc;
+}
+
+// last partial block, last stripe and merge after the segments (or the whole
+// short-input form); out[0] = the batch checksum
+__global__ __launch_bounds__(64) void k_chain_finish(const iggy_batch_header *hp, const uint64_t *nframes_p,
+                                                     CsSource src, const uint64_t *bsums, const uint64_t *state,
+                                                     uint8_t *small, uint64_t *out) {
+    const iggy_batch_header h = *hp;
+    const uint64_t N = *nframes_p;
+    const CsPlan pl = cs_plan(N);
+    const int lane = threadIdx.x & 63;
+    if (pl.long_cs) {
+        const int j = lane & 7;
+        uint64_t acc = pl.nb ? state[j] : kAccInit[j];
         acc += bsums[pl.nb * 8 + j];
         const uint64_t v = src(N - 8 + j);
         acc += __shfl_xor(v, 1);

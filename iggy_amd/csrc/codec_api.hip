@@ -63,6 +63,9 @@ struct DevBuf {
 
 }  // namespace
 
+constexpr int kEncSegs = 4;                   // encode segments (checksum chain overlap); bounds below
+constexpr uint64_t kEncSegMinFrames = 1 << 18;  // below this one segment
+
 struct iggy_codec_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
@@ -76,6 +79,10 @@ struct iggy_codec_ctx {
     DevBuf dsums, derr;
     DevBuf gtiles_s, gtiles_x, gtiles_cnt, gtiles_pre, gtiles_list, gtiles_e, gtiles_base, ggrp, gfpos, gcs, gflen, gbsums;
     int gen_grid = 0;  // co-resident WGs of k_decode_general
+    // encode: the batch-checksum chain of earlier frame segments runs on `side`
+    // while later segments are encoded on the call's stream
+    hipStream_t side = nullptr;
+    hipEvent_t seg_ev[kEncSegs + 1] = {};
     DevBuf dresult;  // iggy_decode_result + iggy_encode_result + u64 scratch
     // sync-API staging
     DevBuf din, dpos, dout;
@@ -294,10 +301,14 @@ int iggy_codec_create(int device, iggy_codec_ctx **out) {
     c->ncu = prop.multiProcessorCount;
     if (const char *d = getenv("IGGY_CODEC_DBG")) c->dbg = (uint32_t)strtoul(d, nullptr, 0);
     if (hipSetDevice(device) != hipSuccess ||
-        hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+        hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking) != hipSuccess) {
+        if (c->stream) (void)hipStreamDestroy(c->stream);
         delete c;
         return IGGY_ERR_DEVICE;
     }
+    for (auto &ev : c->seg_ev)
+        if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) ev = nullptr;
     int r = 0;
     r |= c->dresult.ensure(4096);
     if (hipHostMalloc(&c->h_pinned, 4096, hipHostMallocDefault) != hipSuccess) r = IGGY_ERR_DEVICE;
@@ -362,6 +373,9 @@ void iggy_codec_destroy(iggy_codec_ctx *c) {
         if (c->ev0[w]) (void)hipEventDestroy(c->ev0[w]);
         if (c->ev1[w]) (void)hipEventDestroy(c->ev1[w]);
     }
+    for (auto &ev : c->seg_ev)
+        if (ev) (void)hipEventDestroy(ev);
+    if (c->side) (void)hipStreamDestroy(c->side);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
 }
@@ -644,7 +658,7 @@ static int enqueue_encode(iggy_codec_ctx *c, const iggy_raw_messages *dm, uint64
     r |= c->euh.ensure(n * 8);
     r |= c->etile.ensure(ntiles * 24 + 64);
     r |= c->ecs.ensure(n * 8);
-    r |= c->emisc.ensure(512);
+    r |= c->emisc.ensure(1024);  // misc | header | checksum | small | chain state (512)
     const uint64_t nbk = (44 + 8 * n) / 1024 + 2;
     r |= c->gbsums.ensure(nbk * 64);
     if (r) return IGGY_ERR_DEVICE;
@@ -662,24 +676,76 @@ static int enqueue_encode(iggy_codec_ctx *c, const iggy_raw_messages *dm, uint64
     hipLaunchKernelGGL(k_enc_prep, dim3(ntiles), dim3(256), 0, s, m, es);
     hipLaunchKernelGGL(k_enc_scan, dim3(1), dim3(256), 0, s, ntiles, n, partition_id, es);
     const uint64_t waves = std::min<uint64_t>(n, (uint64_t)c->ncu * 32);
+    CsSource src{es.cs, nullptr, nullptr};
+    // checksum blocks: 44 + 8n bytes; full blocks nb (the chain), then the last one
+    const uint64_t csb = 44 + 8 * n;
+    const uint64_t nb = csb > 240 ? (csb - 1) / 1024 : 0;
+    bool segmented = false;
     if (!m.user_headers_lengths) {
-        // no user headers: lane-group kernel (k_enc_frames only covers a < 16-B payload area)
-        const uint64_t lwg = std::min<uint64_t>((n + 31) / 32, (uint64_t)c->ncu * 8);
-        hipLaunchKernelGGL(k_enc_lanes, dim3(lwg), dim3(256), 0, s, m, es, d_out);
+        // no user headers: lane-group kernel (k_enc_frames only covers a < 16-B payload
+        // area, and runs first so the segments' checksum chain sees its output)
+        hipLaunchKernelGGL(k_enc_frames, dim3((waves + 3) / 4), dim3(256), 0, s, m, es, d_out, 1u);
         hipLaunchKernelGGL(k_enc_short, dim3(std::min<uint64_t>((n + 255) / 256, (uint64_t)c->ncu * 4)), dim3(256),
                            0, s, m, es, d_out);
-        hipLaunchKernelGGL(k_enc_frames, dim3((waves + 3) / 4), dim3(256), 0, s, m, es, d_out, 1u);
+        const uint64_t lwg = std::min<uint64_t>((n + 31) / 32, (uint64_t)c->ncu * 8);
+        int nseg = 1;
+        if (n >= kEncSegMinFrames && nb >= 4 * kEncSegs && c->side) {
+            nseg = kEncSegs;
+            for (auto ev : c->seg_ev)
+                if (!ev) nseg = 1;
+        }
+        segmented = nseg > 1;
+        uint64_t *state = c->emisc.as<uint64_t>(512);
+        for (int k = 0; k < nseg; ++k) {
+            // blocks [B_k, B_k+1) need frames up to 128 B_k+1 - 6: segment k encodes
+            // frames [F_k, F_k+1), F_k = 128 B_k - 5
+            // uneven segments: the last one (whose chain cannot overlap) is ~6 % of the blocks
+            static const uint32_t kSegPermille[kEncSegs + 1] = {0, 400, 750, 940, 1000};
+            auto bound = [&](int q) {
+                if (nseg == 1) return q ? nb : (uint64_t)0;
+                if (c->dbg & 1024) return nb * q / nseg;  // diagnostics: even segments
+                return nb * kSegPermille[q] / 1000;
+            };
+            const uint64_t B0 = bound(k), B1 = bound(k + 1);
+            const uint64_t F0 = k == 0 ? 0 : std::min<uint64_t>(n, 128 * B0 - 5);
+            const uint64_t F1 = k == nseg - 1 ? n : std::min<uint64_t>(n, 128 * B1 - 5);
+            hipLaunchKernelGGL(k_enc_lanes, dim3(lwg), dim3(256), 0, s, m, es, d_out, F0, F1);
+            if (segmented && k < nseg - 1) {
+                HIP_OK(hipEventRecord(c->seg_ev[k], s));
+                HIP_OK(hipStreamWaitEvent(c->side, c->seg_ev[k], 0));
+                hipLaunchKernelGGL(k_bsum_blocks_range, dim3(c->ncu / 2), dim3(256), 0, c->side,
+                                   (const iggy_batch_header *)es.hdr, (const uint64_t *)&es.misc[3], src,
+                                   c->gbsums.as<uint64_t>(), B0, B1);
+                hipLaunchKernelGGL(k_chain_partial, dim3(1), dim3(64), 0, c->side, (const uint64_t *)&es.misc[3],
+                                   (const uint64_t *)c->gbsums.as<uint64_t>(), state, B0, B1);
+            }
+        }
+        if (segmented) {
+            // the last segment's blocks and the partial one, after every frame
+            const uint64_t Bl = (c->dbg & 1024) ? nb * (nseg - 1) / nseg : nb * 940 / 1000;  // last segment
+            HIP_OK(hipEventRecord(c->seg_ev[kEncSegs], c->side));
+            HIP_OK(hipStreamWaitEvent(s, c->seg_ev[kEncSegs], 0));
+            hipLaunchKernelGGL(k_bsum_blocks_range, dim3(c->ncu), dim3(256), 0, s, (const iggy_batch_header *)es.hdr,
+                               (const uint64_t *)&es.misc[3], src, c->gbsums.as<uint64_t>(), Bl, nb + 1);
+            hipLaunchKernelGGL(k_chain_partial, dim3(1), dim3(64), 0, s, (const uint64_t *)&es.misc[3],
+                               (const uint64_t *)c->gbsums.as<uint64_t>(), state, Bl, nb);
+        }
     } else {
         hipLaunchKernelGGL(k_enc_frames, dim3((waves + 3) / 4), dim3(256), 0, s, m, es, d_out, 0u);
     }
     prof_end(c, 1, s);
-    CsSource src{es.cs, nullptr, nullptr};
-    hipLaunchKernelGGL(k_bsum_blocks, dim3(c->ncu * 4), dim3(256), 0, s, (const iggy_batch_header *)es.hdr,
-                       (const uint64_t *)&es.misc[3], src, c->gbsums.as<uint64_t>(), nullptr);
     uint64_t *dcs = c->emisc.as<uint64_t>(256);
-    hipLaunchKernelGGL(k_bsum_chain, dim3(1), dim3(64), 0, s, (const iggy_batch_header *)es.hdr,
-                       (const uint64_t *)&es.misc[3], src, (const uint64_t *)c->gbsums.as<uint64_t>(),
-                       c->emisc.as<uint8_t>(320) /* 192 B of small */, dcs, nullptr);
+    if (segmented) {
+        hipLaunchKernelGGL(k_chain_finish, dim3(1), dim3(64), 0, s, (const iggy_batch_header *)es.hdr,
+                           (const uint64_t *)&es.misc[3], src, (const uint64_t *)c->gbsums.as<uint64_t>(),
+                           (const uint64_t *)c->emisc.as<uint64_t>(512), c->emisc.as<uint8_t>(320), dcs);
+    } else {
+        hipLaunchKernelGGL(k_bsum_blocks, dim3(c->ncu * 4), dim3(256), 0, s, (const iggy_batch_header *)es.hdr,
+                           (const uint64_t *)&es.misc[3], src, c->gbsums.as<uint64_t>(), nullptr);
+        hipLaunchKernelGGL(k_bsum_chain, dim3(1), dim3(64), 0, s, (const iggy_batch_header *)es.hdr,
+                           (const uint64_t *)&es.misc[3], src, (const uint64_t *)c->gbsums.as<uint64_t>(),
+                           c->emisc.as<uint8_t>(320) /* 192 B of small */, dcs, nullptr);
+    }
     hipLaunchKernelGGL(k_enc_finish, dim3(1), dim3(64), 0, s, m, es, partition_id,
                        (const uint64_t *)dcs, d_out, d_res);
     HIP_OK(hipGetLastError());

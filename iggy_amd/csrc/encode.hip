@@ -322,10 +322,11 @@ __global__ __launch_bounds__(256) void k_enc_frames(iggy_raw_messages m, EncScra
 struct EFrame {
     uint64_t i, po, pl;  // i >= count: none
 };
-__device__ __forceinline__ EFrame eframe(const iggy_raw_messages &m, const EncScratch &es, uint64_t i) {
+__device__ __forceinline__ EFrame eframe(const iggy_raw_messages &m, const EncScratch &es, uint64_t i,
+                                         uint64_t n) {
     EFrame f;
-    f.i = i;
-    if (i < m.count) {
+    f.i = i < n ? i : ~0ull;  // past this launch's range: none
+    if (i < n) {
         f.po = es.tile_pl[i / kEncTile] + es.pl_local[i];
         f.pl = m.payload_lengths[i];
     } else {
@@ -374,10 +375,11 @@ __device__ __forceinline__ void eissue(const iggy_raw_messages &m, const EFrame 
     st.ots = m.origin_timestamps[i];
 }
 
-__global__ __launch_bounds__(256, 2) void k_enc_lanes(iggy_raw_messages m, EncScratch es, uint8_t *out) {
+__global__ __launch_bounds__(256, 2) void k_enc_lanes(iggy_raw_messages m, EncScratch es, uint8_t *out,
+                                                       uint64_t f_lo, uint64_t f_hi) {
     const uint64_t ptot = es.misc[4];
     if (ptot < 16) return;  // tiny payload area: k_enc_frames (fallback) encodes it
-    const uint64_t n = m.count;
+    const uint64_t n = f_hi < m.count ? f_hi : m.count;  // this launch: frames [f_lo, f_hi)
     const uint64_t origin = es.misc[0];
     const int lane = threadIdx.x & 63;
     const uint32_t l = lane & 7, mm = l >> 1, par = l & 1, fg = (uint32_t)lane >> 3;
@@ -396,8 +398,8 @@ __global__ __launch_bounds__(256, 2) void k_enc_lanes(iggy_raw_messages m, EncSc
     const uint64_t stride = 8ull * nvw;
     const uint32_t sbase = par + 2 * mm;  // secret word of piece q: sbase + 2q (and + 1)
 
-    EFrame cur = eframe(m, es, 8ull * vw + fg);
-    EFrame nxt = eframe(m, es, cur.i + stride);
+    EFrame cur = eframe(m, es, f_lo + 8ull * vw + fg, n);
+    EFrame nxt = eframe(m, es, cur.i == ~0ull ? ~0ull : cur.i + stride, n);
     uint32_t b = 0;
     uint64_t a0 = init0, a1 = init1;
     uint64_t h0 = 0, h1 = 0, h2 = 0, h3 = 0;  // header words of the current frame
@@ -488,7 +490,7 @@ __global__ __launch_bounds__(256, 2) void k_enc_lanes(iggy_raw_messages m, EncSc
                 es.cs[cur.i] = hsh;
             }
             cur = nxt;
-            nxt = eframe(m, es, cur.i + stride);
+            nxt = eframe(m, es, cur.i == ~0ull ? ~0ull : cur.i + stride, n);
             b = 0;
             a0 = init0;
             a1 = init1;

@@ -244,6 +244,21 @@ def test_encode_matches_oracle(cx, n, lo, hi, with_uh, partition_id):
     assert rc == 0, e
 
 
+@pytest.mark.parametrize("n,lo,hi", [(300_000, 0, 64), (262_144, 100, 1100)])
+def test_encode_segmented_matches_oracle(cx, n, lo, hi):
+    """Batches of >= 2^18 messages encode in segments with the checksum chain of
+    earlier segments on the side stream: byte-identical to the oracle."""
+    from iggy_amd.codec import raw_messages
+    rng = np.random.default_rng(n + lo)
+    pls = rng.integers(lo, hi + 1, size=n).astype(np.uint32)
+    ids, ots, pay, _ = _raw_from_arrays(n, pls, None, rng)
+    raw = raw_messages(ids, ots, pay, pls)
+    rc, e, out = cx.encode_batch(raw, 4)
+    orc, oe, oout = O.encode_batch(raw, 4)
+    _same(rc, e, orc, oe)
+    assert out == oout
+
+
 def test_encode_errors(cx):
     from iggy_amd.codec import raw_messages
     rng = np.random.default_rng(1)
