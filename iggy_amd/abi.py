@@ -162,3 +162,13 @@ assert ctypes.sizeof(WireError) == 32
 assert ctypes.sizeof(PolledMessage) == 80
 assert ctypes.sizeof(DecodeResult) == 128
 assert ctypes.sizeof(EncodeResult) == 128
+
+
+class SegmentRecovery(ctypes.Structure):
+    """iggy_segment_recovery (segment_recovery.rs:425-488 index-less walk)."""
+    _fields_ = [("found", ctypes.c_uint64), ("start_timestamp", ctypes.c_uint64),
+                ("end_timestamp", ctypes.c_uint64), ("end_offset", ctypes.c_uint64),
+                ("walked_bytes", ctypes.c_uint64), ("batches", ctypes.c_uint64)]
+
+    def astuple(self):
+        return tuple(getattr(self, f) for f, _ in self._fields_)

@@ -83,6 +83,7 @@ def lib() -> ctypes.CDLL:
     L.iggy_codec_stamp_batch_device.argtypes = [vp, vp, vp, u64, u64, u64, vp, vp]
     L.iggy_codec_decode_prepare.argtypes = [vp, vp, u64, ci, vp, vp]
     L.iggy_codec_admit_batch.argtypes = [vp, vp, u64, u32, u64, ci, vp, u64, vp, vp]
+    L.iggy_codec_recover_segment.argtypes = [vp, vp, u64, u64, vp]
     L.iggy_codec_profile_enable.argtypes = [vp, ci]
     L.iggy_codec_profile_read.argtypes = [vp, ci, vp, vp]
     L.iggy_codec_error_string.argtypes = [u32, u32]
@@ -240,6 +241,14 @@ class Codec:
                                             checksum_mode, out.ctypes.data, out.size, ctypes.byref(h),
                                             ctypes.byref(e))
         return rc, e, h, (out[:a.size].tobytes() if rc == 0 else None)
+
+    def recover_segment(self, messages, start_offset: int):
+        """recover_segment_bounds' index-less walk (segment_recovery.rs:425-530)
+        -> (rc, SegmentRecovery)."""
+        a = _np(messages)
+        out = abi.SegmentRecovery()
+        rc = self._L.iggy_codec_recover_segment(self._h, _addr(a), a.size, start_offset, ctypes.byref(out))
+        return rc, out
 
     def select_slice_device(self, d_record: int, d_frame_pos: int, nframes: int, query: SliceQuery,
                             d_out: int, d_header: int | None = None, stream: int | None = None) -> int:

@@ -628,6 +628,78 @@ int iggy_codec_admit_batch(iggy_codec_ctx *c, const uint8_t *batch, uint64_t len
     return 0;
 }
 
+// recover_segment_bounds' index-less walk (core/partitions/src/segment_recovery.rs:425-530).
+// The chain of candidate batches depends on headers only (decode, extent, offset
+// contiguity), so the host walks it first; every candidate is then verified on the
+// GPU from one copy of the file (decodes queued back to back, one sync), and the
+// first candidate that fails verification ends the accepted chain.
+int iggy_codec_recover_segment(iggy_codec_ctx *c, const uint8_t *messages, uint64_t len,
+                               uint64_t start_offset, iggy_segment_recovery *out) {
+    if (!c || !out || (!messages && len)) return IGGY_ERR_INVALID_ARGUMENT;
+    HIP_OK(hipSetDevice(c->device));
+    memset(out, 0, sizeof(*out));
+    auto sat = [](uint64_t a, uint64_t b) { return a + b < a ? ~0ull : a + b; };
+    struct Cand { uint64_t pos; iggy_batch_header h; };
+    std::vector<Cand> cand;
+    uint64_t pos = 0, expected = start_offset, maxlen = 0;
+    while (pos < len) {
+        iggy_batch_header h;
+        iggy_wire_error e;
+        if (len - pos < 256 || iggy_batch_header_decode(messages + pos, 256, &h, &e)) break;
+        const uint64_t extent = sat(pos, h.batch_length);
+        if (extent > len || h.base_offset != expected) break;
+        cand.push_back({pos, h});
+        maxlen = std::max(maxlen, h.batch_length);
+        if (h.message_count > 0) expected = sat(sat(h.base_offset, (uint64_t)h.message_count - 1), 1);
+        pos = extent;
+    }
+    size_t accepted = 0;
+    if (!cand.empty()) {
+        const uint64_t span = cand.back().pos + cand.back().h.batch_length;
+        int r = c->din.ensure(span + 16);
+        r |= c->dout.ensure(cand.size() * sizeof(iggy_decode_result));
+        if (r) return IGGY_ERR_DEVICE;
+        r = ensure_decode_scratch(c, maxlen);
+        if (r) return r;
+        HIP_OK(hipMemcpyAsync(c->din.p, messages, span, hipMemcpyHostToDevice, c->stream));
+        iggy_decode_result *d_res = c->dout.as<iggy_decode_result>();
+        for (size_t k = 0; k < cand.size(); ++k) {
+            r = enqueue_decode(c, c->din.as<uint8_t>(cand[k].pos), cand[k].h.batch_length, IGGY_INTEGRITY_VERIFY,
+                               nullptr, 0, d_res + k, c->stream);
+            if (r) return r;
+        }
+        std::vector<iggy_decode_result> res(cand.size());
+        HIP_OK(hipMemcpyAsync(res.data(), d_res, res.size() * sizeof(iggy_decode_result), hipMemcpyDeviceToHost,
+                              c->stream));
+        HIP_OK(hipStreamSynchronize(c->stream));
+        for (; accepted < cand.size(); ++accepted) {
+            if (res[accepted].error.kind == IGGY_ERR_TIMEOUT) {
+                reset_after_timeout(c);
+                return IGGY_ERR_TIMEOUT;
+            }
+            if (res[accepted].error.kind != IGGY_OK) break;
+        }
+    }
+    uint64_t end_offset = start_offset, end_ts = 0, start_ts = 0, walked = 0;
+    bool have_start = false;
+    for (size_t k = 0; k < accepted; ++k) {
+        const iggy_batch_header &h = cand[k].h;
+        if (h.message_count > 0) {
+            end_offset = sat(h.base_offset, (uint64_t)h.message_count - 1);
+            end_ts = h.base_timestamp;
+            if (!have_start) { start_ts = h.base_timestamp; have_start = true; }
+        }
+        walked = cand[k].pos + h.batch_length;
+    }
+    out->found = have_start ? 1 : 0;
+    out->start_timestamp = start_ts;
+    out->end_timestamp = end_ts;
+    out->end_offset = end_offset;
+    out->walked_bytes = walked;
+    out->batches = accepted;
+    return 0;
+}
+
 int iggy_codec_xxh3_64(iggy_codec_ctx *c, const void *data, uint64_t len, uint64_t *out) {
     if (!c || !out || (!data && len)) return IGGY_ERR_INVALID_ARGUMENT;
     HIP_OK(hipSetDevice(c->device));

@@ -347,6 +347,24 @@ int iggy_codec_admit_batch(iggy_codec_ctx *ctx, const uint8_t *batch, uint64_t l
                            uint32_t metadata_messages_count, uint64_t partition_id, int checksum_mode,
                            uint8_t *out, uint64_t cap, iggy_batch_header *hdr_out, iggy_wire_error *err);
 
+/* -------------------------------------------------------- segment recovery */
+/* recover_segment_bounds' index-less arm (core/partitions/src/segment_recovery.rs:425-488,
+ * batch_verifies :518-530): walk the batches of one segment's messages file from
+ * byte 0; a batch is accepted while its header decodes, it fits in the file, its
+ * base_offset continues the chain from start_offset and it passes the Verify
+ * decode (every message checksum + the batch checksum, on the GPU). 48 B. */
+typedef struct iggy_segment_recovery {
+    uint64_t found;            /* 0 = None: no accepted batch carried messages */
+    uint64_t start_timestamp;  /* base_timestamp of the first accepted batch with messages */
+    uint64_t end_timestamp;
+    uint64_t end_offset;       /* last offset of the chain (start_offset when none) */
+    uint64_t walked_bytes;     /* end of the last accepted batch: the torn tail starts here */
+    uint64_t batches;          /* accepted batches */
+} iggy_segment_recovery;
+
+int iggy_codec_recover_segment(iggy_codec_ctx *ctx, const uint8_t *messages, uint64_t len,
+                               uint64_t start_offset, iggy_segment_recovery *out);
+
 /* ------------------------------------------------------------- profiling */
 /* When enabled, the context brackets the dominant kernel of every decode /
  * encode with hipEvents on the launch stream and accumulates its duration. */

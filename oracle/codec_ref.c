@@ -453,6 +453,45 @@ int oracle_admit_batch(const uint8_t *batch, uint64_t len, uint32_t meta_count, 
     return 0;
 }
 
+static uint64_t sat_add_u64(uint64_t a, uint64_t b) { return a + b < a ? ~0ull : a + b; }
+
+/* recover_segment_bounds, index-less arm — core/partitions/src/segment_recovery.rs:425-488 */
+int oracle_recover_segment(const uint8_t *messages, uint64_t len, uint64_t start_offset,
+                           iggy_segment_recovery *out) {
+    memset(out, 0, sizeof(*out));
+    uint64_t position = 0, end_offset = start_offset, end_ts = 0, expected = start_offset;
+    uint64_t start_ts = 0, batches = 0;
+    int have_start = 0;
+    while (position < len) {
+        iggy_batch_header h;
+        iggy_wire_error e;
+        if (len - position < HDR) break;                                         /* read_batch_header :532-541 */
+        if (oracle_batch_header_decode(messages + position, HDR, &h, &e)) break;
+        const uint64_t extent = sat_add_u64(position, h.batch_length);           /* :460-463 */
+        if (extent > len) break;
+        uint64_t n = 0;                                                          /* :473-476, batch_verifies :518-530 */
+        if (h.base_offset != expected ||
+            oracle_decode_batch_slice_with(messages + position, h.batch_length, IGGY_INTEGRITY_VERIFY, &h, NULL,
+                                           0, &n, &e))
+            break;
+        if (h.message_count > 0) {                                               /* :477-484 */
+            end_offset = sat_add_u64(h.base_offset, (uint64_t)h.message_count - 1);
+            end_ts = h.base_timestamp;
+            if (!have_start) { start_ts = h.base_timestamp; have_start = 1; }
+            expected = sat_add_u64(end_offset, 1);
+        }
+        ++batches;
+        position = extent;
+    }
+    out->found = (uint64_t)have_start;
+    out->start_timestamp = start_ts;
+    out->end_timestamp = end_ts;
+    out->end_offset = end_offset;
+    out->walked_bytes = position;
+    out->batches = batches;
+    return 0;
+}
+
 /* select_batch_slice — core/partitions/src/journal.rs:1025-1086, then the header
  * push_selected_batch_fragments serves (journal.rs:1096-1137): a partial selection
  * gets batch_length = 256 + (end - start), message_count = matched and the batch

@@ -67,6 +67,10 @@ int oracle_admit_batch(const uint8_t *batch, uint64_t len, uint32_t meta_count, 
                        int checksum_mode, uint8_t *out, uint64_t cap, iggy_batch_header *h,
                        iggy_wire_error *e);
 
+/* recover_segment_bounds' index-less walk (core/partitions/src/segment_recovery.rs:425-530) */
+int oracle_recover_segment(const uint8_t *messages, uint64_t len, uint64_t start_offset,
+                           iggy_segment_recovery *out);
+
 /* synthetic input generator shared by tests and bench (BASELINE.md:
  * splitmix64, seed 0x16619E3779B97F4A ^ partition). Builds a stamped,
  * checksummed record of n frames; payload length of frame i =

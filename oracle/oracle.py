@@ -63,6 +63,7 @@ def lib() -> ctypes.CDLL:
         L.oracle_select_batch_slice.argtypes = [vp, u64, vp, vp, vp]
         L.oracle_decode_prepare.argtypes = [vp, u64, ctypes.c_int, vp, vp]
         L.oracle_admit_batch.argtypes = [vp, u64, u32, u64, ctypes.c_int, vp, u64, vp, vp]
+        L.oracle_recover_segment.argtypes = [vp, u64, u64, vp]
         _lib = L
     return _lib
 
@@ -174,6 +175,16 @@ def admit_batch(batch, metadata_messages_count: int, partition_id: int, checksum
                                   partition_id, checksum_mode, out.ctypes.data, out.size, ctypes.byref(h),
                                   ctypes.byref(e))
     return rc, e, h, (out[:a.size].tobytes() if rc == 0 else None)
+
+
+def recover_segment(messages, start_offset: int):
+    """recover_segment_bounds' index-less walk -> (rc, SegmentRecovery)"""
+    from iggy_amd.abi import SegmentRecovery
+
+    a = _as_np(messages)
+    out = SegmentRecovery()
+    rc = lib().oracle_recover_segment(a.ctypes.data if a.size else None, a.size, start_offset, ctypes.byref(out))
+    return rc, out
 
 
 def select_slice(record, kind: int, value: int, count: int, ceiling: int = 2**64 - 1, already_matched: int = 0):

@@ -92,6 +92,38 @@ def test_admit_batch_mirrors_server_common_tests():
     assert O.admit_batch(empty, 0, 5)[0] == abi.ERR_INVALID_COMMAND
 
 
+def _segment(sizes, start_offset=100, seed=1):
+    """Batches stamped back to back as a partition's segment file (base offsets
+    contiguous from start_offset)."""
+    recs, off = [], start_offset
+    for k, (n, pl) in enumerate(sizes):
+        r = O.synth_batch(n, pl, pl + 50, 0, seed=seed + k)
+        rc, e, h, r2 = O.stamp_batch(r, off, 1_000 + k)
+        assert rc == 0, e
+        recs.append(np.frombuffer(r2, dtype=np.uint8))
+        off += n
+    return np.concatenate(recs), recs
+
+
+def test_recover_segment_walk():
+    seg, recs = _segment([(5, 100), (7, 300), (3, 10), (9, 2000)])
+    rc, out = O.recover_segment(seg, 100)
+    assert rc == 0 and out.found == 1 and out.batches == 4
+    assert out.end_offset == 100 + 5 + 7 + 3 + 9 - 1 and out.walked_bytes == seg.size
+    assert out.start_timestamp == 1000 and out.end_timestamp == 1003
+    # torn tail: the last batch cut short stops the walk before it
+    rc, out = O.recover_segment(seg[:-10], 100)
+    assert out.batches == 3 and out.walked_bytes == seg.size - recs[-1].size
+    # a corrupt payload in batch 2 (index 1) stops the walk after batch 1
+    bad = seg.copy()
+    bad[recs[0].size + 256 + 48 + 5] ^= 1
+    rc, out = O.recover_segment(bad, 100)
+    assert out.batches == 1 and out.end_offset == 104
+    # an offset gap (wrong start offset from the file name) accepts nothing
+    rc, out = O.recover_segment(seg, 99)
+    assert out.found == 0 and out.batches == 0 and out.walked_bytes == 0 and out.end_offset == 99
+
+
 def test_xxh3_matches_libxxhash_fixtures():
     blob, vecs = xxh3_vectors()
     for v in vecs:

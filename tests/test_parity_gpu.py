@@ -171,6 +171,36 @@ def test_admit_batch_matches_oracle(cx):
                     assert got[3] == exp[3]
 
 
+def test_recover_segment_matches_oracle(cx):
+    recs, off = [], 500
+    for k, (n, lo, hi) in enumerate([(40, 10, 900), (3000, 1024, 1024), (0, 0, 0), (700, 0, 5000), (1, 3, 3),
+                                     (20000, 64, 64)]):
+        if n == 0:  # a header-only batch with no messages (count 0) still chains
+            r = np.zeros(256, dtype=np.uint8)
+            struct.pack_into("<QQQQQ", r, 0, 1, off, 7, 0, 256)
+            h = abi.BatchHeader()
+            h.partition_id, h.base_offset, h.base_timestamp, h.batch_length = 1, off, 7, 256
+            struct.pack_into("<Q", r, 40, O.calculate_batch_checksum(h, b""))
+            recs.append(r)
+            continue
+        r = O.synth_batch(n, lo, hi, 0, seed=k)
+        rc, e, h, r2 = O.stamp_batch(r, off, 2_000 + k)
+        recs.append(np.frombuffer(r2, dtype=np.uint8))
+        off += n
+    seg = np.concatenate(recs)
+    starts = np.cumsum([0] + [r.size for r in recs])
+    cases = [(seg, 500), (seg, 501), (seg[:-1], 500), (seg[: starts[3] + 100], 500)]
+    for k in range(len(recs)):
+        b = seg.copy()
+        b[starts[k] + 256 + (48 + 2 if recs[k].size > 256 else -216)] ^= 0x40
+        cases.append((b, 500))
+    for buf, so in cases:
+        rc, out = cx.recover_segment(buf, so)
+        orc, oout = O.recover_segment(buf, so)
+        assert rc == orc == 0
+        assert out.astuple() == oout.astuple()
+
+
 def _crafted_record(n, lo, hi, fill, seed):
     """A stamped record whose payloads defeat the tile speculation: "zero" payloads
     (every offset inside them is a candidate frame start) or "fake" payloads that
