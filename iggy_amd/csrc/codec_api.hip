@@ -759,7 +759,8 @@ static int enqueue_encode(iggy_codec_ctx *c, const iggy_raw_messages *dm, uint64
         hipLaunchKernelGGL(k_enc_frames, dim3((waves + 3) / 4), dim3(256), 0, s, m, es, d_out, 1u);
         hipLaunchKernelGGL(k_enc_short, dim3(std::min<uint64_t>((n + 255) / 256, (uint64_t)c->ncu * 4)), dim3(256),
                            0, s, m, es, d_out);
-        const uint64_t lwg = std::min<uint64_t>((n + 31) / 32, (uint64_t)c->ncu * 8);
+        // one resident round of lane-group waves (2 WGs of 256 per CU at 240 VGPRs)
+        const uint64_t lwg = std::min<uint64_t>((n + 31) / 32, (uint64_t)c->ncu * ((c->dbg & 2048) ? 8 : 2));
         int nseg = 1;
         if (n >= kEncSegMinFrames && nb >= 4 * kEncSegs && c->side) {
             nseg = kEncSegs;
