@@ -79,6 +79,9 @@ struct iggy_codec_ctx {
     DevBuf dsums, derr;
     DevBuf gtiles_s, gtiles_x, gtiles_cnt, gtiles_pre, gtiles_list, gtiles_e, gtiles_base, ggrp, gfpos, gcs, gflen, gbsums;
     int gen_grid = 0;  // co-resident WGs of k_decode_general
+    // IGGY_CODEC_COOPERATIVE=1: launch it cooperatively (safe for concurrent variable-size
+    // decodes on several streams; ~4 % off the pipelined C2 bench, so off by default)
+    bool coop_general = false;
     // encode: the batch-checksum chain of earlier frame segments runs on `side`
     // while later segments are encoded on the call's stream
     hipStream_t side = nullptr;
@@ -225,12 +228,18 @@ int enqueue_decode(iggy_codec_ctx *c, const uint8_t *d_body, uint64_t len, int i
                            cap, d_res, ds, c->epoch, au, c->dbg);
     prof_end(c, 0, s);
     HIP_OK(hipGetLastError());
-    if (verify)
+    if (c->coop_general) {  // all-or-nothing residency: concurrent general decodes cannot interleave
+        void *args[] = {(void *)&d_body, (void *)&len, (void *)&d_pos, (void *)&cap, (void *)&d_res, (void *)&gs};
+        HIP_OK(hipLaunchCooperativeKernel(verify ? (const void *)k_decode_general<true>
+                                                 : (const void *)k_decode_general<false>,
+                                          dim3(c->gen_grid), dim3(kGenThreads), args, 0, s));
+    } else if (verify) {
         hipLaunchKernelGGL(k_decode_general<true>, dim3(c->gen_grid), dim3(kGenThreads), 0, s, d_body, len, d_pos,
                            cap, d_res, gs);
-    else
+    } else {
         hipLaunchKernelGGL(k_decode_general<false>, dim3(c->gen_grid), dim3(kGenThreads), 0, s, d_body, len,
                            d_pos, cap, d_res, gs);
+    }
     HIP_OK(hipGetLastError());
     return 0;
 }
@@ -300,6 +309,7 @@ int iggy_codec_create(int device, iggy_codec_ctx **out) {
     c->device = device;
     c->ncu = prop.multiProcessorCount;
     if (const char *d = getenv("IGGY_CODEC_DBG")) c->dbg = (uint32_t)strtoul(d, nullptr, 0);
+    if (const char *d = getenv("IGGY_CODEC_COOPERATIVE")) c->coop_general = atoi(d) != 0;
     if (hipSetDevice(device) != hipSuccess ||
         hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
         hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking) != hipSuccess) {
