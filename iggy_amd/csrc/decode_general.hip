@@ -187,45 +187,109 @@ __device__ inline uint64_t first_candidate(const uint8_t *blob, uint64_t bl, uin
     return kNoStart;
 }
 
+// Candidate starts (ascending, at most kPickBatch, all >= from and < hi) from the
+// zero dwords of the first 256-B window at or after `from` that has any;
+// *next = where the search goes on.
+constexpr int kPickBatch = 8;
+__device__ inline int window_candidates(const uint8_t *blob, uint64_t bl, uint64_t from, uint64_t hi,
+                                        uint64_t (&cp)[kPickBatch], uint64_t *next) {
+    if (from >= hi) return 0;
+    const uintptr_t base = (uintptr_t)blob;
+    const uintptr_t a_end = base + hi + 43;  // dwords holding a window of some p < hi
+    const uintptr_t blob_end = base + bl;
+    const uintptr_t wlo = base + from + 40;
+    uintptr_t a = wlo & ~(uintptr_t)15;
+    int nc = 0;
+    auto take = [&](uintptr_t ad) {  // the windows [ad-3, ad] of one zero dword, ascending
+        for (int d = 3; d >= 0 && nc < kPickBatch; --d) {
+            const uintptr_t ws = ad - d;
+            if (ws < wlo) continue;
+            const uint64_t p = (uint64_t)(ws - base) - 40;
+            if (p >= hi) return;
+            cp[nc++] = p;
+        }
+    };
+    while (a < a_end && a + 256 <= blob_end) {
+        uint4 v[16];
+#pragma unroll
+        for (int k = 0; k < 16; ++k) v[k] = *(const uint4 *)(a + 16 * k);
+        uint64_t zmask = 0;  // bit 4k+q: dword q of v[k] is zero
+#pragma unroll
+        for (int k = 0; k < 16; ++k)
+            zmask |= (uint64_t)((v[k].x == 0) | ((v[k].y == 0) << 1) | ((v[k].z == 0) << 2) |
+                                ((v[k].w == 0) << 3)) << (4 * k);
+        while (zmask && nc < kPickBatch) {
+            const int bit = __builtin_ctzll(zmask);
+            zmask &= zmask - 1;
+            const uintptr_t ad = a + 4 * bit;
+            if (ad >= a_end) break;
+            take(ad);
+        }
+        if (nc) {
+            *next = cp[nc - 1] + 1;
+            return nc;
+        }
+        a += 256;
+    }
+    for (; a < a_end && a + 4 <= blob_end && nc < kPickBatch; a += 4)
+        if (*(const uint32_t *)a == 0) take(a);
+    if (nc) *next = cp[nc - 1] + 1;
+    return nc;
+}
+
 // The tile's speculative entry. Frame headers themselves hold zero runs
 // (timestamp delta, user-header length, the high bytes of a small offset
 // delta) that pass the reserved-bytes test a few bytes BEFORE a true start,
-// with random "lengths" that usually still fit the blob. So rather than the
-// first candidate, take the first of up to kPickTries candidates whose chain is
-// confirmed (its successor starts inside the tile and the chain leaves the tile
-// cleanly); failing that, the clean chain with the nearest exit, else the first
-// candidate. Only speed depends on this choice: the link phase re-walks any tile
-// whose pick disagrees with the true entry.
-constexpr int kPickTries = 8;
+// with random "lengths" that usually still fit the blob. So the pick is the
+// first candidate whose chain is confirmed (its successor starts inside the
+// tile); failing that, the candidate whose single frame leaves the tile at the
+// nearest exit, else the first valid candidate. Candidates come a window at a
+// time and are tested together: their headers in one round of loads, their
+// successors in a second. Only speed depends on the pick: the link phase
+// re-walks any tile whose pick disagrees with the true entry.
+constexpr int kPickWindows = 4;
 __device__ inline void pick_start(const uint8_t *blob, uint64_t bl, uint64_t lo, uint64_t hi,
                                   uint32_t *list, uint64_t *s_out, uint64_t *x_out, uint32_t *cnt_out) {
-    uint64_t bs = kNoStart, bx = kNoStart, listed = kNoStart;
-    uint32_t bc = 0;
-    bool bclean = false;
+    uint64_t pick = kNoStart, clean_p = kNoStart, clean_x = kNoStart, first_valid = kNoStart;
     uint64_t from = lo;
-    for (int k = 0; k < kPickTries; ++k) {
-        const uint64_t c = first_candidate(blob, bl, from, hi);
-        if (c == kNoStart) break;
-        uint64_t x;
-        const uint32_t n = walk(blob, bl, c, hi, &x, list, lo);
-        listed = c;
-        const bool clean = !(x & kStopBit);
-        if (clean && n >= 2) {
-            bs = c; bx = x; bc = n;
-            break;
+    for (int w = 0; w < kPickWindows && pick == kNoStart; ++w) {
+        uint64_t cp[kPickBatch], next = hi;
+        const int nc = window_candidates(blob, bl, from, hi, cp, &next);
+        if (!nc) break;
+        uint4 hv[kPickBatch], sv[kPickBatch];
+        uint64_t e[kPickBatch];
+        bool val[kPickBatch];
+#pragma unroll
+        for (int k = 0; k < kPickBatch; ++k)
+            hv[k] = ld128_any(blob + ((k < nc && cp[k] + kFrameHdr <= bl) ? cp[k] + 32 : 0));
+#pragma unroll
+        for (int k = 0; k < kPickBatch; ++k) {
+            e[k] = k < nc ? cp[k] + kFrameHdr + (uint64_t)hv[k].x + hv[k].y : 0;
+            val[k] = k < nc && cp[k] + kFrameHdr <= bl && (hv[k].z | hv[k].w) == 0 && e[k] <= bl;
+            sv[k] = ld128_any(blob + ((val[k] && e[k] < hi && e[k] + kFrameHdr <= bl) ? e[k] + 32 : 0));
         }
-        if (bs == kNoStart || (clean && (!bclean || x < bx))) {
-            bs = c; bx = x; bc = n; bclean = clean;
+#pragma unroll
+        for (int k = 0; k < kPickBatch; ++k) {
+            if (!val[k] || pick != kNoStart) continue;
+            if (first_valid == kNoStart) first_valid = cp[k];
+            if (e[k] < hi) {
+                const bool conf = e[k] + kFrameHdr <= bl && (sv[k].z | sv[k].w) == 0 &&
+                                  e[k] + kFrameHdr + (uint64_t)sv[k].x + sv[k].y <= bl;
+                if (conf) pick = cp[k];
+            } else if (e[k] < clean_x) {
+                clean_p = cp[k];
+                clean_x = e[k];
+            }
         }
-        from = c + 1;
+        from = next;
     }
-    if (bs != kNoStart && bs != listed) {
-        uint64_t x;
-        walk(blob, bl, bs, hi, &x, list, lo);
-    }
-    *s_out = bs;
-    *x_out = bx;
-    *cnt_out = bc;
+    if (pick == kNoStart) pick = clean_p != kNoStart ? clean_p : first_valid;
+    uint64_t x = kNoStart;
+    uint32_t cnt = 0;
+    if (pick != kNoStart) cnt = walk(blob, bl, pick, hi, &x, list, lo);
+    *s_out = pick;
+    *x_out = x;
+    *cnt_out = cnt;
 }
 
 // XXH3 stripe contribution of checksum-input word m (value v)
