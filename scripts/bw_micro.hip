@@ -158,6 +158,17 @@ int main() {
         printf("%-40s %8.4f ms  %7.1f GB/s\n", name, ms, L / (ms * 1e-3) / 1e9);
     };
     char nm[128];
+    if (getenv("BW_MISALIGN")) {  // the same frame-segment reads with 16-B / 4-B / 1-B aligned frame starts
+        for (uint64_t S2 : {1072ull, 1076ull, 1073ull}) {
+            for (uint64_t base : {256ull, 257ull}) {
+                const uint64_t N2 = (L - 512) / S2;
+                snprintf(nm, sizeof nm, "frames d9 unit8 S=%llu base=%llu", (unsigned long long)S2,
+                         (unsigned long long)base);
+                timeit(nm, [&] { hipLaunchKernelGGL((rd_frames<9, 8>), 255, 512, 0, 0, d + base, S2, N2, o); });
+            }
+        }
+        return 0;
+    }
     hipFuncSetAttribute((const void *)lds_frames<0, 64, 4>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
     hipFuncSetAttribute((const void *)lds_frames<0, 8, 4>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
     hipFuncSetAttribute((const void *)lds_frames<1, 64, 4>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
