@@ -328,21 +328,40 @@ __device__ __forceinline__ VFrame vframe(const GeneralScratch &gs, uint64_t f, u
     return v;
 }
 struct VStep {
-    uint4 v[8];  // the 8 pieces of one block
-    uint4 last;  // the frame's last-stripe piece (first block only)
+    uint4 v[8];       // the 8 chunks of one block, loaded from 4-B-aligned addresses
+    uint32_t nx[8];   // the dword after each chunk (the bytes the alignment shifted out)
+    uint4 last;       // the frame's last-stripe chunk (first block only), aligned the same way
+    uint32_t lnx;     // the dword after it
 };
-// the loads of frame v's block b: always 9 (unneeded pieces read the blob start)
+// 16 bytes starting r bytes into (w.x, w.y, w.z, w.w, nb)
+__device__ __forceinline__ uint4 realign(uint4 w, uint32_t nb, uint32_t r) {
+    return make_uint4(__builtin_amdgcn_alignbyte(w.y, w.x, r), __builtin_amdgcn_alignbyte(w.z, w.y, r),
+                      __builtin_amdgcn_alignbyte(w.w, w.z, r), __builtin_amdgcn_alignbyte(nb, w.w, r));
+}
+// the loads of frame v's block b: always 18. Frames start at any byte offset and
+// byte-misaligned 16-B loads stream ~25 % slower (profiles/r01_bw_misalign.txt),
+// so each chunk is loaded from its 4-B-aligned address plus the dword after it
+// (only when the frame is misaligned; that dword holds a byte the hash needs, so
+// it never reaches past the 4-B word of a frame byte) and realigned in registers.
 __device__ __forceinline__ void vissue(const uint8_t *blob, const VFrame &v, uint64_t nwalk, uint32_t b,
                                        uint32_t par, uint32_t poff, uint32_t m, VStep &st) {
     const bool lng = v.f < nwalk && v.L > 240;
     const uint64_t nbF = lng ? (v.L - 1) / 1024 : 0, ns = lng ? ((v.L - 1) - 1024 * nbF) / 64 : 0;
-    const uint8_t *hb = blob + v.p + 8 + 1024ull * b + poff;
+    const uint8_t *H = blob + v.p + 8;
+    const uint32_t r = (uint32_t)((uintptr_t)H & 3);
+    const uint8_t *hb = H - r + 1024ull * b + poff;
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
         const bool use = lng && (b < nbF || 2 * q + par < ns);
         st.v[q] = ld128_any(use ? hb + 128 * q : blob);
+        st.nx[q] = *(const uint32_t *)((use && r) ? hb + 128 * q + 16 : blob);
     }
-    st.last = ld128_any((lng && b == 0) ? blob + v.p + 8 + v.L - 64 + 16 * m : blob);
+    const uint8_t *E = H + v.L;
+    const uint32_t rl = (uint32_t)((uintptr_t)E & 3);
+    const uint8_t *lc = E - rl - 64 + 16 * m;
+    const bool lp = lng && b == 0;
+    st.last = ld128_any(lp ? lc : blob);
+    st.lnx = *(const uint32_t *)((lp && rl) ? lc + 16 : blob);
 }
 
 __device__ inline void verify_frames(const uint8_t *blob, const GeneralScratch &gs, uint64_t nwalk,
@@ -378,12 +397,16 @@ __device__ inline void verify_frames(const uint8_t *blob, const GeneralScratch &
         const bool fin = b + 1 == nsteps;
         if (!fin) vissue(blob, cur, nwalk, b + 1, par, poff, m, Y);
         else vissue(blob, nxt, nwalk, 0, par, poff, m, Y);
-        if (b == 0) lastp = X.last;
+        const uint32_t r = (uint32_t)((uintptr_t)(blob + cur.p + 8) & 3);
+        if (b == 0) lastp = realign(X.last, X.lnx, (uint32_t)((uintptr_t)(blob + cur.p + 8 + L) & 3));
+        uint4 pc[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) pc[q] = realign(X.v[q], X.nx[q], r);
         if (lng) {
             if (b < nbF) {
                 uint64_t p0[4] = {0, 0, 0, 0}, p1[4] = {0, 0, 0, 0};
 #pragma unroll
-                for (int q = 0; q < 8; ++q) piece(p0[q & 3], p1[q & 3], X.v[q], s0[q], s1[q]);
+                for (int q = 0; q < 8; ++q) piece(p0[q & 3], p1[q & 3], pc[q], s0[q], s1[q]);
                 a0 += (p0[0] + p0[1]) + (p0[2] + p0[3]);
                 a1 += (p1[0] + p1[1]) + (p1[2] + p1[3]);
                 a0 += gdpp64<0xB1>(a0);
@@ -394,7 +417,7 @@ __device__ inline void verify_frames(const uint8_t *blob, const GeneralScratch &
             } else {
 #pragma unroll
                 for (int q = 0; q < 8; ++q)
-                    if (2 * q + par < ns) piece(a0, a1, X.v[q], s0[q], s1[q]);
+                    if (2 * q + par < ns) piece(a0, a1, pc[q], s0[q], s1[q]);
             }
             if (fin) {
                 a0 += gdpp64<0xB1>(a0);
