@@ -817,54 +817,41 @@ __global__ __launch_bounds__(kGenThreads) void k_decode_general(const uint8_t *_
     gstamp(gs, 3, rt_now() - t0);
 
     const uint64_t nwalk = __hip_atomic_load(&gs.misc[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    // ---------------- C: scatter the accepted tiles' lists (walk order), one lane per tile
-    for (uint64_t t = gtid; t < ntiles; t += gthreads) {
-        const uint64_t *q = gs.grp + kGrpWords * (t / kGrpTiles);
-        const uint64_t mode = q[5];
-        uint64_t base;
-        if (mode == 1) {
-            const uint32_t pre = gs.tile_pre[t];
-            if (pre == kNotLive) continue;
-            base = q[4] + pre;
-        } else if (mode == 2) {
-            if (gs.tile_e[t] == ~0ull) continue;
-            base = gs.tile_base[t];
-        } else {
-            continue;
-        }
-        const uint32_t cnt = gs.tile_cnt[t];
-        const uint32_t *list = gs.tile_list + t * lcap;
-        const uint64_t lo = t << sh;
-        uint32_t k = 0;
-        for (; k + 4 <= cnt; k += 4) {
-            uint64_t p[4], c[4], ln[4];
-#pragma unroll
-            for (int j = 0; j < 4; ++j) p[j] = lo + list[k + j];
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                if (VERIFY) c[j] = ld64_any(blob + p[j]);
-                ln[j] = ld64_any(blob + p[j] + 32);
-            }
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const uint64_t i = base + k + j;
-                gs.fpos[i] = p[j];
-                if (VERIFY) {
-                    gs.cs[i] = c[j];
-                    gs.flen[i] = 40 + (uint64_t)(uint32_t)ln[j] + (ln[j] >> 32);
+    // ---------------- C: scatter the accepted tiles' lists (walk order). Sixteen lanes per
+    // tile, four tiles per wave: a tile's list entries are spread over its lanes so that one
+    // round of header loads serves up to sixteen frames (a lane-per-tile loop paid one
+    // dependent load round per frame).
+    {
+        const uint32_t sub = (uint32_t)lane >> 4, k0 = (uint32_t)lane & 15;
+        for (uint64_t t4 = wid; t4 * 4 < ntiles; t4 += nwaves) {
+            const uint64_t t = t4 * 4 + sub;
+            uint64_t base = 0;
+            bool live = false;
+            if (t < ntiles) {
+                const uint64_t *q = gs.grp + kGrpWords * (t / kGrpTiles);
+                const uint64_t mode = q[5];
+                if (mode == 1) {
+                    const uint32_t pre = gs.tile_pre[t];
+                    live = pre != kNotLive;
+                    base = q[4] + pre;
+                } else if (mode == 2) {
+                    live = gs.tile_e[t] != ~0ull;
+                    base = gs.tile_base[t];
                 }
-                if (frame_pos && i < cap) frame_pos[i] = p[j];
             }
-        }
-        for (; k < cnt; ++k) {
-            const uint64_t p = lo + list[k], i = base + k;
-            gs.fpos[i] = p;
-            if (VERIFY) {
-                gs.cs[i] = ld64_any(blob + p);
-                const uint64_t ln = ld64_any(blob + p + 32);
-                gs.flen[i] = 40 + (uint64_t)(uint32_t)ln + (ln >> 32);
+            const uint32_t cnt = live ? gs.tile_cnt[t] : 0;
+            const uint32_t *list = gs.tile_list + t * lcap;
+            const uint64_t lo = t << sh;
+            for (uint32_t k = k0; k < cnt; k += 16) {
+                const uint64_t p = lo + list[k], i = base + k;
+                gs.fpos[i] = p;
+                if (VERIFY) {
+                    gs.cs[i] = ld64_any(blob + p);
+                    const uint64_t ln = ld64_any(blob + p + 32);
+                    gs.flen[i] = 40 + (uint64_t)(uint32_t)ln + (ln >> 32);
+                }
+                if (frame_pos && i < cap) frame_pos[i] = p;
             }
-            if (frame_pos && i < cap) frame_pos[i] = p;
         }
     }
     ok &= grid_barrier(gs.bar, nwg * ++phase, t0);
