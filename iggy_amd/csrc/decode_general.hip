@@ -133,60 +133,6 @@ __device__ inline uint32_t walk(const uint8_t *blob, uint64_t bl, uint64_t p, ui
     return cnt;
 }
 
-// Test the candidate window starts whose 8-byte reserved window [ws, ws+8)
-// contains the zero dword at aligned address ad (ws in [ad-3, ad]), increasing.
-__device__ __forceinline__ bool dword_candidates(const uint8_t *blob, uint64_t bl, uint64_t lo,
-                                                 uint64_t hi, uintptr_t ad, uint64_t *out) {
-    const uintptr_t base = (uintptr_t)blob;
-    for (int d = 3; d >= 0; --d) {
-        const uintptr_t ws = ad - d;  // window start = blob + p + 40
-        if (ws < base + lo + 40) continue;
-        const uint64_t p = (uint64_t)(ws - base) - 40;
-        if (p >= hi) return false;
-        uint64_t e;
-        if (candidate(blob, bl, p, &e)) {
-            *out = p;
-            return true;
-        }
-    }
-    return false;
-}
-
-// First candidate start in [lo, hi) (hi <= bl). An all-zero reserved window at
-// p+40 contains the aligned dword at 4*ceil((p+40)/4), so scanning aligned
-// dwords for zeros in increasing order finds every candidate in order. The scan
-// reads 256 B per step with 16 independent 16-B loads.
-__device__ inline uint64_t first_candidate(const uint8_t *blob, uint64_t bl, uint64_t lo,
-                                           uint64_t hi) {
-    if (lo >= hi) return kNoStart;
-    const uintptr_t base = (uintptr_t)blob;
-    const uintptr_t a_end = base + hi + 43;  // dwords holding a window of some p < hi
-    const uintptr_t blob_end = base + bl;
-    uintptr_t a = (base + lo + 40) & ~(uintptr_t)15;
-    uint64_t p;
-    while (a < a_end && a + 256 <= blob_end) {
-        uint4 v[16];
-#pragma unroll
-        for (int k = 0; k < 16; ++k) v[k] = *(const uint4 *)(a + 16 * k);
-        uint64_t zmask = 0;  // bit 4k+q: dword q of v[k] is zero
-#pragma unroll
-        for (int k = 0; k < 16; ++k)
-            zmask |= (uint64_t)((v[k].x == 0) | ((v[k].y == 0) << 1) | ((v[k].z == 0) << 2) |
-                                ((v[k].w == 0) << 3)) << (4 * k);
-        while (zmask) {
-            const int bit = __builtin_ctzll(zmask);
-            zmask &= zmask - 1;
-            const uintptr_t ad = a + 4 * bit;
-            if (ad >= a_end) return kNoStart;
-            if (dword_candidates(blob, bl, lo, hi, ad, &p)) return p;
-        }
-        a += 256;
-    }
-    for (; a < a_end && a + 4 <= blob_end; a += 4)
-        if (*(const uint32_t *)a == 0 && dword_candidates(blob, bl, lo, hi, a, &p)) return p;
-    return kNoStart;
-}
-
 // Candidate starts (ascending, at most kPickBatch, all >= from and < hi) from the
 // zero dwords of the first 256-B window at or after `from` that has any;
 // *next = where the search goes on.
@@ -209,27 +155,38 @@ __device__ inline int window_candidates(const uint8_t *blob, uint64_t bl, uint64
             cp[nc++] = p;
         }
     };
-    while (a < a_end && a + 256 <= blob_end) {
-        uint4 v[16];
+    // 512 B per round (two 256-B windows loaded together): the scan from a tile's
+    // start to the first frame header is the long pole of locate, and the wave
+    // waits for its slowest lane
+    while (a < a_end && a + 512 <= blob_end) {
+        uint4 v[32];
 #pragma unroll
-        for (int k = 0; k < 16; ++k) v[k] = *(const uint4 *)(a + 16 * k);
-        uint64_t zmask = 0;  // bit 4k+q: dword q of v[k] is zero
+        for (int k = 0; k < 32; ++k) v[k] = *(const uint4 *)(a + 16 * k);
+        uint64_t zm[2] = {0, 0};  // bit 4k+q of zm[h]: dword q of v[16h+k] is zero
 #pragma unroll
-        for (int k = 0; k < 16; ++k)
-            zmask |= (uint64_t)((v[k].x == 0) | ((v[k].y == 0) << 1) | ((v[k].z == 0) << 2) |
-                                ((v[k].w == 0) << 3)) << (4 * k);
-        while (zmask && nc < kPickBatch) {
-            const int bit = __builtin_ctzll(zmask);
-            zmask &= zmask - 1;
-            const uintptr_t ad = a + 4 * bit;
-            if (ad >= a_end) break;
-            take(ad);
+        for (int h = 0; h < 2; ++h)
+#pragma unroll
+            for (int k = 0; k < 16; ++k) {
+                const uint4 w = v[16 * h + k];
+                zm[h] |= (uint64_t)((w.x == 0) | ((w.y == 0) << 1) | ((w.z == 0) << 2) |
+                                    ((w.w == 0) << 3)) << (4 * k);
+            }
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            uint64_t zmask = zm[h];
+            while (zmask && nc < kPickBatch) {
+                const int bit = __builtin_ctzll(zmask);
+                zmask &= zmask - 1;
+                const uintptr_t ad = a + 256 * h + 4 * bit;
+                if (ad >= a_end) break;
+                take(ad);
+            }
+            if (nc) {
+                *next = cp[nc - 1] + 1;
+                return nc;
+            }
         }
-        if (nc) {
-            *next = cp[nc - 1] + 1;
-            return nc;
-        }
-        a += 256;
+        a += 512;
     }
     for (; a < a_end && a + 4 <= blob_end && nc < kPickBatch; a += 4)
         if (*(const uint32_t *)a == 0) take(a);
