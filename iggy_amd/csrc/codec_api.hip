@@ -85,7 +85,7 @@ struct iggy_codec_ctx {
     // encode: the batch-checksum chain of earlier frame segments runs on `side`
     // while later segments are encoded on the call's stream
     hipStream_t side = nullptr;
-    hipEvent_t seg_ev[kEncSegs + 1] = {};
+    hipEvent_t seg_ev[kEncSegs + 2] = {};  // segment ends, side-stream end, fork ([kEncSegs + 1])
     DevBuf dresult;  // iggy_decode_result + iggy_encode_result + u64 scratch
     // sync-API staging
     DevBuf din, dpos, dout;
@@ -766,11 +766,6 @@ static int enqueue_encode(iggy_codec_ctx *c, const iggy_raw_messages *dm, uint64
     if (!m.user_headers_lengths) {
         // no user headers: lane-group kernel (k_enc_frames only covers a < 16-B payload
         // area, and runs first so the segments' checksum chain sees its output)
-        hipLaunchKernelGGL(k_enc_frames, dim3((waves + 3) / 4), dim3(256), 0, s, m, es, d_out, 1u);
-        hipLaunchKernelGGL(k_enc_short, dim3(std::min<uint64_t>((n + 255) / 256, (uint64_t)c->ncu * 4)), dim3(256),
-                           0, s, m, es, d_out);
-        // one resident round of lane-group waves (2 WGs of 256 per CU at 240 VGPRs)
-        const uint64_t lwg = std::min<uint64_t>((n + 31) / 32, (uint64_t)c->ncu * ((c->dbg & 2048) ? 8 : 2));
         int nseg = 1;
         if (n >= kEncSegMinFrames && nb >= 4 * kEncSegs && c->side) {
             nseg = kEncSegs;
@@ -778,6 +773,21 @@ static int enqueue_encode(iggy_codec_ctx *c, const iggy_raw_messages *dm, uint64
                 if (!ev) nseg = 1;
         }
         segmented = nseg > 1;
+        hipLaunchKernelGGL(k_enc_frames, dim3((waves + 3) / 4), dim3(256), 0, s, m, es, d_out, 1u);
+        // frames of <= 240 hashed bytes (one lane each, latency-bound): segmented, they
+        // run at the head of the side stream beside the first segment, ahead of every
+        // block-sum range that reads their checksums; k_enc_lanes never writes their
+        // checksum words
+        const dim3 sgrid((uint32_t)std::min<uint64_t>((n + 255) / 256, (uint64_t)c->ncu * 4));
+        if (segmented) {
+            HIP_OK(hipEventRecord(c->seg_ev[kEncSegs + 1], s));
+            HIP_OK(hipStreamWaitEvent(c->side, c->seg_ev[kEncSegs + 1], 0));
+            hipLaunchKernelGGL(k_enc_short, sgrid, dim3(256), 0, c->side, m, es, d_out);
+        } else {
+            hipLaunchKernelGGL(k_enc_short, sgrid, dim3(256), 0, s, m, es, d_out);
+        }
+        // one resident round of lane-group waves (2 WGs of 256 per CU at 240 VGPRs)
+        const uint64_t lwg = std::min<uint64_t>((n + 31) / 32, (uint64_t)c->ncu * ((c->dbg & 2048) ? 8 : 2));
         uint64_t *state = c->emisc.as<uint64_t>(512);
         for (int k = 0; k < nseg; ++k) {
             // blocks [B_k, B_k+1) need frames up to 128 B_k+1 - 6: segment k encodes
