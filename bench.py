@@ -17,16 +17,26 @@ single-stream rate is reported beside it (`config.single_stream_gib_s`), and
 
 Multi-GPU (BASELINE configs[4], "C5"): one rank per GPU, each with its own
 independent partition's batch; no data-path collective (weak scaling). The
-barrier + max-over-ranks timing is the only cross-rank traffic.
+barrier + max-over-ranks timing (gloo, CPU tensors) is the only cross-rank
+traffic. `--gpus N` without a launcher starts the N rank processes itself
+(before anything touches a GPU); under torch.distributed.run the ranks come
+from the environment.
+
+At N = 1 the line also carries, timed in the same run:
+  c3_encode / c3_decode  BASELINE configs[2]: 1 M messages, payloads U[64, 4096] B,
+                         device-resident encode (segmented lane-group path) and the
+                         Verify decode of its output (general walk);
+  c1                     BASELINE configs[0] shapes (10 batches x 1000 x 256 B):
+                         cpu_ref encode/decode and the GPU's per-batch latency
+                         (iggy-bench itself needs a Rust toolchain: not run);
+  cpu_baseline           the oracle's AVX2 restatement of the C2 decode on this
+                         host's cores (1, 8 and 16 threads; reported, not optimised
+                         against).
 
 The synthetic batches are produced on the GPU by the codec's own encoder
 (SendMessagesEncoder semantics, server-twin form with partition_id = rank+1):
 random full-range payload bytes, random non-zero ids, origin timestamps
 1.7e15 + i microseconds.
-
-Output: ONE JSON line on rank 0 with `roofline` (dominant kernel, HIP events
-on the launch stream) and `cpu_baseline` (the oracle's AVX2 restatement of the
-same decode timed on this host's cores; reported, not optimised against).
 """
 from __future__ import annotations
 
@@ -34,17 +44,15 @@ import argparse
 import ctypes
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
 import numpy as np
-import torch
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
-
-from iggy_amd import abi  # noqa: E402
-from iggy_amd.codec import Codec  # noqa: E402
 
 METRIC = "GiB/s device-resident message-batch decode, 1M msgs × 1KiB payload"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s peak
@@ -52,17 +60,81 @@ N_MSG = 1 << 20
 PAYLOAD = 1024
 
 
-def make_batch(cx: Codec, n: int, pl: int, rank: int, dev: torch.device, stream: int):
+def parse_args(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--messages", type=int, default=N_MSG)
+    ap.add_argument("--no-cpu", action="store_true", help="skip the cpu_baseline leg")
+    ap.add_argument("--no-extra", action="store_true", help="skip the c3 / c1 legs")
+    ap.add_argument("--cpu-seconds", type=float, default=4.0)
+    ap.add_argument("--streams", type=int, default=2, help="decode lanes (contexts/streams) steps alternate over")
+    ap.add_argument("--dry", action="store_true",
+                    help="codec-free rehearsal of the launcher, barrier and max-over-ranks timing (no GPU)")
+    return ap.parse_args(argv)
+
+
+# ------------------------------------------------------------------ launcher
+def _free_port() -> int:
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch(n: int, argv: list[str]) -> int:
+    """One rank process per GPU (the parent never touches a GPU: it only waits)."""
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + argv, env=env))
+    rc = 0
+    for p in procs:
+        rc = max(rc, p.wait())
+    return rc
+
+
+# ------------------------------------------------------------- cross-rank
+def max_over_ranks(x: float, dist) -> float:
+    """The bench's only cross-rank traffic: max of a per-rank scalar over gloo (CPU
+    tensors). No data-path collective exists: partitions are independent."""
+    if dist is None:
+        return x
+    import torch
+    t = torch.tensor([x], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def whole_job_gib_s(world: int, batch_bytes: int, steps: int, elapsed: float) -> float:
+    """Aggregate throughput: every rank decodes `steps` batches of `batch_bytes` (weak scaling)."""
+    return world * batch_bytes * steps / elapsed / 2**30
+
+
+# ------------------------------------------------------------- workloads
+def make_batch(cx, n: int, pl_lo: int, pl_hi: int, rank: int, dev, stream: int):
+    """A stamped-form batch (partition_id = rank + 1) encoded on the GPU by the codec
+    itself from random SoA input; payload lengths U[pl_lo, pl_hi]."""
+    import torch
+    from iggy_amd import abi
+
     g = torch.Generator(device=dev)
     g.manual_seed(0x16619E3779B97F4A ^ rank)
-    payload = torch.randint(0, 256, (n * pl,), dtype=torch.uint8, device=dev, generator=g)
-    pls = torch.full((n,), pl, dtype=torch.int32, device=dev)
+    if pl_lo == pl_hi:
+        pls = torch.full((n,), pl_lo, dtype=torch.int32, device=dev)
+    else:
+        pls = torch.randint(pl_lo, pl_hi + 1, (n,), dtype=torch.int32, device=dev, generator=g)
+    total_pl = int(pls.sum().item())
+    payload = torch.randint(0, 256, (total_pl,), dtype=torch.uint8, device=dev, generator=g)
     ids = torch.randint(1, 2**62, (2 * n,), dtype=torch.int64, device=dev, generator=g)
     ots = 1_700_000_000_000_000 + torch.arange(n, dtype=torch.int64, device=dev)
-    total = 256 + n * (48 + pl)
+    total = 256 + 48 * n + total_pl
     out = torch.empty(total, dtype=torch.uint8, device=dev)
     res = torch.zeros(ctypes.sizeof(abi.EncodeResult), dtype=torch.uint8, device=dev)
     raw = abi.RawMessages(n, ids.data_ptr(), ots.data_ptr(), payload.data_ptr(), pls.data_ptr(), None, None)
+    torch.cuda.synchronize(dev)  # the inputs were made on torch's stream, the encode runs on `stream`
     rc = cx.encode_device(raw, rank + 1, out.data_ptr(), total, res.data_ptr(), stream)
     if rc:
         raise RuntimeError(f"encode_device rc={rc}")
@@ -70,20 +142,132 @@ def make_batch(cx: Codec, n: int, pl: int, rank: int, dev: torch.device, stream:
     er = abi.EncodeResult.from_buffer_copy(res.cpu().numpy().tobytes())
     if er.error.kind != 0 or er.batch_length != total:
         raise RuntimeError(f"encode failed: {er.error!r}")
-    del payload, pls, ids, ots
-    return out
+    return out, (raw, ids, ots, payload, pls, res), total_pl
 
 
-def cpu_baseline(n_sample: int, seconds: float):
+def c3_leg(cx, dev, steps: int):
+    """BASELINE configs[2]: 1 M messages, payloads U[64, 4096]: device-resident encode
+    (with per-message checksums and the batch checksum) and the Verify decode of its
+    output, each timed over `steps` back-to-back calls on one stream."""
+    import torch
+    from iggy_amd import abi
+
+    n = N_MSG
+    s = torch.cuda.Stream(dev)
+    out, keep, total_pl = make_batch(cx, n, 64, 4096, 7, dev, s.cuda_stream)
+    raw, _ids, _ots, _pay, _pls, res = keep
+    L = out.numel()
+    dres = torch.zeros(ctypes.sizeof(abi.DecodeResult), dtype=torch.uint8, device=dev)
+    pos = torch.empty(n, dtype=torch.int64, device=dev)
+
+    def timed(fn):
+        for _ in range(3):
+            fn()
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            fn()
+        torch.cuda.synchronize(dev)
+        return (time.perf_counter() - t0) / steps
+
+    enc_s = timed(lambda: cx.encode_device(raw, 8, out.data_ptr(), L, res.data_ptr(), s.cuda_stream))
+    er = abi.EncodeResult.from_buffer_copy(res.cpu().numpy().tobytes())
+    assert er.error.kind == 0 and er.batch_length == L, er.error
+    dec_s = timed(lambda: cx.decode_device(out.data_ptr(), L, abi.INTEGRITY_VERIFY, pos.data_ptr(), n,
+                                           dres.data_ptr(), s.cuda_stream))
+    dr = abi.DecodeResult.from_buffer_copy(dres.cpu().numpy().tobytes())
+    assert dr.error.kind == 0 and dr.frame_count == n, dr.error
+    enc_alg = total_pl + 32 * n + L  # SURVEY 8(d): payload + ids/timestamps/lengths in, batch out
+    dec_alg = L + 8 * n
+    del out, keep, pos
+    return (
+        {"ms": round(enc_s * 1e3, 4), "gib_s": round(L / enc_s / 2**30, 2), "batch_bytes": L,
+         "algorithmic_bytes": enc_alg, "achieved_gbs": round(enc_alg / enc_s / 1e9, 1),
+         "frac": round(enc_alg / enc_s / 1e9 / HBM_PEAK_GBS, 4),
+         "workload": "C3: SendMessagesEncoder::encode on device, 1,048,576 msgs, payloads U[64,4096] B"},
+        {"ms": round(dec_s * 1e3, 4), "gib_s": round(L / dec_s / 2**30, 2), "batch_bytes": L,
+         "algorithmic_bytes": dec_alg, "achieved_gbs": round(dec_alg / dec_s / 1e9, 1),
+         "frac": round(dec_alg / dec_s / 1e9 / HBM_PEAK_GBS, 4), "path": int(dr.path),
+         "workload": "C3 record: decode_batch_slice_with(Verify), variable frame sizes (general walk)"},
+    )
+
+
+def c1_leg(cx, dev, seconds: float):
+    """BASELINE configs[0] shapes: 10 batches x 1000 msgs x 256 B. iggy-bench over
+    TCP needs a Rust toolchain (absent): recorded as not run; cpu_ref (the oracle's
+    restatement, 1 thread) and the GPU's per-batch latency on the same shapes."""
+    import torch
+    from iggy_amd import abi
+    from iggy_amd.codec import raw_messages
+    from oracle import oracle as O  # cpu_ref leg of the bench only
+
+    nb, n, pl = 10, 1000, 256
+    rng = np.random.default_rng(0x16619E3779B97F4A)
+    raws, keep, recs = [], [], []
+    for b in range(nb):
+        ids = rng.integers(1, 2**63, size=2 * n, dtype=np.uint64)
+        ots = (1_700_000_000_000_000 + b * n + np.arange(n)).astype(np.uint64)
+        pay = rng.integers(0, 256, size=n * pl, dtype=np.uint8)
+        pls = np.full(n, pl, dtype=np.uint32)
+        raws.append(raw_messages(ids, ots, pay, pls))
+        keep.append((ids, ots, pay, pls))
+        rc, e, out = O.encode_batch(raws[-1], 0)
+        assert rc == 0
+        recs.append(np.frombuffer(out, dtype=np.uint8).copy())
+    wire = sum(r.size for r in recs)
+
+    def cpu_rate(one):  # one(batch index, reps) -> seconds for reps passes over that batch
+        reps, secs, passes = 16, 0.0, 0
+        while secs < seconds / 2:
+            secs += sum(one(b, reps) for b in range(nb))
+            passes += reps
+        return passes * wire / secs
+
+    enc = cpu_rate(lambda b, reps: O.cpu_encode_bench(raws[b], 0, 1, reps)[0])
+    dec = cpu_rate(lambda b, reps: O.cpu_decode_bench(recs[b], 1, reps)[0])
+    # GPU: device-resident decode of each batch (latency-bound at 304 KB) and the
+    # host round trip through the asynchronous API (H2D, decode, D2H), per batch
+    s = torch.cuda.Stream(dev)
+    drecs = [torch.from_numpy(r).to(dev) for r in recs]
+    dres = torch.zeros(ctypes.sizeof(abi.DecodeResult), dtype=torch.uint8, device=dev)
+    for _ in range(3):
+        for d, r in zip(drecs, recs):
+            cx.decode_device(d.data_ptr(), r.size, 0, None, 0, dres.data_ptr(), s.cuda_stream)
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(10):
+        for d, r in zip(drecs, recs):
+            cx.decode_device(d.data_ptr(), r.size, 0, None, 0, dres.data_ptr(), s.cuda_stream)
+    torch.cuda.synchronize(dev)
+    dev_us = (time.perf_counter() - t0) / (10 * nb) * 1e6
+    t0 = time.perf_counter()
+    for _ in range(5):
+        for group in (recs[:8], recs[8:]):  # at most 8 in flight per context
+            for t in [cx.decode_submit(r, 0) for r in group]:
+                cx.wait(t)
+    host_us = (time.perf_counter() - t0) / (5 * nb) * 1e6
+    return {
+        "workload": "C1 shapes: 10 batches x 1000 msgs x 256 B (iggy-bench over TCP not run: no Rust toolchain)",
+        "iggy_bench": None,
+        "cpu_ref_encode_gib_s": round(enc / 2**30, 3), "cpu_ref_decode_gib_s": round(dec / 2**30, 3),
+        "cpu_ref_threads": 1,
+        "gpu_device_decode_us_per_batch": round(dev_us, 1),
+        "gpu_host_roundtrip_us_per_batch": round(host_us, 1),
+        "wire_bytes": wire,
+    }
+
+
+def cpu_baseline(seconds: float):
     """The oracle's restatement of the same decode on host cores (bounded sample).
 
     The sample is a full C2-shaped record (not cache-resident: 1.05 GiB), each
     thread walking and verifying the whole record serially (the reference's
     execution model: one shard thread per batch); T threads decode independent
-    walks of it concurrently."""
+    walks of it concurrently, T = 1, 8 (one per partition, C5) and 16 (this
+    process's CPU share on the GPU box)."""
     from oracle import oracle as O  # cpu_baseline leg: the only bench use of oracle/
 
-    rec = O.synth_batch(n_sample, PAYLOAD, PAYLOAD)
+    rec = O.synth_batch(N_MSG, PAYLOAD, PAYLOAD)
     nbytes = rec.size
 
     def rate(threads):
@@ -96,9 +280,8 @@ def cpu_baseline(n_sample: int, seconds: float):
             total_reps += reps
         return threads * total_reps * nbytes / total_secs / 2**30
 
-    threads = min(16, os.cpu_count() or 1)
-    r1 = rate(1)
-    rt = rate(threads)
+    share = min(16, os.cpu_count() or 1)
+    rates = {t: rate(t) for t in sorted({1, min(8, share), share})}
     model = ""
     try:
         with open("/proc/cpuinfo") as f:
@@ -110,11 +293,13 @@ def cpu_baseline(n_sample: int, seconds: float):
         pass
     del rec
     return {
-        "value": round(rt, 3), "unit": "GiB/s", "cores": threads, "kind": "port",
-        "sample": f"{n_sample} msgs x {PAYLOAD} B payload ({nbytes} B record, not cache-resident), "
+        "value": round(rates[share], 3), "unit": "GiB/s", "cores": share, "kind": "port",
+        "sample": f"{N_MSG} msgs x {PAYLOAD} B payload ({nbytes} B record, not cache-resident), "
                   f"decode_batch_slice_with(Verify) walked serially per thread, >= {seconds:.0f} s per "
-                  f"thread count; oracle C restatement with AVX2 XXH3, -O3 -march=native",
-        "single_thread_gib_s": round(r1, 3), "cpu_model": model,
+                  f"thread count; oracle C restatement with AVX2 XXH3",
+        "by_threads_gib_s": {str(t): round(v, 3) for t, v in rates.items()},
+        "single_thread_gib_s": round(rates[1], 3), "cpu_model": model,
+        "host_cpus_visible": os.cpu_count(),
         "avx2": bool(O.lib().oracle_has_avx2()),
     }
 
@@ -133,40 +318,12 @@ def pmc_traffic(n: int):
     return d.get("hbm_bytes_per_decode"), d.get("source")
 
 
-def max_over_ranks(x: float, dist, device) -> float:
-    """The bench's only cross-rank traffic: max of a per-rank scalar (RCCL on GPUs,
-    gloo in the CPU tests). No data-path collective exists: partitions are independent."""
-    if dist is None:
-        return x
-    t = torch.tensor([x], dtype=torch.float64, device=device)
-    dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    return float(t.item())
+# --------------------------------------------------------------------- main
+def run(args, world: int, rank: int, local: int, dist):
+    import torch
+    from iggy_amd import abi
+    from iggy_amd.codec import Codec
 
-
-def whole_job_gib_s(world: int, batch_bytes: int, steps: int, elapsed: float) -> float:
-    """Aggregate throughput: every rank decodes `steps` batches of `batch_bytes` (weak scaling)."""
-    return world * batch_bytes * steps / elapsed / 2**30
-
-
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--messages", type=int, default=N_MSG)
-    ap.add_argument("--no-cpu", action="store_true", help="skip the cpu_baseline leg")
-    ap.add_argument("--cpu-seconds", type=float, default=4.0)
-    ap.add_argument("--streams", type=int, default=2, help="decode lanes (contexts/streams) steps alternate over")
-    args = ap.parse_args()
-
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    dist = None
-    if world > 1:
-        import torch.distributed as dist
-
-        dist.init_process_group("nccl", init_method="env://")
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     n = args.messages
@@ -179,7 +336,8 @@ def main():
     for li in range(args.streams):
         cx = Codec(local)
         ts = torch.cuda.Stream(dev)
-        batch = make_batch(cx, n, PAYLOAD, rank * 16 + li, dev, ts.cuda_stream)
+        batch, _keep, _ = make_batch(cx, n, PAYLOAD, PAYLOAD, rank * 16 + li, dev, ts.cuda_stream)
+        del _keep
         cx.reserve(batch.numel())
         lanes.append({
             "cx": cx, "stream": ts.cuda_stream, "batch": batch,
@@ -216,7 +374,7 @@ def main():
     elapsed = time.perf_counter() - t0
     if dist:
         dist.barrier()
-    elapsed = max_over_ranks(elapsed, dist, dev)
+    elapsed = max_over_ranks(elapsed, dist)
     for ln in lanes:  # every timed decode left a clean result
         res = abi.DecodeResult.from_buffer_copy(ln["res"].cpu().numpy().tobytes())
         if res.error.kind != 0 or res.frame_count != n:
@@ -241,57 +399,111 @@ def main():
         step(0)
     torch.cuda.synchronize(dev)
     single_gib_s = L * args.steps / (time.perf_counter() - t1) / 2**30
+    single_gib_s = max_over_ranks(single_gib_s, dist)  # (every rank takes part in the collective)
 
+    extra = {}
+    if world == 1 and not args.no_extra:
+        for ln in lanes[1:]:  # free HBM held by the other lanes' records
+            ln["batch"] = None
+        torch.cuda.empty_cache()
+        extra["c3_encode"], extra["c3_decode"] = c3_leg(lanes[0]["cx"], dev, max(5, args.steps // 2))
+        extra["c1"] = c1_leg(lanes[0]["cx"], dev, args.cpu_seconds)
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
-        cpu = cpu_baseline(N_MSG, args.cpu_seconds)
+        cpu = cpu_baseline(args.cpu_seconds)
 
     traffic, traffic_src = pmc_traffic(n)
-    ms_per_step = elapsed / args.steps * 1e3
     value = whole_job_gib_s(world, L, args.steps, elapsed)
-    if rank == 0:
-        line = {
-            "metric": METRIC,
-            "value": round(value, 2),
-            "unit": "GiB/s",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": round(ms_per_step, 4),
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": "u8",
-            "data": "synthetic (GPU-encoded batches, random payload bytes)",
-            "config": {
-                "workload": "C2: decode_batch_slice_with(Verify) of one device-resident batch per GPU, "
-                            "1,048,576 msgs x 1 KiB payload",
-                "messages_per_gpu": n,
-                "payload_bytes": PAYLOAD,
-                "batch_bytes": L,
-                "outputs": "frame positions (8 B/msg) + result struct",
-                "parallelism": f"{world} independent partitions, one per GPU, no collective",
-                "streams_per_gpu": len(lanes),
-                "single_stream_gib_s": round(single_gib_s, 2),
-            },
-            "roofline": {
-                "bound": "hbm",
-                "achieved": round(achieved, 1),
-                "peak": HBM_PEAK_GBS,
-                "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 4),
-                "traffic": traffic,
-                "traffic_source": traffic_src,
-                "kernel": "k_decode_uniform<true> (one persistent grid: lane-group producers + chain WG), "
-                          "one launch at a time",
-                "kernel_ms": round(k_ms, 4),
-                "algorithmic_bytes": alg_bytes,
-            },
-            "cpu_baseline": cpu,
-        }
-        print(json.dumps(line), flush=True)
+    line = {
+        "metric": METRIC,
+        "value": round(value, 2),
+        "unit": "GiB/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u8",
+        "data": "synthetic (GPU-encoded batches, random payload bytes)",
+        "config": {
+            "workload": "C2: decode_batch_slice_with(Verify) of one device-resident batch per GPU, "
+                        "1,048,576 msgs x 1 KiB payload",
+            "messages_per_gpu": n,
+            "payload_bytes": PAYLOAD,
+            "batch_bytes": L,
+            "outputs": "frame positions (8 B/msg) + result struct",
+            "parallelism": f"{world} independent partitions, one per GPU, no collective",
+            "streams_per_gpu": len(lanes),
+            "single_stream_gib_s": round(single_gib_s, 2),
+            "per_gpu_gib_s": round(value / world, 2),
+            "per_gpu_hbm_frac": round(value / world * 2**30 / 1e9 / HBM_PEAK_GBS, 4),
+        },
+        "roofline": {
+            "bound": "hbm",
+            "achieved": round(achieved, 1),
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4),
+            "traffic": traffic,
+            "traffic_source": traffic_src,
+            "kernel": "k_decode_uniform<true> (one persistent grid: lane-group producers + chain WG), "
+                      "one launch at a time",
+            "kernel_ms": round(k_ms, 4),
+            "algorithmic_bytes": alg_bytes,
+        },
+        "cpu_baseline": cpu,
+    }
+    line.update(extra)
     for ln in lanes:
         ln["cx"].close()
+    return line
+
+
+def run_dry(args, world: int, rank: int, dist):
+    """The launcher / barrier / max-over-ranks path with a CPU stand-in for a step
+    (tests/test_multirank_cpu.py runs it at world 2 on a GPU-less host)."""
+    def step(i):
+        time.sleep(0.001 * (1 + rank))
+
+    for i in range(args.warmup):
+        step(i)
+    if dist:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step(i)
+    elapsed = time.perf_counter() - t0
+    if dist:
+        dist.barrier()
+    elapsed = max_over_ranks(elapsed, dist)
+    L = 256 + args.messages * (48 + PAYLOAD)
+    return {"metric": METRIC, "value": round(whole_job_gib_s(world, L, args.steps, elapsed), 2), "unit": "GiB/s",
+            "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "u8", "data": "dry run (no codec, no GPU)",
+            "config": {"workload": "dry", "parallelism": f"{world} ranks"}}
+
+
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
+    args = parse_args(argv)
+    world = int(os.environ.get("WORLD_SIZE", "0") or 0)
+    if world == 0 and args.gpus > 1:
+        # no launcher: start one rank per GPU ourselves, before any GPU call here
+        sys.exit(launch(args.gpus, argv))
+    world = max(world, 1)
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+
+        dist.init_process_group("gloo", init_method="env://", rank=rank, world_size=world)
+    line = run_dry(args, world, rank, dist) if args.dry else run(args, world, rank, local, dist)
+    if rank == 0:
+        print(json.dumps(line), flush=True)
     if dist:
         dist.destroy_process_group()
 

@@ -21,6 +21,11 @@ ERR_DEVICE = 100
 ERR_INVALID_ARGUMENT = 101
 ERR_CAPACITY = 102
 ERR_TIMEOUT = 103
+ERR_PENDING = 104
+ERR_BUSY = 105
+
+OP_DECODE = 1
+OP_ENCODE = 2
 
 # iggy_validation_reason
 V_NONE = 0
@@ -155,6 +160,21 @@ class SliceResult(ctypes.Structure):
                 self.last_matching_offset) + self.header.astuple()
 
 
+class Completion(ctypes.Structure):
+    """iggy_completion: the outcome of a submitted host-buffer operation."""
+    _fields_ = [
+        ("op", u32),
+        ("_pad0", u32),
+        ("header", BatchHeader),
+        ("error", WireError),
+        ("frame_count", u64),
+        ("computed_checksum", u64),
+        ("bytes", u64),
+        ("_pad1", u64 * 3),
+    ]
+
+
+assert ctypes.sizeof(Completion) == 152
 assert ctypes.sizeof(SliceQuery) == 32
 assert ctypes.sizeof(SliceResult) == 128
 assert ctypes.sizeof(BatchHeader) == 64

@@ -16,8 +16,8 @@ import re
 import numpy as np
 
 from . import abi
-from .abi import (BatchHeader, DecodeResult, EncodeResult, PolledMessage, RawMessages, SliceQuery, SliceResult,
-                  WireError)
+from .abi import (BatchHeader, Completion, DecodeResult, EncodeResult, PolledMessage, RawMessages, SliceQuery,
+                  SliceResult, WireError)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libiggy_codec.so")
@@ -46,14 +46,31 @@ def exported_symbols() -> list[str]:
     return sorted(set(names))
 
 
+def use_library(path: str) -> None:
+    """Diagnostics only: bind this module to another build of the library (the
+    ablation build libiggy_codec_diag.so) before the first lib() call."""
+    global LIB_PATH, _lib
+    if _lib is not None:
+        raise RuntimeError("the codec library is already loaded")
+    LIB_PATH = path
+
+
 def lib() -> ctypes.CDLL:
     global _lib
-    if _lib is not None:
-        return _lib
-    if not os.path.exists(LIB_PATH):
+    if _lib is None:
+        _lib = load(LIB_PATH)
+    return _lib
+
+
+DIAG_LIB_PATH = os.path.join(_HERE, "libiggy_codec_diag.so")
+
+
+def load(path: str) -> ctypes.CDLL:
+    """Load one build of the library and declare its C ABI (lib() is the product build)."""
+    if not os.path.exists(path):
         raise FileNotFoundError(
-            f"{LIB_PATH} missing: build it with `python -c 'import __graft_entry__ as g; g.build()'`")
-    L = ctypes.CDLL(LIB_PATH)
+            f"{path} missing: build it with `python -c 'import __graft_entry__ as g; g.build()'`")
+    L = ctypes.CDLL(path)
     L.iggy_codec_abi_version.restype = u32
     L.iggy_codec_create.argtypes = [ci, ctypes.POINTER(vp)]
     L.iggy_codec_destroy.argtypes = [vp]
@@ -86,9 +103,15 @@ def lib() -> ctypes.CDLL:
     L.iggy_codec_recover_segment.argtypes = [vp, vp, u64, u64, vp]
     L.iggy_codec_profile_enable.argtypes = [vp, ci]
     L.iggy_codec_profile_read.argtypes = [vp, ci, vp, vp]
+    L.iggy_codec_host_register.argtypes = [vp, vp, u64]
+    L.iggy_codec_host_unregister.argtypes = [vp, vp]
+    L.iggy_codec_decode_submit.argtypes = [vp, vp, u64, ci, vp, u64, ctypes.POINTER(u64)]
+    L.iggy_codec_encode_submit.argtypes = [vp, vp, u64, vp, u64, ctypes.POINTER(u64)]
+    L.iggy_codec_poll.argtypes = [vp, u64, vp]
+    L.iggy_codec_wait.argtypes = [vp, u64, vp]
     L.iggy_codec_error_string.argtypes = [u32, u32]
     L.iggy_codec_error_string.restype = ctypes.c_char_p
-    _lib = L
+    L.iggy_codec_debug_set.argtypes = [vp, u32]
     return L
 
 
@@ -105,8 +128,8 @@ def _addr(a: np.ndarray):
 class Codec:
     """One codec context bound to one HIP device (thread-per-core shards each own one)."""
 
-    def __init__(self, device: int = 0):
-        self._L = lib()
+    def __init__(self, device: int = 0, library: ctypes.CDLL | None = None):
+        self._L = library if library is not None else lib()
         h = vp()
         rc = self._L.iggy_codec_create(device, ctypes.byref(h))
         if rc != 0:
@@ -274,6 +297,53 @@ class Codec:
     def xxh3_ranges_device(self, d_data, d_offsets, d_lengths, n, d_out, stream=None) -> int:
         return self._L.iggy_codec_xxh3_64_ranges_device(self._h, d_data, d_offsets, d_lengths, n,
                                                         d_out, stream)
+
+    # ------------------------------------------- asynchronous host buffers
+    def host_register(self, arr: np.ndarray):
+        rc = self._L.iggy_codec_host_register(self._h, arr.ctypes.data, arr.nbytes)
+        if rc:
+            raise CodecError(rc, None, "host_register")
+
+    def host_unregister(self, arr: np.ndarray):
+        rc = self._L.iggy_codec_host_unregister(self._h, arr.ctypes.data)
+        if rc:
+            raise CodecError(rc, None, "host_unregister")
+
+    def decode_submit(self, body: np.ndarray, integrity: int, frame_pos: np.ndarray | None = None) -> int:
+        """-> ticket. `body` (and `frame_pos`) must stay alive until the ticket completes."""
+        t = u64(0)
+        cap = frame_pos.size if frame_pos is not None else 0
+        rc = self._L.iggy_codec_decode_submit(self._h, _addr(body), body.size, integrity,
+                                              frame_pos.ctypes.data if frame_pos is not None else None, cap,
+                                              ctypes.byref(t))
+        if rc:
+            raise CodecError(rc, None, "decode_submit")
+        return t.value
+
+    def encode_submit(self, raw: RawMessages, partition_id: int, out: np.ndarray) -> int:
+        t = u64(0)
+        rc = self._L.iggy_codec_encode_submit(self._h, ctypes.byref(raw), partition_id, out.ctypes.data, out.size,
+                                              ctypes.byref(t))
+        if rc:
+            raise CodecError(rc, None, "encode_submit")
+        return t.value
+
+    def poll(self, ticket: int):
+        """-> Completion, or None while the operation is in flight (never blocks)."""
+        c = Completion()
+        rc = self._L.iggy_codec_poll(self._h, ticket, ctypes.byref(c))
+        if rc == abi.ERR_PENDING:
+            return None
+        if rc:
+            raise CodecError(rc, None, "poll")
+        return c
+
+    def wait(self, ticket: int) -> Completion:
+        c = Completion()
+        rc = self._L.iggy_codec_wait(self._h, ticket, ctypes.byref(c))
+        if rc:
+            raise CodecError(rc, None, "wait")
+        return c
 
     def profile_enable(self, on: bool = True):
         self._L.iggy_codec_profile_enable(self._h, 1 if on else 0)

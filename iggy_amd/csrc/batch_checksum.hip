@@ -112,6 +112,31 @@ __device__ inline uint64_t chain_blocks(const uint64_t *bsums, uint64_t nb, int 
     return acc;
 }
 
+// Header fields (by value) and the frame count (by value, or from a device word an
+// earlier kernel on the stream wrote, e.g. a decode's frame_count) into the device
+// words the checksum kernels read: no host copy on the enqueue path.
+__global__ void k_put_header(iggy_batch_header h, uint64_t n, const uint64_t *n_dev, iggy_batch_header *dh,
+                             uint64_t *dn) {
+    if (threadIdx.x == 0) {
+        *dh = h;
+        *dn = n_dev ? *n_dev : n;
+    }
+}
+
+// admit_wire_request's stamped header (server_common/src/send_messages.rs:529-537):
+// the decoded header with the namespace partition id and a zero checksum field;
+// nothing is hashed unless the decode succeeded.
+__global__ void k_admit_header(const iggy_decode_result *res, uint64_t partition_id, iggy_batch_header *dh,
+                               uint64_t *dn) {
+    if (threadIdx.x == 0) {
+        iggy_batch_header h = res->header;
+        h.partition_id = partition_id;
+        h.batch_checksum = 0;
+        *dh = h;
+        *dn = res->error.kind == IGGY_OK ? res->frame_count : 0;
+    }
+}
+
 // header and frame count come from device memory (written by an earlier kernel
 // on the stream) so nothing has to travel back to the host in between.
 __global__ __launch_bounds__(256) void k_bsum_blocks(const iggy_batch_header *hp,

@@ -63,6 +63,25 @@ struct DevBuf {
 
 }  // namespace
 
+// one asynchronous host-buffer operation in flight (iggy_codec_*_submit / iggy_codec_poll)
+constexpr int kSlots = 8;
+struct Slot {
+    bool busy = false;
+    uint64_t ticket = 0;
+    uint32_t op = 0;
+    uint64_t cap = 0, out_len = 0;
+    uint64_t *frame_pos = nullptr;               // host destination of the decode's positions
+    DevBuf in, pos, out, res;                    // device input / positions / encode output / result
+    DevBuf ids, ots, pay, plen, uhb, uhl;        // encode SoA inputs
+    hipEvent_t ev_in = nullptr, ev_k = nullptr, ev_done = nullptr;
+    void release() {
+        DevBuf *b[] = {&in, &pos, &out, &res, &ids, &ots, &pay, &plen, &uhb, &uhl};
+        for (DevBuf *x : b) x->release();
+        for (hipEvent_t *e : {&ev_in, &ev_k, &ev_done})
+            if (*e) (void)hipEventDestroy(*e), *e = nullptr;
+    }
+};
+
 constexpr int kEncSegs = 4;                   // encode segments (checksum chain overlap); bounds below
 constexpr uint64_t kEncSegMinFrames = 1 << 18;  // below this one segment
 
@@ -72,16 +91,17 @@ struct iggy_codec_ctx {
     int ncu = 256;
     uint32_t epoch = 0;
     int allow_unaligned = 0;
-    uint32_t dbg = 0;  // IGGY_CODEC_DBG: ablation bits for diagnostics only
+    uint32_t dbg = 0;  // IGGY_CODEC_DBG ablation bits: read only by the diagnostic build (kDiagMask)
+    // one stream order per context (its scratch is shared by every enqueue): the
+    // stream of the latest enqueue, and the event a switch to another stream waits on
+    hipStream_t last = nullptr;
+    hipEvent_t order_ev = nullptr;
     // decode scratch
     uint64_t dec_cap_len = 0;
     DevBuf dsync;    // exited | first_bad | spec_fail | bar[4] | misc[16] | small[512]
     DevBuf dsums, derr;
     DevBuf gtiles_s, gtiles_x, gtiles_cnt, gtiles_pre, gtiles_list, gtiles_e, gtiles_base, ggrp, gfpos, gcs, gflen, gbsums;
-    int gen_grid = 0;  // co-resident WGs of k_decode_general
-    // IGGY_CODEC_COOPERATIVE=1: launch it cooperatively (safe for concurrent variable-size
-    // decodes on several streams; ~4 % off the pipelined C2 bench, so off by default)
-    bool coop_general = false;
+    int gen_grid = 0;  // WGs of k_decode_general (the ones that get a CU join its barriers)
     // encode: the batch-checksum chain of earlier frame segments runs on `side`
     // while later segments are encoded on the call's stream
     hipStream_t side = nullptr;
@@ -95,11 +115,17 @@ struct iggy_codec_ctx {
     // big one-shot hash
     DevBuf hbsums;
     // poll
-    DevBuf ppos, pmsgs;
+    DevBuf ppos, pmsgs, pres;
     // slice / device stamp: [0,512) control words + header + small, then tile counts
     DevBuf sl, slres;
     // pinned host mirror of results
     void *h_pinned = nullptr;
+    // asynchronous host-buffer operations: copy-in stream -> the context's stream -> copy-out
+    // stream, so one operation's H2D, another's kernels and a third's D2H overlap
+    hipStream_t h2d = nullptr, d2h = nullptr;
+    Slot slots[kSlots];
+    void *slot_pinned = nullptr;  // kSlots x 256 B: completion records
+    uint64_t seq = 0;
     // profiling
     int profile = 0;
     hipEvent_t ev0[2] = {nullptr, nullptr}, ev1[2] = {nullptr, nullptr};
@@ -157,6 +183,8 @@ DecodeScratch dscratch(iggy_codec_ctx *c) {
     s.sums = c->dsums.as<uint64_t>();
     s.errslot = c->derr.as<uint64_t>();
     s.small = c->dsync.as<uint8_t>(kSyncSmall);
+    s.gbar = c->dsync.as<uint32_t>(kSyncBar);
+    s.gmisc = c->dsync.as<uint64_t>(kSyncMisc);
     s.max_chunks = (c->dsums.cap - 64) / (kUnitSumRows * 8);
     return s;
 }
@@ -177,6 +205,9 @@ GeneralScratch gscratch(iggy_codec_ctx *c) {
     g.bsums = c->gbsums.as<uint64_t>();
     g.misc = c->dsync.as<uint64_t>(kSyncMisc);
     g.bar = c->dsync.as<uint32_t>(kSyncBar);
+    g.u_exited = c->dsync.as<uint32_t>(kSyncExited);
+    g.u_first_bad = c->dsync.as<uint64_t>(kSyncFirstBad);
+    g.u_spec_fail = c->dsync.as<uint64_t>(kSyncSpecFail);
     g.small = c->dsync.as<uint8_t>(kSyncSmall);
     g.ntiles = c->gtiles_s.cap / 8;
     g.max_frames = c->gfpos.cap / 8;
@@ -184,9 +215,37 @@ GeneralScratch gscratch(iggy_codec_ctx *c) {
     return g;
 }
 
-hipStream_t pick(iggy_codec_ctx *c, void *stream) {
-    return stream ? (hipStream_t)stream : c->stream;
+// Every enqueue of a context runs in ONE stream order: the scratch it uses (sync
+// words, unit sums, walk tables, result staging) belongs to the context. An
+// enqueue on another stream than the previous one first makes that stream wait
+// for everything enqueued before (an event recorded on the previous stream, which
+// must therefore still exist). Enqueues on one stream pay nothing.
+hipStream_t bind(iggy_codec_ctx *c, void *stream) {
+    hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+    if (s != c->last) {
+        if (c->last && c->order_ev && hipEventRecord(c->order_ev, c->last) == hipSuccess)
+            (void)hipStreamWaitEvent(s, c->order_ev, 0);
+        c->last = s;
+    }
+    return s;
 }
+
+// The context's device is current for the duration of an entry point; the
+// caller's current device is restored on return (multi-GPU processes keep
+// one context per GPU on arbitrary threads).
+struct DevGuard {
+    int prev = -1, dev;
+    explicit DevGuard(int d) : dev(d) {
+        int cur = -1;
+        if (hipGetDevice(&cur) == hipSuccess && cur != d && hipSetDevice(d) == hipSuccess) prev = cur;
+    }
+    ~DevGuard() {
+        if (prev >= 0) (void)hipSetDevice(prev);
+    }
+};
+
+// diagnostic ablation bits, zero in the product build
+inline uint32_t diag_bits(const iggy_codec_ctx *c) { return c->dbg & kDiagMask; }
 
 void prof_begin(iggy_codec_ctx *c, int which, hipStream_t s) {
     if (!c->profile) return;
@@ -222,18 +281,13 @@ int enqueue_decode(iggy_codec_ctx *c, const uint8_t *d_body, uint64_t len, int i
     prof_begin(c, 0, s);
     if (verify)
         hipLaunchKernelGGL(k_decode_uniform<true>, dim3(grid), dim3(256), kUniformLds, s, d_body, len, d_pos,
-                           cap, d_res, ds, c->epoch, au, c->dbg);
+                           cap, d_res, ds, c->epoch, au, diag_bits(c));
     else
         hipLaunchKernelGGL(k_decode_uniform<false>, dim3(grid), dim3(256), kUniformLds, s, d_body, len, d_pos,
-                           cap, d_res, ds, c->epoch, au, c->dbg);
+                           cap, d_res, ds, c->epoch, au, diag_bits(c));
     prof_end(c, 0, s);
     HIP_OK(hipGetLastError());
-    if (c->coop_general) {  // all-or-nothing residency: concurrent general decodes cannot interleave
-        void *args[] = {(void *)&d_body, (void *)&len, (void *)&d_pos, (void *)&cap, (void *)&d_res, (void *)&gs};
-        HIP_OK(hipLaunchCooperativeKernel(verify ? (const void *)k_decode_general<true>
-                                                 : (const void *)k_decode_general<false>,
-                                          dim3(c->gen_grid), dim3(kGenThreads), args, 0, s));
-    } else if (verify) {
+    if (verify) {
         hipLaunchKernelGGL(k_decode_general<true>, dim3(c->gen_grid), dim3(kGenThreads), 0, s, d_body, len, d_pos,
                            cap, d_res, gs);
     } else {
@@ -308,8 +362,8 @@ int iggy_codec_create(int device, iggy_codec_ctx **out) {
     if (!c) return IGGY_ERR_DEVICE;
     c->device = device;
     c->ncu = prop.multiProcessorCount;
-    if (const char *d = getenv("IGGY_CODEC_DBG")) c->dbg = (uint32_t)strtoul(d, nullptr, 0);
-    if (const char *d = getenv("IGGY_CODEC_COOPERATIVE")) c->coop_general = atoi(d) != 0;
+    if (kDiagMask)  // diagnostic build only
+        if (const char *d = getenv("IGGY_CODEC_DBG")) c->dbg = (uint32_t)strtoul(d, nullptr, 0);
     if (hipSetDevice(device) != hipSuccess ||
         hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
         hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking) != hipSuccess) {
@@ -319,7 +373,9 @@ int iggy_codec_create(int device, iggy_codec_ctx **out) {
     }
     for (auto &ev : c->seg_ev)
         if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) ev = nullptr;
+    c->last = c->stream;
     int r = 0;
+    if (hipEventCreateWithFlags(&c->order_ev, hipEventDisableTiming) != hipSuccess) r = IGGY_ERR_DEVICE;
     r |= c->dresult.ensure(4096);
     if (hipHostMalloc(&c->h_pinned, 4096, hipHostMallocDefault) != hipSuccess) r = IGGY_ERR_DEVICE;
     if (!r) {
@@ -376,7 +432,7 @@ void iggy_codec_destroy(iggy_codec_ctx *c) {
                       &c->gtiles_cnt, &c->gtiles_pre, &c->gtiles_list, &c->gtiles_e, &c->gtiles_base, &c->ggrp, &c->gfpos, &c->gcs, &c->gflen,
                       &c->gbsums, &c->dresult, &c->din, &c->dpos, &c->dout, &c->epl, &c->euh,
                       &c->etile, &c->ecs, &c->emisc, &c->eids, &c->eots, &c->epay, &c->eplen,
-                      &c->euhb, &c->euhl, &c->hbsums, &c->ppos, &c->pmsgs, &c->sl, &c->slres};
+                      &c->euhb, &c->euhl, &c->hbsums, &c->ppos, &c->pmsgs, &c->pres, &c->sl, &c->slres};
     for (DevBuf *b : bufs) b->release();
     if (c->h_pinned) (void)hipHostFree(c->h_pinned);
     for (int w = 0; w < 2; ++w) {
@@ -385,6 +441,11 @@ void iggy_codec_destroy(iggy_codec_ctx *c) {
     }
     for (auto &ev : c->seg_ev)
         if (ev) (void)hipEventDestroy(ev);
+    if (c->order_ev) (void)hipEventDestroy(c->order_ev);
+    for (Slot &sl : c->slots) sl.release();
+    if (c->slot_pinned) (void)hipHostFree(c->slot_pinned);
+    if (c->h2d) (void)hipStreamSynchronize(c->h2d), (void)hipStreamDestroy(c->h2d);
+    if (c->d2h) (void)hipStreamSynchronize(c->d2h), (void)hipStreamDestroy(c->d2h);
     if (c->side) (void)hipStreamDestroy(c->side);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
@@ -392,7 +453,8 @@ void iggy_codec_destroy(iggy_codec_ctx *c) {
 
 int iggy_codec_reserve(iggy_codec_ctx *c, uint64_t max_batch_bytes, uint64_t max_frames) {
     if (!c) return IGGY_ERR_INVALID_ARGUMENT;
-    HIP_OK(hipSetDevice(c->device));
+    DevGuard dg(c->device);
+    bind(c, nullptr);
     (void)max_frames;
     return ensure_decode_scratch(c, max_batch_bytes);
 }
@@ -462,7 +524,8 @@ int iggy_codec_decode_batch(iggy_codec_ctx *c, const uint8_t *body, uint64_t len
                             iggy_batch_header *hdr, uint64_t *frame_pos, uint64_t cap,
                             uint64_t *nframes, iggy_wire_error *err) {
     if (!c || (!body && len)) return IGGY_ERR_INVALID_ARGUMENT;
-    HIP_OK(hipSetDevice(c->device));
+    DevGuard dg(c->device);
+    bind(c, nullptr);
     iggy_decode_result res;
     int r = decode_host(c, body, len, integrity, &res, frame_pos, cap, false);
     if (r) return r;
@@ -477,20 +540,38 @@ int iggy_codec_decode_batch(iggy_codec_ctx *c, const uint8_t *body, uint64_t len
     return 0;
 }
 
+// Stage [256-B header built from *h][blob] in the context's input buffer: two
+// copies straight from the caller's memory (no host-side concatenation).
+static int stage_record(iggy_codec_ctx *c, const iggy_batch_header &h, const uint8_t *blob, uint64_t blob_len) {
+    if (c->din.ensure(256 + blob_len + 16)) return IGGY_ERR_DEVICE;
+    uint8_t *hb = (uint8_t *)c->h_pinned + 2048;  // pinned: the copy is truly async
+    iggy_batch_header_encode(&h, hb);
+    HIP_OK(hipMemcpyAsync(c->din.p, hb, 256, hipMemcpyHostToDevice, c->stream));
+    if (blob_len) HIP_OK(hipMemcpyAsync(c->din.as<uint8_t>(256), blob, blob_len, hipMemcpyHostToDevice, c->stream));
+    return 0;
+}
+
 int iggy_codec_verify_and_recompute_batch_checksum(iggy_codec_ctx *c, const iggy_batch_header *hdr,
                                                    const uint8_t *blob, uint64_t blob_len,
                                                    uint64_t *out, iggy_wire_error *err) {
     if (!c || !hdr || (!blob && blob_len)) return IGGY_ERR_INVALID_ARGUMENT;
-    // re-materialise the record (header fields as given, batch_length = 256 + blob)
-    std::vector<uint8_t> rec(256 + blob_len);
+    DevGuard dg(c->device);
+    bind(c, nullptr);
+    // the BatchRef's header fields as given; batch_length is the record's own
+    // (256 + blob), as for every BatchRef a decode hands out (batch.rs:391-406)
     iggy_batch_header h = *hdr;
-    iggy_batch_header_encode(&h, rec.data());
-    uint64_t bl = 256 + blob_len;
-    memcpy(rec.data() + 32, &bl, 8);
-    if (blob_len) memcpy(rec.data() + 256, blob, blob_len);
-    iggy_decode_result res;
-    int r = decode_host(c, rec.data(), rec.size(), IGGY_INTEGRITY_VERIFY, &res, nullptr, 0, false);
+    h.batch_length = 256 + blob_len;
+    int r = stage_record(c, h, blob, blob_len);
     if (r) return r;
+    iggy_decode_result *d_res = c->dresult.as<iggy_decode_result>();
+    r = enqueue_decode(c, c->din.as<uint8_t>(), 256 + blob_len, IGGY_INTEGRITY_VERIFY, nullptr, 0, d_res, c->stream);
+    if (r) return r;
+    iggy_decode_result *h_res = (iggy_decode_result *)c->h_pinned;
+    HIP_OK(hipMemcpyAsync(h_res, d_res, sizeof(*h_res), hipMemcpyDeviceToHost, c->stream));
+    HIP_OK(hipStreamSynchronize(c->stream));
+    const iggy_decode_result res = *h_res;
+    if (res.error.kind == IGGY_ERR_TIMEOUT) reset_after_timeout(c);
+    // the stored batch checksum is the caller's business here (batch.rs:474-506)
     if (res.error.kind == IGGY_ERR_INVALID_BATCH_CHECKSUM || res.error.kind == IGGY_OK) {
         if (out) *out = res.computed_checksum;
         set_err(err, IGGY_OK);
@@ -500,11 +581,12 @@ int iggy_codec_verify_and_recompute_batch_checksum(iggy_codec_ctx *c, const iggy
     return (int)res.error.kind;
 }
 
-static int checksum_of_walk(iggy_codec_ctx *c, const iggy_batch_header *hdr, const uint8_t *d_blob,
-                            const uint64_t *d_pos, const uint64_t *d_n, uint64_t *d_out, hipStream_t s) {
-    // hdr is host: stage it in the result area
+static int checksum_of_walk(iggy_codec_ctx *c, const iggy_batch_header *hdr, uint64_t nframes,
+                            const uint8_t *d_blob, const uint64_t *d_pos, uint64_t *d_out, hipStream_t s) {
+    // header fields and frame count travel as kernel arguments (no host copy)
     iggy_batch_header *dh = c->dresult.as<iggy_batch_header>(2048);
-    HIP_OK(hipMemcpyAsync(dh, hdr, sizeof(*hdr), hipMemcpyHostToDevice, s));
+    uint64_t *d_n = c->dresult.as<uint64_t>(3096);
+    hipLaunchKernelGGL(k_put_header, dim3(1), dim3(64), 0, s, *hdr, nframes, (const uint64_t *)nullptr, dh, d_n);
     CsSource src{nullptr, d_blob, d_pos};
     hipLaunchKernelGGL(k_bsum_blocks, dim3(c->ncu * 4), dim3(256), 0, s, dh, d_n, src,
                        c->gbsums.as<uint64_t>(), nullptr);
@@ -515,36 +597,52 @@ static int checksum_of_walk(iggy_codec_ctx *c, const iggy_batch_header *hdr, con
     return 0;
 }
 
+// The frames BatchIteratorWithOffsets yields over the staged record (a LayoutOnly
+// decode: its frame_count is the walk's, whatever error ends it) and the batch
+// checksum over them with header fields *hdr, all in one enqueue.
+static int enqueue_checksum_of_staged(iggy_codec_ctx *c, const iggy_batch_header &hdr, uint64_t blob_len,
+                                      uint64_t *d_out) {
+    const uint64_t cap = blob_len / 48 + 1;
+    int r = c->dpos.ensure((cap + 1) * 8);
+    r |= c->gbsums.ensure(((44 + 8 * cap) / 1024 + 2) * 64);
+    if (r) return IGGY_ERR_DEVICE;
+    iggy_decode_result *d_res = c->dresult.as<iggy_decode_result>();
+    r = enqueue_decode(c, c->din.as<uint8_t>(), 256 + blob_len, IGGY_INTEGRITY_LAYOUT_ONLY, c->dpos.as<uint64_t>(),
+                       cap, d_res, c->stream);
+    if (r) return r;
+    iggy_batch_header *dh = c->dresult.as<iggy_batch_header>(2048);
+    uint64_t *d_n = c->dresult.as<uint64_t>(3096);
+    hipLaunchKernelGGL(k_put_header, dim3(1), dim3(64), 0, c->stream, hdr, (uint64_t)0,
+                       (const uint64_t *)&d_res->frame_count, dh, d_n);
+    CsSource src{nullptr, c->din.as<uint8_t>(256), c->dpos.as<uint64_t>()};
+    hipLaunchKernelGGL(k_bsum_blocks, dim3(c->ncu * 4), dim3(256), 0, c->stream, dh, d_n, src,
+                       c->gbsums.as<uint64_t>(), nullptr);
+    hipLaunchKernelGGL(k_bsum_chain, dim3(1), dim3(64), 0, c->stream, dh, d_n, src,
+                       (const uint64_t *)c->gbsums.as<uint64_t>(), c->dsync.as<uint8_t>(kSyncSmall), d_out, nullptr);
+    HIP_OK(hipGetLastError());
+    return 0;
+}
+
 int iggy_codec_calculate_batch_checksum(iggy_codec_ctx *c, const iggy_batch_header *hdr,
                                         const uint8_t *blob, uint64_t blob_len, uint64_t *out) {
     if (!c || !hdr || !out || (!blob && blob_len)) return IGGY_ERR_INVALID_ARGUMENT;
-    HIP_OK(hipSetDevice(c->device));
-    // walk the blob (layout) to find the frames the infallible iterator yields
-    std::vector<uint8_t> rec(256 + blob_len);
+    DevGuard dg(c->device);
+    bind(c, nullptr);
+    // the walk sees a header of this blob's length and no message count (only the
+    // frames matter); the checksum hashes the caller's header fields
     iggy_batch_header h = *hdr;
     h.batch_length = 256 + blob_len;
     h.message_count = 0;
-    iggy_batch_header_encode(&h, rec.data());
-    if (blob_len) memcpy(rec.data() + 256, blob, blob_len);
-    iggy_decode_result res;
-    int r = c->dpos.ensure((blob_len / 48 + 2) * 8);
+    h.batch_checksum = 0;
+    int r = stage_record(c, h, blob, blob_len);
     if (r) return r;
-    r = decode_host(c, rec.data(), rec.size(), IGGY_INTEGRITY_LAYOUT_ONLY, &res, nullptr, 0, true);
+    uint64_t *d_out = c->dresult.as<uint64_t>(3080);
+    r = enqueue_checksum_of_staged(c, *hdr, blob_len, d_out);
     if (r) return r;
-    // positions: re-run the walk with the frame_pos output on device
-    r = enqueue_decode(c, c->din.as<uint8_t>(), rec.size(), IGGY_INTEGRITY_LAYOUT_ONLY,
-                       c->dpos.as<uint64_t>(), blob_len / 48 + 1, c->dresult.as<iggy_decode_result>(),
-                       c->stream);
-    if (r) return r;
-    uint64_t *dn = c->dresult.as<uint64_t>(3072);
-    uint64_t n = res.frame_count;
-    HIP_OK(hipMemcpyAsync(dn, &n, 8, hipMemcpyHostToDevice, c->stream));
-    uint64_t *dout = c->dresult.as<uint64_t>(3080);
-    iggy_batch_header hc = *hdr;  // checksum uses the caller's header fields
-    r = checksum_of_walk(c, &hc, c->din.as<uint8_t>(256), c->dpos.as<uint64_t>(), dn, dout, c->stream);
-    if (r) return r;
-    HIP_OK(hipMemcpyAsync(out, dout, 8, hipMemcpyDeviceToHost, c->stream));
+    uint64_t *h_out = (uint64_t *)((uint8_t *)c->h_pinned + 1536);
+    HIP_OK(hipMemcpyAsync(h_out, d_out, 8, hipMemcpyDeviceToHost, c->stream));
     HIP_OK(hipStreamSynchronize(c->stream));
+    *out = *h_out;
     return 0;
 }
 
@@ -612,9 +710,49 @@ int iggy_codec_admit_batch(iggy_codec_ctx *c, const uint8_t *batch, uint64_t len
                            uint32_t metadata_messages_count, uint64_t partition_id, int checksum_mode,
                            uint8_t *out, uint64_t cap, iggy_batch_header *hdr_out, iggy_wire_error *err) {
     if (!c || (!batch && len) || !out) return IGGY_ERR_INVALID_ARGUMENT;
-    iggy_batch_header h;
-    int r = iggy_codec_decode_batch(c, batch, len, IGGY_INTEGRITY_VERIFY, &h, nullptr, 0, nullptr, err);
-    if (r) return server_error(r, err);
+    DevGuard dg(c->device);
+    bind(c, nullptr);
+    set_err(err, IGGY_OK);
+    // one H2D copy and one Verify decode (positions kept on the device); the stamped
+    // header's checksum (send_messages.rs:529-537) is computed from those positions in
+    // the same enqueue, before the host has seen the verdict (discarded on failure)
+    const uint64_t pcap = len / 48 + 1;
+    int r = c->din.ensure(len + 16);
+    r |= c->dpos.ensure((pcap + 1) * 8);
+    r |= c->gbsums.ensure(((44 + 8 * pcap) / 1024 + 2) * 64);
+    if (r) return IGGY_ERR_DEVICE;
+    if (len) HIP_OK(hipMemcpyAsync(c->din.p, batch, len, hipMemcpyHostToDevice, c->stream));
+    iggy_decode_result *d_res = c->dresult.as<iggy_decode_result>();
+    r = enqueue_decode(c, c->din.as<uint8_t>(), len, IGGY_INTEGRITY_VERIFY, c->dpos.as<uint64_t>(), pcap, d_res,
+                       c->stream);
+    if (r) return r;
+    uint64_t *d_cs = c->dresult.as<uint64_t>(3080);
+    const bool compute = checksum_mode == IGGY_CHECKSUM_COMPUTE;
+    if (compute) {
+        iggy_batch_header *dh = c->dresult.as<iggy_batch_header>(2048);
+        uint64_t *d_n = c->dresult.as<uint64_t>(3096);
+        hipLaunchKernelGGL(k_admit_header, dim3(1), dim3(64), 0, c->stream, (const iggy_decode_result *)d_res,
+                           partition_id, dh, d_n);
+        CsSource src{nullptr, c->din.as<uint8_t>(256), c->dpos.as<uint64_t>()};
+        hipLaunchKernelGGL(k_bsum_blocks, dim3(c->ncu * 4), dim3(256), 0, c->stream, dh, d_n, src,
+                           c->gbsums.as<uint64_t>(), nullptr);
+        hipLaunchKernelGGL(k_bsum_chain, dim3(1), dim3(64), 0, c->stream, dh, d_n, src,
+                           (const uint64_t *)c->gbsums.as<uint64_t>(), c->dsync.as<uint8_t>(kSyncSmall), d_cs,
+                           nullptr);
+        HIP_OK(hipGetLastError());
+    }
+    iggy_decode_result *h_res = (iggy_decode_result *)c->h_pinned;
+    uint64_t *h_cs = (uint64_t *)((uint8_t *)c->h_pinned + 1536);
+    HIP_OK(hipMemcpyAsync(h_res, d_res, sizeof(*h_res), hipMemcpyDeviceToHost, c->stream));
+    if (compute) HIP_OK(hipMemcpyAsync(h_cs, d_cs, 8, hipMemcpyDeviceToHost, c->stream));
+    HIP_OK(hipStreamSynchronize(c->stream));
+    const iggy_decode_result res = *h_res;
+    if (res.error.kind == IGGY_ERR_TIMEOUT) reset_after_timeout(c);
+    if (res.error.kind != IGGY_OK) {
+        fill_err(err, res.error);
+        return server_error((int)res.error.kind, err);
+    }
+    iggy_batch_header h = res.header;
     if (h.message_count == 0 || h.message_count != metadata_messages_count || len != h.batch_length) {
         set_err(err, IGGY_ERR_INVALID_COMMAND);
         return IGGY_ERR_INVALID_COMMAND;
@@ -625,11 +763,7 @@ int iggy_codec_admit_batch(iggy_codec_ctx *c, const uint8_t *batch, uint64_t len
     }
     memcpy(out, batch, len);
     h.partition_id = partition_id;
-    h.batch_checksum = 0;
-    if (checksum_mode == IGGY_CHECKSUM_COMPUTE) {
-        r = iggy_codec_calculate_batch_checksum(c, &h, out + 256, len - 256, &h.batch_checksum);
-        if (r) return r;
-    }
+    h.batch_checksum = compute ? *h_cs : 0;
     uint8_t hb[256];
     iggy_batch_header_encode(&h, hb);
     memcpy(out, hb, 256);
@@ -646,7 +780,8 @@ int iggy_codec_admit_batch(iggy_codec_ctx *c, const uint8_t *batch, uint64_t len
 int iggy_codec_recover_segment(iggy_codec_ctx *c, const uint8_t *messages, uint64_t len,
                                uint64_t start_offset, iggy_segment_recovery *out) {
     if (!c || !out || (!messages && len)) return IGGY_ERR_INVALID_ARGUMENT;
-    HIP_OK(hipSetDevice(c->device));
+    DevGuard dg(c->device);
+    bind(c, nullptr);
     memset(out, 0, sizeof(*out));
     auto sat = [](uint64_t a, uint64_t b) { return a + b < a ? ~0ull : a + b; };
     struct Cand { uint64_t pos; iggy_batch_header h; };
@@ -712,7 +847,8 @@ int iggy_codec_recover_segment(iggy_codec_ctx *c, const uint8_t *messages, uint6
 
 int iggy_codec_xxh3_64(iggy_codec_ctx *c, const void *data, uint64_t len, uint64_t *out) {
     if (!c || !out || (!data && len)) return IGGY_ERR_INVALID_ARGUMENT;
-    HIP_OK(hipSetDevice(c->device));
+    DevGuard dg(c->device);
+    bind(c, nullptr);
     int r = c->din.ensure(len + 16);
     const uint64_t nb = len ? (len - 1) / 1024 + 1 : 1;
     r |= c->hbsums.ensure(nb * 64 + 64);
@@ -732,7 +868,7 @@ int iggy_codec_xxh3_64(iggy_codec_ctx *c, const void *data, uint64_t len, uint64
 
 // ---------------------------------------------------------------- encode
 static int enqueue_encode(iggy_codec_ctx *c, const iggy_raw_messages *dm, uint64_t partition_id,
-                          uint8_t *d_out, iggy_encode_result *d_res, hipStream_t s) {
+                          uint8_t *d_out, uint64_t cap, iggy_encode_result *d_res, hipStream_t s) {
     const uint64_t n = dm->count;
     const uint64_t ntiles = (n + kEncTile - 1) / kEncTile;
     int r = 0;
@@ -756,7 +892,7 @@ static int enqueue_encode(iggy_codec_ctx *c, const iggy_raw_messages *dm, uint64
     iggy_raw_messages m = *dm;
     prof_begin(c, 1, s);
     hipLaunchKernelGGL(k_enc_prep, dim3(ntiles), dim3(256), 0, s, m, es);
-    hipLaunchKernelGGL(k_enc_scan, dim3(1), dim3(256), 0, s, ntiles, n, partition_id, es);
+    hipLaunchKernelGGL(k_enc_scan, dim3(1), dim3(256), 0, s, ntiles, n, partition_id, cap, es);
     const uint64_t waves = std::min<uint64_t>(n, (uint64_t)c->ncu * 32);
     CsSource src{es.cs, nullptr, nullptr};
     // checksum blocks: 44 + 8n bytes; full blocks nb (the chain), then the last one
@@ -787,7 +923,7 @@ static int enqueue_encode(iggy_codec_ctx *c, const iggy_raw_messages *dm, uint64
             hipLaunchKernelGGL(k_enc_short, sgrid, dim3(256), 0, s, m, es, d_out);
         }
         // one resident round of lane-group waves (2 WGs of 256 per CU at 240 VGPRs)
-        const uint64_t lwg = std::min<uint64_t>((n + 31) / 32, (uint64_t)c->ncu * ((c->dbg & 2048) ? 8 : 2));
+        const uint64_t lwg = std::min<uint64_t>((n + 31) / 32, (uint64_t)c->ncu * ((diag_bits(c) & 2048) ? 8 : 2));
         uint64_t *state = c->emisc.as<uint64_t>(512);
         for (int k = 0; k < nseg; ++k) {
             // blocks [B_k, B_k+1) need frames up to 128 B_k+1 - 6: segment k encodes
@@ -796,7 +932,7 @@ static int enqueue_encode(iggy_codec_ctx *c, const iggy_raw_messages *dm, uint64
             static const uint32_t kSegPermille[kEncSegs + 1] = {0, 400, 750, 940, 1000};
             auto bound = [&](int q) {
                 if (nseg == 1) return q ? nb : (uint64_t)0;
-                if (c->dbg & 1024) return nb * q / nseg;  // diagnostics: even segments
+                if (diag_bits(c) & 1024) return nb * q / nseg;  // diagnostics: even segments
                 return nb * kSegPermille[q] / 1000;
             };
             const uint64_t B0 = bound(k), B1 = bound(k + 1);
@@ -815,7 +951,7 @@ static int enqueue_encode(iggy_codec_ctx *c, const iggy_raw_messages *dm, uint64
         }
         if (segmented) {
             // the last segment's blocks and the partial one, after every frame
-            const uint64_t Bl = (c->dbg & 1024) ? nb * (nseg - 1) / nseg : nb * 940 / 1000;  // last segment
+            const uint64_t Bl = (diag_bits(c) & 1024) ? nb * (nseg - 1) / nseg : nb * 940 / 1000;  // last segment
             HIP_OK(hipEventRecord(c->seg_ev[kEncSegs], c->side));
             HIP_OK(hipStreamWaitEvent(s, c->seg_ev[kEncSegs], 0));
             hipLaunchKernelGGL(k_bsum_blocks_range, dim3(c->ncu), dim3(256), 0, s, (const iggy_batch_header *)es.hdr,
@@ -839,7 +975,7 @@ static int enqueue_encode(iggy_codec_ctx *c, const iggy_raw_messages *dm, uint64
                            (const uint64_t *)&es.misc[3], src, (const uint64_t *)c->gbsums.as<uint64_t>(),
                            c->emisc.as<uint8_t>(320) /* 192 B of small */, dcs, nullptr);
     }
-    hipLaunchKernelGGL(k_enc_finish, dim3(1), dim3(64), 0, s, m, es, partition_id,
+    hipLaunchKernelGGL(k_enc_finish, dim3(1), dim3(64), 0, s, m, es, partition_id, cap,
                        (const uint64_t *)dcs, d_out, d_res);
     HIP_OK(hipGetLastError());
     return 0;
@@ -857,7 +993,8 @@ int iggy_codec_encode_batch(iggy_codec_ctx *c, const iggy_raw_messages *m, uint6
         set_err(err, IGGY_ERR_PAYLOAD_TOO_LARGE, 0, m->count, 0xFFFFFFFFull);
         return IGGY_ERR_PAYLOAD_TOO_LARGE;
     }
-    HIP_OK(hipSetDevice(c->device));
+    DevGuard dg(c->device);
+    bind(c, nullptr);
     const uint64_t n = m->count;
     uint64_t spl = 0, suh = 0;
     for (uint64_t i = 0; i < n; ++i) {
@@ -897,7 +1034,7 @@ int iggy_codec_encode_batch(iggy_codec_ctx *c, const iggy_raw_messages *m, uint6
     dm.user_headers = has_uh ? c->euhb.as<uint8_t>() : nullptr;
     dm.user_headers_lengths = has_uh ? c->euhl.as<uint32_t>() : nullptr;
     iggy_encode_result *d_res = c->dresult.as<iggy_encode_result>(512);
-    r = enqueue_encode(c, &dm, partition_id, c->dout.as<uint8_t>(), d_res, s);
+    r = enqueue_encode(c, &dm, partition_id, c->dout.as<uint8_t>(), need, d_res, s);
     if (r) return r;
     iggy_encode_result *h_res = (iggy_encode_result *)((uint8_t *)c->h_pinned + 512);
     HIP_OK(hipMemcpyAsync(h_res, d_res, sizeof(*h_res), hipMemcpyDeviceToHost, s));
@@ -916,8 +1053,10 @@ int iggy_codec_encode_batch_device(iggy_codec_ctx *c, const iggy_raw_messages *m
                                    iggy_encode_result *d_result, void *stream) {
     if (!c || !msgs || !d_out || !d_result || msgs->count == 0 || msgs->count > 0xFFFFFFFFull)
         return IGGY_ERR_INVALID_ARGUMENT;
-    (void)cap;
-    return enqueue_encode(c, msgs, partition_id, d_out, d_result, pick(c, stream));
+    DevGuard dg(c->device);
+    // cap is checked on the device against the scanned batch length: a batch that
+    // does not fit writes nothing and reports IGGY_ERR_CAPACITY in *d_result
+    return enqueue_encode(c, msgs, partition_id, d_out, cap, d_result, bind(c, stream));
 }
 
 // ------------------------------------------------------------- poll decode
@@ -925,31 +1064,19 @@ int iggy_codec_poll_decode(iggy_codec_ctx *c, const uint8_t *buf, uint64_t len, 
                            iggy_polled_message *out, uint64_t cap, uint64_t *n_out,
                            iggy_wire_error *err) {
     if (!c || (!buf && len)) return IGGY_ERR_INVALID_ARGUMENT;
-    HIP_OK(hipSetDevice(c->device));
+    DevGuard dg(c->device);
+    bind(c, nullptr);
     set_err(err, IGGY_OK);
-    uint64_t n = 0, position = 0;
     if (n_out) *n_out = 0;
-    int r = 0;
-    r |= c->din.ensure(len + 16);
-    r |= c->ppos.ensure((len / 48 + 2) * 8);
-    r |= c->pmsgs.ensure((len / 48 + 2) * sizeof(iggy_polled_message));
-    if (r) return IGGY_ERR_DEVICE;
-    if (len) HIP_OK(hipMemcpyAsync(c->din.p, buf, len, hipMemcpyHostToDevice, c->stream));
-    iggy_decode_result *d_res = c->dresult.as<iggy_decode_result>();
-    iggy_decode_result *h_res = (iggy_decode_result *)c->h_pinned;
-    // copy the messages decoded so far back to the caller (the iterator yields
-    // them before its error, poll_messages.rs:135-163)
-    auto flush = [&](uint64_t count) -> int {
-        if (count) {
-            HIP_OK(hipMemcpyAsync(out, c->pmsgs.p, count * sizeof(iggy_polled_message),
-                                  hipMemcpyDeviceToHost, c->stream));
-        }
-        HIP_OK(hipStreamSynchronize(c->stream));
-        if (n_out) *n_out = count;
-        return 0;
-    };
+    // 1. the record chain from the 256-B headers (polled_messages.rs:99-106,
+    //    poll_messages.rs:123-125); the header walk's own failure, if any, comes
+    //    after every record before it
+    struct Rec { uint64_t pos, bl, pbase; };
+    std::vector<Rec> recs;
+    int stop_rc = 0;
+    iggy_wire_error stop_err{};
+    uint64_t position = 0, pwords = 0;
     while (position < len) {
-        // record header: host-side (256 B), per polled_messages.rs:99-106 / poll_messages.rs:123-125
         iggy_batch_header h;
         iggy_wire_error he;
         const int hr = iggy_batch_header_decode(buf + position, len - position, &h, &he);
@@ -959,50 +1086,78 @@ int iggy_codec_poll_decode(iggy_codec_ctx *c, const uint8_t *buf, uint64_t len, 
                 return IGGY_ERR_INVALID_MESSAGE_PAYLOAD_LENGTH;
             }
         } else if (hr) {
-            fill_err(err, he);
-            if ((r = flush(n))) return r;
-            return hr;
+            stop_rc = hr;
+            stop_err = he;
+            break;
         }
-        // frame walk of this record on the device (layout only)
-        r = enqueue_decode(c, c->din.as<uint8_t>(position), len - position, IGGY_INTEGRITY_LAYOUT_ONLY,
-                           c->ppos.as<uint64_t>(), len / 48 + 1, d_res, c->stream);
+        const uint64_t avail = std::min<uint64_t>(h.batch_length, len - position);
+        recs.push_back({position, h.batch_length, pwords});
+        pwords += avail / 48 + 1;
+        if (h.batch_length > len - position) break;  // its decode reports the EOF
+        position += h.batch_length;
+    }
+    // 2. every record's frame walk (LayoutOnly), back to back on the device: one
+    //    copy of the body, one enqueue per record, one sync
+    const size_t K = recs.size();
+    int r = c->din.ensure(len + 16);
+    r |= c->ppos.ensure((pwords + 1) * 8);
+    r |= c->pres.ensure((K + 1) * sizeof(iggy_decode_result));
+    r |= c->pmsgs.ensure((len / 48 + 2) * sizeof(iggy_polled_message));
+    if (r) return IGGY_ERR_DEVICE;
+    if (len) HIP_OK(hipMemcpyAsync(c->din.p, buf, len, hipMemcpyHostToDevice, c->stream));
+    iggy_decode_result *d_res = c->pres.as<iggy_decode_result>();
+    for (size_t k = 0; k < K; ++k) {
+        r = enqueue_decode(c, c->din.as<uint8_t>(recs[k].pos), len - recs[k].pos, IGGY_INTEGRITY_LAYOUT_ONLY,
+                           c->ppos.as<uint64_t>(8 * recs[k].pbase), std::min<uint64_t>(recs[k].bl, len - recs[k].pos) / 48 + 1,
+                           d_res + k, c->stream);
         if (r) return r;
-        HIP_OK(hipMemcpyAsync(h_res, d_res, sizeof(*h_res), hipMemcpyDeviceToHost, c->stream));
-        HIP_OK(hipStreamSynchronize(c->stream));
-        const iggy_decode_result res = *h_res;
-        if (res.error.kind == IGGY_ERR_TIMEOUT) {
+    }
+    std::vector<iggy_decode_result> res(K);
+    if (K) HIP_OK(hipMemcpyAsync(res.data(), d_res, K * sizeof(iggy_decode_result), hipMemcpyDeviceToHost, c->stream));
+    HIP_OK(hipStreamSynchronize(c->stream));
+    // 3. verdicts in record order; messages expanded on the device, one more sync
+    uint64_t n = 0;
+    int rc = 0;
+    for (size_t k = 0; k < K && !rc; ++k) {
+        const iggy_decode_result &rs = res[k];
+        if (rs.error.kind == IGGY_ERR_TIMEOUT) {
             reset_after_timeout(c);
-            fill_err(err, res.error);
+            fill_err(err, rs.error);
             return IGGY_ERR_TIMEOUT;
         }
-        const uint64_t bl = h.batch_length - 256;
-        const uint64_t nf = res.frame_count;
         if (mode == IGGY_POLL_MODE_SDK) {
             // the SDK walk only needs the frames to tile the record (no count check)
-            if (res.covered != bl) {
+            if (rs.covered != recs[k].bl - 256) {
                 set_err(err, IGGY_ERR_INVALID_MESSAGE_PAYLOAD_LENGTH);
                 return IGGY_ERR_INVALID_MESSAGE_PAYLOAD_LENGTH;
             }
-        } else if (res.error.kind != IGGY_OK) {
-            fill_err(err, res.error);
-            if ((r = flush(n))) return r;
-            return (int)res.error.kind;
+        } else if (rs.error.kind != IGGY_OK) {  // yielded after the messages before it
+            fill_err(err, rs.error);
+            rc = (int)rs.error.kind;
+            break;
         }
+        const uint64_t nf = rs.frame_count;
         if (n + nf > cap) {
             set_err(err, IGGY_ERR_CAPACITY, 0, n + nf, cap);
-            if (n_out) *n_out = n;
-            return IGGY_ERR_CAPACITY;
+            rc = IGGY_ERR_CAPACITY;
+            break;
         }
         if (nf) {
             hipLaunchKernelGGL(k_poll_fill, dim3((uint32_t)std::min<uint64_t>((nf + 255) / 256, 65535)), dim3(256), 0,
-                               c->stream, c->din.as<uint8_t>(), position, c->ppos.as<uint64_t>(), nf,
-                               c->pmsgs.as<iggy_polled_message>(n * sizeof(iggy_polled_message)));
+                               c->stream, c->din.as<uint8_t>(), recs[k].pos, c->ppos.as<uint64_t>(8 * recs[k].pbase),
+                               nf, c->pmsgs.as<iggy_polled_message>(n * sizeof(iggy_polled_message)));
             HIP_OK(hipGetLastError());
         }
         n += nf;
-        position += h.batch_length;
     }
-    return flush(n);
+    if (!rc && stop_rc) {
+        fill_err(err, stop_err);
+        rc = stop_rc;
+    }
+    if (n) HIP_OK(hipMemcpyAsync(out, c->pmsgs.p, n * sizeof(iggy_polled_message), hipMemcpyDeviceToHost, c->stream));
+    HIP_OK(hipStreamSynchronize(c->stream));
+    if (n_out) *n_out = n;
+    return rc;
 }
 
 // ------------------------------------------------------------ device APIs
@@ -1010,20 +1165,20 @@ int iggy_codec_decode_batch_device(iggy_codec_ctx *c, const uint8_t *d_body, uin
                                    int integrity, uint64_t *d_frame_pos, uint64_t cap,
                                    iggy_decode_result *d_result, void *stream) {
     if (!c || !d_result || (!d_body && len)) return IGGY_ERR_INVALID_ARGUMENT;
+    DevGuard dg(c->device);
     return enqueue_decode(c, d_body, len, integrity, d_frame_pos, d_frame_pos ? cap : 0, d_result,
-                          pick(c, stream));
+                          bind(c, stream));
 }
 
 int iggy_codec_batch_checksum_device(iggy_codec_ctx *c, const iggy_batch_header *hdr,
                                      const uint8_t *d_blob, const uint64_t *d_frame_pos,
                                      uint64_t nframes, uint64_t *d_out, void *stream) {
-    if (!c || !hdr || !d_out) return IGGY_ERR_INVALID_ARGUMENT;
-    hipStream_t s = pick(c, stream);
+    if (!c || !hdr || !d_out || (nframes && (!d_blob || !d_frame_pos))) return IGGY_ERR_INVALID_ARGUMENT;
+    DevGuard dg(c->device);
+    hipStream_t s = bind(c, stream);
     int r = c->gbsums.ensure(((44 + 8 * nframes) / 1024 + 2) * 64);
     if (r) return r;
-    uint64_t *dn = c->dresult.as<uint64_t>(3096);
-    HIP_OK(hipMemcpyAsync(dn, &nframes, 8, hipMemcpyHostToDevice, s));
-    return checksum_of_walk(c, hdr, d_blob, d_frame_pos, dn, d_out, s);
+    return checksum_of_walk(c, hdr, nframes, d_blob, d_frame_pos, d_out, s);
 }
 
 int iggy_codec_xxh3_64_ranges_device(iggy_codec_ctx *c, const uint8_t *d_data, const uint64_t *d_offsets,
@@ -1031,8 +1186,9 @@ int iggy_codec_xxh3_64_ranges_device(iggy_codec_ctx *c, const uint8_t *d_data, c
                                      void *stream) {
     if (!c || !d_out || (n && (!d_data || !d_offsets || !d_lengths))) return IGGY_ERR_INVALID_ARGUMENT;
     if (!n) return 0;
+    DevGuard dg(c->device);
     const uint64_t blocks = std::min<uint64_t>((n + 255) / 256, (uint64_t)c->ncu * 16);
-    hipLaunchKernelGGL(k_xxh3_ranges, dim3((uint32_t)blocks), dim3(256), 0, pick(c, stream), d_data,
+    hipLaunchKernelGGL(k_xxh3_ranges, dim3((uint32_t)blocks), dim3(256), 0, bind(c, stream), d_data,
                        d_offsets, d_lengths, n, d_out);
     HIP_OK(hipGetLastError());
     return 0;
@@ -1044,7 +1200,8 @@ int iggy_codec_select_slice_device(iggy_codec_ctx *c, const uint8_t *d_record, c
                                    uint8_t *d_header_out, void *stream) {
     if (!c || !d_record || !q || !d_out || (nframes && !d_frame_pos)) return IGGY_ERR_INVALID_ARGUMENT;
     if (q->kind != IGGY_LOOKUP_OFFSET && q->kind != IGGY_LOOKUP_TIMESTAMP) return IGGY_ERR_INVALID_ARGUMENT;
-    hipStream_t s = pick(c, stream);
+    DevGuard dg(c->device);
+    hipStream_t s = bind(c, stream);
     const uint64_t ntiles = (nframes + kSliceTile - 1) / kSliceTile;
     int r = c->sl.ensure(512 + ntiles * 4);
     r |= c->gbsums.ensure(((44 + 8 * nframes) / 1024 + 2) * 64);
@@ -1081,7 +1238,8 @@ int iggy_codec_select_slice_device(iggy_codec_ctx *c, const uint8_t *d_record, c
 int iggy_codec_select_slice(iggy_codec_ctx *c, const uint8_t *record, uint64_t len, const iggy_slice_query *q,
                             iggy_slice_result *out, uint8_t *header_out, iggy_wire_error *err) {
     if (!c || !q || !out || (!record && len)) return IGGY_ERR_INVALID_ARGUMENT;
-    HIP_OK(hipSetDevice(c->device));
+    DevGuard dg(c->device);
+    bind(c, nullptr);
     set_err(err, IGGY_OK);
     const uint64_t cap = len / kFrameHdr + 1;
     int r = c->din.ensure(len + 16);
@@ -1120,7 +1278,8 @@ int iggy_codec_stamp_batch_device(iggy_codec_ctx *c, uint8_t *d_record, const ui
                                   uint64_t nframes, uint64_t base_offset, uint64_t base_timestamp,
                                   iggy_batch_header *d_header, void *stream) {
     if (!c || !d_record || (nframes && !d_frame_pos)) return IGGY_ERR_INVALID_ARGUMENT;
-    hipStream_t s = pick(c, stream);
+    DevGuard dg(c->device);
+    hipStream_t s = bind(c, stream);
     int r = c->sl.ensure(512 + 4);
     r |= c->gbsums.ensure(((44 + 8 * nframes) / 1024 + 2) * 64);
     if (r) return IGGY_ERR_DEVICE;
@@ -1137,6 +1296,212 @@ int iggy_codec_stamp_batch_device(iggy_codec_ctx *c, uint8_t *d_record, const ui
                        (const uint64_t *)dcs, d_header);
     HIP_OK(hipGetLastError());
     return 0;
+}
+
+// ------------------------------------------------ asynchronous host buffers
+// Shard threads have no blocking pool (server_common/src/executor.rs:80-88): a
+// host-buffer decode/encode is submitted (async H2D into a device slot on the copy-in
+// stream, the kernels on the context's stream, results and outputs back on the
+// copy-out stream) and its ticket polled from the reactor. Kernels only ever read
+// device memory; a caller buffer registered with iggy_codec_host_register is copied
+// at link speed without a bounce.
+namespace {
+int async_init(iggy_codec_ctx *c) {
+    if (c->h2d) return 0;
+    if (hipStreamCreateWithFlags(&c->h2d, hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithFlags(&c->d2h, hipStreamNonBlocking) != hipSuccess ||
+        hipHostMalloc(&c->slot_pinned, kSlots * 256, hipHostMallocDefault) != hipSuccess)
+        return IGGY_ERR_DEVICE;
+    for (Slot &sl : c->slots)
+        if (hipEventCreateWithFlags(&sl.ev_in, hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&sl.ev_k, hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&sl.ev_done, hipEventDisableTiming) != hipSuccess)
+            return IGGY_ERR_DEVICE;
+    return 0;
+}
+int take_slot(iggy_codec_ctx *c, uint32_t op, int *idx) {
+    int r = async_init(c);
+    if (r) return r;
+    for (int k = 0; k < kSlots; ++k)
+        if (!c->slots[k].busy) {
+            Slot &sl = c->slots[k];
+            sl.busy = true;
+            sl.op = op;
+            sl.ticket = (++c->seq << 4) | (uint64_t)k;
+            *idx = k;
+            return 0;
+        }
+    return IGGY_ERR_BUSY;
+}
+}  // namespace
+
+int iggy_codec_host_register(iggy_codec_ctx *c, void *ptr, uint64_t len) {
+    if (!c || !ptr || !len) return IGGY_ERR_INVALID_ARGUMENT;
+    DevGuard dg(c->device);
+    HIP_OK(hipHostRegister(ptr, len, hipHostRegisterDefault));
+    return 0;
+}
+
+int iggy_codec_host_unregister(iggy_codec_ctx *c, void *ptr) {
+    if (!c || !ptr) return IGGY_ERR_INVALID_ARGUMENT;
+    DevGuard dg(c->device);
+    HIP_OK(hipHostUnregister(ptr));
+    return 0;
+}
+
+int iggy_codec_decode_submit(iggy_codec_ctx *c, const uint8_t *body, uint64_t len, int integrity,
+                             uint64_t *frame_pos, uint64_t cap, iggy_ticket *ticket) {
+    if (!c || !ticket || (!body && len)) return IGGY_ERR_INVALID_ARGUMENT;
+    DevGuard dg(c->device);
+    int k = 0;
+    int r = take_slot(c, IGGY_OP_DECODE, &k);
+    if (r) return r;
+    Slot &sl = c->slots[k];
+    const uint64_t pcap = frame_pos ? std::min<uint64_t>(cap, len / 48 + 1) : 0;
+    r = sl.in.ensure(len + 16);
+    r |= sl.pos.ensure((pcap + 1) * 8);
+    r |= sl.res.ensure(256);
+    if (!r) r = ensure_decode_scratch(c, len);
+    if (r) {
+        sl.busy = false;
+        return IGGY_ERR_DEVICE;
+    }
+    sl.cap = cap;
+    sl.frame_pos = frame_pos;
+    if (len) HIP_OK(hipMemcpyAsync(sl.in.p, body, len, hipMemcpyHostToDevice, c->h2d));
+    HIP_OK(hipEventRecord(sl.ev_in, c->h2d));
+    hipStream_t s = bind(c, nullptr);
+    HIP_OK(hipStreamWaitEvent(s, sl.ev_in, 0));
+    iggy_decode_result *d_res = sl.res.as<iggy_decode_result>();
+    r = enqueue_decode(c, sl.in.as<uint8_t>(), len, integrity, pcap ? sl.pos.as<uint64_t>() : nullptr, pcap, d_res, s);
+    if (r) {
+        sl.busy = false;
+        return r;
+    }
+    HIP_OK(hipEventRecord(sl.ev_k, s));
+    HIP_OK(hipStreamWaitEvent(c->d2h, sl.ev_k, 0));
+    HIP_OK(hipMemcpyAsync((uint8_t *)c->slot_pinned + 256 * k, d_res, sizeof(iggy_decode_result),
+                          hipMemcpyDeviceToHost, c->d2h));
+    if (pcap) HIP_OK(hipMemcpyAsync(frame_pos, sl.pos.p, pcap * 8, hipMemcpyDeviceToHost, c->d2h));
+    HIP_OK(hipEventRecord(sl.ev_done, c->d2h));
+    *ticket = sl.ticket;
+    return 0;
+}
+
+int iggy_codec_encode_submit(iggy_codec_ctx *c, const iggy_raw_messages *m, uint64_t partition_id, uint8_t *out,
+                             uint64_t cap, iggy_ticket *ticket) {
+    if (!c || !m || !ticket) return IGGY_ERR_INVALID_ARGUMENT;
+    if (m->count == 0 || m->count > 0xFFFFFFFFull || !out) return IGGY_ERR_INVALID_ARGUMENT;
+    DevGuard dg(c->device);
+    const uint64_t n = m->count;
+    uint64_t spl = 0, suh = 0;
+    for (uint64_t i = 0; i < n; ++i) {
+        spl += m->payload_lengths[i];
+        suh += m->user_headers_lengths ? m->user_headers_lengths[i] : 0;
+    }
+    const uint64_t need = 256 + 48 * n + spl + suh;
+    int k = 0;
+    int r = take_slot(c, IGGY_OP_ENCODE, &k);
+    if (r) return r;
+    Slot &sl = c->slots[k];
+    const bool has_uh = m->user_headers_lengths != nullptr;
+    r = sl.ids.ensure(n * 16);
+    r |= sl.ots.ensure(n * 8);
+    r |= sl.pay.ensure(spl + 16);
+    r |= sl.plen.ensure(n * 4);
+    r |= sl.uhb.ensure(suh + 16);
+    r |= sl.uhl.ensure(n * 4);
+    r |= sl.out.ensure(need + 16);
+    r |= sl.res.ensure(256);
+    if (r) {
+        sl.busy = false;
+        return IGGY_ERR_DEVICE;
+    }
+    sl.cap = cap;
+    sl.out_len = need;
+    sl.frame_pos = nullptr;
+    hipStream_t h = c->h2d;
+    HIP_OK(hipMemcpyAsync(sl.ids.p, m->ids, n * 16, hipMemcpyHostToDevice, h));
+    HIP_OK(hipMemcpyAsync(sl.ots.p, m->origin_timestamps, n * 8, hipMemcpyHostToDevice, h));
+    if (spl) HIP_OK(hipMemcpyAsync(sl.pay.p, m->payloads, spl, hipMemcpyHostToDevice, h));
+    HIP_OK(hipMemcpyAsync(sl.plen.p, m->payload_lengths, n * 4, hipMemcpyHostToDevice, h));
+    if (has_uh) {
+        if (suh) HIP_OK(hipMemcpyAsync(sl.uhb.p, m->user_headers, suh, hipMemcpyHostToDevice, h));
+        HIP_OK(hipMemcpyAsync(sl.uhl.p, m->user_headers_lengths, n * 4, hipMemcpyHostToDevice, h));
+    }
+    HIP_OK(hipEventRecord(sl.ev_in, h));
+    hipStream_t s = bind(c, nullptr);
+    HIP_OK(hipStreamWaitEvent(s, sl.ev_in, 0));
+    iggy_raw_messages dm;
+    dm.count = n;
+    dm.ids = sl.ids.as<uint64_t>();
+    dm.origin_timestamps = sl.ots.as<uint64_t>();
+    dm.payloads = sl.pay.as<uint8_t>();
+    dm.payload_lengths = sl.plen.as<uint32_t>();
+    dm.user_headers = has_uh ? sl.uhb.as<uint8_t>() : nullptr;
+    dm.user_headers_lengths = has_uh ? sl.uhl.as<uint32_t>() : nullptr;
+    iggy_encode_result *d_res = sl.res.as<iggy_encode_result>();
+    // a batch that does not fit `cap` is reported by the device (nothing is written)
+    r = enqueue_encode(c, &dm, partition_id, sl.out.as<uint8_t>(), cap, d_res, s);
+    if (r) {
+        sl.busy = false;
+        return r;
+    }
+    HIP_OK(hipEventRecord(sl.ev_k, s));
+    HIP_OK(hipStreamWaitEvent(c->d2h, sl.ev_k, 0));
+    HIP_OK(hipMemcpyAsync((uint8_t *)c->slot_pinned + 256 * k, d_res, sizeof(iggy_encode_result),
+                          hipMemcpyDeviceToHost, c->d2h));
+    if (cap >= need) HIP_OK(hipMemcpyAsync(out, sl.out.p, need, hipMemcpyDeviceToHost, c->d2h));
+    HIP_OK(hipEventRecord(sl.ev_done, c->d2h));
+    *ticket = sl.ticket;
+    return 0;
+}
+
+int iggy_codec_poll(iggy_codec_ctx *c, iggy_ticket ticket, iggy_completion *out) {
+    if (!c || !out) return IGGY_ERR_INVALID_ARGUMENT;
+    Slot &sl = c->slots[ticket & (kSlots - 1)];
+    if (!sl.busy || sl.ticket != ticket) return IGGY_ERR_INVALID_ARGUMENT;
+    DevGuard dg(c->device);
+    const hipError_t q = hipEventQuery(sl.ev_done);
+    if (q == hipErrorNotReady) {
+        (void)hipGetLastError();  // not an error: leave no sticky status for the caller's HIP code
+        return IGGY_ERR_PENDING;
+    }
+    sl.busy = false;
+    if (q != hipSuccess) return IGGY_ERR_DEVICE;
+    memset(out, 0, sizeof(*out));
+    out->op = sl.op;
+    const uint8_t *rec = (const uint8_t *)c->slot_pinned + 256 * (ticket & (kSlots - 1));
+    if (sl.op == IGGY_OP_DECODE) {
+        iggy_decode_result res;
+        memcpy(&res, rec, sizeof(res));
+        if (res.error.kind == IGGY_ERR_TIMEOUT) reset_after_timeout(c);
+        out->header = res.header;
+        out->error = res.error;
+        out->frame_count = res.frame_count;
+        out->computed_checksum = res.computed_checksum;
+        if (res.error.kind == IGGY_OK && sl.frame_pos && res.frame_count > sl.cap) {
+            out->error = iggy_wire_error{IGGY_ERR_CAPACITY, 0, res.frame_count, sl.cap, 0};
+        }
+    } else {
+        iggy_encode_result res;
+        memcpy(&res, rec, sizeof(res));
+        out->header = res.header;
+        out->error = res.error;
+        out->bytes = res.error.kind == IGGY_OK ? res.batch_length : 0;
+    }
+    return 0;
+}
+
+int iggy_codec_wait(iggy_codec_ctx *c, iggy_ticket ticket, iggy_completion *out) {
+    if (!c || !out) return IGGY_ERR_INVALID_ARGUMENT;
+    Slot &sl = c->slots[ticket & (kSlots - 1)];
+    if (!sl.busy || sl.ticket != ticket) return IGGY_ERR_INVALID_ARGUMENT;
+    {
+        DevGuard dg(c->device);
+        HIP_OK(hipEventSynchronize(sl.ev_done));
+    }
+    return iggy_codec_poll(c, ticket, out);
 }
 
 // -------------------------------------------------------------- profiling
@@ -1177,6 +1542,13 @@ int iggy_codec_debug_read(iggy_codec_ctx *c, void *out, uint64_t bytes) {
     HIP_OK(hipDeviceSynchronize());
     HIP_OK(hipMemcpy(out, c->dsync.as<uint8_t>(kSyncSmall), std::min<uint64_t>(bytes, kSyncBytes - kSyncSmall),
                      hipMemcpyDeviceToHost));
+    return 0;
+}
+// Diagnostics only: set the ablation bits of a context (no effect in the product
+// build, where kDiagMask is zero).
+int iggy_codec_debug_set(iggy_codec_ctx *c, uint32_t bits) {
+    if (!c) return IGGY_ERR_INVALID_ARGUMENT;
+    c->dbg = bits;
     return 0;
 }
 int iggy_codec_debug_clear(iggy_codec_ctx *c) {

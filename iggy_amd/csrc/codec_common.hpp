@@ -21,6 +21,16 @@ constexpr uint32_t kHdr = 256;
 constexpr uint32_t kFrameHdr = 48;
 constexpr uint64_t kNone = 0;  // "no index" in the max-encoded slots below
 
+// Ablation / diagnostic bits (loads only, no chain, forced kernel forms, progress
+// stamps) exist only in the separate diagnostic build (`make diag` ->
+// libiggy_codec_diag.so, -DIGGY_CODEC_DIAG). In the product library the mask is
+// zero, so every such branch is compiled out and nothing can switch verification off.
+#ifdef IGGY_CODEC_DIAG
+constexpr uint32_t kDiagMask = 0xFFFFFFFFu;
+#else
+constexpr uint32_t kDiagMask = 0u;
+#endif
+
 // Device-side status values in iggy_decode_result::status
 constexpr uint32_t kStatusDone = 0;
 constexpr uint32_t kStatusNeedGeneral = 1;

@@ -2,8 +2,8 @@
 // for records with arbitrary frame sizes: the exact serial walk of
 // BatchIteratorWithOffsets (batch.rs:329-355) rebuilt in parallel.
 //
-// One persistent launch (grid = every co-resident WG, bounded grid barriers)
-// that returns immediately unless the uniform-stride kernel left
+// One persistent launch (bounded grid barriers over the workgroups that joined:
+// join_members) that returns immediately unless the uniform-stride kernel left
 // result->status == kStatusNeedGeneral. The blob is cut into tiles of
 // T = 2^sh bytes, sized from the header's message count to hold 8-16 frames
 // (4 KiB <= T <= 1 MiB); a group is 256 tiles, 4 per lane of one wave. Phases:
@@ -64,7 +64,10 @@ struct GeneralScratch {
     uint64_t *flen;      // [max_frames] hashed lengths (frame size - 8) in walk order
     uint64_t *bsums;     // [max_blocks * 8]
     uint64_t *misc;      // [16]: 0 nwalk, 1 end (with stop bit), 2 first_bad enc
-    uint32_t *bar;       // [4]: arrive counter, exit counter
+    uint32_t *bar;       // [4]: 0 barrier arrivals, 2 registration (count | kRegClosed), 3 members
+                         // (all re-armed by k_decode_uniform, which always runs first on the stream)
+    uint32_t *u_exited;  // the uniform kernel's sync words, re-armed here for the next decode
+    uint64_t *u_first_bad, *u_spec_fail;
     uint8_t *small;      // >= 512 B
     uint64_t ntiles, max_frames, max_blocks;  // ntiles: capacity in kTileMin tiles
 };
@@ -100,10 +103,47 @@ __device__ bool grid_barrier(uint32_t *bar, uint32_t target, uint64_t t0) {
     return ok;
 }
 
-// phase clock (diagnostics): WG 0 stamps the ticks since entry after every
+// phase clock (diagnostics): member 0 stamps the ticks since entry after every
 // barrier at small+512 (u64 [1..6]); [8..] are counters of the link phase
-__device__ __forceinline__ void gstamp(const GeneralScratch &gs, int idx, uint64_t v) {
-    if (blockIdx.x == 0 && threadIdx.x == 0) ((uint64_t *)(gs.small + 512))[idx] = v;
+__device__ __forceinline__ void gstamp(const GeneralScratch &gs, uint32_t member, int idx, uint64_t v) {
+    if (member == 0 && threadIdx.x == 0) ((uint64_t *)(gs.small + 512))[idx] = v;
+}
+
+// Membership: the grid barriers below may only count workgroups that are running.
+// Every WG registers with one atomic add; the first to register (member 0) waits a
+// bounded time for the rest of the grid, then closes registration with an atomic
+// or. WGs that register after the close (still queued behind other work on a
+// shared GPU: another context's decode, another process) exit at once, and the
+// members split the work. So the barriers never wait for a workgroup that is not
+// resident, whatever else holds the chip, and no cooperative launch is needed.
+constexpr uint32_t kRegClosed = 1u << 31;
+constexpr uint32_t kNotMember = ~0u;
+constexpr uint64_t kJoinTicks = 2000;  // 20 us at 100 MHz: the whole grid normally joins in < 2 us
+__device__ inline void join_members(const GeneralScratch &gs, uint64_t t0, uint32_t *s_mem) {
+    if (threadIdx.x == 0) {
+        uint32_t me = kNotMember, nm = 0;
+        const uint32_t t = __hip_atomic_fetch_add(&gs.bar[2], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (!(t & kRegClosed)) {
+            if (t == 0) {
+                while ((__hip_atomic_load(&gs.bar[2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & ~kRegClosed) <
+                           gridDim.x &&
+                       rt_now() - t0 < kJoinTicks)
+                    __builtin_amdgcn_s_sleep(1);
+                const uint32_t old =
+                    __hip_atomic_fetch_or(&gs.bar[2], kRegClosed, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                nm = old & ~kRegClosed;
+                __hip_atomic_store(&gs.bar[3], nm, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            } else {
+                while ((nm = __hip_atomic_load(&gs.bar[3], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) == 0 &&
+                       rt_now() - t0 < kSpinLimitTicks)
+                    __builtin_amdgcn_s_sleep(1);
+            }
+            if (nm) me = t;
+        }
+        s_mem[0] = me;
+        s_mem[1] = nm;
+    }
+    __syncthreads();
 }
 
 // tile size: 8-16 frames of the header's average size, a power of two in range
@@ -420,10 +460,22 @@ __global__ __launch_bounds__(kGenThreads) void k_decode_general(const uint8_t *_
                                                         uint64_t len, uint64_t *frame_pos,
                                                         uint64_t cap, iggy_decode_result *result,
                                                         GeneralScratch gs) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        // the uniform kernel of this decode has completed (stream order): re-arm its
+        // sync words for the next decode, whether or not it finished cleanly
+        __hip_atomic_store(gs.u_exited, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(gs.u_first_bad, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(gs.u_spec_fail, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
     if (__hip_atomic_load(&result->status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) !=
         kStatusNeedGeneral)
         return;
     const uint64_t t0 = rt_now();
+    __shared__ uint32_t s_mem[2];
+    join_members(gs, t0, s_mem);
+    const uint32_t member = s_mem[0];
+    if (member == kNotMember) return;  // registered after the close: the members do the work
+    const uint32_t nwg = s_mem[1];     // members (all resident)
     const iggy_batch_header h = result->header;
     const uint8_t *blob = body + kHdr;
     const uint64_t bl = h.batch_length - kHdr;
@@ -432,8 +484,7 @@ __global__ __launch_bounds__(kGenThreads) void k_decode_general(const uint8_t *_
     const uint64_t ntiles = (bl + T - 1) >> sh;
     const uint64_t ngroups = (ntiles + kGrpTiles - 1) / kGrpTiles;
     const uint64_t lcap = tile_list_cap(sh);
-    const uint32_t nwg = gridDim.x;
-    const uint64_t gtid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint64_t gtid = (uint64_t)member * blockDim.x + threadIdx.x;
     const uint64_t gthreads = (uint64_t)nwg * blockDim.x;
     const int lane = threadIdx.x & 63;
     const uint32_t wave = threadIdx.x >> 6;
@@ -458,7 +509,7 @@ __global__ __launch_bounds__(kGenThreads) void k_decode_general(const uint8_t *_
         gs.tile_x[t] = x;
     }
     ok &= grid_barrier(gs.bar, nwg * ++phase, t0);
-    gstamp(gs, 1, rt_now() - t0);
+    gstamp(gs, member, 1, rt_now() - t0);
 
     // ---------------- B1: group summaries (one wave per 256 tiles, 4 per lane)
     for (uint64_t g = wid; g < ngroups; g += nwaves) {
@@ -531,10 +582,10 @@ __global__ __launch_bounds__(kGenThreads) void k_decode_general(const uint8_t *_
         }
     }
     ok &= grid_barrier(gs.bar, nwg * ++phase, t0);
-    gstamp(gs, 2, rt_now() - t0);
+    gstamp(gs, member, 2, rt_now() - t0);
 
     // ---------------- B2: link (one wave)
-    if (blockIdx.x == 0 && wave == 0) {
+    if (member == 0 && wave == 0) {
         uint64_t e = 0;      // true entry into the next group
         uint64_t total = 0;  // frames accepted so far
         bool ended = false;  // the walk stopped (stop bit) or reached the blob end
@@ -771,7 +822,7 @@ __global__ __launch_bounds__(kGenThreads) void k_decode_general(const uint8_t *_
         }
     }
     ok &= grid_barrier(gs.bar, nwg * ++phase, t0);
-    gstamp(gs, 3, rt_now() - t0);
+    gstamp(gs, member, 3, rt_now() - t0);
 
     const uint64_t nwalk = __hip_atomic_load(&gs.misc[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     // ---------------- C: scatter the accepted tiles' lists (walk order). Sixteen lanes per
@@ -812,7 +863,7 @@ __global__ __launch_bounds__(kGenThreads) void k_decode_general(const uint8_t *_
         }
     }
     ok &= grid_barrier(gs.bar, nwg * ++phase, t0);
-    gstamp(gs, 4, rt_now() - t0);
+    gstamp(gs, member, 4, rt_now() - t0);
 
     // ---------------- E: checksum-input block sums (one wave per block)
     const uint64_t n = 44 + 8 * nwalk;
@@ -850,11 +901,11 @@ __global__ __launch_bounds__(kGenThreads) void k_decode_general(const uint8_t *_
         }
     }
     ok &= grid_barrier(gs.bar, nwg * ++phase, t0);
-    gstamp(gs, 5, rt_now() - t0);
+    gstamp(gs, member, 5, rt_now() - t0);
 
     // ---------------- D + F: chain (wave 0 of WG 0) beside frame verification
     uint64_t computed = 0;
-    if (blockIdx.x == 0 && wave == 0) {
+    if (member == 0 && wave == 0) {
         if (long_cs) {
             const int j = lane & 7;
             uint64_t acc = chain_blocks(gs.bsums, nb, lane);
@@ -883,15 +934,15 @@ __global__ __launch_bounds__(kGenThreads) void k_decode_general(const uint8_t *_
             computed = xxh3_64_lane(s, n);
         }
     } else if (VERIFY) {
-        const uint32_t vw = blockIdx.x * (blockDim.x >> 6) + wave - 1;
+        const uint32_t vw = member * (blockDim.x >> 6) + wave - 1;
         const uint32_t nvw = nwg * (blockDim.x >> 6) - 1;
         verify_frames(blob, gs, nwalk, vw, nvw, lane);
     }
     ok &= grid_barrier(gs.bar, nwg * ++phase, t0);
-    gstamp(gs, 6, rt_now() - t0);
+    gstamp(gs, member, 6, rt_now() - t0);
 
     // ---------------- resolution (wave 0 of WG 0)
-    if (blockIdx.x == 0 && wave == 0 && lane == 0) {
+    if (member == 0 && wave == 0 && lane == 0) {
         HeaderInfo hi;
         hi.h = h;
         const uint64_t end = __hip_atomic_load(&gs.misc[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -916,16 +967,7 @@ __global__ __launch_bounds__(kGenThreads) void k_decode_general(const uint8_t *_
         }
         write_result(result, hi, kind, reason, a, b, c, nwalk, computed, 2, kStatusDone, end & ~kStopBit);
     }
-    // retire: the last WG out re-arms the barrier words and misc for the next call
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        const uint32_t prev = __hip_atomic_fetch_add(&gs.bar[1], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-        if (prev == nwg - 1) {
-            __hip_atomic_store(&gs.bar[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(&gs.bar[1], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(&gs.misc[2], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-    }
+    // barrier, registration and misc[2] are re-armed by the next decode's uniform kernel
     (void)len;
 }
 

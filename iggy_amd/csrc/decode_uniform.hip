@@ -44,6 +44,8 @@ struct DecodeScratch {
                           // (half | epoch << 32); see publish_unit_sums
     uint64_t *errslot;    // [max_chunks*4][2] (stored, computed) per wave
     uint8_t *small;       // >= 512 B: short batch-checksum inputs
+    uint32_t *gbar;       // the general kernel's barrier / registration words and its
+    uint64_t *gmisc;      // first-bad slot: re-armed here (see k_decode_general)
     uint64_t max_chunks;
 };
 
@@ -1002,6 +1004,10 @@ __device__ __forceinline__ void consumer(const uint8_t *body, const HeaderInfo &
     }
 
     const uint64_t t_start = rt_now();
+    if (dbg & 4096) {  // diagnostics: give up at once, as a timed-out wait does (producers run on)
+        if (wave == 0 && lane == 0) write_result(result, hi, IGGY_ERR_TIMEOUT, 0, 0, 0, 0, 0, 0, 1, kStatusDone, 0);
+        return;
+    }
     if (wave == 0 && lane == 0) dbg_stamp(sc, dbg, 0);
     bool timed_out = false;
     uint64_t computed = 0;
@@ -1145,7 +1151,7 @@ __device__ __forceinline__ void consumer(const uint8_t *body, const HeaderInfo &
     dbg_stamp(sc, dbg, 21);
     if (timed_out) {
         write_result(result, hi, IGGY_ERR_TIMEOUT, 0, 0, 0, 0, 0, 0, 1, kStatusDone, 0);
-        return;  // scratch left dirty on purpose: the host re-initialises it
+        return;  // the sync words are re-armed by this decode's general kernel (k_decode_general)
     }
     uint64_t fb_enc = __hip_atomic_load(sc.first_bad, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (tail_bad && fb_enc == 0) fb_enc = ~(pl.N - 1);  // producers only report smaller indices
@@ -1211,8 +1217,17 @@ __global__ __launch_bounds__(256, 1) void k_decode_uniform(const uint8_t *__rest
                                                            uint32_t epoch, uint32_t allow_unaligned,
                                                            uint32_t dbg) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    dbg &= kDiagMask;  // product build: no ablation bit survives
     const int lane = threadIdx.x & 63;
     const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        // the previous decode's general kernel has completed (stream order): re-arm its
+        // barrier, registration and first-bad words for this decode's general kernel
+        __hip_atomic_store(&sc.gbar[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&sc.gbar[2], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&sc.gbar[3], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&sc.gmisc[2], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
     HeaderInfo hi;
     parse_header(body, len, hi);
     UPlan pl;

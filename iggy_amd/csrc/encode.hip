@@ -28,7 +28,8 @@ struct EncScratch {
     uint64_t *tile_uh;    // [ntiles]
     uint64_t *tile_min;   // [ntiles] minimum origin timestamp
     uint64_t *cs;         // [n] frame checksums
-    uint64_t *misc;       // [8]: 0 min origin, 1 blob bytes, 2 ts-error (~index, max), 3 n, 4 payload bytes
+    uint64_t *misc;       // [8]: 0 min origin, 1 blob bytes, 2 ts-error (~index, max), 3 n, 4 payload bytes,
+                          //      5 batch does not fit the output capacity (nothing is written)
     iggy_batch_header *hdr;  // header being built
 };
 
@@ -84,7 +85,7 @@ __global__ __launch_bounds__(256) void k_enc_prep(iggy_raw_messages m, EncScratc
 }
 
 __global__ __launch_bounds__(256) void k_enc_scan(uint64_t ntiles, uint64_t n, uint64_t partition_id,
-                                                  EncScratch es) {
+                                                  uint64_t cap, EncScratch es) {
     __shared__ uint64_t s_pl[256], s_uh[256], s_min[256];
     __shared__ uint64_t carry_pl, carry_uh, carry_min;
     const uint32_t tid = threadIdx.x;
@@ -128,6 +129,7 @@ __global__ __launch_bounds__(256) void k_enc_scan(uint64_t ntiles, uint64_t n, u
         es.misc[2] = 0;
         es.misc[3] = n;
         es.misc[4] = carry_pl;  // total payload bytes (bounds the lane-group kernel's loads)
+        es.misc[5] = 256 + es.misc[1] > cap ? 1 : 0;
         iggy_batch_header h{};
         h.partition_id = partition_id;
         h.base_offset = 0;
@@ -201,7 +203,7 @@ __device__ inline uint64_t xxh3_short_stream(const FrameStream &fs) {
 __global__ __launch_bounds__(256) void k_enc_frames(iggy_raw_messages m, EncScratch es,
                                                     uint8_t *out, uint32_t fallback_only) {
     // fallback_only: the lane-group kernel ran unless the payload area is < 16 B
-    if (fallback_only && es.misc[4] >= 16) return;
+    if (es.misc[5] || (fallback_only && es.misc[4] >= 16)) return;
     const int lane = threadIdx.x & 63;
     const uint64_t n = m.count;
     const uint64_t origin = es.misc[0];
@@ -378,7 +380,7 @@ __device__ __forceinline__ void eissue(const iggy_raw_messages &m, const EFrame 
 __global__ __launch_bounds__(256, 2) void k_enc_lanes(iggy_raw_messages m, EncScratch es, uint8_t *out,
                                                        uint64_t f_lo, uint64_t f_hi) {
     const uint64_t ptot = es.misc[4];
-    if (ptot < 16) return;  // tiny payload area: k_enc_frames (fallback) encodes it
+    if (ptot < 16 || es.misc[5]) return;  // tiny payload area: k_enc_frames (fallback) encodes it
     const uint64_t n = f_hi < m.count ? f_hi : m.count;  // this launch: frames [f_lo, f_hi)
     const uint64_t origin = es.misc[0];
     const int lane = threadIdx.x & 63;
@@ -511,7 +513,7 @@ __global__ __launch_bounds__(256, 2) void k_enc_lanes(iggy_raw_messages m, EncSc
 // Frames of <= 240 hashed bytes of a lane-group encode: one lane each hashes the
 // stream (XXH3 17-128 / 129-240 paths) from the SoA input and backpatches.
 __global__ __launch_bounds__(256) void k_enc_short(iggy_raw_messages m, EncScratch es, uint8_t *out) {
-    if (es.misc[4] < 16) return;  // the fallback kernel encoded everything
+    if (es.misc[4] < 16 || es.misc[5]) return;  // the fallback kernel encoded everything
     const uint64_t n = m.count;
     const uint64_t origin = es.misc[0];
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
@@ -538,15 +540,20 @@ __global__ __launch_bounds__(256) void k_enc_short(iggy_raw_messages m, EncScrat
 }
 
 // error precedence (send_messages.rs:131-174) and the 256-B header
-__global__ void k_enc_finish(iggy_raw_messages m, EncScratch es, uint64_t partition_id,
+__global__ void k_enc_finish(iggy_raw_messages m, EncScratch es, uint64_t partition_id, uint64_t cap,
                              const uint64_t *checksum, uint8_t *out, iggy_encode_result *res) {
     const int t = threadIdx.x;
     iggy_batch_header h = *es.hdr;
     h.batch_checksum = *checksum;
     const uint64_t ts_enc = es.misc[2];
+    const bool over = es.misc[5] != 0;
     uint32_t kind = IGGY_OK;
     uint64_t a = 0, b = 0;
-    if (ts_enc) {
+    if (over) {  // the caller's buffer cannot hold the batch: nothing was written
+        kind = IGGY_ERR_CAPACITY;
+        a = h.batch_length;
+        b = cap;
+    } else if (ts_enc) {
         kind = IGGY_ERR_INVALID_TIMESTAMP_DELTA;
         a = m.origin_timestamps[~ts_enc] - es.misc[0];
     } else if (partition_id == 0 && h.batch_length > 0xFFFFFFFFull) {
@@ -555,7 +562,7 @@ __global__ void k_enc_finish(iggy_raw_messages m, EncScratch es, uint64_t partit
         b = 0xFFFFFFFFull;
     }
     // header bytes: 64 threads x 4 bytes
-    {
+    if (!over) {
         const uint32_t off = 4 * t;
         uint32_t w = 0;
         if (off < 48) {

@@ -19,11 +19,18 @@
  *    fill an `iggy_wire_error` that mirrors `WireError`
  *    (core/binary_protocol/src/error.rs:24-68) field by field.
  *  - the caller owns every buffer; the library never frees caller memory.
- *  - host-buffer entry points are synchronous; `_device` entry points take
- *    device pointers, enqueue on `stream` and return immediately (results land
- *    in a device-resident result struct).
+ *  - host-buffer entry points are synchronous, except the `_submit` /
+ *    iggy_codec_poll pair (for shard threads that must never block);
+ *    `_device` entry points take device pointers, enqueue on `stream` and
+ *    return immediately (results land in a device-resident result struct).
  *  - a context is used by one thread at a time (Iggy shards are
  *    thread-per-core); distinct contexts are independent.
+ *  - every enqueue of one context runs in ONE stream order (its scratch is
+ *    shared): a `_device` call on another stream than the context's previous
+ *    enqueue first waits for that previous stream's work (so that stream must
+ *    still exist). Calls on one stream pay nothing for this.
+ *  - every entry point makes the context's device current for its duration
+ *    and restores the caller's current device on return.
  *  - there is NO CPU fallback: without a usable gfx950 device
  *    iggy_codec_create fails with IGGY_ERR_DEVICE.
  */
@@ -73,7 +80,9 @@ typedef enum iggy_error_kind {
     IGGY_ERR_DEVICE = 100,
     IGGY_ERR_INVALID_ARGUMENT = 101,
     IGGY_ERR_CAPACITY = 102,  /* output capacity too small; a = required */
-    IGGY_ERR_TIMEOUT = 103    /* a device-side bounded wait gave up (bug guard) */
+    IGGY_ERR_TIMEOUT = 103,   /* a device-side bounded wait gave up (bug guard) */
+    IGGY_ERR_PENDING = 104,   /* iggy_codec_poll: the operation has not finished yet */
+    IGGY_ERR_BUSY = 105       /* every asynchronous slot of the context is in flight */
 } iggy_error_kind;
 
 /* The fixed `WireError::Validation` strings of the path, by id. */
@@ -364,6 +373,56 @@ typedef struct iggy_segment_recovery {
 
 int iggy_codec_recover_segment(iggy_codec_ctx *ctx, const uint8_t *messages, uint64_t len,
                                uint64_t start_offset, iggy_segment_recovery *out);
+
+/* ------------------------------------------- asynchronous (host buffers) */
+/* Server shard threads run one compio reactor each with NO blocking pool
+ * (server_common/src/executor.rs:80-88, core/server/src/bootstrap.rs:720-760),
+ * so a host-buffer codec call must not block them. A `_submit` copies the
+ * caller's buffer to a device slot (async H2D on the context's copy-in
+ * stream), enqueues the same kernels as the synchronous call on the context's
+ * stream and the result / output copies on its copy-out stream, and returns a
+ * ticket at once; iggy_codec_poll tells whether it has finished. Successive
+ * submits overlap (one operation's H2D, another's kernels, a third's D2H).
+ * Kernels never read host memory. Caller buffers must stay valid (and
+ * unmodified, for inputs) until the ticket completes. Copies from pageable
+ * memory are staged by the HIP runtime and block the caller for their
+ * duration: register long-lived buffers (the server's 4096-aligned
+ * Owned<MESSAGE_ALIGN> pool, server_common/src/iobuf.rs) once with
+ * iggy_codec_host_register. At most 8 operations per context are in flight
+ * (IGGY_ERR_BUSY otherwise). */
+typedef uint64_t iggy_ticket;
+#define IGGY_OP_DECODE 1u
+#define IGGY_OP_ENCODE 2u
+typedef struct iggy_completion {
+    uint32_t op;                  /* IGGY_OP_* */
+    uint32_t _pad0;
+    iggy_batch_header header;     /* decode: the record's header; encode: the written header */
+    iggy_wire_error error;        /* the operation's verdict (kind IGGY_OK = success) */
+    uint64_t frame_count;         /* decode: frames walked */
+    uint64_t computed_checksum;   /* decode (Verify): recomputed batch checksum */
+    uint64_t bytes;               /* encode: batch bytes written to `out` */
+    uint64_t _pad1[3];
+} iggy_completion;
+
+/* Page-lock a caller buffer for the context's device (hipHostRegister) / undo it. */
+int iggy_codec_host_register(iggy_codec_ctx *ctx, void *ptr, uint64_t len);
+int iggy_codec_host_unregister(iggy_codec_ctx *ctx, void *ptr);
+/* decode_batch_slice_with (batch.rs:391-422) of a host record; frame_pos
+ * (nullable, host) receives up to `cap` blob-relative frame starts (entries
+ * past frame_count are unspecified; more frames than cap -> IGGY_ERR_CAPACITY
+ * in the completion). */
+int iggy_codec_decode_submit(iggy_codec_ctx *ctx, const uint8_t *body, uint64_t len, int integrity,
+                             uint64_t *frame_pos, uint64_t cap, iggy_ticket *ticket);
+/* SendMessagesEncoder::encode batch section (send_messages.rs:89-181) from host
+ * SoA input into `out` (host, cap bytes; a batch larger than cap writes nothing
+ * and completes with IGGY_ERR_CAPACITY). */
+int iggy_codec_encode_submit(iggy_codec_ctx *ctx, const iggy_raw_messages *msgs, uint64_t partition_id,
+                             uint8_t *out, uint64_t cap, iggy_ticket *ticket);
+/* 0: finished, *out filled (out->error is the operation's own verdict) and the
+ * ticket retired; IGGY_ERR_PENDING: not yet; never blocks. */
+int iggy_codec_poll(iggy_codec_ctx *ctx, iggy_ticket ticket, iggy_completion *out);
+/* Blocking form of iggy_codec_poll (tests, SDK tasks that may block). */
+int iggy_codec_wait(iggy_codec_ctx *ctx, iggy_ticket ticket, iggy_completion *out);
 
 /* ------------------------------------------------------------- profiling */
 /* When enabled, the context brackets the dominant kernel of every decode /

@@ -92,3 +92,54 @@ double oracle_cpu_decode_bench(const uint8_t *body, uint64_t len, int threads, i
     free(jobs);
     return (double)(t1.tv_sec - t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - t0.tv_nsec);
 }
+
+/* SendMessagesEncoder::encode (send_messages.rs:89-181) restated in codec_ref.c,
+ * timed the same way: `threads` threads each encode the same SoA input into a
+ * buffer of their own, `reps` times. Returns seconds; *bytes_out = batch bytes
+ * of one encode (0 on any error). */
+typedef struct {
+    const iggy_raw_messages *m;
+    uint64_t partition_id, need, bytes;
+    int reps, ok;
+} enc_job_t;
+
+static void *enc_worker(void *arg) {
+    enc_job_t *j = (enc_job_t *)arg;
+    uint8_t *out = (uint8_t *)malloc(j->need + 16);
+    j->ok = out != NULL;
+    for (int r = 0; r < j->reps && j->ok; r++) {
+        uint64_t n = 0;
+        iggy_wire_error e;
+        j->ok &= oracle_encode_batch(j->m, j->partition_id, out, j->need, &n, &e) == 0;
+        j->bytes = n;
+    }
+    free(out);
+    return NULL;
+}
+
+double oracle_cpu_encode_bench(const iggy_raw_messages *m, uint64_t partition_id, int threads, int reps,
+                               uint64_t *bytes_out) {
+    if (threads < 1) threads = 1;
+    const uint64_t need = oracle_encoded_batch_size(m);
+    pthread_t *tid = (pthread_t *)malloc(sizeof(pthread_t) * threads);
+    enc_job_t *jobs = (enc_job_t *)calloc(threads, sizeof(enc_job_t));
+    struct timespec t0, t1;
+    clock_gettime(CLOCK_MONOTONIC, &t0);
+    for (int t = 0; t < threads; t++) {
+        jobs[t].m = m;
+        jobs[t].partition_id = partition_id;
+        jobs[t].need = need;
+        jobs[t].reps = reps;
+        pthread_create(&tid[t], NULL, enc_worker, &jobs[t]);
+    }
+    int ok = 1;
+    for (int t = 0; t < threads; t++) {
+        pthread_join(tid[t], NULL);
+        ok &= jobs[t].ok;
+    }
+    clock_gettime(CLOCK_MONOTONIC, &t1);
+    if (bytes_out) *bytes_out = ok ? jobs[0].bytes : 0;
+    free(tid);
+    free(jobs);
+    return (double)(t1.tv_sec - t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - t0.tv_nsec);
+}

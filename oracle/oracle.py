@@ -60,6 +60,8 @@ def lib() -> ctypes.CDLL:
         L.oracle_cpu_decode_bench.restype = ctypes.c_double
         L.oracle_cpu_decode_bench.argtypes = [vp, u64, ctypes.c_int, ctypes.c_int, vp]
         L.oracle_has_avx2.restype = ctypes.c_int
+        L.oracle_cpu_encode_bench.restype = ctypes.c_double
+        L.oracle_cpu_encode_bench.argtypes = [vp, u64, ctypes.c_int, ctypes.c_int, vp]
         L.oracle_select_batch_slice.argtypes = [vp, u64, vp, vp, vp]
         L.oracle_decode_prepare.argtypes = [vp, u64, ctypes.c_int, vp, vp]
         L.oracle_admit_batch.argtypes = [vp, u64, u32, u64, ctypes.c_int, vp, u64, vp, vp]
@@ -221,3 +223,9 @@ def cpu_decode_bench(body, threads: int, reps: int):
     c = u64(0)
     secs = lib().oracle_cpu_decode_bench(a.ctypes.data, a.size, threads, reps, ctypes.byref(c))
     return secs, c.value
+
+
+def cpu_encode_bench(raw: "RawMessages", partition_id: int, threads: int, reps: int):
+    b = u64(0)
+    secs = lib().oracle_cpu_encode_bench(ctypes.byref(raw), partition_id, threads, reps, ctypes.byref(b))
+    return secs, b.value

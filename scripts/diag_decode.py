@@ -15,6 +15,9 @@ import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from iggy_amd import abi  # noqa: E402
+from iggy_amd import codec as _codec  # noqa: E402
+
+_codec.use_library(_codec.DIAG_LIB_PATH)  # ablation bits live only in the diagnostic build
 from iggy_amd.codec import Codec  # noqa: E402
 import bench  # noqa: E402
 
@@ -34,7 +37,7 @@ def main():
     torch.cuda.set_stream(ts)
     stream = ts.cuda_stream
     assert stream != 0
-    batch = bench.make_batch(ctxs[0], n, pl, 0, dev, stream)
+    batch = bench.make_batch(ctxs[0], n, pl, pl, 0, dev, stream)[0]
     L = batch.numel()
     if os.environ.get("DIAG_HIPMALLOC"):  # the record in a plain hipMalloc buffer instead of torch's allocator
         hip = ctypes.CDLL("libamdhip64.so")

@@ -14,6 +14,9 @@ import torch
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 from iggy_amd import abi  # noqa: E402
+from iggy_amd import codec as _codec  # noqa: E402
+
+_codec.use_library(_codec.DIAG_LIB_PATH)  # ablation bits live only in the diagnostic build
 from iggy_amd.codec import Codec  # noqa: E402
 
 
