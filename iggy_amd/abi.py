@@ -192,3 +192,28 @@ class SegmentRecovery(ctypes.Structure):
 
     def astuple(self):
         return tuple(getattr(self, f) for f, _ in self._fields_)
+
+
+class ChunkFragment(ctypes.Structure):
+    """iggy_chunk_fragment (push_selected_batch_fragments, journal.rs:1096-1137)."""
+    _fields_ = [("batch_pos", u64), ("full_body", u32), ("matched_messages", u32), ("body_start", u64),
+                ("body_end", u64), ("last_matching_offset", u64), ("_pad", u64)]
+
+    def astuple(self):
+        return (self.batch_pos, self.full_body, self.matched_messages, self.body_start, self.body_end,
+                self.last_matching_offset)
+
+
+class ChunkWalk(ctypes.Structure):
+    """iggy_chunk_walk (ChunkWalk + carried state, poll_plan.rs:950-1011)."""
+    _fields_ = [("consumed", u64), ("corrupt", u32), ("matched", u32), ("last_matching_offset", u64),
+                ("has_last_matching_offset", u32), ("fragments", u32), ("error", WireError), ("batches", u64)]
+
+    def astuple(self):
+        return (self.consumed, self.corrupt, self.matched,
+                self.last_matching_offset if self.has_last_matching_offset else None, self.fragments,
+                self.error.astuple(), self.batches)
+
+
+assert ctypes.sizeof(ChunkFragment) == 48
+assert ctypes.sizeof(ChunkWalk) == 72

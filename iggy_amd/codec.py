@@ -70,6 +70,14 @@ def load(path: str) -> ctypes.CDLL:
     if not os.path.exists(path):
         raise FileNotFoundError(
             f"{path} missing: build it with `python -c 'import __graft_entry__ as g; g.build()'`")
+    # PyTorch-ROCm ships its own libamdhip64.so.7 / libhsa-runtime64.so.1 under the
+    # same sonames as /opt/rocm's. Whichever loads first serves the whole process;
+    # load torch's first (when torch is installed) so that torch and the codec share
+    # one HIP runtime and torch's lazy GPU init never runs beside another runtime.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     L = ctypes.CDLL(path)
     L.iggy_codec_abi_version.restype = u32
     L.iggy_codec_create.argtypes = [ci, ctypes.POINTER(vp)]
@@ -101,6 +109,7 @@ def load(path: str) -> ctypes.CDLL:
     L.iggy_codec_decode_prepare.argtypes = [vp, vp, u64, ci, vp, vp]
     L.iggy_codec_admit_batch.argtypes = [vp, vp, u64, u32, u64, ci, vp, u64, vp, vp]
     L.iggy_codec_recover_segment.argtypes = [vp, vp, u64, u64, vp]
+    L.iggy_codec_walk_disk_chunk.argtypes = [vp, vp, u64, vp, ci, vp, vp, u64, vp]
     L.iggy_codec_profile_enable.argtypes = [vp, ci]
     L.iggy_codec_profile_read.argtypes = [vp, ci, vp, vp]
     L.iggy_codec_host_register.argtypes = [vp, vp, u64]
@@ -272,6 +281,19 @@ class Codec:
         out = abi.SegmentRecovery()
         rc = self._L.iggy_codec_recover_segment(self._h, _addr(a), a.size, start_offset, ctypes.byref(out))
         return rc, out
+
+    def walk_disk_chunk(self, chunk, kind: int, value: int, count: int, ceiling: int = 2**64 - 1,
+                        already_matched: int = 0, integrity: int = abi.INTEGRITY_VERIFY, cap: int = 64):
+        """walk_disk_chunk (poll_plan.rs:950-1011) -> (rc, ChunkWalk, [ChunkFragment], [header bytes])."""
+        a = _np(chunk)
+        q = SliceQuery(kind, count, value, ceiling, already_matched, 0)
+        frags = (abi.ChunkFragment * max(cap, 1))()
+        hdrs = np.zeros(256 * max(cap, 1), dtype=np.uint8)
+        w = abi.ChunkWalk()
+        rc = self._L.iggy_codec_walk_disk_chunk(self._h, _addr(a), a.size, ctypes.byref(q), integrity, frags,
+                                                hdrs.ctypes.data, cap, ctypes.byref(w))
+        n = min(w.fragments, cap)
+        return rc, w, [frags[i] for i in range(n)], [hdrs[256 * i: 256 * i + 256].tobytes() for i in range(n)]
 
     def select_slice_device(self, d_record: int, d_frame_pos: int, nframes: int, query: SliceQuery,
                             d_out: int, d_header: int | None = None, stream: int | None = None) -> int:

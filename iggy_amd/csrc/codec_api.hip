@@ -116,6 +116,7 @@ struct iggy_codec_ctx {
     DevBuf hbsums;
     // poll
     DevBuf ppos, pmsgs, pres;
+    DevBuf cwk;  // disk-chunk walk: state, gates, per-batch slice results, fragments
     // slice / device stamp: [0,512) control words + header + small, then tile counts
     DevBuf sl, slres;
     // pinned host mirror of results
@@ -432,7 +433,7 @@ void iggy_codec_destroy(iggy_codec_ctx *c) {
                       &c->gtiles_cnt, &c->gtiles_pre, &c->gtiles_list, &c->gtiles_e, &c->gtiles_base, &c->ggrp, &c->gfpos, &c->gcs, &c->gflen,
                       &c->gbsums, &c->dresult, &c->din, &c->dpos, &c->dout, &c->epl, &c->euh,
                       &c->etile, &c->ecs, &c->emisc, &c->eids, &c->eots, &c->epay, &c->eplen,
-                      &c->euhb, &c->euhl, &c->hbsums, &c->ppos, &c->pmsgs, &c->pres, &c->sl, &c->slres};
+                      &c->euhb, &c->euhl, &c->hbsums, &c->ppos, &c->pmsgs, &c->pres, &c->cwk, &c->sl, &c->slres};
     for (DevBuf *b : bufs) b->release();
     if (c->h_pinned) (void)hipHostFree(c->h_pinned);
     for (int w = 0; w < 2; ++w) {
@@ -1195,13 +1196,11 @@ int iggy_codec_xxh3_64_ranges_device(iggy_codec_ctx *c, const uint8_t *d_data, c
 }
 
 // ------------------------------------------------- poll-path slicing / stamp
-int iggy_codec_select_slice_device(iggy_codec_ctx *c, const uint8_t *d_record, const uint64_t *d_frame_pos,
-                                   uint64_t nframes, const iggy_slice_query *q, iggy_slice_result *d_out,
-                                   uint8_t *d_header_out, void *stream) {
-    if (!c || !d_record || !q || !d_out || (nframes && !d_frame_pos)) return IGGY_ERR_INVALID_ARGUMENT;
-    if (q->kind != IGGY_LOOKUP_OFFSET && q->kind != IGGY_LOOKUP_TIMESTAMP) return IGGY_ERR_INVALID_ARGUMENT;
-    DevGuard dg(c->device);
-    hipStream_t s = bind(c, stream);
+// select_batch_slice + served header on a decoded device record (gate / d_matched:
+// chunk walks, see k_chunk_gate)
+static int enqueue_select(iggy_codec_ctx *c, const uint8_t *d_record, const uint64_t *d_frame_pos, uint64_t nframes,
+                          const iggy_slice_query &qq, iggy_slice_result *d_out, uint8_t *d_header_out, hipStream_t s,
+                          const uint32_t *gate = nullptr, const uint32_t *d_matched = nullptr) {
     const uint64_t ntiles = (nframes + kSliceTile - 1) / kSliceTile;
     int r = c->sl.ensure(512 + ntiles * 4);
     r |= c->gbsums.ensure(((44 + 8 * nframes) / 1024 + 2) * 64);
@@ -1215,15 +1214,14 @@ int iggy_codec_select_slice_device(iggy_codec_ctx *c, const uint8_t *d_record, c
     ss.hdr = c->sl.as<iggy_batch_header>(64);
     ss.tile_cnt = c->sl.as<uint32_t>(512);
     HIP_OK(hipMemsetAsync(ss.stop, 0xff, 8, s));
-    const iggy_slice_query qq = *q;
     if (nframes) {
         const uint32_t g = (uint32_t)std::min<uint64_t>((nframes + 255) / 256, (uint64_t)c->ncu * 8);
-        hipLaunchKernelGGL(k_slice_stop, dim3(g), dim3(256), 0, s, d_record, d_frame_pos, nframes, qq, ss.stop);
+        hipLaunchKernelGGL(k_slice_stop, dim3(g), dim3(256), 0, s, d_record, d_frame_pos, nframes, qq, ss.stop, gate);
         hipLaunchKernelGGL(k_slice_count, dim3((uint32_t)ntiles), dim3(256), 0, s, d_record, d_frame_pos, nframes, qq,
-                           (const uint64_t *)ss.stop, ss.tile_cnt);
+                           (const uint64_t *)ss.stop, ss.tile_cnt, gate);
     }
     hipLaunchKernelGGL(k_slice_pick, dim3(1), dim3(256), 0, s, d_record, d_frame_pos, nframes, qq,
-                       (const uint32_t *)ss.tile_cnt, ntiles, ss, d_out);
+                       (const uint32_t *)ss.tile_cnt, ntiles, ss, d_out, gate, d_matched);
     CsSource src{nullptr, d_record + kHdr, d_frame_pos, ss.first};
     hipLaunchKernelGGL(k_bsum_blocks, dim3(c->ncu * 4), dim3(256), 0, s, (const iggy_batch_header *)ss.hdr,
                        (const uint64_t *)ss.nsel, src, c->gbsums.as<uint64_t>(), (const uint32_t *)ss.skip);
@@ -1233,6 +1231,100 @@ int iggy_codec_select_slice_device(iggy_codec_ctx *c, const uint8_t *d_record, c
     hipLaunchKernelGGL(k_slice_finish, dim3(1), dim3(64), 0, s, d_record, ss, d_out, d_header_out);
     HIP_OK(hipGetLastError());
     return 0;
+}
+
+int iggy_codec_select_slice_device(iggy_codec_ctx *c, const uint8_t *d_record, const uint64_t *d_frame_pos,
+                                   uint64_t nframes, const iggy_slice_query *q, iggy_slice_result *d_out,
+                                   uint8_t *d_header_out, void *stream) {
+    if (!c || !d_record || !q || !d_out || (nframes && !d_frame_pos)) return IGGY_ERR_INVALID_ARGUMENT;
+    if (q->kind != IGGY_LOOKUP_OFFSET && q->kind != IGGY_LOOKUP_TIMESTAMP) return IGGY_ERR_INVALID_ARGUMENT;
+    DevGuard dg(c->device);
+    hipStream_t s = bind(c, stream);
+    return enqueue_select(c, d_record, d_frame_pos, nframes, *q, d_out, d_header_out, s);
+}
+
+int iggy_codec_walk_disk_chunk(iggy_codec_ctx *c, const uint8_t *chunk, uint64_t len, const iggy_slice_query *q,
+                               int integrity, iggy_chunk_fragment *frags, uint8_t *headers, uint64_t cap,
+                               iggy_chunk_walk *out) {
+    if (!c || !q || !out || (!chunk && len) || (cap && !frags)) return IGGY_ERR_INVALID_ARGUMENT;
+    if (q->kind != IGGY_LOOKUP_OFFSET && q->kind != IGGY_LOOKUP_TIMESTAMP) return IGGY_ERR_INVALID_ARGUMENT;
+    DevGuard dg(c->device);
+    bind(c, nullptr);
+    memset(out, 0, sizeof(*out));
+    // the batch extents follow from the 256-B headers alone (host); a header that does
+    // not decode or a batch that does not fit is the last candidate (its decode fails)
+    struct Cand { uint64_t pos, bl, nframes, pbase; };
+    std::vector<Cand> cand;
+    uint64_t cursor = 0, pwords = 0, maxn = 0;
+    while (cursor + 256 <= len) {
+        iggy_batch_header h;
+        iggy_wire_error he;
+        const bool ok = iggy_batch_header_decode(chunk + cursor, len - cursor, &h, &he) == 0;
+        const bool fits = ok && h.batch_length <= len - cursor;
+        const uint64_t nf = fits ? (h.batch_length - 256) / 48 + 1 : 1;
+        cand.push_back({cursor, fits ? h.batch_length : 0, fits ? (uint64_t)h.message_count : 0, pwords});
+        pwords += nf;
+        maxn = std::max(maxn, nf);
+        if (!fits) break;
+        cursor += h.batch_length;
+    }
+    const uint64_t K = cand.size();
+    // device: the chunk once; per batch its Verify / LayoutOnly decode, the gate, the
+    // selection (match count from the previous batch) and the fragment push; one sync
+    const uint64_t kState = 256, kSlot = 512;
+    int r = c->din.ensure(len + 16);
+    r |= c->dpos.ensure((pwords + 1) * 8);
+    r |= c->pres.ensure((K + 1) * sizeof(iggy_decode_result));
+    r |= c->cwk.ensure(kState + K * (kSlot + 8) + cap * (sizeof(iggy_chunk_fragment) + 256) + 64);
+    if (!r) r = ensure_decode_scratch(c, len);
+    if (r) return IGGY_ERR_DEVICE;
+    hipStream_t s = c->stream;
+    ChunkState *st = c->cwk.as<ChunkState>(0);
+    uint32_t *gates = c->cwk.as<uint32_t>(kState);
+    uint8_t *slots = c->cwk.as<uint8_t>(kState + K * 8);
+    iggy_chunk_fragment *d_frags = c->cwk.as<iggy_chunk_fragment>(kState + K * (kSlot + 8));
+    uint8_t *d_hdrs = (uint8_t *)(d_frags + cap);
+    if (len) HIP_OK(hipMemcpyAsync(c->din.p, chunk, len, hipMemcpyHostToDevice, s));
+    hipLaunchKernelGGL(k_chunk_init, dim3(1), dim3(64), 0, s, st, q->already_matched);
+    iggy_decode_result *d_res = c->pres.as<iggy_decode_result>();
+    for (uint64_t k = 0; k < K; ++k) {
+        const Cand &cd = cand[k];
+        const uint8_t *rec = c->din.as<uint8_t>(cd.pos);
+        uint64_t *pos = c->dpos.as<uint64_t>(8 * cd.pbase);
+        r = enqueue_decode(c, rec, len - cd.pos, integrity, pos, cd.bl ? (cd.bl - 256) / 48 + 1 : 0, d_res + k, s);
+        if (r) return r;
+        hipLaunchKernelGGL(k_chunk_gate, dim3(1), dim3(64), 0, s, (const iggy_decode_result *)(d_res + k), cd.pos,
+                           q->count, st, gates + k);
+        if (!cd.bl) break;  // its decode failed (the gate stops the walk there)
+        iggy_slice_result *sr = (iggy_slice_result *)(slots + k * kSlot);
+        uint8_t *hb = slots + k * kSlot + 256;
+        r = enqueue_select(c, rec, pos, cd.nframes, *q, sr, hb, s, gates + k, &st->matched);
+        if (r) return r;
+        hipLaunchKernelGGL(k_chunk_after, dim3(1), dim3(64), 0, s, (const iggy_slice_result *)sr,
+                           (const uint8_t *)hb, cd.pos, cd.bl, st, (const uint32_t *)(gates + k), d_frags, d_hdrs, cap);
+    }
+    HIP_OK(hipGetLastError());
+    ChunkState hs{};
+    HIP_OK(hipMemcpyAsync(&hs, st, sizeof(hs), hipMemcpyDeviceToHost, s));
+    HIP_OK(hipStreamSynchronize(s));
+    const uint64_t nf = std::min<uint64_t>(hs.nfrag, cap);
+    if (nf) {
+        HIP_OK(hipMemcpy(frags, d_frags, nf * sizeof(iggy_chunk_fragment), hipMemcpyDeviceToHost));
+        if (headers) HIP_OK(hipMemcpy(headers, d_hdrs, nf * 256, hipMemcpyDeviceToHost));
+    }
+    if (hs.error.kind == IGGY_ERR_TIMEOUT) {  // a bug guard fired, not a verdict on the chunk
+        reset_after_timeout(c);
+        return IGGY_ERR_TIMEOUT;
+    }
+    out->consumed = std::min<uint64_t>(hs.consumed, len);
+    out->corrupt = hs.corrupt;
+    out->matched = hs.matched;
+    out->last_matching_offset = hs.last_matching_offset;
+    out->has_last_matching_offset = (uint32_t)hs.has_last;
+    out->fragments = hs.nfrag;
+    out->error = hs.error;
+    out->batches = hs.batches;
+    return hs.nfrag > cap ? IGGY_ERR_CAPACITY : 0;
 }
 
 int iggy_codec_select_slice(iggy_codec_ctx *c, const uint8_t *record, uint64_t len, const iggy_slice_query *q,

@@ -40,8 +40,12 @@ __device__ __forceinline__ bool slice_selected(const iggy_slice_query &q, uint64
     return q.kind == IGGY_LOOKUP_OFFSET ? off >= q.value : base_ts >= q.value;  // journal.rs:1052-1065
 }
 
+// `gate` (nullable, device): 1 = this batch is not selected from at all (a chunk
+// walk that already stopped); `d_matched` (nullable, device) replaces
+// q.already_matched with the running count of a chunk walk.
 __global__ __launch_bounds__(256) void k_slice_stop(const uint8_t *rec, const uint64_t *pos, uint64_t n,
-                                                    iggy_slice_query q, uint64_t *stop) {
+                                                    iggy_slice_query q, uint64_t *stop, const uint32_t *gate) {
+    if (gate && *gate) return;
     const uint64_t base = ld64_any(rec + 8);
     const uint8_t *blob = rec + kHdr;
     uint64_t mine = ~0ull;
@@ -55,7 +59,9 @@ __global__ __launch_bounds__(256) void k_slice_stop(const uint8_t *rec, const ui
 }
 
 __global__ __launch_bounds__(256) void k_slice_count(const uint8_t *rec, const uint64_t *pos, uint64_t n,
-                                                     iggy_slice_query q, const uint64_t *stop, uint32_t *tile_cnt) {
+                                                     iggy_slice_query q, const uint64_t *stop, uint32_t *tile_cnt,
+                                                     const uint32_t *gate) {
+    if (gate && *gate) return;
     __shared__ uint32_t part[4];
     const uint64_t base = ld64_any(rec + 8), bts = ld64_any(rec + 16);
     const uint8_t *blob = rec + kHdr;
@@ -109,8 +115,19 @@ __device__ uint64_t slice_nth(const uint8_t *blob, const uint64_t *pos, uint64_t
 
 __global__ __launch_bounds__(256) void k_slice_pick(const uint8_t *rec, const uint64_t *pos, uint64_t n,
                                                     iggy_slice_query q, const uint32_t *tile_cnt, uint64_t ntiles,
-                                                    SliceScratch ss, iggy_slice_result *res) {
+                                                    SliceScratch ss, iggy_slice_result *res, const uint32_t *gate,
+                                                    const uint32_t *d_matched) {
     __shared__ uint32_t sh[257];
+    if (gate && *gate) {
+        if (threadIdx.x == 0) {
+            *res = iggy_slice_result{};
+            *ss.skip = 1;
+            *ss.nsel = 0;
+            *ss.first = 0;
+        }
+        return;
+    }
+    if (d_matched) q.already_matched = *d_matched;
     __shared__ uint64_t plan[5];  // first tile, last tile, need in the last tile, matched, status
     const uint8_t *blob = rec + kHdr;
     iggy_batch_header h{};
@@ -238,6 +255,80 @@ __global__ void k_stamp_finish(uint8_t *rec, const iggy_batch_header *hdr, const
         *(u32_ua *)(rec + off) = (off & 4) ? (uint32_t)(v >> 32) : (uint32_t)v;
     }
     if (t == 0 && out) *out = h;
+}
+
+// ---- walk_disk_chunk (core/partitions/src/poll_plan.rs:950-1011): the walk's
+// state lives on the device so that every batch of a chunk is verified, gated and
+// selected in one enqueue (the running match count feeds the next selection).
+struct ChunkState {
+    uint32_t stopped, corrupt, matched, nfrag;
+    uint64_t consumed, last_matching_offset, has_last, batches;
+    iggy_wire_error error;
+};
+
+__global__ void k_chunk_init(ChunkState *st, uint32_t already_matched) {
+    if (threadIdx.x == 0) {
+        ChunkState z{};
+        z.matched = already_matched;
+        *st = z;
+    }
+}
+
+// before batch k: the loop condition (:963) and the decode verdict (:964-988)
+__global__ void k_chunk_gate(const iggy_decode_result *res, uint64_t pos, uint32_t count, ChunkState *st,
+                             uint32_t *gate) {
+    if (threadIdx.x != 0) return;
+    uint32_t g = 1;
+    if (!st->stopped) {
+        if (st->matched >= count) {
+            st->stopped = 1;
+            st->consumed = pos;
+        } else if (res->error.kind != IGGY_OK) {
+            // InvalidBatchChecksum: damaged at rest (:966-983); anything else: incomplete tail (:984-987)
+            st->stopped = 1;
+            st->consumed = pos;
+            st->corrupt = res->error.kind == IGGY_ERR_INVALID_BATCH_CHECKSUM ? 1u : 0u;
+            st->error = res->error;
+        } else {
+            g = 0;
+        }
+    }
+    *gate = g;
+}
+
+// after batch k's selection: push_selected_batch_fragments (journal.rs:1096-1137)
+// and the cursor advance (:1003)
+__global__ void k_chunk_after(const iggy_slice_result *sr, const uint8_t *hdr_bytes, uint64_t pos, uint64_t total,
+                              ChunkState *st, const uint32_t *gate, iggy_chunk_fragment *frags, uint8_t *headers,
+                              uint64_t cap) {
+    if (*gate) return;
+    const int t = threadIdx.x;  // 64 threads
+    const uint32_t idx = st->nfrag;
+    const bool sel = sr->selected != 0;
+    __syncthreads();
+    if (sel && idx < cap) {
+        if (headers) *(u32_ua *)(headers + 256ull * idx + 4 * t) = *(const u32_ua *)(hdr_bytes + 4 * t);
+        if (t == 0) {
+            iggy_chunk_fragment f{};
+            f.batch_pos = pos;
+            f.full_body = sr->full_body;
+            f.matched_messages = sr->matched_messages;
+            f.body_start = sr->full_body ? pos : pos + kHdr + sr->start;
+            f.body_end = sr->full_body ? pos + total : pos + kHdr + sr->end;
+            f.last_matching_offset = sr->last_matching_offset;
+            frags[idx] = f;
+        }
+    }
+    if (t == 0) {
+        if (sel) {
+            st->nfrag = idx + 1;
+            st->matched += sr->matched_messages;
+            st->last_matching_offset = sr->last_matching_offset;
+            st->has_last = 1;
+        }
+        st->consumed = pos + total;
+        st->batches += 1;
+    }
 }
 
 }  // namespace iggy

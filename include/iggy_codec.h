@@ -314,6 +314,45 @@ int iggy_codec_select_slice_device(iggy_codec_ctx *ctx, const uint8_t *d_record,
                                    const iggy_slice_query *query, iggy_slice_result *d_out,
                                    uint8_t *d_header_out, void *stream);
 
+/* ------------------------------------------------------- disk-poll chunk walk */
+/* One fragment push_selected_batch_fragments (journal.rs:1096-1137) emits for a
+ * selected batch: the whole record by reference (full_body), or the rewritten
+ * header (headers[k], 256 B) followed by the chunk bytes [body_start, body_end). 48 B. */
+typedef struct iggy_chunk_fragment {
+    uint64_t batch_pos;             /* chunk offset of the batch's 256-B header */
+    uint32_t full_body;
+    uint32_t matched_messages;
+    uint64_t body_start, body_end;  /* chunk byte range served (full body: the whole record) */
+    uint64_t last_matching_offset;
+    uint64_t _pad;
+} iggy_chunk_fragment;
+
+/* ChunkWalk plus the walk's carried state (poll_plan.rs:950-1011). 72 B. */
+typedef struct iggy_chunk_walk {
+    uint64_t consumed;                /* ChunkWalk.consumed: where the caller re-reads from */
+    uint32_t corrupt;                 /* ChunkWalk.corrupt: a batch failed its batch checksum */
+    uint32_t matched;                 /* `matched` after the walk (query->already_matched before) */
+    uint64_t last_matching_offset;    /* valid when has_last_matching_offset */
+    uint32_t has_last_matching_offset;
+    uint32_t fragments;               /* fragments pushed (may exceed the capacity: then CAPACITY) */
+    iggy_wire_error error;            /* the decode error that ended the walk, if any */
+    uint64_t batches;                 /* batches decoded and selected from */
+} iggy_chunk_walk;
+
+/* walk_disk_chunk (core/partitions/src/poll_plan.rs:950-1011) over one chunk of
+ * stamped [256 B header][blob] records read from a segment (host memory). From
+ * byte 0, while query->already_matched < query->count and a header fits: decode
+ * with `integrity` (Verify when system.partition.validate_checksum); a batch
+ * failing its batch checksum stops the walk as corrupt at rest (:966-983), any
+ * other decode error as an incomplete tail (:984-987); otherwise
+ * select_batch_slice with the running match count (journal.rs:1025-1086) and
+ * push its fragments. Every batch is verified and selected on the GPU, the match
+ * count carried from batch to batch on the device (one copy in, one sync).
+ * frags / headers (nullable, 256 B per fragment) hold up to cap fragments. */
+int iggy_codec_walk_disk_chunk(iggy_codec_ctx *ctx, const uint8_t *chunk, uint64_t len,
+                               const iggy_slice_query *query, int integrity, iggy_chunk_fragment *frags,
+                               uint8_t *headers, uint64_t cap, iggy_chunk_walk *out);
+
 /* stamp_prepare_for_persistence core (server_common/src/send_messages.rs:642-663) on a
  * device-resident record whose frames were walked by a decode (d_frame_pos/nframes):
  * base_offset and base_timestamp written, batch checksum recomputed, header rewritten

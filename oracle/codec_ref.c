@@ -547,6 +547,60 @@ int oracle_select_batch_slice(const uint8_t *record, uint64_t len, const iggy_sl
     return 0;
 }
 
+/* walk_disk_chunk — core/partitions/src/poll_plan.rs:950-1011, with
+ * select_batch_slice + push_selected_batch_fragments (core/partitions/src/journal.rs:1025-1137).
+ * `decode_batch_slice_with` there is server_common's wrapper (errors mapped by
+ * batch_error): InvalidBatchChecksum marks the chunk corrupt at rest (:966-983),
+ * every other error is an incomplete tail (:984-987). */
+int oracle_walk_disk_chunk(const uint8_t *chunk, uint64_t len, const iggy_slice_query *q, int integrity,
+                           iggy_chunk_fragment *frags, uint8_t *headers, uint64_t cap, iggy_chunk_walk *out) {
+    memset(out, 0, sizeof(*out));
+    uint32_t matched = q->already_matched;
+    uint64_t cursor = 0, nfrag = 0;
+    while (matched < q->count && cursor + HDR <= len) {                   /* :963 */
+        iggy_batch_header h;
+        iggy_wire_error e;
+        int rc = oracle_decode_batch_slice_with(chunk + cursor, len - cursor, integrity, &h, NULL, 0, NULL, &e);
+        if (rc == IGGY_ERR_INVALID_BATCH_CHECKSUM) {                      /* :966-983 */
+            out->corrupt = 1;
+            out->error = e;
+            break;
+        }
+        if (rc) {                                                         /* :984-987 */
+            out->error = e;
+            break;
+        }
+        out->batches++;
+        iggy_slice_query qq = *q;
+        qq.already_matched = matched;
+        iggy_slice_result r;
+        uint8_t hb[256];
+        oracle_select_batch_slice(chunk + cursor, h.batch_length, &qq, &r, hb);
+        if (r.selected) {                                                 /* journal.rs:1096-1137 */
+            if (nfrag < cap) {
+                iggy_chunk_fragment *f = &frags[nfrag];
+                memset(f, 0, sizeof(*f));
+                f->batch_pos = cursor;
+                f->full_body = r.full_body;
+                f->body_start = r.full_body ? cursor : cursor + HDR + r.start;
+                f->body_end = r.full_body ? cursor + h.batch_length : cursor + HDR + r.end;
+                f->matched_messages = r.matched_messages;
+                f->last_matching_offset = r.last_matching_offset;
+                if (headers) memcpy(headers + 256 * nfrag, hb, 256);
+            }
+            nfrag++;
+            matched += r.matched_messages;
+            out->last_matching_offset = r.last_matching_offset;
+            out->has_last_matching_offset = 1;
+        }
+        cursor += h.batch_length;                                         /* :1003 */
+    }
+    out->consumed = cursor < len ? cursor : len;
+    out->matched = matched;
+    out->fragments = nfrag;
+    return nfrag > cap ? IGGY_ERR_CAPACITY : 0;
+}
+
 /* ---------------------------------------------------- synthetic inputs */
 static inline uint64_t splitmix64(uint64_t *s) {
     uint64_t z = (*s += 0x9E3779B97F4A7C15ull);

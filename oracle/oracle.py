@@ -66,6 +66,7 @@ def lib() -> ctypes.CDLL:
         L.oracle_decode_prepare.argtypes = [vp, u64, ctypes.c_int, vp, vp]
         L.oracle_admit_batch.argtypes = [vp, u64, u32, u64, ctypes.c_int, vp, u64, vp, vp]
         L.oracle_recover_segment.argtypes = [vp, u64, u64, vp]
+        L.oracle_walk_disk_chunk.argtypes = [vp, u64, vp, ctypes.c_int, vp, vp, u64, vp]
         _lib = L
     return _lib
 
@@ -229,3 +230,20 @@ def cpu_encode_bench(raw: "RawMessages", partition_id: int, threads: int, reps: 
     b = u64(0)
     secs = lib().oracle_cpu_encode_bench(ctypes.byref(raw), partition_id, threads, reps, ctypes.byref(b))
     return secs, b.value
+
+
+def walk_disk_chunk(chunk, kind: int, value: int, count: int, ceiling: int = 2**64 - 1, already_matched: int = 0,
+                    integrity: int = 0, cap: int = 64):
+    """walk_disk_chunk (poll_plan.rs:950-1011) -> (rc, ChunkWalk, [ChunkFragment], [header bytes])"""
+    import numpy as np
+    from iggy_amd.abi import ChunkFragment, ChunkWalk
+
+    a = _as_np(chunk)
+    q = SliceQuery(kind, count, value, ceiling, already_matched, 0)
+    frags = (ChunkFragment * max(cap, 1))()
+    hdrs = np.zeros(256 * max(cap, 1), dtype=np.uint8)
+    w = ChunkWalk()
+    rc = lib().oracle_walk_disk_chunk(a.ctypes.data if a.size else None, a.size, ctypes.byref(q), integrity, frags,
+                                      hdrs.ctypes.data, cap, ctypes.byref(w))
+    n = min(w.fragments, cap)
+    return rc, w, [frags[i] for i in range(n)], [hdrs[256 * i: 256 * i + 256].tobytes() for i in range(n)]

@@ -3,6 +3,10 @@ import sys
 
 import pytest
 
+# torch first: its bundled HIP runtime then serves the codec library too (same
+# sonames; see iggy_amd/codec.py load())
+import torch  # noqa: F401,E402
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 if ROOT not in sys.path:
     sys.path.insert(0, ROOT)

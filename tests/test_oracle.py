@@ -276,3 +276,27 @@ def test_select_slice_non_monotone_offsets_keep_unselected_inside():
     assert rc == 0 and r.selected
     assert (r.start, r.end, r.matched_messages, r.last_matching_offset) == (1 * S, 5 * S, 3, 9)
     assert r.header.message_count == 3 and r.header.batch_length == 256 + 4 * S
+
+
+def test_oracle_walk_disk_chunk_semantics():
+    """poll_plan.rs:950-1011 on composed chunks: fragments follow select_batch_slice per
+    batch with the running match count; Verify stops on a batch checksum as corrupt."""
+    recs, off = [], 100
+    for k, n in enumerate((10, 20, 5)):
+        r = O.synth_batch(n, 50, 50, 0, seed=k)
+        rc, e, h, out = O.stamp_batch(r, off, 1000 + k)
+        recs.append(np.frombuffer(out, dtype=np.uint8).copy())
+        off += n
+    chunk = np.concatenate(recs)
+    starts = np.cumsum([0] + [r.size for r in recs])
+    rc, w, fr, hd = O.walk_disk_chunk(chunk, abi.LOOKUP_OFFSET, 105, 12)
+    assert rc == 0 and w.matched == 12 and w.fragments == 2 and w.batches == 2
+    assert w.consumed == starts[2]            # stopped by the count before batch 2
+    assert fr[0].full_body == 0 and fr[0].matched_messages == 5 and fr[1].matched_messages == 7
+    assert w.last_matching_offset == 116
+    bad = chunk.copy()
+    bad[starts[1] + 41] ^= 1                  # batch 1's checksum byte
+    rc, w, fr, hd = O.walk_disk_chunk(bad, abi.LOOKUP_OFFSET, 0, 100, integrity=0)
+    assert w.corrupt == 1 and w.consumed == starts[1] and w.fragments == 1
+    rc, w, fr, hd = O.walk_disk_chunk(bad, abi.LOOKUP_OFFSET, 0, 100, integrity=1)
+    assert w.corrupt == 0 and w.consumed == chunk.size and w.matched == 35

@@ -525,3 +525,79 @@ def test_c3_full_size_encode_decode(cx, c3_raw):
     struct.pack_into("<I", bad, 256 + int(of[600_000]) + 36, 77)
     for integ in (abi.INTEGRITY_VERIFY, abi.INTEGRITY_LAYOUT_ONLY):
         _check_decode_integrity(cx, bad, integ)
+
+
+# ---- walk_disk_chunk: core/partitions/src/poll_plan.rs:950-1011
+def _segment_chunk(shapes, base_offset=1000, seed=3):
+    """Consecutive stamped batches (offsets continue across batches), as a segment
+    chunk reads them from disk; -> (chunk, batch starts)."""
+    recs, off = [], base_offset
+    for k, (n, lo, hi) in enumerate(shapes):
+        r = O.synth_batch(n, lo, hi, 0, seed=seed * 100 + k)
+        rc, e, h, out = O.stamp_batch(r, off, 5000 + 10 * k)
+        recs.append(np.frombuffer(out, dtype=np.uint8).copy())
+        off += n
+    starts = np.cumsum([0] + [r.size for r in recs])
+    return np.concatenate(recs), starts
+
+
+_CHUNK_SHAPES = [(40, 10, 900), (3000, 1024, 1024), (1, 5, 5), (700, 0, 3000), (25, 64, 64), (5000, 100, 100)]
+
+
+def _walk_same(cx, chunk, *args, **kw):
+    rc, w, fr, hd = cx.walk_disk_chunk(chunk, *args, **kw)
+    orc, ow, ofr, ohd = O.walk_disk_chunk(chunk, *args, **kw)
+    assert rc == orc, (w.astuple(), ow.astuple())
+    assert w.astuple() == ow.astuple()
+    assert [f.astuple() for f in fr] == [f.astuple() for f in ofr]
+    assert hd == ohd
+    return w
+
+
+@pytest.mark.parametrize("q", [(abi.LOOKUP_OFFSET, 0, 10**9, 2**64 - 1), (abi.LOOKUP_OFFSET, 1020, 30, 2**64 - 1),
+                               (abi.LOOKUP_OFFSET, 1030, 5000, 2**64 - 1), (abi.LOOKUP_OFFSET, 2000, 10**6, 4200),
+                               (abi.LOOKUP_OFFSET, 4040, 1, 2**64 - 1), (abi.LOOKUP_OFFSET, 10**9, 5, 2**64 - 1),
+                               (abi.LOOKUP_TIMESTAMP, 5015, 100, 2**64 - 1), (abi.LOOKUP_TIMESTAMP, 0, 3500, 2**64 - 1)])
+@pytest.mark.parametrize("integrity", [0, 1])
+def test_walk_disk_chunk_clean(cx, q, integrity):
+    chunk, starts = _segment_chunk(_CHUNK_SHAPES)
+    kind, value, count, ceiling = q
+    for already in (0, 7):
+        _walk_same(cx, chunk, kind, value, count, ceiling, already, integrity)
+
+
+def test_walk_disk_chunk_tails_and_corruption(cx):
+    chunk, starts = _segment_chunk(_CHUNK_SHAPES)
+    q = (abi.LOOKUP_OFFSET, 1000, 10**9)
+    cases = []
+    cases.append(chunk[: starts[3] + 1000])          # torn tail inside batch 3
+    cases.append(chunk[: starts[4] + 100])           # torn inside a header
+    cases.append(chunk[: starts[2] + 255])           # less than a header left
+    b = chunk.copy(); b[starts[2] + 40] ^= 1; cases.append(b)          # batch checksum: corrupt at rest (Verify)
+    b = chunk.copy(); b[starts[1] + 256 + 1072 * 7 + 500] ^= 4; cases.append(b)  # body byte: message checksum
+    b = chunk.copy(); b[starts[3] + 100] = 9; cases.append(b)           # reserved header byte: tail
+    b = chunk.copy(); b[starts[4] + 256 + 40] = 1; cases.append(b)      # frame reserved: layout break
+    cases.append(np.concatenate([chunk, np.zeros(300, dtype=np.uint8)]))  # zero padding after the last batch
+    for c in cases:
+        for integrity in (0, 1):
+            w = _walk_same(cx, c, *q, integrity=integrity)
+    # the batch-checksum case is corrupt under Verify only, and consumed stops at that batch
+    b = chunk.copy(); b[starts[2] + 40] ^= 1
+    w = _walk_same(cx, b, *q, integrity=0)
+    assert w.corrupt == 1 and w.consumed == starts[2] and w.error.kind == abi.ERR_INVALID_BATCH_CHECKSUM
+    w = _walk_same(cx, b, *q, integrity=1)
+    assert w.corrupt == 0 and w.consumed == len(b)
+    # a message-checksum failure is an incomplete tail, not corruption (poll_plan.rs:984-987)
+    b = chunk.copy(); b[starts[1] + 256 + 1072 * 7 + 500] ^= 4
+    w = _walk_same(cx, b, *q, integrity=0)
+    assert w.corrupt == 0 and w.consumed == starts[1] and w.error.kind == abi.ERR_INVALID_MESSAGE_CHECKSUM
+
+
+def test_walk_disk_chunk_capacity_and_matched(cx):
+    chunk, starts = _segment_chunk(_CHUNK_SHAPES)
+    rc, w, fr, hd = cx.walk_disk_chunk(chunk, abi.LOOKUP_OFFSET, 0, 10**9, cap=2)
+    orc, ow, ofr, ohd = O.walk_disk_chunk(chunk, abi.LOOKUP_OFFSET, 0, 10**9, cap=2)
+    assert rc == orc == abi.ERR_CAPACITY and w.astuple() == ow.astuple() and len(fr) == 2
+    # already matched everything: nothing decoded, nothing consumed
+    w = _walk_same(cx, chunk, abi.LOOKUP_OFFSET, 0, 50, 2**64 - 1, 50)
+    assert w.consumed == 0 and w.batches == 0 and w.fragments == 0

@@ -27,6 +27,15 @@ def cx():
 
 
 def _torch():
+    import os
+    if os.environ.get("IGGY_TEST_DIAG"):  # diagnostics: the HIP state torch will initialise on top of
+        hip = ctypes.CDLL("libamdhip64.so")
+        n = ctypes.c_int(-1)
+        rc = hip.hipGetDeviceCount(ctypes.byref(n))
+        print(f"\n[diag] peek={hip.hipPeekAtLastError()} getDeviceCount rc={rc} n={n.value} "
+              f"HIP_VISIBLE_DEVICES={os.environ.get('HIP_VISIBLE_DEVICES')} "
+              f"ROCR_VISIBLE_DEVICES={os.environ.get('ROCR_VISIBLE_DEVICES')} "
+              f"CUDA_VISIBLE_DEVICES={os.environ.get('CUDA_VISIBLE_DEVICES')}", flush=True)
     import torch
     return torch
 
