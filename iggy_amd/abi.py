@@ -217,3 +217,21 @@ class ChunkWalk(ctypes.Structure):
 
 assert ctypes.sizeof(ChunkFragment) == 48
 assert ctypes.sizeof(ChunkWalk) == 72
+
+
+SEG_OK, SEG_BATCH, SEG_BASE_OFFSET_MISMATCH, SEG_NON_CONTIGUOUS, SEG_OFFSET_OVERFLOW, SEG_EMPTY = range(6)
+ERR_INVALID_MESSAGES_COUNT = 23
+
+
+class SegmentWalk(ctypes.Structure):
+    """iggy_segment_walk (walk_segment_payload, state_transfer.rs:715-833)."""
+    _fields_ = [("error", u32), ("_pad", u32), ("position", u64), ("expected", u64), ("actual", u64),
+                ("source", WireError), ("end_offset", u64), ("start_timestamp", u64), ("end_timestamp", u64),
+                ("max_timestamp", u64), ("batches", u64), ("index_entries", u64)]
+
+    def astuple(self):
+        return (self.error, self.position, self.expected, self.actual, self.source.astuple(), self.end_offset,
+                self.start_timestamp, self.end_timestamp, self.max_timestamp, self.batches, self.index_entries)
+
+
+assert ctypes.sizeof(SegmentWalk) == 112

@@ -110,6 +110,8 @@ def load(path: str) -> ctypes.CDLL:
     L.iggy_codec_admit_batch.argtypes = [vp, vp, u64, u32, u64, ci, vp, u64, vp, vp]
     L.iggy_codec_recover_segment.argtypes = [vp, vp, u64, u64, vp]
     L.iggy_codec_walk_disk_chunk.argtypes = [vp, vp, u64, vp, ci, vp, vp, u64, vp]
+    L.iggy_codec_walk_segment_payload.argtypes = [vp, vp, u64, u64, vp, u64, vp]
+    L.iggy_codec_segment_write_device.argtypes = [vp, ci, u64, vp, u64, ci, ctypes.POINTER(u64)]
     L.iggy_codec_profile_enable.argtypes = [vp, ci]
     L.iggy_codec_profile_read.argtypes = [vp, ci, vp, vp]
     L.iggy_codec_host_register.argtypes = [vp, vp, u64]
@@ -294,6 +296,25 @@ class Codec:
                                                 hdrs.ctypes.data, cap, ctypes.byref(w))
         n = min(w.fragments, cap)
         return rc, w, [frags[i] for i in range(n)], [hdrs[256 * i: 256 * i + 256].tobytes() for i in range(n)]
+
+    def walk_segment_payload(self, payload, base_offset: int, index_cap: int = 4096):
+        """walk_segment_payload (state_transfer.rs:715-833) -> (rc, SegmentWalk, index bytes)."""
+        a = _np(payload)
+        idx = np.zeros(24 * max(index_cap, 1), dtype=np.uint8)
+        w = abi.SegmentWalk()
+        rc = self._L.iggy_codec_walk_segment_payload(self._h, _addr(a), a.size, base_offset, idx.ctypes.data,
+                                                     index_cap, ctypes.byref(w))
+        n = min(w.index_entries, index_cap)
+        return rc, w, idx[: 24 * n].tobytes()
+
+    def segment_write_device(self, fd: int, position: int, d_bytes: int, length: int, fsync: bool = False) -> int:
+        """MessagesWriter::save_frozen_batches for device-resident batches -> bytes written."""
+        w = u64(0)
+        rc = self._L.iggy_codec_segment_write_device(self._h, fd, position, d_bytes, length, 1 if fsync else 0,
+                                                     ctypes.byref(w))
+        if rc:
+            raise CodecError(rc, None, "segment_write_device")
+        return w.value
 
     def select_slice_device(self, d_record: int, d_frame_pos: int, nframes: int, query: SliceQuery,
                             d_out: int, d_header: int | None = None, stream: int | None = None) -> int:

@@ -7,6 +7,9 @@
 // no CPU fallback: without a usable gfx950 device iggy_codec_create fails.
 #include <hip/hip_runtime.h>
 
+#include <errno.h>
+#include <unistd.h>
+
 #include <algorithm>
 #include <cstdio>
 #include <cstdlib>
@@ -117,6 +120,9 @@ struct iggy_codec_ctx {
     // poll
     DevBuf ppos, pmsgs, pres;
     DevBuf cwk;  // disk-chunk walk: state, gates, per-batch slice results, fragments
+    // segment writer: pinned staging halves and their copy events
+    void *wstage = nullptr;
+    hipEvent_t wev[2] = {nullptr, nullptr};
     // slice / device stamp: [0,512) control words + header + small, then tile counts
     DevBuf sl, slres;
     // pinned host mirror of results
@@ -443,6 +449,9 @@ void iggy_codec_destroy(iggy_codec_ctx *c) {
     for (auto &ev : c->seg_ev)
         if (ev) (void)hipEventDestroy(ev);
     if (c->order_ev) (void)hipEventDestroy(c->order_ev);
+    if (c->wstage) (void)hipHostFree(c->wstage);
+    for (auto &ev : c->wev)
+        if (ev) (void)hipEventDestroy(ev);
     for (Slot &sl : c->slots) sl.release();
     if (c->slot_pinned) (void)hipHostFree(c->slot_pinned);
     if (c->h2d) (void)hipStreamSynchronize(c->h2d), (void)hipStreamDestroy(c->h2d);
@@ -843,6 +852,168 @@ int iggy_codec_recover_segment(iggy_codec_ctx *c, const uint8_t *messages, uint6
     out->end_offset = end_offset;
     out->walked_bytes = walked;
     out->batches = accepted;
+    return 0;
+}
+
+// walk_segment_payload (core/partitions/src/state_transfer.rs:715-833). The batch
+// extents follow from the headers (host); every batch is Verify-decoded on the GPU
+// (one copy, all queued, one sync); the verdicts and the header-level checks are
+// then applied in walk order, so the first invalid byte decides, as in the reference.
+int iggy_codec_walk_segment_payload(iggy_codec_ctx *c, const uint8_t *bytes, uint64_t len, uint64_t base_offset,
+                                    uint8_t *index_out, uint64_t index_cap, iggy_segment_walk *out) {
+    if (!c || !out || (!bytes && len)) return IGGY_ERR_INVALID_ARGUMENT;
+    DevGuard dg(c->device);
+    bind(c, nullptr);
+    memset(out, 0, sizeof(*out));
+    struct Cand { uint64_t pos; iggy_batch_header h; bool ok; };
+    std::vector<Cand> cand;
+    uint64_t pos = 0, maxlen = 256;
+    while (pos < len) {
+        iggy_batch_header h{};
+        iggy_wire_error e;
+        const bool ok = iggy_batch_header_decode(bytes + pos, len - pos, &h, &e) == 0 && h.batch_length <= len - pos;
+        cand.push_back({pos, h, ok});
+        if (!ok) break;  // its decode reports the error at this position
+        maxlen = std::max(maxlen, h.batch_length);
+        pos += h.batch_length;
+    }
+    std::vector<iggy_decode_result> res(cand.size());
+    if (!cand.empty()) {
+        int r = c->din.ensure(len + 16);
+        r |= c->pres.ensure(cand.size() * sizeof(iggy_decode_result));
+        if (!r) r = ensure_decode_scratch(c, maxlen);
+        if (r) return r ? r : IGGY_ERR_DEVICE;
+        HIP_OK(hipMemcpyAsync(c->din.p, bytes, len, hipMemcpyHostToDevice, c->stream));
+        iggy_decode_result *d_res = c->pres.as<iggy_decode_result>();
+        for (size_t k = 0; k < cand.size(); ++k) {
+            r = enqueue_decode(c, c->din.as<uint8_t>(cand[k].pos), len - cand[k].pos, IGGY_INTEGRITY_VERIFY, nullptr,
+                               0, d_res + k, c->stream);
+            if (r) return r;
+        }
+        HIP_OK(hipMemcpyAsync(res.data(), d_res, res.size() * sizeof(iggy_decode_result), hipMemcpyDeviceToHost,
+                              c->stream));
+        HIP_OK(hipStreamSynchronize(c->stream));
+    }
+    uint64_t next_offset = base_offset, indexed = 0, nidx = 0;
+    bool have_stats = false, have_index = false;
+    for (size_t k = 0; k < cand.size(); ++k) {
+        const iggy_decode_result &rs = res[k];
+        const uint64_t position = cand[k].pos;
+        if (rs.error.kind == IGGY_ERR_TIMEOUT) {
+            reset_after_timeout(c);
+            return IGGY_ERR_TIMEOUT;
+        }
+        if (rs.error.kind != IGGY_OK) {  // :750-755, batch_error's mapping
+            out->error = IGGY_SEG_BATCH;
+            out->position = position;
+            out->source = rs.error;
+            server_error((int)rs.error.kind, &out->source);
+            return 0;
+        }
+        const iggy_batch_header &h = rs.header;
+        if (!have_stats && h.base_offset != base_offset) {
+            out->error = IGGY_SEG_BASE_OFFSET_MISMATCH;
+            out->expected = base_offset;
+            out->actual = h.base_offset;
+            return 0;
+        }
+        if (h.base_offset != next_offset) {
+            out->error = IGGY_SEG_NON_CONTIGUOUS;
+            out->expected = next_offset;
+            out->actual = h.base_offset;
+            return 0;
+        }
+        if (h.message_count == 0) {
+            out->error = IGGY_SEG_BATCH;
+            out->position = position;
+            set_err(&out->source, IGGY_ERR_INVALID_MESSAGES_COUNT);
+            return 0;
+        }
+        const uint64_t add = (uint64_t)h.message_count - 1;
+        if (h.base_offset > ~0ull - add) {
+            out->error = IGGY_SEG_OFFSET_OVERFLOW;
+            out->position = position;
+            return 0;
+        }
+        const uint64_t batch_end = h.base_offset + add, ts = h.base_timestamp;
+        if (!have_index || position - indexed >= 64 * 1024) {  // INDEX_STRIDE_BYTES (:2799)
+            have_index = true;
+            indexed = position;
+            if (index_out && nidx < index_cap) {
+                memcpy(index_out + 24 * nidx + 0, &h.base_offset, 8);
+                memcpy(index_out + 24 * nidx + 8, &ts, 8);
+                memcpy(index_out + 24 * nidx + 16, &position, 8);
+            }
+            ++nidx;
+        }
+        if (!have_stats) {
+            out->start_timestamp = ts;
+            out->max_timestamp = ts;
+        } else if (ts > out->max_timestamp) {
+            out->max_timestamp = ts;
+        }
+        have_stats = true;
+        out->end_offset = batch_end;
+        out->end_timestamp = ts;
+        out->batches++;
+        if (batch_end == ~0ull) {
+            out->error = IGGY_SEG_OFFSET_OVERFLOW;
+            out->position = position;
+            return 0;
+        }
+        next_offset = batch_end + 1;
+    }
+    out->index_entries = nidx;
+    if (!have_stats) {
+        out->error = IGGY_SEG_EMPTY;
+        return 0;
+    }
+    return nidx > index_cap && index_out ? IGGY_ERR_CAPACITY : 0;
+}
+
+int iggy_codec_segment_write_device(iggy_codec_ctx *c, int fd, uint64_t position, const uint8_t *d_bytes,
+                                    uint64_t len, int fsync, uint64_t *written) {
+    if (!c || fd < 0 || (!d_bytes && len)) return IGGY_ERR_INVALID_ARGUMENT;
+    DevGuard dg(c->device);
+    bind(c, nullptr);
+    if (written) *written = 0;
+    constexpr uint64_t kPiece = 8ull << 20;  // two 8 MiB pinned halves
+    if (!c->wstage) {
+        if (hipHostMalloc(&c->wstage, 2 * kPiece, hipHostMallocDefault) != hipSuccess) {
+            c->wstage = nullptr;
+            return IGGY_ERR_DEVICE;
+        }
+        for (auto &ev : c->wev)
+            if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) return IGGY_ERR_DEVICE;
+    }
+    const uint64_t npieces = (len + kPiece - 1) / kPiece;
+    auto issue = [&](uint64_t k) -> int {
+        const uint64_t off = k * kPiece, n = std::min(kPiece, len - off);
+        HIP_OK(hipMemcpyAsync((uint8_t *)c->wstage + (k & 1) * kPiece, d_bytes + off, n, hipMemcpyDeviceToHost,
+                              c->stream));
+        HIP_OK(hipEventRecord(c->wev[k & 1], c->stream));
+        return 0;
+    };
+    int r = npieces ? issue(0) : 0;
+    for (uint64_t k = 0; k < npieces && !r; ++k) {
+        HIP_OK(hipEventSynchronize(c->wev[k & 1]));
+        if (k + 1 < npieces) r = issue(k + 1);  // the next piece's copy runs under this pwrite
+        const uint64_t off = k * kPiece, n = std::min(kPiece, len - off);
+        const uint8_t *src = (const uint8_t *)c->wstage + (k & 1) * kPiece;
+        uint64_t done = 0;
+        while (done < n) {
+            const ssize_t w = pwrite(fd, src + done, n - done, (off_t)(position + off + done));
+            if (w <= 0) {
+                if (w < 0 && errno == EINTR) continue;
+                (void)hipStreamSynchronize(c->stream);
+                return IGGY_ERR_DEVICE;
+            }
+            done += (uint64_t)w;
+        }
+        if (written) *written += n;
+    }
+    if (r) return r;
+    if (fsync && fdatasync(fd) != 0) return IGGY_ERR_DEVICE;
     return 0;
 }
 

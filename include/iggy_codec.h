@@ -76,6 +76,9 @@ typedef enum iggy_error_kind {
     /* IggyError::InvalidCommand: batch_error's mapping of every structural WireError
      * on the server paths (server_common/src/send_messages.rs:52-66) */
     IGGY_ERR_INVALID_COMMAND = 22,
+    /* IggyError::InvalidMessagesCount: a transferred segment batch with no messages
+     * (core/partitions/src/state_transfer.rs:766-771) */
+    IGGY_ERR_INVALID_MESSAGES_COUNT = 23,
     /* library-level failures (not wire errors) */
     IGGY_ERR_DEVICE = 100,
     IGGY_ERR_INVALID_ARGUMENT = 101,
@@ -412,6 +415,49 @@ typedef struct iggy_segment_recovery {
 
 int iggy_codec_recover_segment(iggy_codec_ctx *ctx, const uint8_t *messages, uint64_t len,
                                uint64_t start_offset, iggy_segment_recovery *out);
+
+/* SegmentWalkError (core/partitions/src/state_transfer.rs:664-709) */
+typedef enum iggy_segment_walk_error {
+    IGGY_SEG_OK = 0,
+    IGGY_SEG_BATCH = 1,                 /* position, source */
+    IGGY_SEG_BASE_OFFSET_MISMATCH = 2,  /* expected (manifest), actual */
+    IGGY_SEG_NON_CONTIGUOUS = 3,        /* expected, actual */
+    IGGY_SEG_OFFSET_OVERFLOW = 4,       /* position */
+    IGGY_SEG_EMPTY = 5
+} iggy_segment_walk_error;
+
+/* walk_segment_payload's outcome: SegmentWalkStats + the rebuilt sparse index. 112 B. */
+typedef struct iggy_segment_walk {
+    uint32_t error;                 /* iggy_segment_walk_error */
+    uint32_t _pad;
+    uint64_t position;              /* BATCH / OFFSET_OVERFLOW: byte position of the batch */
+    uint64_t expected, actual;      /* BASE_OFFSET_MISMATCH / NON_CONTIGUOUS */
+    iggy_wire_error source;         /* BATCH: the decode error as batch_error maps it
+                                       (server_common/src/send_messages.rs:52-66), or
+                                       IGGY_ERR_INVALID_MESSAGES_COUNT */
+    uint64_t end_offset, start_timestamp, end_timestamp, max_timestamp;  /* error == OK */
+    uint64_t batches;
+    uint64_t index_entries;         /* 24-B IggyIndex entries (iggy_index.rs:17-41) produced */
+} iggy_segment_walk;
+
+/* walk_segment_payload (core/partitions/src/state_transfer.rs:715-833): every batch
+ * of a transferred segment `.log` payload Verify-decoded (all message checksums and
+ * the batch checksum, on the GPU: one copy, every batch queued, one sync), offset
+ * continuity from the manifest's base_offset, the stats, and the locally rebuilt
+ * sparse index: one 24-B (base_offset, base_timestamp, position) entry for the first
+ * batch and then every >= 64 KiB (INDEX_STRIDE_BYTES, :2799). index_out (nullable)
+ * receives up to index_cap entries (IGGY_ERR_CAPACITY when more were produced). */
+int iggy_codec_walk_segment_payload(iggy_codec_ctx *ctx, const uint8_t *bytes, uint64_t len, uint64_t base_offset,
+                                    uint8_t *index_out, uint64_t index_cap, iggy_segment_walk *out);
+
+/* MessagesWriter::save_frozen_batches (core/partitions/src/messages_writer.rs:100-118)
+ * for stamped batches resident on the device: `len` bytes at d_bytes are copied to
+ * the host through the context's pinned staging (two halves in flight: the D2H of
+ * one piece overlaps the pwrite of the previous one) and written to the segment
+ * file descriptor `fd` at byte `position`; fdatasync afterwards when `fsync` is
+ * set. *written = bytes written. IGGY_ERR_DEVICE on an I/O failure (errno kept). */
+int iggy_codec_segment_write_device(iggy_codec_ctx *ctx, int fd, uint64_t position, const uint8_t *d_bytes,
+                                    uint64_t len, int fsync, uint64_t *written);
 
 /* ------------------------------------------- asynchronous (host buffers) */
 /* Server shard threads run one compio reactor each with NO blocking pool

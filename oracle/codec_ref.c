@@ -547,6 +547,91 @@ int oracle_select_batch_slice(const uint8_t *record, uint64_t len, const iggy_sl
     return 0;
 }
 
+/* walk_segment_payload — core/partitions/src/state_transfer.rs:715-833; decode_batch_slice
+ * there is server_common's Verify wrapper (errors mapped by batch_error,
+ * server_common/src/send_messages.rs:52-66). */
+static uint32_t batch_error_kind(int rc) {
+    return (rc == IGGY_ERR_INVALID_BATCH_CHECKSUM || rc == IGGY_ERR_INVALID_MESSAGE_CHECKSUM) ? (uint32_t)rc
+                                                                                             : IGGY_ERR_INVALID_COMMAND;
+}
+int oracle_walk_segment_payload(const uint8_t *bytes, uint64_t len, uint64_t base_offset, uint8_t *index_out,
+                                uint64_t index_cap, iggy_segment_walk *out) {
+    memset(out, 0, sizeof(*out));
+    uint64_t position = 0, next_offset = base_offset, indexed = 0, nidx = 0;
+    int have_stats = 0, have_index = 0;
+    while (position < len) {                                              /* :741 */
+        iggy_batch_header h;
+        iggy_wire_error e;
+        int rc = oracle_decode_batch_slice_with(bytes + position, len - position, IGGY_INTEGRITY_VERIFY, &h, NULL,
+                                                0, NULL, &e);
+        if (rc) {                                                         /* :750-755 */
+            out->error = IGGY_SEG_BATCH;
+            out->position = position;
+            if (batch_error_kind(rc) == IGGY_ERR_INVALID_COMMAND) set_err(&out->source, IGGY_ERR_INVALID_COMMAND, 0, 0, 0, 0);
+            else out->source = e;
+            return 0;
+        }
+        if (!have_stats && h.base_offset != base_offset) {                /* :757-762 */
+            out->error = IGGY_SEG_BASE_OFFSET_MISMATCH;
+            out->expected = base_offset;
+            out->actual = h.base_offset;
+            return 0;
+        }
+        if (h.base_offset != next_offset) {                               /* :763-768 */
+            out->error = IGGY_SEG_NON_CONTIGUOUS;
+            out->expected = next_offset;
+            out->actual = h.base_offset;
+            return 0;
+        }
+        if (h.message_count == 0) {                                       /* :769-774 */
+            out->error = IGGY_SEG_BATCH;
+            out->position = position;
+            set_err(&out->source, IGGY_ERR_INVALID_MESSAGES_COUNT, 0, 0, 0, 0);
+            return 0;
+        }
+        const uint64_t add = (uint64_t)h.message_count - 1;
+        if (h.base_offset > UINT64_MAX - add) {                           /* :777-783 checked_add */
+            out->error = IGGY_SEG_OFFSET_OVERFLOW;
+            out->position = position;
+            return 0;
+        }
+        const uint64_t batch_end = h.base_offset + add, ts = h.base_timestamp;
+        if (!have_index || position - indexed >= 64 * 1024) {             /* :799-806, INDEX_STRIDE_BYTES */
+            have_index = 1;
+            indexed = position;
+            if (index_out && nidx < index_cap) {
+                wr64(index_out + 24 * nidx + 0, h.base_offset);
+                wr64(index_out + 24 * nidx + 8, ts);
+                wr64(index_out + 24 * nidx + 16, position);
+            }
+            nidx++;
+        }
+        if (!have_stats) {                                                /* :807-820 */
+            out->start_timestamp = ts;
+            out->max_timestamp = ts;
+        } else if (ts > out->max_timestamp) {
+            out->max_timestamp = ts;
+        }
+        have_stats = 1;
+        out->end_offset = batch_end;
+        out->end_timestamp = ts;
+        out->batches++;
+        if (batch_end == UINT64_MAX) {                                    /* :821-825 */
+            out->error = IGGY_SEG_OFFSET_OVERFLOW;
+            out->position = position;
+            return 0;
+        }
+        next_offset = batch_end + 1;
+        position += h.batch_length;                                       /* :830 */
+    }
+    out->index_entries = nidx;
+    if (!have_stats) {
+        out->error = IGGY_SEG_EMPTY;
+        return 0;
+    }
+    return nidx > index_cap && index_out ? IGGY_ERR_CAPACITY : 0;
+}
+
 /* walk_disk_chunk — core/partitions/src/poll_plan.rs:950-1011, with
  * select_batch_slice + push_selected_batch_fragments (core/partitions/src/journal.rs:1025-1137).
  * `decode_batch_slice_with` there is server_common's wrapper (errors mapped by

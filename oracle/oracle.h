@@ -56,6 +56,9 @@ int oracle_stamp_batch(uint8_t *batch, uint64_t len, uint64_t base_offset,
 
 /* select_batch_slice + push_selected_batch_fragments header rewrite
  * (core/partitions/src/journal.rs:1025-1137) on a record that decodes. */
+/* walk_segment_payload (core/partitions/src/state_transfer.rs:715-833). */
+int oracle_walk_segment_payload(const uint8_t *bytes, uint64_t len, uint64_t base_offset, uint8_t *index_out,
+                                uint64_t index_cap, iggy_segment_walk *out);
 /* walk_disk_chunk (core/partitions/src/poll_plan.rs:950-1011). */
 int oracle_walk_disk_chunk(const uint8_t *chunk, uint64_t len, const iggy_slice_query *q, int integrity,
                            iggy_chunk_fragment *frags, uint8_t *headers, uint64_t cap, iggy_chunk_walk *out);

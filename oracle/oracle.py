@@ -67,6 +67,7 @@ def lib() -> ctypes.CDLL:
         L.oracle_admit_batch.argtypes = [vp, u64, u32, u64, ctypes.c_int, vp, u64, vp, vp]
         L.oracle_recover_segment.argtypes = [vp, u64, u64, vp]
         L.oracle_walk_disk_chunk.argtypes = [vp, u64, vp, ctypes.c_int, vp, vp, u64, vp]
+        L.oracle_walk_segment_payload.argtypes = [vp, u64, u64, vp, u64, vp]
         _lib = L
     return _lib
 
@@ -247,3 +248,17 @@ def walk_disk_chunk(chunk, kind: int, value: int, count: int, ceiling: int = 2**
                                       hdrs.ctypes.data, cap, ctypes.byref(w))
     n = min(w.fragments, cap)
     return rc, w, [frags[i] for i in range(n)], [hdrs[256 * i: 256 * i + 256].tobytes() for i in range(n)]
+
+
+def walk_segment_payload(payload, base_offset: int, index_cap: int = 4096):
+    """walk_segment_payload (state_transfer.rs:715-833) -> (rc, SegmentWalk, index bytes)"""
+    import numpy as np
+    from iggy_amd.abi import SegmentWalk
+
+    a = _as_np(payload)
+    idx = np.zeros(24 * max(index_cap, 1), dtype=np.uint8)
+    w = SegmentWalk()
+    rc = lib().oracle_walk_segment_payload(a.ctypes.data if a.size else None, a.size, base_offset, idx.ctypes.data,
+                                           index_cap, ctypes.byref(w))
+    n = min(w.index_entries, index_cap)
+    return rc, w, idx[: 24 * n].tobytes()

@@ -6,10 +6,17 @@ Per batch (the path starts and ends in host memory):
     --H2D--> encode_device --D2H--> wire bytes in pinned host memory (the "socket")
     --H2D--> decode_device(Verify) --D2H--> frame positions + result (the segment index)
 
-Two contexts on two streams alternate batches, so copies of one batch overlap
-kernels of the other. Reports the end-to-end GiB/s (batch bytes / wall time),
-the PCIe bytes moved, and each phase's share measured on an isolated batch.
-Writes one JSON line (recorded in DESIGN.md; never the bench `value`).
+Two modes:
+  streams : two contexts on two streams alternate whole batches (round 1).
+  async   : the product's asynchronous host API. The producer context encodes
+            (iggy_codec_encode_submit: H2D of the SoA on its copy-in stream, the
+            kernels, D2H of the wire bytes on its copy-out stream) and the server
+            context decodes each finished batch (iggy_codec_decode_submit), so the
+            two copy directions and the kernels of different batches overlap
+            (full duplex on the link).
+Reports the end-to-end GiB/s (batch bytes / wall time), the PCIe bytes moved,
+and each phase's share measured on an isolated batch. Writes one JSON line
+(recorded in DESIGN.md; never the bench `value`).
 """
 import argparse
 import ctypes
@@ -90,10 +97,45 @@ class Lane:
         assert int(self.h_pos[1]) == 48 + self.pl
 
 
+def run_async(src, n, batches):
+    """Producer context encodes, server context decodes, through submit / wait."""
+    import numpy as np
+    from iggy_amd.codec import raw_messages
+    A, B = Codec(0), Codec(0)
+    total = 256 + n * (48 + PL)
+    ids, ots, pay, pls = (src[k].numpy() for k in ("ids", "ots", "pay", "pls"))
+    raw = raw_messages(ids.view(np.uint64), ots.view(np.uint64), pay, pls.view(np.uint32))
+    wires = [torch.empty(total, dtype=torch.uint8).pin_memory().numpy() for _ in range(3)]
+    poss = [torch.empty(n, dtype=torch.int64).pin_memory().numpy().view(np.uint64) for _ in range(3)]
+
+    def once():
+        te, td = {}, {}
+        for b in range(batches + 2):
+            if b < batches:
+                te[b] = A.encode_submit(raw, 1, wires[b % 3])
+            if 1 <= b <= batches:
+                c = A.wait(te[b - 1])
+                assert c.error.kind == 0 and c.bytes == total, c.error
+                td[b - 1] = B.decode_submit(wires[(b - 1) % 3], abi.INTEGRITY_VERIFY, poss[(b - 1) % 3])
+            if b >= 2:
+                c = B.wait(td[b - 2])
+                assert c.error.kind == 0 and c.frame_count == n, c.error
+        assert int(poss[0][1]) == 48 + PL
+
+    once()  # warm: slots and scratch sized
+    t0 = time.perf_counter()
+    once()
+    wall = time.perf_counter() - t0
+    A.close()
+    B.close()
+    return wall
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batches", type=int, default=16)
     ap.add_argument("--messages", type=int, default=N)
+    ap.add_argument("--mode", choices=["streams", "async"], default="async")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
@@ -105,6 +147,8 @@ def main():
         "pay": torch.randint(0, 256, (n * PL,), dtype=torch.uint8, generator=g).pin_memory(),
         "pls": torch.full((n,), PL, dtype=torch.int32).pin_memory(),
     }
+    if args.mode == "async":
+        wall_async = run_async(src, n, args.batches)
     lanes = [Lane(dev, n, PL), Lane(dev, n, PL)]
     # warm + isolated phase timings
     for ln in lanes:
@@ -119,7 +163,8 @@ def main():
     for b in range(args.batches):
         lanes[b % 2].run(src)
     torch.cuda.synchronize()
-    wall = time.perf_counter() - t0
+    wall_streams = time.perf_counter() - t0
+    wall = wall_async if args.mode == "async" else wall_streams
     for ln in lanes:
         ln.check()
     batch_bytes = lanes[0].total
@@ -128,8 +173,9 @@ def main():
     copy_ms = phases["h2d_soa"] + phases["wire_d2h_h2d"] + phases["d2h_out"]
     total_ms = sum(phases.values())
     line = {
-        "config": "C4: encode->decode incl. pinned H2D/D2H, %d msgs x %d B per batch, %d batches, 2 streams"
-                  % (n, PL, args.batches),
+        "config": "C4: encode->decode incl. pinned H2D/D2H, %d msgs x %d B per batch, %d batches, mode %s"
+                  % (n, PL, args.batches, args.mode),
+        "streams_mode_e2e_gib_s": round(args.batches * lanes[0].total / wall_streams / 2**30, 3),
         "e2e_gib_s": round(args.batches * batch_bytes / wall / 2**30, 3),
         "ms_per_batch": round(wall / args.batches * 1e3, 3),
         "pcie_bytes_per_batch": pcie_per_batch,

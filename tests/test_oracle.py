@@ -300,3 +300,28 @@ def test_oracle_walk_disk_chunk_semantics():
     assert w.corrupt == 1 and w.consumed == starts[1] and w.fragments == 1
     rc, w, fr, hd = O.walk_disk_chunk(bad, abi.LOOKUP_OFFSET, 0, 100, integrity=1)
     assert w.corrupt == 0 and w.consumed == chunk.size and w.matched == 35
+
+
+def test_oracle_walk_segment_payload_semantics():
+    """state_transfer.rs:715-833: stats, a 24-B index entry for the first batch and
+    every >= 64 KiB, and the first invalid byte's error."""
+    recs, off = [], 500
+    for k, (n, pl) in enumerate(((100, 1000), (30, 50), (200, 1000), (10, 10))):
+        r = O.synth_batch(n, pl, pl, 0, seed=k)
+        rc, e, h, out = O.stamp_batch(r, off, 2000 + (k * 7) % 3)
+        recs.append(np.frombuffer(out, dtype=np.uint8).copy())
+        off += n
+    seg = np.concatenate(recs)
+    starts = np.cumsum([0] + [r.size for r in recs])
+    rc, w, idx = O.walk_segment_payload(seg, 500)
+    assert rc == 0 and w.error == abi.SEG_OK and w.batches == 4 and w.end_offset == 839
+    assert (w.start_timestamp, w.end_timestamp, w.max_timestamp) == (2000, 2000, 2002)
+    ents = [struct.unpack_from("<QQQ", idx, 24 * i) for i in range(w.index_entries)]
+    assert ents[0] == (500, 2000, 0)
+    assert all(e[2] in starts for e in ents) and ents[1][2] >= 65536
+    rc, w, _ = O.walk_segment_payload(seg, 501)
+    assert w.error == abi.SEG_BASE_OFFSET_MISMATCH and (w.expected, w.actual) == (501, 500)
+    rc, w, _ = O.walk_segment_payload(seg[: starts[2] + 10], 500)
+    assert w.error == abi.SEG_BATCH and w.position == starts[2] and w.source.kind == abi.ERR_INVALID_COMMAND
+    rc, w, _ = O.walk_segment_payload(seg[:0], 500)
+    assert w.error == abi.SEG_EMPTY
