@@ -160,11 +160,11 @@ int ensure_decode_scratch(iggy_codec_ctx *c, uint64_t len) {
         if (r) return r;
         HIP_OK(hipMemset(c->dsync.p, 0, kSyncBytes));
     }
-    // 16 epoch-tagged halves per unit (64 frames), 4 units per chunk; zeroed so
-    // no stale tag can match a live epoch
-    r |= c->dsums.ensure(max_chunks * kUnitSumRows * 8 + 64);
+    // one 128-B block record per 128 frames (2 per chunk, decode_uniform.hip); zeroed
+    // so no stale tag can match a live epoch
+    r |= c->dsums.ensure(max_chunks * kChunkSumWords * 8 + 64);
     if (!r && c->dsums.p) HIP_OK(hipMemset(c->dsums.p, 0, c->dsums.cap));
-    r |= c->derr.ensure(max_chunks * 4 * 16);
+    r |= c->derr.ensure(max_chunks * 32 * 16);  // (stored, computed) per 8-frame group
     r |= c->gtiles_s.ensure(ntiles * 8);
     r |= c->gtiles_x.ensure(ntiles * 8);
     r |= c->gtiles_cnt.ensure(ntiles * 4);
@@ -192,7 +192,7 @@ DecodeScratch dscratch(iggy_codec_ctx *c) {
     s.small = c->dsync.as<uint8_t>(kSyncSmall);
     s.gbar = c->dsync.as<uint32_t>(kSyncBar);
     s.gmisc = c->dsync.as<uint64_t>(kSyncMisc);
-    s.max_chunks = (c->dsums.cap - 64) / (kUnitSumRows * 8);
+    s.max_chunks = (c->dsums.cap - 64) / (kChunkSumWords * 8);
     return s;
 }
 
@@ -278,7 +278,10 @@ int enqueue_decode(iggy_codec_ctx *c, const uint8_t *d_body, uint64_t len, int i
                    uint64_t *d_pos, uint64_t cap, iggy_decode_result *d_res, hipStream_t s) {
     int r = ensure_decode_scratch(c, len);
     if (r) return r;
-    if (++c->epoch == 0) c->epoch = 1;
+    if (++c->epoch > kEpochMask) {  // 24-bit tags: re-zero the block records before reusing one
+        c->epoch = 1;
+        HIP_OK(hipMemsetAsync(c->dsums.p, 0, c->dsums.cap, s));
+    }
     const bool verify = integrity == IGGY_INTEGRITY_VERIFY;
     DecodeScratch ds = dscratch(c);
     GeneralScratch gs = gscratch(c);
@@ -287,10 +290,10 @@ int enqueue_decode(iggy_codec_ctx *c, const uint8_t *d_body, uint64_t len, int i
     const uint32_t au = (uint32_t)c->allow_unaligned;
     prof_begin(c, 0, s);
     if (verify)
-        hipLaunchKernelGGL(k_decode_uniform<true>, dim3(grid), dim3(256), kUniformLds, s, d_body, len, d_pos,
+        hipLaunchKernelGGL(k_decode_uniform<true>, dim3(grid), dim3(kUniformThreads), kUniformLds, s, d_body, len, d_pos,
                            cap, d_res, ds, c->epoch, au, diag_bits(c));
     else
-        hipLaunchKernelGGL(k_decode_uniform<false>, dim3(grid), dim3(256), kUniformLds, s, d_body, len, d_pos,
+        hipLaunchKernelGGL(k_decode_uniform<false>, dim3(grid), dim3(kUniformThreads), kUniformLds, s, d_body, len, d_pos,
                            cap, d_res, ds, c->epoch, au, diag_bits(c));
     prof_end(c, 0, s);
     HIP_OK(hipGetLastError());
@@ -1816,7 +1819,7 @@ int iggy_codec_debug_set(iggy_codec_ctx *c, uint32_t bits) {
 }
 int iggy_codec_debug_clear(iggy_codec_ctx *c) {
     if (!c) return IGGY_ERR_INVALID_ARGUMENT;
-    HIP_OK(hipMemset(c->dsync.as<uint8_t>(kSyncSmall + 256), 0, 256));
+    HIP_OK(hipMemset(c->dsync.as<uint8_t>(kSyncSmall + 256), 0, 512));
     return 0;
 }
 

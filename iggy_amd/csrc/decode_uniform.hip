@@ -40,9 +40,9 @@ struct DecodeScratch {
     uint32_t *exited;     // producer waves that finished (reset by consumer)
     uint64_t *first_bad;  // ~index of first checksum mismatch (max-encoded), 0 = none
     uint64_t *spec_fail;  // ~index of first frame whose header breaks the stride
-    uint64_t *sums;       // [kUnitSumRows][max_chunks] column-per-chunk, epoch-tagged 32-bit halves
+    uint64_t *sums;       // [max_chunks][8 units][32] epoch-tagged 32-bit halves (256 B per unit)
                           // (half | epoch << 32); see publish_unit_sums
-    uint64_t *errslot;    // [max_chunks*4][2] (stored, computed) per wave
+    uint64_t *errslot;    // [max_chunks*32][2] (stored, computed) of the first mismatch per 8-frame group
     uint8_t *small;       // >= 512 B: short batch-checksum inputs
     uint32_t *gbar;       // the general kernel's barrier / registration words and its
     uint64_t *gmisc;      // first-bad slot: re-armed here (see k_decode_general)
@@ -58,7 +58,8 @@ constexpr uint32_t kLdsBytes = kSideOff + 4 * 64 * kSideLane;  // 155648
 // filled by kGatherWaves gatherer waves, drained by the chain wave
 constexpr uint32_t kBatch = 64;
 constexpr uint32_t kRing = 8;
-constexpr uint32_t kGatherWaves = 3;  // consumer WG waves 1..3; wave 0 (the chain) has SIMD 0 alone
+constexpr uint32_t kGatherWaves = 4;  // consumer WG waves 1..4; wave 0 runs the chain at raised priority
+constexpr uint32_t kUniformThreads = 320;  // 4 producer waves + 1 publisher wave per WG (consumer: chain + 4 gatherers)
 constexpr uint32_t kCtlOff = kRing * kBatch * 16 * 8;  // 64 KiB
 struct ChainCtl {
     uint32_t staged[kRing];  // (batch index + 1) << 7 | leading chunks of the slot staged so far
@@ -66,10 +67,6 @@ struct ChainCtl {
     uint32_t abort;         // a gatherer or the chain wave gave up (spin limit)
 };
 constexpr uint32_t kConsumerLds = kCtlOff + 64;
-// lane-group producers: kLgSlots x 10 KiB per wave (set where kLgSlots is)
-constexpr uint32_t kLgLds = 4 * 4 * 10 * 1024;
-constexpr uint32_t kUniformLds = kLgLds > kLdsBytes ? kLgLds : kLdsBytes;  // the grid's dynamic LDS
-static_assert(kConsumerLds <= kLgLds && kConsumerLds <= kLdsBytes, "consumer WG fits either grid's LDS");
 static_assert(kCtlOff + sizeof(ChainCtl) <= kConsumerLds, "consumer LDS");
 static_assert(kLdsBytes <= 160 * 1024, "LDS budget");
 
@@ -376,58 +373,59 @@ __device__ inline uint64_t short_hash(const uint8_t *slot, int lane, uint64_t L)
     return avalanche(acc);
 }
 
-// ------------------------------------------------------------- unit sums
-// A unit = 64 consecutive frames [256c - 6 + 64w, +64) (chunk c, quarter w).
-// Its interior batch-checksum words m = 256c + 64w + t (t < 63) are
-// hi32(cs_{m-6}) | lo32(cs_{m-5}) << 32: reduce them to 8 accumulator partial
-// sums and publish them as 16 epoch-tagged 32-bit halves, plus the two halves
-// of the unit's boundary words (lo32 of its first frame's checksum, hi32 of its
-// last), so the gatherer never reads the record. No flag, no fence: each 8-B
-// store is single-copy atomic and the gatherer checks every tag.
-// Layout: row (18w + t), column c, so a gatherer wave (lane = chunk) reads
-// every row with one coalesced 512-B load.
-// `stored` = stored checksum of frame 256c - 6 + 64w + lane.
-constexpr uint32_t kUnitRows = 18;
-constexpr uint32_t kUnitSumRows = 4 * kUnitRows;
-__device__ __forceinline__ uint64_t *unit_row(const DecodeScratch &sc, uint64_t c, uint32_t w, uint32_t t) {
-    return sc.sums + (uint64_t)(w * kUnitRows + t) * sc.max_chunks + c;
+// ---- block records: what the producers hand the batch-checksum chain
+// The chain consumes, per 1024-B block b of the checksum input (words m = 128b ..
+// 128b + 127, word m = hi32(cs_{m-6}) | lo32(cs_{m-5}) << 32 for the stored frame
+// checksums cs), the block's 8 accumulator partial sums. Block b is summed by the
+// producer WG that hashed its frames 128b - 6 .. 128b + 121 and published as ONE
+// 128-B line: 16 granules [data32 | spare8 << 32 | tag24 << 40], granule t = half
+// (t & 1) of acc[t >> 1] over words 128b .. 128b + 126; the spare bytes of granules
+// 0-3 carry lo32(cs_{128b-6}), of 4-7 hi32(cs_{128b+121}), from which the gatherer
+// forms the block's last word (it spans into block b + 1). No flag, no fence: each
+// 8-B store is single-copy atomic and the gatherer checks every tag.
+// Why lines: the gatherer's CU gets ~1/256 of HBM bandwidth under the producers'
+// full read stream (~20 GB/s), so it must read few bytes -- 1 MiB for C2. (32-frame
+// unit records, 144 B each, read 8 MiB: the chain waited ~200 us on them; 8-B
+// column-major granules written by many CUs cost ~100 us of partial-line writes.)
+constexpr uint32_t kBlockWords = 16;                     // granules per block record
+constexpr uint32_t kChunkSumWords = 2 * kBlockWords;     // u64 per 256-frame chunk
+constexpr uint32_t kUnitsPerChunk = 8;                   // 32-frame lane-group units
+constexpr uint32_t kEpochMask = 0xFFFFFF;                // host: tags wrap -> sums re-zeroed
+__device__ __forceinline__ uint64_t *block_rec(const DecodeScratch &sc, uint64_t b) {
+    return sc.sums + b * kBlockWords;
 }
-// cs_sec = secret word of checksum word m (stripe (m >> 3) & 15, lane m & 7)
-__device__ __forceinline__ uint64_t unit_cs_secret(uint64_t unit, int lane) {
-    const uint32_t tid = (uint32_t)((unit & 3) * 64 + lane);
-    return kSecretW8[((tid >> 3) & 15) + (tid & 7)];
-}
-__device__ __forceinline__ void publish_unit_sums(uint64_t Mreg, const DecodeScratch &sc, uint32_t epoch,
-                                                  uint64_t unit, int lane, uint64_t stored, uint64_t cs_sec) {
-    const uint32_t tid = (uint32_t)((unit & 3) * 64 + lane);
-    const uint64_t next = __shfl_down(stored, 1);
-    const uint64_t m = 256 * (unit >> 2) + tid;
-    uint64_t x = 0, y = 0;  // x -> acc[j], y -> acc[j^1]
-    if (lane < 63 && m >= 6 && m < Mreg) {
-        const uint64_t v = (stored >> 32) | (next << 32);
-        y = v;
-        x = mul32x32(v ^ cs_sec);
+// word m's contribution: acc[m & 7] += mul32x32(v ^ secret), acc[(m & 7) ^ 1] += v
+__device__ __forceinline__ void word_contrib(uint64_t Mreg, uint64_t m, uint64_t cur, uint64_t nxt, bool use,
+                                             uint64_t &x, uint64_t &y) {
+    if (use && m >= 6 && m < Mreg) {
+        const uint64_t v = (cur >> 32) | (nxt << 32);
+        y += v;
+        x += mul32x32(v ^ kSecretW8[((m >> 3) & 15) + (m & 7)]);
     }
+}
+// lanes hold words with m & 7 == lane & 7: returns acc[j] on lanes j < 8
+__device__ __forceinline__ uint64_t reduce_acc8(uint64_t x, uint64_t y) {
     x += __shfl_xor(x, 8); y += __shfl_xor(y, 8);
     x += __shfl_xor(x, 16); y += __shfl_xor(y, 16);
     x += __shfl_xor(x, 32); y += __shfl_xor(y, 32);
-    const uint64_t t8 = x + __shfl_xor(y, 1);  // lane t (< 8): partial acc[t]
-    const uint64_t tag = (uint64_t)epoch << 32;
-    const uint64_t c = unit >> 2;
-    const uint32_t w = (uint32_t)(unit & 3);
-    if (lane < 8) {
-        __hip_atomic_store(unit_row(sc, c, w, 2 * lane), (t8 & 0xffffffffull) | tag, __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(unit_row(sc, c, w, 2 * lane + 1), (t8 >> 32) | tag, __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
-    }
-    if (lane == 0)
-        __hip_atomic_store(unit_row(sc, c, w, 16), (stored & 0xffffffffull) | tag, __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
-    if (lane == 63)
-        __hip_atomic_store(unit_row(sc, c, w, 17), (stored >> 32) | tag, __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
+    return x + __shfl_xor(y, 1);
 }
+// t8: acc[j] on lanes j < 8 (all lanes call); first_lo / last_hi wave-uniform
+__device__ __forceinline__ void publish_block(const DecodeScratch &sc, uint32_t epoch, uint64_t b, int lane,
+                                              uint64_t t8, uint32_t first_lo, uint32_t last_hi) {
+    const uint32_t t = (uint32_t)lane & 15;
+    const uint64_t a = __shfl(t8, (int)(t >> 1));
+    const uint32_t data = (t & 1) ? (uint32_t)(a >> 32) : (uint32_t)a;
+    const uint32_t sp = t < 4 ? (first_lo >> (8 * t)) & 0xffu : t < 8 ? (last_hi >> (8 * (t - 4))) & 0xffu : 0u;
+    if (lane < 16)
+        __hip_atomic_store(block_rec(sc, b) + t, (uint64_t)data | ((uint64_t)sp << 32) | ((uint64_t)epoch << 40),
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// LDS-staged producers: waves 2k and 2k+1 hold the two halves of block 2c + k; the
+// odd wave hands its partial sums over in LDS (after the producer rings)
+constexpr uint32_t kXchOff = kLdsBytes;
+constexpr uint32_t kXchBytes = 512;  // [2][128 B] partials + first_lo|last_hi, then full[2], taken[2]
+__device__ __forceinline__ uint32_t *xch_flags(uint8_t *smem) { return (uint32_t *)(smem + kXchOff + 256); }
 
 // ------------------------------------------------------------- producer
 // One wave's whole life: every chunk of this WG, streamed through its ring.
@@ -454,6 +452,8 @@ __device__ __forceinline__ void produce(const uint8_t *blob, const UPlan &pl, ui
     };
     for (int d = 0; d < DEPTH; ++d) issue_next();
 
+    const uint64_t t_start = rt_now();
+    uint32_t it = 0;  // chunks done (the wave pair's exchange generation)
     for (uint64_t c = g; c < pl.nchunks; c += nprod) {
         const int64_t i = (int64_t)(256 * c) - 6 + 64 * (int64_t)wave + lane;
         const bool fvalid = i >= 0 && (uint64_t)i < pl.N;
@@ -470,7 +470,7 @@ __device__ __forceinline__ void produce(const uint8_t *blob, const UPlan &pl, ui
             else run_phase<PH, VERIFY>(smem + slot_last, side, lane, p, pl, st);
             ++k;
         }
-        if (dbg & 8) continue;
+        if (dbg & 8) { ++it; continue; }
         // ---- per-frame result
         uint64_t h = 0;
         if (VERIFY) {
@@ -506,7 +506,7 @@ __device__ __forceinline__ void produce(const uint8_t *blob, const UPlan &pl, ui
             const int leader = __builtin_ctzll(mb);
             if (lane == leader) {
                 atomicMax((unsigned long long *)sc.first_bad, (unsigned long long)~(uint64_t)i);
-                const uint64_t slot = c * 4 + wave;
+                const uint64_t slot = (uint64_t)(i + 6) >> 3;  // the frame's 8-frame group
                 __hip_atomic_store(&sc.errslot[2 * slot], stored, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 __hip_atomic_store(&sc.errslot[2 * slot + 1], h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
@@ -516,27 +516,71 @@ __device__ __forceinline__ void produce(const uint8_t *blob, const UPlan &pl, ui
             const int leader = __builtin_ctzll(sb);
             if (lane == leader) atomicMax((unsigned long long *)sc.spec_fail, (unsigned long long)~(uint64_t)i);
         }
-        if (VERIFY && pl.long_cs)
-            publish_unit_sums(pl.Mreg, sc, epoch, c * 4 + wave, lane, stored, unit_cs_secret(c * 4 + wave, lane));
+        if (VERIFY && pl.long_cs) {
+            // words m = i + 6 of this wave's 64 frames; lane 63's word spans into the
+            // next wave's frames (the even wave adds it after the exchange; the odd
+            // wave's is the block's last word, added by the gatherer)
+            const uint64_t m = (uint64_t)(i + 6);
+            uint64_t x = 0, y = 0;
+            word_contrib(pl.Mreg, m, stored, __shfl_down(stored, 1), lane < 63, x, y);
+            uint64_t t8 = reduce_acc8(x, y);
+            const uint32_t first_lo = (uint32_t)__shfl(stored, 0);
+            const uint32_t last_hi = (uint32_t)(__shfl(stored, 63) >> 32);
+            const uint32_t k = wave >> 1;
+            uint64_t *xv = (uint64_t *)(smem + kXchOff + 128u * k);
+            uint32_t *full = xch_flags(smem) + k, *taken = xch_flags(smem) + 2 + k;
+            bool ok = true;
+            if (wave & 1) {  // hand over once the even wave has taken the previous pair
+                while (__hip_atomic_load(taken, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != it) {
+                    __builtin_amdgcn_s_sleep(1);
+                    if (rt_now() - t_start > kSpinLimitTicks) { ok = false; break; }  // bug guard
+                }
+                if (lane < 8) xv[lane] = t8;
+                if (lane == 8) xv[8] = (uint64_t)first_lo | ((uint64_t)last_hi << 32);
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                if (ok && lane == 0) __hip_atomic_store(full, it + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            } else {
+                while (__hip_atomic_load(full, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != it + 1) {
+                    __builtin_amdgcn_s_sleep(1);
+                    if (rt_now() - t_start > kSpinLimitTicks) { ok = false; break; }
+                }
+                const uint64_t pt8 = xv[lane & 7];
+                const uint64_t pfl = xv[8];
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                if (lane == 0) __hip_atomic_store(taken, it + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                // the word joining the halves: hi32 of this wave's last frame, lo32 of the odd wave's first
+                uint64_t bx = 0, by = 0;
+                word_contrib(pl.Mreg, m - lane + 63, (uint64_t)last_hi << 32, pfl, true, bx, by);
+                t8 += pt8 + (lane == 7 ? bx : 0) + (lane == 6 ? by : 0);
+                if (ok) publish_block(sc, epoch, 2 * c + k, lane, t8, first_lo, (uint32_t)(pfl >> 32));
+            }
+        }
+        ++it;
     }
     wait_vm(0);
     if (lane == 0) __hip_atomic_fetch_add(sc.exited, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // ------------------------------------------------------- lane-group producer
-// Long frames (hashed length L > 240) under Verify. No LDS: 8 lanes per frame,
-// 8 frames per wave-instruction, every lane loading 16 B straight into VGPRs,
-// so one instruction reads 8 x 128 contiguous bytes (one 128-B segment of each
-// of 8 frames). This register-direct shape streams at ~6.4 TB/s on MI355X
-// (scripts/bw_micro.hip) where the LDS-DMA shape peaked at ~5.3 TB/s.
+// Long frames (hashed length L > 240) under Verify. 8 lanes per frame, 8 frames
+// (one "group") per wave-instruction: lane i of instruction k loads 16 B of frame
+// (i >> 3), so one instruction moves one 128-B segment of each of 8 frames. The
+// bytes are staged through LDS by global_load_lds_dwordx4 (the wave never waits on
+// a load it just issued: an explicit constant vmcnt keeps 3 steps in flight).
 //
 // Lane l of a frame group loads piece (m = l>>1) of stripe (2q + (l&1)) of
 // segment q: hashed words 2m, 2m+1, i.e. accumulators acc[2m], acc[2m+1] of
 // that stripe (acc[j] += mul32x32(w_j ^ s), acc[j^1] += w_j stays lane-local).
 // The two lanes of a pair hold partial sums of even / odd stripes; they are
 // combined (DPP quad_perm) at every 1024-B block end, scrambled, and carried
-// by the even lane. A unit = 64 frames = 8 groups processed in order; the next
-// (group, block) step's loads are in flight while the current one hashes.
+// by the even lane.
+//
+// Work order: a sweep over 128-frame blocks. Producer WG g takes blocks g, g + NP,
+// ...; at step j it takes unit (j & 3) of its block (j >> 2) (32 frames) and its
+// wave w the unit's 8-frame group w, so the chip reads a window of NP blocks at a
+// time and block b is done early (the batch-checksum chain starts after the first
+// blocks, not after each WG's first chunk). The 4 waves deposit each unit's stored
+// checksums in LDS; the WG's fifth wave sums and publishes each block.
 template <int CTRL>
 __device__ __forceinline__ uint64_t dpp64(uint64_t x) {
     const uint32_t lo = (uint32_t)__builtin_amdgcn_mov_dpp((int)(uint32_t)x, CTRL, 0xF, 0xF, false);
@@ -556,38 +600,37 @@ __device__ __forceinline__ uint64_t swz_xor4(uint64_t x) {  // ds_swizzle bit mo
 struct LgPlan {
     uint64_t S, N, L, nbF, ns, nchunks, Mreg;
     bool long_cs, nt, nopub;
+    uint32_t dbg;
 };
 __device__ __forceinline__ LgPlan lg_plan(const UPlan &p) {
     LgPlan q;
     q.S = p.S; q.N = p.N; q.L = p.L; q.nbF = p.nbF; q.ns = p.ns; q.nchunks = p.nchunks; q.Mreg = p.Mreg;
-    q.long_cs = p.long_cs; q.nt = p.nt; q.nopub = p.nopub;
+    q.long_cs = p.long_cs; q.nt = p.nt; q.nopub = p.nopub; q.dbg = 0;
     return q;
 }
 
 struct LgBuf {
-    uint4 v[8];       // 8 segments x 16 B of one block (or the partial block)
-    uint4 last;       // last stripe piece (final step only)
-    uint64_t stored;  // stored checksum (final step only)
+    uint4 v[8];  // 8 segments x 16 B of one block (or the partial block)
+    uint4 x;     // final step: the last-stripe piece (even lanes) / the stored checksum (odd lanes)
 };
 
 struct LgLane {  // per-lane constants
     uint32_t l, m, par, fg, poff;
     uint64_t s0[8], s1[8];
     uint64_t key0, key1, init0, init1, last0, last1, mrg0, mrg1;
-    uint64_t css0, css1;  // batch-checksum word secrets for even / odd units
 };
 
-__device__ __forceinline__ int64_t lg_frame_index(uint64_t u, uint32_t g, uint32_t fg) {
-    return (int64_t)(256 * (u >> 2)) - 6 + 64 * (int64_t)(u & 3) + 8 * (int64_t)g + fg;
+__device__ __forceinline__ int64_t lg_frame_index(uint64_t u, uint32_t w, uint32_t fg) {
+    return (int64_t)(32 * u) - 6 + 8 * (int64_t)w + fg;
 }
 
 // A frame group takes nsteps = nbF + (ns > 0) steps (at least 1): one per full
 // 1024-B block, plus one for the partial block when it has stripes. Every step
-// issues exactly 10 loads (8 pieces, last-stripe piece, stored checksum); the
-// last two are real only on the group's final step (elsewhere they re-read the
-// frame start and land in a sink). The constant count lets the compiler's
-// vmcnt bookkeeping wait for THIS step's loads while the next step's stay in
-// flight. C2 (L = 1064: nbF = 1, ns = 0) runs one 10-load step per group.
+// issues exactly 9 loads (8 pieces, then the last-stripe piece in even lanes and
+// the stored checksum in odd lanes); the ninth is real only on the group's final
+// step (elsewhere it re-reads the frame start and lands in a sink). The constant
+// count lets the wave wait for THIS step's loads while the next steps' stay in
+// flight. C2 (L = 1064: nbF = 1, ns = 0) runs one 9-load step per group.
 // uses of x cannot move above this point; forces x to be materialised here
 __device__ __forceinline__ void pin_after_wait(uint64_t &x) { asm volatile("" : "+v"(x)); }
 
@@ -596,16 +639,16 @@ __device__ __forceinline__ uint32_t lg_nsteps(const LgPlan &pl) {
     return n ? n : 1u;
 }
 
-// Issue one step: 10 x global_load_lds_dwordx4 (8 pieces, last-stripe piece,
-// frame start for the stored checksum) into the 10-KiB LDS slot `slot`; lane i
-// of instruction k lands at slot + 1024k + 16i, so each lane later reads back
+// Issue one step: 9 x global_load_lds_dwordx4 into the 9-KiB LDS slot `slot`; lane
+// i of instruction k lands at slot + 1024k + 16i, so each lane later reads back
 // exactly its own 16 B. The loads bypass VGPRs: the wave waits for them with an
 // explicit vmcnt, and never blocks on the step it has just issued.
-constexpr uint32_t kLgStepBytes = 10 * 1024;
+constexpr uint32_t kLgLoads = 9;
+constexpr uint32_t kLgStepBytes = kLgLoads * 1024;
 template <bool ONE>
 __device__ __forceinline__ void lg_issue(const uint8_t *blob, const LgPlan &pl, const LgLane &c, uint64_t u,
-                                         uint32_t g, uint32_t b, uint32_t nsteps, uint32_t slot) {
-    const int64_t i = lg_frame_index(u, g, c.fg);
+                                         uint32_t w, uint32_t b, uint32_t nsteps, uint32_t slot) {
+    const int64_t i = lg_frame_index(u, w, c.fg);
     const bool valid = i >= 0 && (uint64_t)i < pl.N;
     const uint8_t *fb = blob + (valid ? (uint64_t)i : 0) * pl.S;
     const uint8_t *hb = fb + 8 + 1024ull * b + c.poff;
@@ -624,15 +667,13 @@ __device__ __forceinline__ void lg_issue(const uint8_t *blob, const LgPlan &pl, 
 #pragma unroll
         for (int q = 0; q < 8; ++q) glds16((2 * q + c.par < pl.ns) ? hb + 128 * q : fb, slot + 1024u * q);
     }
-    glds16(fin ? fb + 8 + pl.L - 64 + 16 * c.m : fb, slot + 8u * 1024u);
-    glds16(fb, slot + 9u * 1024u);
+    glds16(fin && !c.par ? fb + 8 + pl.L - 64 + 16 * c.m : fb, slot + 8u * 1024u);
 }
 __device__ __forceinline__ void lg_read(const uint8_t *smem, uint32_t slot, int lane, LgBuf &B) {
     const uint8_t *p = smem + slot + 16u * (uint32_t)lane;
 #pragma unroll
     for (int q = 0; q < 8; ++q) B.v[q] = *(const uint4 *)(p + 1024u * q);
-    B.last = *(const uint4 *)(p + 8u * 1024u);
-    B.stored = *(const uint64_t *)(p + 9u * 1024u);
+    B.x = *(const uint4 *)(p + 8u * 1024u);
 }
 
 __device__ __forceinline__ void lg_piece(uint64_t &a0, uint64_t &a1, uint4 p, uint64_t s0, uint64_t s1) {
@@ -643,29 +684,30 @@ __device__ __forceinline__ void lg_piece(uint64_t &a0, uint64_t &a1, uint4 p, ui
 }
 
 struct LgState {
-    uint64_t a0, a1, cs_mine;
-    uint32_t sink;  // full steps' `last` / `stored` values land here (keeps their loads live)
-    bool sbad, unit_err;
+    uint64_t a0, a1, stored;
+    uint32_t sink;  // filler loads' values land here (keeps their loads live)
+    bool sbad;
 };
 
+// One step of one frame group. Returns true on the group's final step (the
+// frame's hash compared, st.stored = its stored checksum in the even lanes).
 template <bool ONE>
-__device__ __forceinline__ void lg_process(const LgPlan &pl, const LgLane &c, const DecodeScratch &sc,
-                                           uint32_t epoch, uint64_t *frame_pos, uint64_t cap, uint64_t u,
-                                           uint32_t g, uint32_t b, uint32_t nsteps, const LgBuf &B, LgState &st,
-                                           int lane) {
+__device__ __forceinline__ bool lg_process(const LgPlan &pl, const LgLane &c, const DecodeScratch &sc,
+                                           uint64_t *frame_pos, uint64_t cap, uint64_t u, uint32_t w, uint32_t b,
+                                           uint32_t nsteps, const LgBuf &B, LgState &st, int lane) {
     if (pl.nt) {  // diagnostics (dbg bit 64): staging only, no hashing
 #pragma unroll
         for (int q = 0; q < 8; ++q) st.sink += B.v[q].x ^ B.v[q].w;
-        st.sink += B.last.y ^ (uint32_t)B.stored;
-        return;
+        st.sink += B.x.y ^ B.x.x;
+        st.stored = 0;
+        return ONE || b + 1 == nsteps;
     }
     if (ONE || b == 0) {
-        if (g == 0) st.unit_err = false;
         st.a0 = c.init0;
         st.a1 = c.init1;
         // frame header: hashed word 3 = user_headers_len | payload_len (lane 2),
         // hashed word 4 = reserved (lane 4); both in the first segment
-        const int64_t i = lg_frame_index(u, g, c.fg);
+        const int64_t i = lg_frame_index(u, w, c.fg);
         const bool valid = i >= 0 && (uint64_t)i < pl.N;
         const uint4 h0 = B.v[0];
         st.sbad = valid && ((c.l == 2 && (uint64_t)kFrameHdr + h0.z + h0.w != pl.S) ||
@@ -692,33 +734,32 @@ __device__ __forceinline__ void lg_process(const LgPlan &pl, const LgLane &c, co
         }
     }
     if (!ONE && b + 1 != nsteps) {
-        // not the final step: those loads were fillers (consume every register they write)
-        st.sink += B.last.x ^ B.last.y ^ B.last.z ^ B.last.w ^ (uint32_t)B.stored ^ (uint32_t)(B.stored >> 32);
-        return;
+        st.sink += B.x.x ^ B.x.y ^ B.x.z ^ B.x.w;  // a filler load: consume the registers it writes
+        return false;
     }
-    // final step of the frame group: fold the pair, last stripe, merge, checks
+    // final step of the frame group: fold the pair, last stripe (even lanes), merge
     st.a0 += dpp64<kDppXor1>(st.a0);
     st.a1 += dpp64<kDppXor1>(st.a1);
-    lg_piece(st.a0, st.a1, B.last, c.last0, c.last1);
+    lg_piece(st.a0, st.a1, B.x, c.last0, c.last1);  // odd lanes: garbage, never used
     uint64_t t = fold64(st.a0 ^ c.mrg0, st.a1 ^ c.mrg1);
-    t += dpp64<kDppXor2>(t);
+    t += dpp64<kDppXor2>(t);  // the even lanes of the four m sum among themselves
     t += swz_xor4(t);
     const uint64_t h = avalanche(pl.L * P64_1 + t);
-    const int64_t i = lg_frame_index(u, g, c.fg);
+    const int64_t i = lg_frame_index(u, w, c.fg);
     const bool valid = i >= 0 && (uint64_t)i < pl.N;
-    const uint64_t stored = B.stored;
-    const bool mism = valid && h != stored;
-    // stored checksums, lane-per-frame, for the unit's batch-checksum words
-    const uint64_t mine = __shfl(stored, (int)(8 * c.l));
-    if (c.fg == g) st.cs_mine = mine;  // lane 8g + k <- frame 8g + k
+    // the stored checksum, loaded by the odd lane of each pair, for the even lane
+    const uint64_t sraw = (uint64_t)B.x.x | ((uint64_t)B.x.y << 32);
+    const uint64_t stored = dpp64<kDppXor1>(sraw);
+    st.stored = stored;
+    const bool mism = valid && !c.par && h != stored;
     const uint64_t mb = __ballot(mism);
-    if (mb && !st.unit_err) {  // groups run in index order: the first one is the unit's first
-        st.unit_err = true;
+    if (mb) {  // the group's first mismatching frame (lowest lane)
         const int leader = __builtin_ctzll(mb);
         if (lane == leader) {
             atomicMax((unsigned long long *)sc.first_bad, (unsigned long long)~(uint64_t)i);
-            __hip_atomic_store(&sc.errslot[2 * u], stored, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(&sc.errslot[2 * u + 1], h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const uint64_t grp = 4 * u + w;  // (i + 6) >> 3
+            __hip_atomic_store(&sc.errslot[2 * grp], stored, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(&sc.errslot[2 * grp + 1], h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
     }
     const uint64_t sb = __ballot(st.sbad);
@@ -726,45 +767,87 @@ __device__ __forceinline__ void lg_process(const LgPlan &pl, const LgLane &c, co
         const int leader = __builtin_ctzll(sb);
         if (lane == leader) atomicMax((unsigned long long *)sc.spec_fail, (unsigned long long)~(uint64_t)i);
     }
-    if (g == 7 && !pl.nopub) {  // unit complete
-        const int64_t fi = lg_frame_index(u, 0, 0) + lane;
-        if (frame_pos && fi >= 0 && (uint64_t)fi < pl.N && (uint64_t)fi < cap) frame_pos[fi] = (uint64_t)fi * pl.S;
-        if (pl.long_cs) publish_unit_sums(pl.Mreg, sc, epoch, u, lane, st.cs_mine, (u & 1) ? c.css1 : c.css0);
+    if (c.l == 0 && !pl.nopub && valid && (uint64_t)i < cap && frame_pos) frame_pos[i] = (uint64_t)i * pl.S;
+    return true;
+}
+
+// ---- per-WG unit combine in LDS (after the lane-group rings)
+// The 4 producer waves deposit each unit's stored checksums in LDS; the WG's fifth
+// wave publishes the unit's sums. Publishing from the producer waves themselves
+// cost +81 us per C2 decode: a producer's constant-vmcnt wait three steps later
+// must also cover its write-through stores, whose acknowledgements are slow under
+// the full read stream (diag ablation, scripts/diag_decode.py dbg 1 vs 129).
+constexpr uint32_t kLgSlots = 4;    // per wave: 1 step being hashed + 3 in flight (36 KiB)
+constexpr uint32_t kUcSlots = 16;   // units the producers may run ahead of the publisher (4 blocks)
+constexpr uint32_t kUcOff = 4 * kLgSlots * kLgStepBytes;  // [kUcSlots][32] u64, then cnt[], gen[]
+constexpr uint32_t kLgLds = kUcOff + kUcSlots * 256 + 2 * 4 * kUcSlots;
+__device__ __forceinline__ uint32_t *uc_cnt(uint8_t *smem) { return (uint32_t *)(smem + kUcOff + 256u * kUcSlots); }
+__device__ __forceinline__ uint32_t *uc_gen(uint8_t *smem) { return uc_cnt(smem) + kUcSlots; }
+
+// Producer wave w deposits its group's 8 stored checksums for the WG's j-th unit
+// (slot j % kUcSlots, once the publisher has released that slot's previous unit).
+__device__ __forceinline__ void lg_deposit(uint8_t *smem, const LgLane &c, uint64_t j, uint32_t wave, int lane,
+                                           uint64_t stored, uint64_t t_start) {
+    const uint32_t s = (uint32_t)(j % kUcSlots), gen = (uint32_t)(j / kUcSlots);
+    uint64_t *slotv = (uint64_t *)(smem + kUcOff + 256u * s);
+    while (__hip_atomic_load(&uc_gen(smem)[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != gen) {
+        __builtin_amdgcn_s_sleep(1);
+        if (rt_now() - t_start > kSpinLimitTicks) return;  // bug guard: the consumer times out
+    }
+    if (c.l == 0) slotv[8 * wave + c.fg] = stored;
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if (lane == 0) __hip_atomic_fetch_add(&uc_cnt(smem)[s], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+// The publisher wave: blocks g, g + np, ... in order, each as soon as its 4 units
+// are deposited: words t = 0..126 of the block from its 128 stored checksums (two
+// per lane), then the slots are released and the block record stored.
+__device__ __forceinline__ void lg_publisher(uint8_t *smem, const LgPlan &pl, const DecodeScratch &sc,
+                                             uint32_t epoch, uint32_t g, uint32_t np, int lane, uint32_t dbg) {
+    const uint64_t t_start = rt_now();
+    const uint64_t blocks = 2 * pl.nchunks;
+    if (g >= blocks) return;
+    const uint64_t mine = (blocks - g + np - 1) / np;
+    const uint64_t *vals = (const uint64_t *)(smem + kUcOff);
+    for (uint64_t jb = 0; jb < mine; ++jb) {
+        const uint32_t s0 = (uint32_t)((4 * jb) % kUcSlots), gen = (uint32_t)((4 * jb) / kUcSlots);
+        bool ok = true;
+        for (uint32_t q = 0; q < 4 && ok; ++q) {
+            while (__hip_atomic_load(&uc_cnt(smem)[s0 + q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != 4u) {
+                __builtin_amdgcn_s_sleep(1);
+                if (rt_now() - t_start > kSpinLimitTicks) { ok = false; break; }  // bug guard
+            }
+        }
+        if (!ok) return;
+        // block-relative checksum t lives in slot s0 + (t >> 5), entry t & 31
+        const uint64_t *bv = vals + 32u * s0;
+        const uint64_t c0 = bv[lane], n0 = bv[lane + 1], c1 = bv[64 + lane];
+        const uint64_t n1 = lane < 63 ? bv[65 + lane] : 0;
+        const uint32_t first_lo = (uint32_t)bv[0];
+        const uint32_t last_hi = (uint32_t)(bv[127] >> 32);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if (lane < 4) {
+            __hip_atomic_store(&uc_cnt(smem)[s0 + lane], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            __hip_atomic_store(&uc_gen(smem)[s0 + lane], gen + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+        if (!pl.long_cs || pl.nopub) continue;
+        const uint64_t b = g + jb * np;
+        uint64_t x = 0, y = 0;
+        word_contrib(pl.Mreg, 128 * b + lane, c0, n0, true, x, y);
+        word_contrib(pl.Mreg, 128 * b + 64 + lane, c1, n1, lane < 63, x, y);
+        publish_block(sc, epoch, b, lane, reduce_acc8(x, y), first_lo, last_hi);
+        if ((dbg & 512) && b < 2 && lane == 0) ((uint64_t *)(sc.small + 256))[10 + b] = rt_now();
     }
 }
 
-template <bool PIN>
-__device__ __forceinline__ void lg_lane_init(LgLane &c, int lane) {
-    c.l = lane & 7; c.m = c.l >> 1; c.par = c.l & 1; c.fg = (uint32_t)lane >> 3;
-    c.poff = 16 * (c.m + 4 * c.par);
-#pragma unroll
-    for (int q = 0; q < 8; ++q) {
-        c.s0[q] = kSecretW8[2 * q + c.par + 2 * c.m];
-        c.s1[q] = kSecretW8[2 * q + c.par + 2 * c.m + 1];
-    }
-    c.key0 = kSecretW8[16 + 2 * c.m]; c.key1 = kSecretW8[17 + 2 * c.m];
-    c.init0 = c.par ? 0 : kAccInit[2 * c.m]; c.init1 = c.par ? 0 : kAccInit[2 * c.m + 1];
-    c.last0 = kSecretLast[2 * c.m]; c.last1 = kSecretLast[2 * c.m + 1];
-    c.mrg0 = kSecretMerge[2 * c.m]; c.mrg1 = kSecretMerge[2 * c.m + 1];
-    c.css0 = unit_cs_secret(0, lane); c.css1 = unit_cs_secret(1, lane);
-    if (PIN) {
-#pragma unroll
-        for (int q = 0; q < 8; ++q) { pin_after_wait(c.s0[q]); pin_after_wait(c.s1[q]); }
-        pin_after_wait(c.key0); pin_after_wait(c.key1); pin_after_wait(c.init0); pin_after_wait(c.init1);
-        pin_after_wait(c.last0); pin_after_wait(c.last1); pin_after_wait(c.mrg0); pin_after_wait(c.mrg1);
-        pin_after_wait(c.css0); pin_after_wait(c.css1);
-    }
-}
-
-constexpr uint32_t kLgSlots = 4;  // per wave: 1 step being hashed + 3 in flight (40 KiB)
-static_assert(4 * kLgSlots * kLgStepBytes == kLgLds, "LDS sizing");
 // ONE: every frame group is a single full-block step (nbF == 1, ns == 0, i.e.
 // 1024 < L <= 1088: the C2 shape), so the step code has no partial-block or
-// filler paths.
+// filler paths. g / np: this WG among the producer WGs.
 template <uint32_t SLOTS, bool ONE>
 __device__ __forceinline__ void produce_lg(const uint8_t *blob, const LgPlan &pl, uint64_t *frame_pos, uint64_t cap,
-                                           const DecodeScratch &sc, uint32_t epoch, uint32_t gw, uint32_t nw,
+                                           const DecodeScratch &sc, uint32_t epoch, uint32_t g, uint32_t np,
                                            uint32_t wave, int lane, uint8_t *smem) {
+    const uint64_t t_start = rt_now();
     LgLane c;
     c.l = lane & 7; c.m = c.l >> 1; c.par = c.l & 1; c.fg = (uint32_t)lane >> 3;
     c.poff = 16 * (c.m + 4 * c.par);
@@ -777,33 +860,33 @@ __device__ __forceinline__ void produce_lg(const uint8_t *blob, const LgPlan &pl
     c.init0 = c.par ? 0 : kAccInit[2 * c.m]; c.init1 = c.par ? 0 : kAccInit[2 * c.m + 1];
     c.last0 = kSecretLast[2 * c.m]; c.last1 = kSecretLast[2 * c.m + 1];
     c.mrg0 = kSecretMerge[2 * c.m]; c.mrg1 = kSecretMerge[2 * c.m + 1];
-    c.css0 = unit_cs_secret(0, lane); c.css1 = unit_cs_secret(1, lane);
     // materialise every lane constant here: the hot loop then holds no
     // compiler-tracked load, so its only vmcnt waits are the explicit ones
 #pragma unroll
     for (int q = 0; q < 8; ++q) { pin_after_wait(c.s0[q]); pin_after_wait(c.s1[q]); }
     pin_after_wait(c.key0); pin_after_wait(c.key1); pin_after_wait(c.init0); pin_after_wait(c.init1);
     pin_after_wait(c.last0); pin_after_wait(c.last1); pin_after_wait(c.mrg0); pin_after_wait(c.mrg1);
-    pin_after_wait(c.css0); pin_after_wait(c.css1);
-    const uint64_t units = 4 * pl.nchunks;
-    const uint32_t nblk = ONE ? 1u : lg_nsteps(pl);  // steps per frame group
-    if (gw >= units) return;
-    const uint64_t total = (units - gw + nw - 1) / nw * 8 * nblk;  // steps of this wave
+    const uint64_t blocks = 2 * pl.nchunks;                // 128-frame blocks (tail blocks hold invalid frames)
+    const uint32_t nblk = ONE ? 1u : lg_nsteps(pl);       // steps per frame group
+    if (g >= blocks) return;
+    const uint64_t mine = 4 * ((blocks - g + np - 1) / np);  // units of blocks g, g + np, ...
+    const uint64_t total = mine * nblk;                   // steps of this wave
+    auto unit_of = [&](uint64_t j) -> uint64_t { return 4 * (g + (j >> 2) * np) + (j & 3); };
 
     LgState st;
-    st.a0 = c.init0; st.a1 = c.init1; st.cs_mine = 0; st.sbad = false; st.unit_err = false; st.sink = 0;
-    // processing cursor (pu, pg, pb) and issue cursor (iu, ig, ib) up to SLOTS-1 steps ahead
-    uint64_t pu = gw, iu = gw;
-    uint32_t pg = 0, pb = 0, ig = 0, ib = 0;
-    auto advance = [&](uint64_t &u, uint32_t &g, uint32_t &b) {
-        if (ONE || ++b == nblk) { b = 0; if (++g == 8) { g = 0; u += nw; } }
+    st.a0 = c.init0; st.a1 = c.init1; st.stored = 0; st.sbad = false; st.sink = 0;
+    // processing cursor (pj, pb) and issue cursor (ij, ib), up to SLOTS steps ahead
+    uint64_t pj = 0, ij = 0;
+    uint32_t pb = 0, ib = 0;
+    auto advance = [&](uint64_t &j, uint32_t &b) {
+        if (ONE || ++b == nblk) { b = 0; ++j; }
     };
     const uint32_t ring = wave * (SLOTS * kLgStepBytes);
     uint32_t iss = 0;  // steps issued
     auto issue_next = [&]() {
-        if (iu >= units) return;
-        lg_issue<ONE>(blob, pl, c, iu, ig, ib, nblk, ring + (iss % SLOTS) * kLgStepBytes);
-        advance(iu, ig, ib);
+        if (ij >= mine) return;
+        lg_issue<ONE>(blob, pl, c, unit_of(ij), wave, ib, nblk, ring + (iss % SLOTS) * kLgStepBytes);
+        advance(ij, ib);
         ++iss;
     };
     // every slot holds a step in flight; a slot is refilled as soon as its step has
@@ -811,25 +894,35 @@ __device__ __forceinline__ void produce_lg(const uint8_t *blob, const LgPlan &pl
     for (uint32_t d = 0; d < SLOTS; ++d) issue_next();
     for (uint64_t k = 0; k < total; ++k) {
         // step k landed; the later steps stay in flight (the last SLOTS-1 steps drain all)
-        if (k + SLOTS <= total) wait_vm_const<10 * (SLOTS - 1)>();
+        if (k + SLOTS <= total) wait_vm_const<kLgLoads * (SLOTS - 1)>();
         else wait_vm_const<0>();
         LgBuf B;
         const uint32_t slot = ring + (k % SLOTS) * kLgStepBytes;
         lg_read(smem, slot, lane, B);
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // slot read out before it is refilled
+        if ((pl.dbg & 512) && g == 0 && wave == 0 && lane == 0 && k < 4)
+            ((uint64_t *)(sc.small + 256))[12 + k] = rt_now();  // diagnostics: WG 0's first steps landed
         issue_next();  // step k + SLOTS into the slot just read
-        lg_process<ONE>(pl, c, sc, epoch, frame_pos, cap, pu, pg, pb, nblk, B, st, lane);
-        advance(pu, pg, pb);
+        const uint64_t u = unit_of(pj);
+        if (lg_process<ONE>(pl, c, sc, frame_pos, cap, u, wave, pb, nblk, B, st, lane))
+            lg_deposit(smem, c, pj, wave, lane, st.stored, t_start);
+        advance(pj, pb);
     }
     wait_vm(0);
     if (st.sink == 0x5eed5eedu && pl.N == 0) sc.small[lane] = 1;  // never true (N >= 1); keeps `sink` live
 }
 
+constexpr uint32_t kUniformLds = kLgLds > kXchOff + kXchBytes ? kLgLds : kXchOff + kXchBytes;  // dynamic LDS
+static_assert(kConsumerLds <= kLgLds && kConsumerLds <= kLdsBytes, "consumer WG fits either grid's LDS");
+static_assert(kUniformLds <= 160 * 1024, "LDS budget");
+
 // ------------------------------------------------------------- consumer
 // diagnostics (dbg bit 512): s_memrealtime stamps (100 MHz) of the consumer's
 // progress in sc.small[256..], read back with iggy_codec_debug_read:
 // [0] consumer start, [1] batch 0 staged, [2 + bi/8] batch bi (bi % 8 == 0),
-// [20] chain done, [21] all producers exited, [22] latest producer exit.
+// [10], [11] blocks 0, 1 published, [12 + k] WG 0 wave 0's step k landed (k < 4),
+// [20] chain done, [21] all producers exited, [22] latest producer exit,
+// [23 + bi/8] batch bi fully staged by its gatherer (bi % 8 == 0).
 __device__ __forceinline__ void dbg_stamp(const DecodeScratch &sc, uint32_t dbg, int idx) {
     if (dbg & 512) ((uint64_t *)(sc.small + 256))[idx] = rt_now();
 }
@@ -838,11 +931,15 @@ __device__ __forceinline__ uint64_t chain_batches(const UPlan &pl) {
     return ((pl.nb >> 1) + 1 + kBatch - 1) / kBatch;  // chunks 0 .. nb/2 hold blocks 0 .. nb
 }
 
+typedef uint32_t g4 __attribute__((ext_vector_type(4)));
+constexpr int kAuxSc1 = 16;  // buffer-load cache policy: sc1 (agent-coherent, as an agent-scope atomic load)
+
 // Gatherer wave gw (0..kGatherWaves-1) of the consumer WG: batches gw, gw + kGatherWaves, ...
-// Waits for the 4 producer waves of each of its 64 chunks, loads their partial
-// sums and the 4 wave-boundary words, and stages 16 block-sum words per chunk.
+// Lane c of a batch loads the block records of blocks 2c and 2c + 1 (256 B) and
+// stages their 16 accumulator sums, completed by the blocks' last words.
 __device__ __forceinline__ void gather(const uint8_t *blob, const UPlan &pl, const DecodeScratch &sc,
-                                       uint32_t epoch, uint32_t gw, uint8_t *smem, uint64_t t_start) {
+                                       uint32_t epoch, uint32_t gw, uint8_t *smem, uint64_t t_start,
+                                       uint32_t dbg) {
     const int lane = threadIdx.x & 63;
     ChainCtl *ctl = (ChainCtl *)(smem + kCtlOff);
     uint64_t *ring = (uint64_t *)smem;
@@ -852,36 +949,45 @@ __device__ __forceinline__ void gather(const uint8_t *blob, const UPlan &pl, con
         return __hip_atomic_load(&ctl->abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != 0 ||
                rt_now() - t_start > kSpinLimitTicks;
     };
+    const uint32_t tag = epoch << 8;  // high dword of a granule: spare8 | tag24 << 8
+    uint64_t npass = 0, npoll = 0, twait = 0;  // diagnostics (dbg 512)
     for (uint64_t bi = gw; bi < nbatch; bi += kGatherWaves) {
         const uint32_t slot = (uint32_t)(bi % kRing);
         bool abort = false;
+        const uint64_t tw0 = rt_now();
         while (bi >= kRing && (uint64_t)__hip_atomic_load(&ctl->consumed, __ATOMIC_ACQUIRE,
                                                           __HIP_MEMORY_SCOPE_WORKGROUP) + kRing <= bi) {
             __builtin_amdgcn_s_sleep(1);
             if (give_up()) { abort = true; break; }
         }
-        const uint64_t c = bi * kBatch + lane;
+        if (dbg & 512) twait += rt_now() - tw0;  // ring-full wait
+        const uint64_t cbase = bi * kBatch;
+        const uint64_t c = cbase + lane;
         const bool live = c < need && c < pl.nchunks;
         const bool has_next = live && c + 1 < pl.nchunks;
-        auto tag_ok = [&](uint64_t v) { return (uint32_t)(v >> 32) == epoch; };
-        // Progressive staging: every pass loads the 73 tagged granules of each chunk
-        // not staged yet (16 sum halves + 2 boundary halves per unit and the next
-        // chunk's first boundary half), stages the chunks whose tags all match, and
-        // publishes how many LEADING chunks of the batch are staged, so the chain
-        // starts on chunk 0 as soon as its 4 producer waves are done (not when the
-        // whole 64-chunk batch is). Between passes it polls one tagged word per unit
-        // of the lowest unstaged chunk.
+        // coherent 16-B loads (sc1: past this XCD's L1, as agent-scope atomic loads);
+        // out-of-range lanes read zeros
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+            (void *)block_rec(sc, 2 * cbase), 0,
+            (int)min<uint64_t>((sc.max_chunks - cbase) * kChunkSumWords * 8, 1u << 30), 0x00020000);
+        // Progressive staging: every pass loads the 32 tagged granules of each chunk
+        // (and lane 63 the next batch's first block's 4 spare-carrying granules),
+        // stages the chunks whose tags (and the next chunk's) all match, and publishes
+        // how many LEADING chunks of the batch are staged, so the chain starts on
+        // chunk 0 as soon as its 2 blocks are published. Between passes it polls the
+        // last granule of each block of the lowest unstaged chunk.
         bool staged = !live;
         uint32_t published = 0;
         for (bool first = true; !abort; first = false) {
+            if (dbg & 512) ++npass;
             if (!first) {
                 while (!abort) {
+                    if (dbg & 512) ++npoll;
                     bool ok = true;
                     if (!staged) {
-#pragma unroll
-                        for (int w = 0; w < 4; ++w)
-                            ok &= tag_ok(__hip_atomic_load(unit_row(sc, c, w, 17), __ATOMIC_RELAXED,
-                                                           __HIP_MEMORY_SCOPE_AGENT));
+                        const g4 a = __builtin_amdgcn_raw_buffer_load_b128(rs, (uint32_t)lane * 256u + 112u, 0, kAuxSc1);
+                        const g4 b = __builtin_amdgcn_raw_buffer_load_b128(rs, (uint32_t)lane * 256u + 240u, 0, kAuxSc1);
+                        ok = (a.w >> 8) == epoch && (b.w >> 8) == epoch;
                     }
                     const uint64_t pend = __ballot(!staged);
                     const uint64_t bad = __ballot(!ok);
@@ -891,61 +997,52 @@ __device__ __forceinline__ void gather(const uint8_t *blob, const UPlan &pl, con
                 }
                 if (abort) break;
             }
-            bool ok = true;
-            uint64_t B[16];
-            uint32_t first_lo[5], last_hi[4];
+            g4 r[16];
 #pragma unroll
-            for (int t = 0; t < 16; ++t) B[t] = 0;
+            for (int q = 0; q < 16; ++q)
+                r[q] = __builtin_amdgcn_raw_buffer_load_b128(rs, (uint32_t)lane * 256u + 16u * q, 0, kAuxSc1);
+            g4 nx0 = {0, 0, 0, 0}, nx1 = {0, 0, 0, 0};
+            if (lane == 63 && has_next) {  // the next batch's first chunk, block 2(c + 1)
+                nx0 = __builtin_amdgcn_raw_buffer_load_b128(rs, 64u * 256u, 0, kAuxSc1);
+                nx1 = __builtin_amdgcn_raw_buffer_load_b128(rs, 64u * 256u + 16u, 0, kAuxSc1);
+            }
+            bool own = true;
 #pragma unroll
-            for (int w = 0; w < 5; ++w) first_lo[w] = 0;
+            for (int q = 0; q < 16; ++q) own &= ((r[q].y & ~0xffu) == tag) & ((r[q].w & ~0xffu) == tag);
+            // spare bytes: granules 0-3 lo32(cs of the block's first frame), 4-7 hi32(cs of its last)
+            auto spare = [](const g4 &p, const g4 &q2) -> uint32_t {
+                return (p.y & 0xff) | (p.w & 0xff) << 8 | (q2.y & 0xff) << 16 | (q2.w & 0xff) << 24;
+            };
+            const uint32_t first0 = spare(r[0], r[1]), last0 = spare(r[2], r[3]);
+            const uint32_t first1 = spare(r[8], r[9]), last1 = spare(r[10], r[11]);
+            // the next chunk's first block's first frame: from lane c + 1 (or the loads above)
+            const bool nx_ok = ((nx0.y & ~0xffu) == tag) & ((nx0.w & ~0xffu) == tag) &
+                               ((nx1.y & ~0xffu) == tag) & ((nx1.w & ~0xffu) == tag);
+            uint32_t next_first = (uint32_t)__shfl_down((int)first0, 1);
+            bool next_ok = __shfl_down((int)own, 1) != 0;
+            if (lane == 63) { next_first = spare(nx0, nx1); next_ok = nx_ok; }
+            const bool ok = own && (!has_next || next_ok);
+            if (!staged && ok) {
+                uint64_t B[16];
 #pragma unroll
-            for (int w = 0; w < 4; ++w) last_hi[w] = 0;
-            if (!staged) {
-#pragma unroll
-                for (int w = 0; w < 4; ++w) {
-#pragma unroll
-                    for (int t = 0; t < 8; ++t) {
-                        const uint64_t lo = __hip_atomic_load(unit_row(sc, c, w, 2 * t), __ATOMIC_RELAXED,
-                                                              __HIP_MEMORY_SCOPE_AGENT);
-                        const uint64_t hi = __hip_atomic_load(unit_row(sc, c, w, 2 * t + 1), __ATOMIC_RELAXED,
-                                                              __HIP_MEMORY_SCOPE_AGENT);
-                        ok &= tag_ok(lo) & tag_ok(hi);
-                        // units 0, 1 of chunk c -> block 2c; units 2, 3 -> block 2c+1
-                        B[8 * (w >> 1) + t] += (lo & 0xffffffffull) | (hi << 32);
+                for (int t = 0; t < 8; ++t) {
+                    B[t] = (uint64_t)r[t].x | ((uint64_t)r[t].z << 32);
+                    B[8 + t] = (uint64_t)r[8 + t].x | ((uint64_t)r[8 + t].z << 32);
+                }
+                // the blocks' last words m = 256c + 127, 256c + 255: j = 7 of stripe 15
+                auto last_word = [&](uint64_t m, uint32_t hi32, uint32_t lo32, uint64_t &b6, uint64_t &b7) {
+                    if (m >= 6 && m < pl.Mreg) {
+                        const uint64_t v = (uint64_t)hi32 | ((uint64_t)lo32 << 32);
+                        b6 += v;
+                        b7 += mul32x32(v ^ kSecretW8[15 + 7]);
                     }
-                    const uint64_t f = __hip_atomic_load(unit_row(sc, c, w, 16), __ATOMIC_RELAXED,
-                                                         __HIP_MEMORY_SCOPE_AGENT);
-                    const uint64_t l = __hip_atomic_load(unit_row(sc, c, w, 17), __ATOMIC_RELAXED,
-                                                         __HIP_MEMORY_SCOPE_AGENT);
-                    ok &= tag_ok(f) & tag_ok(l);
-                    first_lo[w] = (uint32_t)f;
-                    last_hi[w] = (uint32_t)l;
-                }
-                if (has_next) {
-                    const uint64_t f = __hip_atomic_load(unit_row(sc, c + 1, 0, 16), __ATOMIC_RELAXED,
-                                                         __HIP_MEMORY_SCOPE_AGENT);
-                    ok &= tag_ok(f);
-                    first_lo[4] = (uint32_t)f;
-                }
-                if (ok) {
+                };
+                last_word(256 * c + 127, last0, first1, B[6], B[7]);
+                last_word(256 * c + 255, last1, has_next ? next_first : 0u, B[14], B[15]);
+                uint64_t *dst = ring + ((uint64_t)slot * kBatch + lane) * 16;
 #pragma unroll
-                    for (int w = 0; w < 4; ++w) {
-                        // unit-boundary word m = 256c + 64w + 63 = hi32(cs of the unit's last frame)
-                        //                                        | lo32(cs of the next unit's first frame) << 32
-                        const uint64_t m = 256 * c + 64 * w + 63;
-                        if (m >= 6 && m < pl.Mreg) {
-                            const uint64_t v = (uint64_t)last_hi[w] | ((uint64_t)first_lo[w + 1] << 32);
-                            // lane j = 7 of stripe (8w + 7) mod 16: acc[6] += v, acc[7] += mul
-                            const int hb = w >> 1;
-                            B[8 * hb + 6] += v;
-                            B[8 * hb + 7] += mul32x32(v ^ kSecretW8[((8 * w + 7) & 15) + 7]);
-                        }
-                    }
-                    uint64_t *dst = ring + ((uint64_t)slot * kBatch + lane) * 16;
-#pragma unroll
-                    for (int t = 0; t < 16; ++t) dst[t] = B[t];
-                    staged = true;
-                }
+                for (int t = 0; t < 16; ++t) dst[t] = B[t];
+                staged = true;
             }
             const uint64_t notyet = __ballot(!staged);
             const uint32_t k = notyet ? (uint32_t)__builtin_ctzll(notyet) : 64u;
@@ -955,7 +1052,10 @@ __device__ __forceinline__ void gather(const uint8_t *blob, const UPlan &pl, con
                                        __HIP_MEMORY_SCOPE_WORKGROUP);
                 published = k;
             }
-            if (k == 64) break;
+            if (k == 64) {
+                if (lane == 0 && (bi & 7) == 0) dbg_stamp(sc, dbg, 23 + (int)(bi >> 3));
+                break;
+            }
             if (give_up()) abort = true;
         }
         if (abort) {
@@ -963,11 +1063,15 @@ __device__ __forceinline__ void gather(const uint8_t *blob, const UPlan &pl, con
             return;
         }
     }
+    if ((dbg & 512) && lane == 0) {
+        uint64_t *d = (uint64_t *)(sc.small + 512) + 4 * gw;
+        d[0] = npass; d[1] = npoll; d[2] = twait; d[3] = rt_now() - t_start;
+    }
 }
 
 // The consumer WG (block 0): wave 0 runs the serial batch-checksum chain
 // (batch.rs:439-459 / 474-505) and the precedence resolution of
-// decode_batch_slice_with (batch.rs:395-421); waves 1..3 gather its inputs.
+// decode_batch_slice_with (batch.rs:395-421); waves 1..4 gather its inputs.
 template <bool VERIFY>
 __device__ __forceinline__ void consumer(const uint8_t *body, const HeaderInfo &hi, const UPlan &pl,
                                          iggy_decode_result *result, const DecodeScratch &sc,
@@ -1017,10 +1121,11 @@ __device__ __forceinline__ void consumer(const uint8_t *body, const HeaderInfo &
         __syncthreads();
     }
     if (wave != 0) {  // gatherer waves feed the chain wave through the LDS ring
-        if (chain && wave <= kGatherWaves) gather(blob, pl, sc, epoch, wave - 1, smem, t_start);
+        if (chain && wave <= kGatherWaves) gather(blob, pl, sc, epoch, wave - 1, smem, t_start, dbg);
         return;
     }
     if (chain) {
+        __builtin_amdgcn_s_setprio(3);  // a gatherer shares this wave's SIMD: the chain issues first
         ChainCtl *ctl = (ChainCtl *)(smem + kCtlOff);
         const uint64_t *ring = (const uint64_t *)smem;
         const int j = lane & 7;
@@ -1161,7 +1266,7 @@ __device__ __forceinline__ void consumer(const uint8_t *body, const HeaderInfo &
     uint32_t kind = IGGY_OK, reason = 0, status = kStatusDone;
     uint64_t a = 0, b = 0, c = 0, nframes = pl.N;
     auto msg_err = [&](uint64_t idx) {
-        const uint64_t slot = ((idx + 6) >> 8) * 4 + (((idx + 6) >> 6) & 3);
+        const uint64_t slot = (idx + 6) >> 3;  // the frame's 8-frame group
         kind = IGGY_ERR_INVALID_MESSAGE_CHECKSUM;
         if (tail_bad && idx == pl.N - 1) {
             a = tail_stored;
@@ -1211,7 +1316,7 @@ __device__ __forceinline__ bool uniform_uses_lg(const UPlan &pl, uint32_t dbg) {
 // Producers never wait for the consumer, so a grid that is only partly resident
 // (or kernels serialised by a profiler) still completes.
 template <bool VERIFY>
-__global__ __launch_bounds__(256, 1) void k_decode_uniform(const uint8_t *__restrict__ body, uint64_t len,
+__global__ __launch_bounds__(kUniformThreads, 1) void k_decode_uniform(const uint8_t *__restrict__ body, uint64_t len,
                                                            uint64_t *frame_pos, uint64_t cap,
                                                            iggy_decode_result *result, DecodeScratch sc,
                                                            uint32_t epoch, uint32_t allow_unaligned,
@@ -1245,11 +1350,18 @@ __global__ __launch_bounds__(256, 1) void k_decode_uniform(const uint8_t *__rest
     if (VERIFY && lg) {
         pl.nt = (dbg & 64) != 0;
         pl.nopub = (dbg & 128) != 0;
-        const LgPlan lp = lg_plan(pl);
+        LgPlan lp = lg_plan(pl);
+        lp.dbg = dbg;
+        if (threadIdx.x < 2 * kUcSlots) uc_cnt(smem)[threadIdx.x] = 0;  // unit-combine counters, generations
+        __syncthreads();
+        if (wave == 4) {  // the WG's publisher
+            lg_publisher(smem, lp, sc, epoch, g, nprod, lane, dbg);
+            return;
+        }
         if (lp.nbF == 1 && lp.ns == 0)
-            produce_lg<kLgSlots, true>(blob, lp, frame_pos, cap, sc, epoch, g * 4 + wave, nprod * 4, wave, lane, smem);
+            produce_lg<kLgSlots, true>(blob, lp, frame_pos, cap, sc, epoch, g, nprod, wave, lane, smem);
         else
-            produce_lg<kLgSlots, false>(blob, lp, frame_pos, cap, sc, epoch, g * 4 + wave, nprod * 4, wave, lane, smem);
+            produce_lg<kLgSlots, false>(blob, lp, frame_pos, cap, sc, epoch, g, nprod, wave, lane, smem);
         // Exit count: relaxed after this wave's own vmcnt drain. Everything the
         // consumer reads after it (first_bad, spec_fail, errslot, unit sums) was
         // written by device atomics or sc1 stores and is read with sc1 loads, so no
@@ -1261,6 +1373,9 @@ __global__ __launch_bounds__(256, 1) void k_decode_uniform(const uint8_t *__rest
         if (lane == 0) __hip_atomic_fetch_add(sc.exited, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         return;
     }
+    if (threadIdx.x < 4) xch_flags(smem)[threadIdx.x] = 0;  // the wave pairs' exchange flags
+    __syncthreads();
+    if (wave >= 4) return;  // the LDS-staged producers are waves 0-3
     pl.nt = (dbg & 16) != 0;
     if (VERIFY && pl.long_frames)
         produce<8, 4, 3, VERIFY>(blob, pl, frame_pos, cap, sc, epoch, g, nprod, wave, lane, smem, dbg);

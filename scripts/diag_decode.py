@@ -37,7 +37,7 @@ def main():
     torch.cuda.set_stream(ts)
     stream = ts.cuda_stream
     assert stream != 0
-    batch = bench.make_batch(ctxs[0], n, pl, pl, 0, dev, stream)[0]
+    batch = bench.make_batch(next(iter(ctxs.values())), n, pl, pl, 0, dev, stream)[0]
     L = batch.numel()
     if os.environ.get("DIAG_HIPMALLOC"):  # the record in a plain hipMalloc buffer instead of torch's allocator
         hip = ctypes.CDLL("libamdhip64.so")
@@ -67,7 +67,7 @@ def main():
     for integ in (0, 1):
         for rnd in range(3):
             for v, cx in ctxs.items():
-                if integ == 1 and v != 0:
+                if integ == 1 and v != variants[0]:
                     continue
                 for _ in range(2):
                     rc = cx.decode_device(batch.data_ptr(), L, integ, d_pos.data_ptr(), n, d_res.data_ptr(), stream)
@@ -86,6 +86,26 @@ def main():
                 r = abi.DecodeResult.from_buffer_copy(d_res.cpu().numpy().tobytes())
                 print(f"integ={integ} dbg={v} round={rnd} ms={ms:.4f} GiB/s={L/ms/1e-3/2**30:.1f} "
                       f"err={r.error.kind} frames={r.frame_count} path={r.path}", flush=True)
+                if v & 512 and rnd == 2:  # progress stamps (10 ns ticks) of one more decode
+                    L_ = cx._L
+                    L_.iggy_codec_debug_clear.argtypes = [ctypes.c_void_p]
+                    L_.iggy_codec_debug_read.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64]
+                    assert L_.iggy_codec_debug_clear(cx._h) == 0
+                    rc = cx.decode_device(batch.data_ptr(), L, integ, d_pos.data_ptr(), n, d_res.data_ptr(), stream)
+                    buf = (ctypes.c_uint64 * 96)()
+                    assert L_.iggy_codec_debug_read(cx._h, buf, 768) == 0
+                    for gw in range(4):
+                        npass, npoll, twait, tend = list(buf)[64 + 4 * gw: 68 + 4 * gw]
+                        print(f"  gatherer {gw}: passes {npass} polls {npoll} ring-wait {twait / 100:.1f} us"
+                              f" end {tend / 100:.1f} us", flush=True)
+                    st = list(buf)[32:64]
+                    t0 = st[0]
+                    rel = lambda x: f"{(x - t0) / 100:.1f}" if x else "-"  # noqa: E731
+                    print("  chain  batch 0,8,..: " + " ".join([rel(st[1])] + [rel(x) for x in st[3:10]])
+                          + f"  done {rel(st[20])}  producers exited {rel(st[21])}", flush=True)
+                    print("  staged batch 0,8,..: " + " ".join(rel(x) for x in st[23:31]), flush=True)
+                    print("  blocks 0,1 published: " + " ".join(rel(x) for x in st[10:12])
+                          + "  WG 0 steps 0-3 landed: " + " ".join(rel(x) for x in st[12:16]), flush=True)
 
 
 if __name__ == "__main__":
