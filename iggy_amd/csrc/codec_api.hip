@@ -92,6 +92,10 @@ struct iggy_codec_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
     int ncu = 256;
+    // uniform decode grid: one WG per CU but one. A pipelined decode's consumer WG
+    // (the previous batch's chain tail) then never holds back one of the next
+    // decode's producer WGs. IGGY_CODEC_UNIFORM_GRID overrides (tuning).
+    int ugrid = 255;
     uint32_t epoch = 0;
     int allow_unaligned = 0;
     uint32_t dbg = 0;  // IGGY_CODEC_DBG ablation bits: read only by the diagnostic build (kDiagMask)
@@ -286,7 +290,7 @@ int enqueue_decode(iggy_codec_ctx *c, const uint8_t *d_body, uint64_t len, int i
     DecodeScratch ds = dscratch(c);
     GeneralScratch gs = gscratch(c);
     // one persistent grid: one WG per CU, block 0 the consumer (chain) WG
-    const uint32_t grid = (uint32_t)std::max(2, c->ncu);
+    const uint32_t grid = (uint32_t)c->ugrid;
     const uint32_t au = (uint32_t)c->allow_unaligned;
     prof_begin(c, 0, s);
     if (verify)
@@ -372,6 +376,11 @@ int iggy_codec_create(int device, iggy_codec_ctx **out) {
     if (!c) return IGGY_ERR_DEVICE;
     c->device = device;
     c->ncu = prop.multiProcessorCount;
+    c->ugrid = std::max(2, c->ncu - 1);
+    if (const char *g = getenv("IGGY_CODEC_UNIFORM_GRID")) {
+        const long v = strtol(g, nullptr, 0);
+        if (v >= 2 && v <= c->ncu) c->ugrid = (int)v;
+    }
     if (kDiagMask)  // diagnostic build only
         if (const char *d = getenv("IGGY_CODEC_DBG")) c->dbg = (uint32_t)strtoul(d, nullptr, 0);
     if (hipSetDevice(device) != hipSuccess ||

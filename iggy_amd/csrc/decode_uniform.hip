@@ -836,7 +836,7 @@ __device__ __forceinline__ void lg_publisher(uint8_t *smem, const LgPlan &pl, co
         word_contrib(pl.Mreg, 128 * b + lane, c0, n0, true, x, y);
         word_contrib(pl.Mreg, 128 * b + 64 + lane, c1, n1, lane < 63, x, y);
         publish_block(sc, epoch, b, lane, reduce_acc8(x, y), first_lo, last_hi);
-        if ((dbg & 512) && b < 2 && lane == 0) ((uint64_t *)(sc.small + 256))[10 + b] = rt_now();
+        if ((dbg & 512) && b < 2 && lane == 0) ((uint64_t *)(sc.small + 256))[11 + b] = rt_now();
     }
 }
 
@@ -889,6 +889,15 @@ __device__ __forceinline__ void produce_lg(const uint8_t *blob, const LgPlan &pl
         advance(ij, ib);
         ++iss;
     };
+    // Staggered start: WG group g / 16 issues its first steps (g / 16) * stagger
+    // ticks after the kernel starts, so the first blocks -- the ones the serial
+    // checksum chain needs first -- are not queued behind the whole chip's first
+    // burst of loads.
+    {
+        const uint32_t stagger = (pl.dbg >> 16) & 0xff;
+        const uint64_t until = t_start + (uint64_t)(g >> 4) * stagger;
+        while (stagger && rt_now() < until) __builtin_amdgcn_s_sleep(1);
+    }
     // every slot holds a step in flight; a slot is refilled as soon as its step has
     // been read into registers, so SLOTS steps stay in flight while one is hashed
     for (uint32_t d = 0; d < SLOTS; ++d) issue_next();
@@ -901,7 +910,7 @@ __device__ __forceinline__ void produce_lg(const uint8_t *blob, const LgPlan &pl
         lg_read(smem, slot, lane, B);
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // slot read out before it is refilled
         if ((pl.dbg & 512) && g == 0 && wave == 0 && lane == 0 && k < 4)
-            ((uint64_t *)(sc.small + 256))[12 + k] = rt_now();  // diagnostics: WG 0's first steps landed
+            ((uint64_t *)(sc.small + 256))[13 + k] = rt_now();  // diagnostics: WG 0's first steps landed
         issue_next();  // step k + SLOTS into the slot just read
         const uint64_t u = unit_of(pj);
         if (lg_process<ONE>(pl, c, sc, frame_pos, cap, u, wave, pb, nblk, B, st, lane))
@@ -920,7 +929,7 @@ static_assert(kUniformLds <= 160 * 1024, "LDS budget");
 // diagnostics (dbg bit 512): s_memrealtime stamps (100 MHz) of the consumer's
 // progress in sc.small[256..], read back with iggy_codec_debug_read:
 // [0] consumer start, [1] batch 0 staged, [2 + bi/8] batch bi (bi % 8 == 0),
-// [10], [11] blocks 0, 1 published, [12 + k] WG 0 wave 0's step k landed (k < 4),
+// [11], [12] blocks 0, 1 published, [13 + k] WG 0 wave 0's step k landed (k < 4),
 // [20] chain done, [21] all producers exited, [22] latest producer exit,
 // [23 + bi/8] batch bi fully staged by its gatherer (bi % 8 == 0).
 __device__ __forceinline__ void dbg_stamp(const DecodeScratch &sc, uint32_t dbg, int idx) {

@@ -15,14 +15,19 @@
 #include <stdio.h>
 #include <stdlib.h>
 
+template <bool NT>
 __device__ __forceinline__ void glds(const void *g, uint32_t lds) {
-    asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off"
-                 :: "v"(g), "s"(__builtin_amdgcn_readfirstlane(lds)) : "memory", "m0");
+    if (NT)
+        asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off nt"
+                     :: "v"(g), "s"(__builtin_amdgcn_readfirstlane(lds)) : "memory", "m0");
+    else
+        asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off"
+                     :: "v"(g), "s"(__builtin_amdgcn_readfirstlane(lds)) : "memory", "m0");
 }
 template <int N>
 __device__ __forceinline__ void wvm() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
 
-template <int ORDER, int LOADS, int SLOTS>
+template <int ORDER, int LOADS, int SLOTS, bool NT = false>
 __global__ __launch_bounds__(256, 1) void k_order(const uint8_t *__restrict__ blob, uint64_t S, uint64_t N,
                                                   uint64_t *out) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
@@ -38,6 +43,7 @@ __global__ __launch_bounds__(256, 1) void k_order(const uint8_t *__restrict__ bl
     auto group_of = [&](uint64_t k) -> uint64_t {
         if (ORDER == 0) return (gw + (k / 8) * nw) * 8 + (k % 8);
         if (ORDER == 1) return (g + (k / 8) * nwg) * 32 + (k % 8) * 4 + wave;
+        if (ORDER == 3) return (g + (k / 4) * nwg) * 16 + (k % 4) * 4 + wave;  // 128-frame blocks per WG
         return k * nw + gw;
     };
     uint64_t mine = 0;
@@ -47,12 +53,12 @@ __global__ __launch_bounds__(256, 1) void k_order(const uint8_t *__restrict__ bl
         const uint8_t *fb = blob + (f < N ? f : 0) * S;
         const uint32_t slot = ring + (uint32_t)(k % SLOTS) * kStep;
 #pragma unroll
-        for (int q = 0; q < 8; ++q) glds(fb + 8 + 128 * q + poff, slot + 1024 * q);
+        for (int q = 0; q < 8; ++q) glds<NT>(fb + 8 + 128 * q + poff, slot + 1024 * q);
         if (LOADS == 10) {
-            glds(fb + 8 + 1000 + 16 * m, slot + 8192);
-            glds(fb, slot + 9216);
+            glds<NT>(fb + 8 + 1000 + 16 * m, slot + 8192);
+            glds<NT>(fb, slot + 9216);
         } else {  // 9 loads: even lanes the last-stripe piece, odd lanes the stored checksum
-            glds(par ? fb : fb + 8 + 1000 + 16 * m, slot + 8192);
+            glds<NT>(par ? fb : fb + 8 + 1000 + 16 * m, slot + 8192);
         }
     };
     uint32_t x = 0;
@@ -113,14 +119,12 @@ int main() {
                L / (sum / reps * 1e-3) / 1e9, best, L / (best * 1e-3) / 1e9);
     };
     for (int rep = 0; rep < 2; ++rep) {
-        timeit("unit64   10 loads 4 slots", (const void *)k_order<0, 10, 4>, 4 * 4 * 10240);
-        timeit("chunk-il 10 loads 4 slots", (const void *)k_order<1, 10, 4>, 4 * 4 * 10240);
-        timeit("unit8    10 loads 4 slots", (const void *)k_order<2, 10, 4>, 4 * 4 * 10240);
-        timeit("unit64    9 loads 4 slots", (const void *)k_order<0, 9, 4>, 4 * 4 * 9216);
-        timeit("chunk-il  9 loads 4 slots", (const void *)k_order<1, 9, 4>, 4 * 4 * 9216);
         timeit("unit8     9 loads 4 slots", (const void *)k_order<2, 9, 4>, 4 * 4 * 9216);
-        timeit("unit64   10 loads 3 slots", (const void *)k_order<0, 10, 3>, 4 * 3 * 10240);
-        timeit("chunk-il 10 loads 3 slots", (const void *)k_order<1, 10, 3>, 4 * 3 * 10240);
+        timeit("block128  9 loads 4 slots", (const void *)k_order<3, 9, 4>, 4 * 4 * 9216);
+        timeit("unit8     9 loads 4 slots nt", (const void *)k_order<2, 9, 4, true>, 4 * 4 * 9216);
+        timeit("block128  9 loads 4 slots nt", (const void *)k_order<3, 9, 4, true>, 4 * 4 * 9216);
+        timeit("block128  9 loads 3 slots nt", (const void *)k_order<3, 9, 3, true>, 4 * 3 * 9216);
+        timeit("unit64   10 loads 4 slots", (const void *)k_order<0, 10, 4>, 4 * 4 * 10240);
     }
     return 0;
 }
