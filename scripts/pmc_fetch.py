@@ -3,8 +3,10 @@ profiles/pmc_fetch.json: HBM bytes fetched per decode by the uniform decode's
 producer grid (k_uniform_lg for C2), corrected per MI355X_MICROARCH.md (gfx950
 FETCH_SIZE reports half the bytes of a wide streaming read: x2).
 
-usage: python scripts/pmc_fetch.py gpurun_out/pmc1/run_results.db [messages] [payload]
+usage: python scripts/pmc_fetch.py <pmc_counter_collection.csv | rocpd .db> [messages] [payload]
+(scripts/profile_round.sh writes gpurun_out/prof_<tag>/pmc1/pmc_counter_collection.csv)
 """
+import csv
 import json
 import os
 import sqlite3
@@ -18,10 +20,18 @@ def main():
     db_path = sys.argv[1]
     n = int(sys.argv[2]) if len(sys.argv) > 2 else 1 << 20
     pl = int(sys.argv[3]) if len(sys.argv) > 3 else 1024
-    db = sqlite3.connect(db_path)
-    rows = list(db.execute(
-        "select kernel_name, value, dispatch_id from counters_collection where counter_name = 'FETCH_SIZE' "
-        "order by dispatch_id"))
+    if db_path.endswith(".csv"):
+        acc = {}
+        for r in csv.DictReader(open(db_path)):
+            if r["Counter_Name"] == "FETCH_SIZE":
+                key = (r["Kernel_Name"], r["Dispatch_Id"])
+                acc[key] = acc.get(key, 0.0) + float(r["Counter_Value"])
+        rows = [(k[0], v, int(k[1])) for k, v in sorted(acc.items(), key=lambda kv: int(kv[0][1]))]
+    else:
+        db = sqlite3.connect(db_path)
+        rows = list(db.execute(
+            "select kernel_name, value, dispatch_id from counters_collection where counter_name = 'FETCH_SIZE' "
+            "order by dispatch_id"))
     per_kernel = {}
     for name, kb, _ in rows:
         per_kernel.setdefault(name.split("(")[0], []).append(kb)
