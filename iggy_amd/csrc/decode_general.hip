@@ -297,7 +297,12 @@ __device__ __forceinline__ void word_contrib(uint64_t m, uint64_t v, uint64_t &x
     x = mul32x32(v ^ kSecretW8[sib + j]);
 }
 
-// Frame verification. Lane group fg (8 lanes) of verify wave vw hashes frames
+// Frame verification. (C3 experiments, scripts/diag_general.py: byte-balanced
+// contiguous ranges per group, or a wave's groups claiming its frames as they
+// finish, cut the slowest group's 17 % lead over the mean but made the mean 12-16 %
+// slower -- the chip-wide front of consecutive frames is worth more; hashing the
+// <= 240 B frames inside the loop pushed the kernel past 256 VGPRs and spilled.)
+// Lane group fg (8 lanes) of verify wave vw hashes frames
 // f = 8 vw + fg + j * 8 nvw, j = 0, 1, ... at its own pace: every wave step
 // each group hashes one 1024-B block of its current frame while the next block
 // (or the next frame's first block and last stripe) is loading into the other
@@ -362,7 +367,7 @@ __device__ __forceinline__ void vissue(const uint8_t *blob, const VFrame &v, uin
 }
 
 __device__ inline void verify_frames(const uint8_t *blob, const GeneralScratch &gs, uint64_t nwalk,
-                                     uint32_t vw, uint32_t nvw, int lane) {
+                                     uint32_t vw, uint32_t nvw, int lane, uint64_t t0) {
     const uint32_t l = lane & 7, m = l >> 1, par = l & 1, fg = (uint32_t)lane >> 3;
     const uint32_t poff = 16 * (m + 4 * par);
     uint64_t s0[8], s1[8];
@@ -445,6 +450,12 @@ __device__ inline void verify_frames(const uint8_t *blob, const GeneralScratch &
         step(B, A);
     }
     if (l == 0 && bad != ~0ull) atomicMax((unsigned long long *)&gs.misc[2], (unsigned long long)~bad);
+    uint64_t *vstat = (uint64_t *)(gs.small + 512) + 14;  // phase clock: [14] last / [15] sum of loop ends
+    if (lane == 0) {
+        const uint64_t d = rt_now() - t0;
+        atomicMax((unsigned long long *)&vstat[0], (unsigned long long)d);
+        atomicAdd((unsigned long long *)&vstat[1], (unsigned long long)d);
+    }
     // frames of <= 240 hashed bytes: one lane each, after the streaming loop
     const uint64_t tid = 64ull * vw + lane, nth = 64ull * nvw;
     for (uint64_t f = tid; f < nwalk; f += nth) {
@@ -452,6 +463,7 @@ __device__ inline void verify_frames(const uint8_t *blob, const GeneralScratch &
         if (L <= 240 && xxh3_64_lane(blob + gs.fpos[f] + 8, L) != gs.cs[f])
             atomicMax((unsigned long long *)&gs.misc[2], (unsigned long long)~f);
     }
+    if (lane == 0) atomicMax((unsigned long long *)&vstat[2], (unsigned long long)(rt_now() - t0));  // [16]
 }
 
 // ------------------------------------------------------------------ kernel
@@ -510,6 +522,7 @@ __global__ __launch_bounds__(kGenThreads) void k_decode_general(const uint8_t *_
     }
     ok &= grid_barrier(gs.bar, nwg * ++phase, t0);
     gstamp(gs, member, 1, rt_now() - t0);
+    gstamp(gs, member, 14, 0); gstamp(gs, member, 15, 0); gstamp(gs, member, 16, 0);  // verify clock (below)
 
     // ---------------- B1: group summaries (one wave per 256 tiles, 4 per lane)
     for (uint64_t g = wid; g < ngroups; g += nwaves) {
@@ -936,7 +949,8 @@ __global__ __launch_bounds__(kGenThreads) void k_decode_general(const uint8_t *_
     } else if (VERIFY) {
         const uint32_t vw = member * (blockDim.x >> 6) + wave - 1;
         const uint32_t nvw = nwg * (blockDim.x >> 6) - 1;
-        verify_frames(blob, gs, nwalk, vw, nvw, lane);
+        if (vw == 0 && lane == 0) ((uint64_t *)(gs.small + 512))[17] = nvw;
+        verify_frames(blob, gs, nwalk, vw, nvw, lane, t0);
     }
     ok &= grid_barrier(gs.bar, nwg * ++phase, t0);
     gstamp(gs, member, 6, rt_now() - t0);

@@ -86,7 +86,7 @@ def main():
                 r = abi.DecodeResult.from_buffer_copy(d_res.cpu().numpy().tobytes())
                 print(f"integ={integ} dbg={v} round={rnd} ms={ms:.4f} GiB/s={L/ms/1e-3/2**30:.1f} "
                       f"err={r.error.kind} frames={r.frame_count} path={r.path}", flush=True)
-                if v & 512 and rnd == 2:  # progress stamps (10 ns ticks) of one more decode
+                if v & 512 and rnd == 2 and integ == 0:  # progress stamps (10 ns ticks) of one more decode
                     L_ = cx._L
                     L_.iggy_codec_debug_clear.argtypes = [ctypes.c_void_p]
                     L_.iggy_codec_debug_read.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64]
@@ -104,8 +104,8 @@ def main():
                     print("  chain  batch 0,8,..: " + " ".join([rel(st[1])] + [rel(x) for x in st[3:10]])
                           + f"  done {rel(st[20])}  producers exited {rel(st[21])}", flush=True)
                     print("  staged batch 0,8,..: " + " ".join(rel(x) for x in st[23:31]), flush=True)
-                    print("  blocks 0,1 published: " + " ".join(rel(x) for x in st[10:12])
-                          + "  WG 0 steps 0-3 landed: " + " ".join(rel(x) for x in st[12:16]), flush=True)
+                    print("  blocks 0,1 published: " + " ".join(rel(x) for x in st[11:13])
+                          + "  WG 0 steps 0-3 landed: " + " ".join(rel(x) for x in st[13:17]), flush=True)
 
 
 if __name__ == "__main__":

@@ -55,11 +55,15 @@ def main():
         cx._L.iggy_codec_debug_read(cx.handle, buf, 768)
         ms = (time.perf_counter() - t0) * 1e3
         dr = abi.DecodeResult.from_buffer_copy(d_res.cpu().numpy().tobytes())
-        st = list(buf[64:80])
+        st = list(buf[64:82])
         line = {"iter": it, "host_ms": round(ms, 3), "err": dr.error.kind, "frames": dr.frame_count,
                 "phase_us": [round(st[i] / 100, 1) for i in range(1, 7)],
                 "fast_steps": st[8], "summary_groups": st[9], "span_groups": st[10], "repaired_groups": st[11],
-                "ntiles": st[12], "tile_shift": st[13]}
+                "ntiles": st[12], "tile_shift": st[13],
+                "verify_loop_end_max_us": round(st[14] / 100, 1), "verify_short_end_max_us": round(st[16] / 100, 1)}
+        nvw = st[17]
+        if nvw:
+            line["verify_loop_end_mean_us"] = round(st[15] / nvw / 100, 1)
         print(json.dumps(line), flush=True)
     cx.close()
 
