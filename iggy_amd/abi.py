@@ -235,3 +235,15 @@ class SegmentWalk(ctypes.Structure):
 
 
 assert ctypes.sizeof(SegmentWalk) == 112
+
+
+ERR_CANNOT_DECRYPT_DATA = 24
+
+
+class CryptResult(ctypes.Structure):
+    """iggy_crypt_result (encrypt_batch_request / decrypt_batch_record,
+    server_common/src/send_messages.rs:293-415)."""
+    _fields_ = [("error", WireError), ("out_len", u64), ("frame_count", u64), ("batch_checksum", u64)]
+
+
+assert ctypes.sizeof(CryptResult) == 56

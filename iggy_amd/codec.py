@@ -112,6 +112,8 @@ def load(path: str) -> ctypes.CDLL:
     L.iggy_codec_walk_disk_chunk.argtypes = [vp, vp, u64, vp, ci, vp, vp, u64, vp]
     L.iggy_codec_walk_segment_payload.argtypes = [vp, vp, u64, u64, vp, u64, vp]
     L.iggy_codec_segment_write_device.argtypes = [vp, ci, u64, vp, u64, ci, ctypes.POINTER(u64)]
+    L.iggy_codec_encrypt_batch_device.argtypes = [vp, vp, vp, u64, vp, vp, u64, vp, vp]
+    L.iggy_codec_decrypt_batch_device.argtypes = [vp, vp, vp, u64, vp, u64, vp, vp]
     L.iggy_codec_profile_enable.argtypes = [vp, ci]
     L.iggy_codec_profile_read.argtypes = [vp, ci, vp, vp]
     L.iggy_codec_host_register.argtypes = [vp, vp, u64]
@@ -315,6 +317,24 @@ class Codec:
         if rc:
             raise CodecError(rc, None, "segment_write_device")
         return w.value
+
+    def encrypt_batch_device(self, key: bytes, d_record: int, length: int, d_nonces: int, d_out: int, cap: int,
+                             d_result: int, stream: int | None = None) -> int:
+        """encrypt_batch_request's batch re-encode (send_messages.rs:293-355) on device buffers;
+        d_nonces: 24 B per message (payload nonce, user-headers nonce). Result: abi.CryptResult."""
+        if len(key) != 32:
+            raise ValueError("AES-256 key must be 32 bytes")
+        k = ctypes.create_string_buffer(bytes(key), 32)
+        return self._L.iggy_codec_encrypt_batch_device(self._h, k, d_record, length, d_nonces, d_out, cap,
+                                                       d_result, stream)
+
+    def decrypt_batch_device(self, key: bytes, d_record: int, length: int, d_out: int, cap: int, d_result: int,
+                             stream: int | None = None) -> int:
+        """decrypt_batch_record (send_messages.rs:357-415) on device buffers. Result: abi.CryptResult."""
+        if len(key) != 32:
+            raise ValueError("AES-256 key must be 32 bytes")
+        k = ctypes.create_string_buffer(bytes(key), 32)
+        return self._L.iggy_codec_decrypt_batch_device(self._h, k, d_record, length, d_out, cap, d_result, stream)
 
     def select_slice_device(self, d_record: int, d_frame_pos: int, nframes: int, query: SliceQuery,
                             d_out: int, d_header: int | None = None, stream: int | None = None) -> int:

@@ -79,6 +79,10 @@ typedef enum iggy_error_kind {
     /* IggyError::InvalidMessagesCount: a transferred segment batch with no messages
      * (core/partitions/src/state_transfer.rs:766-771) */
     IGGY_ERR_INVALID_MESSAGES_COUNT = 23,
+    /* IggyError::CannotDecryptData: a section of frame a (b = 0 payload, 1 user
+     * headers) is shorter than nonce + tag or fails the GCM tag
+     * (core/common/src/utils/crypto.rs:80-90, server_common/src/send_messages.rs:385-399) */
+    IGGY_ERR_CANNOT_DECRYPT_DATA = 24,
     /* library-level failures (not wire errors) */
     IGGY_ERR_DEVICE = 100,
     IGGY_ERR_INVALID_ARGUMENT = 101,
@@ -272,6 +276,38 @@ int iggy_codec_batch_checksum_device(iggy_codec_ctx *ctx, const iggy_batch_heade
 int iggy_codec_xxh3_64_ranges_device(iggy_codec_ctx *ctx, const uint8_t *d_data,
                                      const uint64_t *d_offsets, const uint32_t *d_lengths,
                                      uint64_t n, uint64_t *d_out, void *stream);
+
+/* --------------------------------------- at-rest encryption */
+/* AES-256-GCM re-encode of a canonical batch record on the device:
+ * encrypt_batch_request (core/server_common/src/send_messages.rs:293-355) and
+ * decrypt_batch_record (:357-415) with Aes256GcmEncryptor
+ * (core/common/src/utils/crypto.rs:47-90). Every message's payload (always) and
+ * user headers (when non-empty) become nonce(12) || ciphertext || tag(16) with
+ * empty associated data (decrypt: the reverse); id, offset_delta and
+ * timestamp_delta are kept, lengths, per-message checksums, batch_length and the
+ * batch checksum are restamped; every other header field is kept.
+ * Encrypt verifies the input first (decode_batch_slice = Verify; its error comes
+ * back as is); decrypt checks layout only and requires len == batch_length
+ * (IGGY_ERR_INVALID_COMMAND otherwise). The reference draws each nonce from the
+ * OS RNG; here the caller supplies them: d_nonces holds 24 B per message, the
+ * payload's nonce then the user headers' (read only when the message has user
+ * headers). The encrypted record is at most len + 56 * message_count bytes, the
+ * decrypted one at most len. Output [256 B header][frames] at d_out (cap bytes);
+ * *d_result is written on the stream. key: 32 host bytes. */
+typedef struct iggy_crypt_result {
+    iggy_wire_error error;  /* the input's decode error, IGGY_ERR_INVALID_COMMAND,
+                               IGGY_ERR_CANNOT_DECRYPT_DATA, IGGY_ERR_CAPACITY (a = bytes needed) */
+    uint64_t out_len;        /* bytes of the re-encoded record, header included */
+    uint64_t frame_count;
+    uint64_t batch_checksum; /* of the re-encoded record */
+} iggy_crypt_result;
+
+int iggy_codec_encrypt_batch_device(iggy_codec_ctx *ctx, const uint8_t *key, const uint8_t *d_record,
+                                    uint64_t len, const uint8_t *d_nonces, uint8_t *d_out, uint64_t cap,
+                                    iggy_crypt_result *d_result, void *stream);
+int iggy_codec_decrypt_batch_device(iggy_codec_ctx *ctx, const uint8_t *key, const uint8_t *d_record,
+                                    uint64_t len, uint8_t *d_out, uint64_t cap, iggy_crypt_result *d_result,
+                                    void *stream);
 
 /* ------------------------------------------------- poll-path slicing (a17+) */
 /* MessageLookup (core/partitions/src/journal.rs:68-95). */

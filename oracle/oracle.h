@@ -73,6 +73,17 @@ int oracle_admit_batch(const uint8_t *batch, uint64_t len, uint32_t meta_count, 
                        int checksum_mode, uint8_t *out, uint64_t cap, iggy_batch_header *h,
                        iggy_wire_error *e);
 
+/* At-rest encryption (crypt_ref.c): AES-256-GCM sections (crypto.rs:70-90) and the
+ * batch re-encodes encrypt_batch_request / decrypt_batch_record
+ * (core/server_common/src/send_messages.rs:293-415). nonces: 24 B per message. */
+void oracle_aes256_block(const uint8_t key[32], const uint8_t in[16], uint8_t out[16]);
+void oracle_gcm_seal(const uint8_t key[32], const uint8_t nonce[12], const uint8_t *pt, uint64_t n, uint8_t *out);
+int oracle_gcm_open(const uint8_t key[32], const uint8_t *data, uint64_t n, uint8_t *pt);
+int oracle_encrypt_batch(const uint8_t key[32], const uint8_t *record, uint64_t len, const uint8_t *nonces,
+                         uint8_t *out, uint64_t cap, uint64_t *out_len, iggy_wire_error *e);
+int oracle_decrypt_batch(const uint8_t key[32], const uint8_t *record, uint64_t len, uint8_t *out, uint64_t cap,
+                         uint64_t *out_len, iggy_wire_error *e);
+
 /* recover_segment_bounds' index-less walk (core/partitions/src/segment_recovery.rs:425-530) */
 int oracle_recover_segment(const uint8_t *messages, uint64_t len, uint64_t start_offset,
                            iggy_segment_recovery *out);

@@ -68,6 +68,11 @@ def lib() -> ctypes.CDLL:
         L.oracle_recover_segment.argtypes = [vp, u64, u64, vp]
         L.oracle_walk_disk_chunk.argtypes = [vp, u64, vp, ctypes.c_int, vp, vp, u64, vp]
         L.oracle_walk_segment_payload.argtypes = [vp, u64, u64, vp, u64, vp]
+        L.oracle_aes256_block.argtypes = [vp, vp, vp]
+        L.oracle_gcm_seal.argtypes = [vp, vp, vp, u64, vp]
+        L.oracle_gcm_open.argtypes = [vp, vp, u64, vp]
+        L.oracle_encrypt_batch.argtypes = [vp, vp, u64, vp, vp, u64, vp, vp]
+        L.oracle_decrypt_batch.argtypes = [vp, vp, u64, vp, u64, vp, vp]
         _lib = L
     return _lib
 
@@ -262,3 +267,67 @@ def walk_segment_payload(payload, base_offset: int, index_cap: int = 4096):
                                            index_cap, ctypes.byref(w))
     n = min(w.index_entries, index_cap)
     return rc, w, idx[: 24 * n].tobytes()
+
+
+# ------------------------------------------------------------ at-rest encryption
+def aes256_block(key: bytes, block: bytes) -> bytes:
+    import numpy as np
+
+    k = np.frombuffer(bytes(key), dtype=np.uint8).copy()
+    b = np.frombuffer(bytes(block), dtype=np.uint8).copy()
+    out = np.zeros(16, dtype=np.uint8)
+    lib().oracle_aes256_block(k.ctypes.data, b.ctypes.data, out.ctypes.data)
+    return out.tobytes()
+
+
+def gcm_seal(key: bytes, nonce: bytes, pt: bytes) -> bytes:
+    """Aes256GcmEncryptor::encrypt with the given nonce -> nonce || ct || tag"""
+    import numpy as np
+
+    k = np.frombuffer(bytes(key), dtype=np.uint8).copy()
+    nn = np.frombuffer(bytes(nonce), dtype=np.uint8).copy()
+    p = _as_np(pt)
+    out = np.zeros(len(pt) + 28, dtype=np.uint8)
+    lib().oracle_gcm_seal(k.ctypes.data, nn.ctypes.data, p.ctypes.data if p.size else None, p.size, out.ctypes.data)
+    return out.tobytes()
+
+
+def gcm_open(key: bytes, data: bytes):
+    """Aes256GcmEncryptor::decrypt -> plaintext bytes, or None (CannotDecryptData)"""
+    import numpy as np
+
+    k = np.frombuffer(bytes(key), dtype=np.uint8).copy()
+    d = _as_np(data)
+    out = np.zeros(max(len(data) - 28, 1), dtype=np.uint8)
+    rc = lib().oracle_gcm_open(k.ctypes.data, d.ctypes.data if d.size else None, d.size, out.ctypes.data)
+    return None if rc else out[: max(len(data) - 28, 0)].tobytes()
+
+
+def encrypt_batch(key: bytes, record, nonces):
+    """encrypt_batch_request's batch transform -> (rc, WireError, bytes)"""
+    import numpy as np
+
+    k = np.frombuffer(bytes(key), dtype=np.uint8).copy()
+    a = _as_np(record)
+    nn = _as_np(nonces)
+    cap = a.size + 56 * (a.size // 48 + 1) + 256
+    out = np.zeros(cap, dtype=np.uint8)
+    n = u64(0)
+    e = WireError()
+    rc = lib().oracle_encrypt_batch(k.ctypes.data, a.ctypes.data, a.size, nn.ctypes.data if nn.size else None,
+                                    out.ctypes.data, cap, ctypes.byref(n), ctypes.byref(e))
+    return rc, e, out[: n.value].tobytes() if rc == 0 else b""
+
+
+def decrypt_batch(key: bytes, record):
+    """decrypt_batch_record -> (rc, WireError, bytes)"""
+    import numpy as np
+
+    k = np.frombuffer(bytes(key), dtype=np.uint8).copy()
+    a = _as_np(record)
+    out = np.zeros(max(a.size, 256), dtype=np.uint8)
+    n = u64(0)
+    e = WireError()
+    rc = lib().oracle_decrypt_batch(k.ctypes.data, a.ctypes.data, a.size, out.ctypes.data, out.size,
+                                    ctypes.byref(n), ctypes.byref(e))
+    return rc, e, out[: n.value].tobytes() if rc == 0 else b""
