@@ -192,6 +192,62 @@ def c3_leg(cx, dev, steps: int):
     )
 
 
+def crypt_leg(cx, dev, rec, n: int, steps: int, cpu: bool):
+    """the at-rest encryption re-encode (encrypt_batch_request /
+    decrypt_batch_record) of the C2 record on device, each timed over `steps`
+    back-to-back calls; the CPU baseline is OpenSSL's AES-256-GCM on 1 KiB sections
+    (the crypto alone, a lower bound on the reference's per-message re-encode)."""
+    import torch
+    from iggy_amd import abi
+
+    L = rec.numel()
+    s = torch.cuda.Stream(dev)
+    key = bytes(range(32))
+    nonces = torch.randint(0, 256, (24 * n,), dtype=torch.uint8, device=dev)
+    cap = L + 28 * n
+    enc = torch.empty(cap, dtype=torch.uint8, device=dev)
+    dec = torch.empty(L, dtype=torch.uint8, device=dev)
+    res = torch.zeros(ctypes.sizeof(abi.CryptResult), dtype=torch.uint8, device=dev)
+    torch.cuda.synchronize(dev)
+
+    def timed(fn):
+        for _ in range(2):
+            fn()
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            fn()
+        torch.cuda.synchronize(dev)
+        return (time.perf_counter() - t0) / steps
+
+    enc_s = timed(lambda: cx.encrypt_batch_device(key, rec.data_ptr(), L, nonces.data_ptr(), enc.data_ptr(), cap,
+                                                  res.data_ptr(), s.cuda_stream))
+    r = abi.CryptResult.from_buffer_copy(res.cpu().numpy().tobytes())
+    assert r.error.kind == 0 and r.out_len == cap, r.error
+    dec_s = timed(lambda: cx.decrypt_batch_device(key, enc.data_ptr(), cap, dec.data_ptr(), L, res.data_ptr(),
+                                                  s.cuda_stream))
+    r = abi.CryptResult.from_buffer_copy(res.cpu().numpy().tobytes())
+    assert r.error.kind == 0 and r.out_len == L, r.error
+    assert torch.equal(dec, rec), "decrypt(encrypt(x)) != x"
+    out = {"workload": "encrypt_batch_request / decrypt_batch_record on the C2 record (1,048,576 x 1 KiB), "
+                       "AES-256-GCM per payload",
+           "encrypt_ms": round(enc_s * 1e3, 3), "decrypt_ms": round(dec_s * 1e3, 3),
+           "encrypt_gib_s": round(L / enc_s / 2**30, 2), "decrypt_gib_s": round(cap / dec_s / 2**30, 2),
+           "round_trip_exact": True}
+    if cpu:
+        from oracle import oracle as O  # cpu_baseline leg only
+        by = {}
+        for t in (1, 16):
+            nsec = 60000
+            sec = O.cpu_gcm_bench(t, nsec, 1024)
+            if sec > 0:
+                by[str(t)] = round(t * nsec * 1024 / sec / 2**30, 3)
+        out["cpu_openssl_gcm_gib_s"] = by
+        out["cpu_note"] = "OpenSSL EVP_aes_256_gcm seal of 1 KiB sections, no framing or re-hash"
+    del enc, dec, nonces
+    return out
+
+
 def c1_leg(cx, dev, seconds: float):
     """BASELINE configs[0] shapes: 10 batches x 1000 msgs x 256 B. iggy-bench over
     TCP needs a Rust toolchain (absent): recorded as not run; cpu_ref (the oracle's
@@ -405,6 +461,10 @@ def run(args, world: int, rank: int, local: int, dist):
     if world == 1 and not args.no_extra:
         for ln in lanes[1:]:  # free HBM held by the other lanes' records
             ln["batch"] = None
+        torch.cuda.empty_cache()
+        extra["crypt_c2"] = crypt_leg(lanes[0]["cx"], dev, lanes[0]["batch"], n, max(5, args.steps // 4),
+                                      rank == 0 and not args.no_cpu)
+        lanes[0]["batch"] = None
         torch.cuda.empty_cache()
         extra["c3_encode"], extra["c3_decode"] = c3_leg(lanes[0]["cx"], dev, max(5, args.steps // 2))
         extra["c1"] = c1_leg(lanes[0]["cx"], dev, args.cpu_seconds)

@@ -1495,7 +1495,9 @@ int enqueue_crypt(iggy_codec_ctx *c, bool enc, const uint8_t *key, const uint8_t
     hipStream_t s = bind(c, stream);
     const uint64_t nmax = (len > kHdr ? (len - kHdr) / kFrameHdr : 0) + 1;
     const uint64_t ntiles = (nmax + kCryptTile - 1) / kCryptTile;
+    const void *cr_before = c->cr.p;
     int r = c->cr.ensure(kCrArrays + (2 * nmax + ntiles + 2) * 8);
+    if (c->cr.p != cr_before) c->cr_key_set = false;  // a grown buffer lost the tables
     r |= c->dpos.ensure((nmax + 1) * 8);
     r |= c->gbsums.ensure(((44 + 8 * nmax) / 1024 + 2) * 64);
     if (r) return IGGY_ERR_DEVICE;

@@ -143,3 +143,89 @@ double oracle_cpu_encode_bench(const iggy_raw_messages *m, uint64_t partition_id
     free(jobs);
     return (double)(t1.tv_sec - t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - t0.tv_nsec);
 }
+
+/* ---------------------------------------------------------------------------
+ * CPU baseline of the at-rest encryption re-encode's crypto: AES-256-GCM seal of
+ * nsec sections of secsize bytes per thread through the system OpenSSL
+ * (libcrypto EVP_aes_256_gcm, AES-NI / PCLMULQDQ when the CPU has them) -- the
+ * same algorithm the reference's `aes-gcm` crate runs per section
+ * (crypto.rs:70-78). libcrypto is opened at run time (no link dependency);
+ * returns seconds, or -1 when it is unavailable. */
+#include <dlfcn.h>
+typedef struct {
+    void *(*ctx_new)(void);
+    void (*ctx_free)(void *);
+    const void *(*cipher)(void);
+    int (*init)(void *, const void *, void *, const unsigned char *, const unsigned char *);
+    int (*update)(void *, unsigned char *, int *, const unsigned char *, int);
+    int (*final)(void *, unsigned char *, int *);
+    int (*ctrl)(void *, int, int, void *);
+} evp_t;
+typedef struct {
+    const evp_t *e;
+    int nsec, secsize, ok;
+} gcm_job_t;
+static void *gcm_worker(void *arg) {
+    gcm_job_t *j = (gcm_job_t *)arg;
+    unsigned char key[32], iv[12], tag[16];
+    for (int i = 0; i < 32; ++i) key[i] = (unsigned char)(i * 7 + 1);
+    memset(iv, 3, 12);
+    unsigned char *in = (unsigned char *)malloc(j->secsize + 16), *out = (unsigned char *)malloc(j->secsize + 32);
+    memset(in, 0x5a, j->secsize);
+    void *c = j->e->ctx_new();
+    j->ok = c != NULL;
+    /* the key schedule once per thread (as a long-lived Aes256GcmEncryptor), a fresh
+     * nonce per section */
+    if (j->ok) j->ok &= j->e->init(c, j->e->cipher(), NULL, key, NULL) == 1;
+    for (int s = 0; s < j->nsec && j->ok; ++s) {
+        int ol = 0, fl = 0;
+        iv[0] = (unsigned char)s; iv[1] = (unsigned char)(s >> 8); iv[2] = (unsigned char)(s >> 16);
+        j->ok &= j->e->init(c, NULL, NULL, NULL, iv) == 1;
+        j->ok &= j->e->update(c, out, &ol, in, j->secsize) == 1;
+        j->ok &= j->e->final(c, out + ol, &fl) == 1;
+        j->ok &= j->e->ctrl(c, 0x10 /* EVP_CTRL_GCM_GET_TAG */, 16, tag) == 1;
+    }
+    if (c) j->e->ctx_free(c);
+    free(in);
+    free(out);
+    return NULL;
+}
+double oracle_cpu_gcm_bench(int threads, int nsec, int secsize) {
+    static evp_t e;
+    static int loaded = 0;
+    if (!loaded) {
+        void *h = dlopen("libcrypto.so.3", RTLD_NOW | RTLD_LOCAL);
+        if (!h) return -1.0;
+        e.ctx_new = (void *(*)(void))dlsym(h, "EVP_CIPHER_CTX_new");
+        e.ctx_free = (void (*)(void *))dlsym(h, "EVP_CIPHER_CTX_free");
+        e.cipher = (const void *(*)(void))dlsym(h, "EVP_aes_256_gcm");
+        e.init = (int (*)(void *, const void *, void *, const unsigned char *, const unsigned char *))dlsym(
+            h, "EVP_EncryptInit_ex");
+        e.update = (int (*)(void *, unsigned char *, int *, const unsigned char *, int))dlsym(h, "EVP_EncryptUpdate");
+        e.final = (int (*)(void *, unsigned char *, int *))dlsym(h, "EVP_EncryptFinal_ex");
+        e.ctrl = (int (*)(void *, int, int, void *))dlsym(h, "EVP_CIPHER_CTX_ctrl");
+        if (!e.ctx_new || !e.ctx_free || !e.cipher || !e.init || !e.update || !e.final || !e.ctrl) return -1.0;
+        loaded = 1;
+    }
+    if (threads < 1) threads = 1;
+    pthread_t *tid = (pthread_t *)malloc(sizeof(pthread_t) * threads);
+    gcm_job_t *jobs = (gcm_job_t *)calloc(threads, sizeof(gcm_job_t));
+    struct timespec t0, t1;
+    clock_gettime(CLOCK_MONOTONIC, &t0);
+    for (int t = 0; t < threads; t++) {
+        jobs[t].e = &e;
+        jobs[t].nsec = nsec;
+        jobs[t].secsize = secsize;
+        pthread_create(&tid[t], NULL, gcm_worker, &jobs[t]);
+    }
+    int ok = 1;
+    for (int t = 0; t < threads; t++) {
+        pthread_join(tid[t], NULL);
+        ok &= jobs[t].ok;
+    }
+    clock_gettime(CLOCK_MONOTONIC, &t1);
+    free(tid);
+    free(jobs);
+    if (!ok) return -1.0;
+    return (double)(t1.tv_sec - t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - t0.tv_nsec);
+}

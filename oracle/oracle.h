@@ -81,6 +81,9 @@ void oracle_gcm_seal(const uint8_t key[32], const uint8_t nonce[12], const uint8
 int oracle_gcm_open(const uint8_t key[32], const uint8_t *data, uint64_t n, uint8_t *pt);
 int oracle_encrypt_batch(const uint8_t key[32], const uint8_t *record, uint64_t len, const uint8_t *nonces,
                          uint8_t *out, uint64_t cap, uint64_t *out_len, iggy_wire_error *e);
+/* CPU baseline: AES-256-GCM seal of nsec sections of secsize B per thread via the
+ * system libcrypto (opened at run time); seconds, or -1 when unavailable. */
+double oracle_cpu_gcm_bench(int threads, int nsec, int secsize);
 int oracle_decrypt_batch(const uint8_t key[32], const uint8_t *record, uint64_t len, uint8_t *out, uint64_t cap,
                          uint64_t *out_len, iggy_wire_error *e);
 

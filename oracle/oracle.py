@@ -73,6 +73,8 @@ def lib() -> ctypes.CDLL:
         L.oracle_gcm_open.argtypes = [vp, vp, u64, vp]
         L.oracle_encrypt_batch.argtypes = [vp, vp, u64, vp, vp, u64, vp, vp]
         L.oracle_decrypt_batch.argtypes = [vp, vp, u64, vp, u64, vp, vp]
+        L.oracle_cpu_gcm_bench.restype = ctypes.c_double
+        L.oracle_cpu_gcm_bench.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int]
         _lib = L
     return _lib
 
@@ -331,3 +333,8 @@ def decrypt_batch(key: bytes, record):
     rc = lib().oracle_decrypt_batch(k.ctypes.data, a.ctypes.data, a.size, out.ctypes.data, out.size,
                                     ctypes.byref(n), ctypes.byref(e))
     return rc, e, out[: n.value].tobytes() if rc == 0 else b""
+
+
+def cpu_gcm_bench(threads: int, nsec: int, secsize: int) -> float:
+    """seconds for threads x nsec AES-256-GCM seals of secsize bytes (OpenSSL); -1 if unavailable"""
+    return lib().oracle_cpu_gcm_bench(threads, nsec, secsize)
