@@ -247,3 +247,78 @@ class CryptResult(ctypes.Structure):
 
 
 assert ctypes.sizeof(CryptResult) == 56
+
+
+# ---- SDK request body / poll prefix / producer (include/iggy_codec.h "SDK" sections)
+ERR_INVALID_UTF8 = 7
+ERR_UNKNOWN_DISCRIMINANT = 8
+V_NUMERIC_ID_LENGTH = 6
+V_STRING_ID_EMPTY = 7
+V_BALANCED_LENGTH = 8
+V_PARTITION_ID_LENGTH = 9
+V_MESSAGES_KEY_EMPTY = 10
+TYPE_WIRE_IDENTIFIER = 1
+TYPE_WIRE_PARTITIONING = 2
+ID_NUMERIC = 1
+ID_STRING = 2
+PART_BALANCED = 1
+PART_PARTITION_ID = 2
+PART_MESSAGES_KEY = 3
+MAX_BATCH_LENGTH = 1_000_000
+
+
+class Identifier(ctypes.Structure):
+    """WireIdentifier (primitives/identifier.rs:97-180)."""
+    _fields_ = [("kind", u32), ("length", u32), ("value", ctypes.c_uint8 * 256)]
+
+    @classmethod
+    def numeric(cls, v: int) -> "Identifier":
+        return cls.raw(ID_NUMERIC, int(v).to_bytes(4, "little"))
+
+    @classmethod
+    def named(cls, s) -> "Identifier":
+        return cls.raw(ID_STRING, s.encode() if isinstance(s, str) else bytes(s))
+
+    @classmethod
+    def raw(cls, kind: int, value: bytes) -> "Identifier":
+        x = cls()
+        x.kind, x.length = kind, len(value)
+        ctypes.memmove(x.value, value, len(value))
+        return x
+
+    def value_bytes(self) -> bytes:
+        return bytes(self.value[: self.length])
+
+
+class Partitioning(Identifier):
+    """WirePartitioning (primitives/partitioning.rs:24-100) — same layout."""
+
+    @classmethod
+    def balanced(cls) -> "Partitioning":
+        return cls.raw(PART_BALANCED, b"")
+
+    @classmethod
+    def partition_id(cls, v: int) -> "Partitioning":
+        return cls.raw(PART_PARTITION_ID, int(v).to_bytes(4, "little"))
+
+    @classmethod
+    def messages_key(cls, key: bytes) -> "Partitioning":
+        return cls.raw(PART_MESSAGES_KEY, bytes(key))
+
+
+class SendMessagesHeader(ctypes.Structure):
+    _fields_ = [("stream_id", Identifier), ("topic_id", Identifier), ("partitioning", Partitioning),
+                ("messages_count", u32), ("_pad", u32)]
+
+
+class PolledPrefix(ctypes.Structure):
+    _fields_ = [("partition_id", u32), ("count", u32), ("current_offset", u64)]
+
+
+class ProducerConfig(ctypes.Structure):
+    _fields_ = [("batch_length", u64), ("batch_size", u64), ("direct", u32), ("_pad", u32), ("_reserved", u64)]
+
+
+class ProducerRequest(ctypes.Structure):
+    _fields_ = [("offset", u64), ("length", u64), ("first_message", u64), ("messages", u64),
+                ("entry", u32), ("sent", u32), ("error", WireError)]

@@ -16,7 +16,8 @@ import re
 import numpy as np
 
 from . import abi
-from .abi import (BatchHeader, Completion, DecodeResult, EncodeResult, PolledMessage, RawMessages, SliceQuery,
+from .abi import (BatchHeader, Completion, DecodeResult, EncodeResult, Identifier, Partitioning, PolledMessage,
+                  PolledPrefix, ProducerConfig, ProducerRequest, RawMessages, SendMessagesHeader, SliceQuery,
                   SliceResult, WireError)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
@@ -125,6 +126,18 @@ def load(path: str) -> ctypes.CDLL:
     L.iggy_codec_error_string.argtypes = [u32, u32]
     L.iggy_codec_error_string.restype = ctypes.c_char_p
     L.iggy_codec_debug_set.argtypes = [vp, u32]
+    L.iggy_send_messages_header_encode.argtypes = [vp, vp, u64, ctypes.POINTER(u64)]
+    L.iggy_send_messages_header_decode.argtypes = [vp, u64, vp, ctypes.POINTER(u64), vp]
+    L.iggy_send_messages_encoded_size.argtypes = [vp, vp]
+    L.iggy_send_messages_encoded_size.restype = u64
+    L.iggy_codec_send_messages_encode.argtypes = [vp, vp, vp, vp, u64, ctypes.POINTER(u64), vp]
+    L.iggy_codec_polled_messages_from_bytes.argtypes = [vp, vp, u64, vp, vp, u64, ctypes.POINTER(u64), vp]
+    L.iggy_producer_create.argtypes = [vp, vp, ctypes.POINTER(vp)]
+    L.iggy_producer_destroy.argtypes = [vp]
+    L.iggy_producer_destroy.restype = None
+    L.iggy_producer_append.argtypes = [vp, vp, vp, vp, vp, ctypes.POINTER(ci)]
+    L.iggy_producer_pending.argtypes = [vp, ctypes.POINTER(u64), ctypes.POINTER(u64), ctypes.POINTER(u64)]
+    L.iggy_producer_flush.argtypes = [vp, vp, u64, vp, u64, ctypes.POINTER(u64), vp]
     return L
 
 
@@ -136,6 +149,26 @@ def _np(buf) -> np.ndarray:
 
 def _addr(a: np.ndarray):
     return a.ctypes.data if a.size else None
+
+
+def send_messages_header_encode(h: SendMessagesHeader) -> bytes:
+    """SendMessagesHeader WireEncode (send_messages.rs:209-220): metadata fields, no length prefix."""
+    n = u64(0)
+    out = np.zeros(1024, dtype=np.uint8)
+    rc = lib().iggy_send_messages_header_encode(ctypes.byref(h), out.ctypes.data, out.size, ctypes.byref(n))
+    if rc:
+        raise CodecError(rc, None, "send_messages_header_encode")
+    return out[: n.value].tobytes()
+
+
+def send_messages_header_decode(buf):
+    """SendMessagesHeader::decode (send_messages.rs:222-241) -> (rc, WireError, header, consumed)."""
+    a = _np(buf)
+    h = SendMessagesHeader()
+    n = u64(0)
+    e = WireError()
+    rc = lib().iggy_send_messages_header_decode(_addr(a), a.size, ctypes.byref(h), ctypes.byref(n), ctypes.byref(e))
+    return rc, e, h, n.value
 
 
 class Codec:
@@ -427,3 +460,54 @@ def raw_messages(ids: np.ndarray, origin_timestamps: np.ndarray, payloads: np.nd
                        payloads.ctypes.data if payloads.size else None, payload_lengths.ctypes.data,
                        user_headers.ctypes.data if user_headers is not None and user_headers.size else None,
                        user_headers_lengths.ctypes.data if user_headers_lengths is not None else None)
+
+
+class Producer:
+    """The SDK producer's buffer in front of the GPU encoder (producer_sharding.rs:136-247,
+    producer.rs:406-470): append() per send call, flush() -> SendMessages request bodies."""
+
+    def __init__(self, codec: Codec, batch_length: int = 0, batch_size: int = 0, direct: bool = False):
+        self._L = codec._L
+        self._codec = codec
+        cfg = ProducerConfig(batch_length, batch_size, 1 if direct else 0, 0, 0)
+        h = vp()
+        rc = self._L.iggy_producer_create(codec.handle, ctypes.byref(cfg), ctypes.byref(h))
+        if rc:
+            raise CodecError(rc, None, "iggy_producer_create")
+        self._h = h
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self._L.iggy_producer_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def append(self, stream: Identifier, topic: Identifier, part: Partitioning, raw: RawMessages) -> bool:
+        due = ci(0)
+        rc = self._L.iggy_producer_append(self._h, ctypes.byref(stream), ctypes.byref(topic), ctypes.byref(part),
+                                          ctypes.byref(raw), ctypes.byref(due))
+        if rc:
+            raise CodecError(rc, None, "iggy_producer_append")
+        return bool(due.value)
+
+    def pending(self):
+        e, b, m = u64(0), u64(0), u64(0)
+        self._L.iggy_producer_pending(self._h, ctypes.byref(e), ctypes.byref(b), ctypes.byref(m))
+        return e.value, b.value, m.value
+
+    def flush(self, cap: int, max_reqs: int = 4096, out: np.ndarray | None = None):
+        """-> (rc, WireError, out bytes, [ProducerRequest])."""
+        if out is None:
+            out = np.zeros(max(cap, 1), dtype=np.uint8)
+        reqs = (ProducerRequest * max(max_reqs, 1))()
+        n = u64(0)
+        e = WireError()
+        rc = self._L.iggy_producer_flush(self._h, out.ctypes.data, cap, reqs, max_reqs, ctypes.byref(n),
+                                         ctypes.byref(e))
+        return rc, e, out, [reqs[i] for i in range(n.value)]
+

@@ -2051,12 +2051,19 @@ const char *iggy_codec_error_string(uint32_t kind, uint32_t reason) {
                 case IGGY_V_FRAMES_DO_NOT_TILE: return "batch frames do not tile message_count exactly";
                 case IGGY_V_FRAME_RESERVED: return "message frame reserved bytes must be zero";
                 case IGGY_V_EMPTY_BATCH: return "cannot encode an empty message batch";
+                case IGGY_V_NUMERIC_ID_LENGTH: return "numeric identifier must be 4 bytes";
+                case IGGY_V_STRING_ID_EMPTY: return "string identifier cannot be empty";
+                case IGGY_V_BALANCED_LENGTH: return "balanced partitioning must have length 0";
+                case IGGY_V_PARTITION_ID_LENGTH: return "partition_id partitioning must have length 4";
+                case IGGY_V_MESSAGES_KEY_EMPTY: return "messages_key partitioning cannot have empty key";
                 default: return "validation failed";
             }
         case IGGY_ERR_INVALID_BATCH_CHECKSUM: return "invalid batch checksum";
         case IGGY_ERR_INVALID_MESSAGE_CHECKSUM: return "invalid message checksum";
         case IGGY_ERR_INVALID_TIMESTAMP_DELTA: return "message timestamp delta exceeds the batch maximum";
         case IGGY_ERR_PAYLOAD_TOO_LARGE: return "payload too large";
+        case IGGY_ERR_INVALID_UTF8: return "invalid utf-8";
+        case IGGY_ERR_UNKNOWN_DISCRIMINANT: return "unknown discriminant";
         case IGGY_ERR_INVALID_NUMBER_ENCODING: return "invalid number encoding";
         case IGGY_ERR_INVALID_MESSAGE_PAYLOAD_LENGTH: return "invalid message payload length";
         case IGGY_ERR_DEVICE: return "device error";

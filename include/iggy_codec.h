@@ -70,6 +70,8 @@ typedef enum iggy_error_kind {
     IGGY_ERR_INVALID_MESSAGE_CHECKSUM = 4,  /* a=stored b=computed c=offset */
     IGGY_ERR_INVALID_TIMESTAMP_DELTA = 5,   /* a=delta                     */
     IGGY_ERR_PAYLOAD_TOO_LARGE = 6,         /* a=size b=max                */
+    IGGY_ERR_INVALID_UTF8 = 7,              /* a=offset                    */
+    IGGY_ERR_UNKNOWN_DISCRIMINANT = 8,      /* a=type (IGGY_TYPE_*) b=value c=offset */
     /* IggyError mapping used by the SDK poll decode (polled_messages.rs:59-60) */
     IGGY_ERR_INVALID_NUMBER_ENCODING = 20,
     IGGY_ERR_INVALID_MESSAGE_PAYLOAD_LENGTH = 21,
@@ -99,8 +101,18 @@ typedef enum iggy_validation_reason {
     IGGY_V_BATCH_RESERVED = 2,       /* "batch header reserved bytes must be zero"        batch.rs:120-122 */
     IGGY_V_FRAMES_DO_NOT_TILE = 3,   /* "batch frames do not tile message_count exactly"  batch.rs:501-503 */
     IGGY_V_FRAME_RESERVED = 4,       /* "message frame reserved bytes must be zero"       batch.rs:255-257 */
-    IGGY_V_EMPTY_BATCH = 5           /* "cannot encode an empty message batch"  send_messages.rs:97-99 */
+    IGGY_V_EMPTY_BATCH = 5,          /* "cannot encode an empty message batch"  send_messages.rs:97-99 */
+    /* SendMessagesHeader metadata (binary_protocol/src/primitives/); a = the length found */
+    IGGY_V_NUMERIC_ID_LENGTH = 6,    /* "numeric identifier must be 4 bytes, got {a}"           identifier.rs:202-206 */
+    IGGY_V_STRING_ID_EMPTY = 7,      /* "string identifier cannot be empty"                     identifier.rs:215-219 */
+    IGGY_V_BALANCED_LENGTH = 8,      /* "balanced partitioning must have length 0, got {a}"     partitioning.rs:111-115 */
+    IGGY_V_PARTITION_ID_LENGTH = 9,  /* "partition_id partitioning must have length 4, got {a}" partitioning.rs:119-123 */
+    IGGY_V_MESSAGES_KEY_EMPTY = 10   /* "messages_key partitioning cannot have empty key"       partitioning.rs:128-132 */
 } iggy_validation_reason;
+
+/* UnknownDiscriminant.type_name (error.rs:39-44) */
+#define IGGY_TYPE_WIRE_IDENTIFIER 1u
+#define IGGY_TYPE_WIRE_PARTITIONING 2u
 
 typedef struct iggy_wire_error {
     uint32_t kind;    /* iggy_error_kind */
@@ -544,6 +556,122 @@ int iggy_codec_encode_submit(iggy_codec_ctx *ctx, const iggy_raw_messages *msgs,
 int iggy_codec_poll(iggy_codec_ctx *ctx, iggy_ticket ticket, iggy_completion *out);
 /* Blocking form of iggy_codec_poll (tests, SDK tasks that may block). */
 int iggy_codec_wait(iggy_codec_ctx *ctx, iggy_ticket ticket, iggy_completion *out);
+
+/* ------------------------------------ SDK request body and poll response (a9, a10, a12, a18) */
+/* WireIdentifier (binary_protocol/src/primitives/identifier.rs:97-231): kind 1 =
+ * numeric (length 4, u32 LE in value[0..4]), kind 2 = string (length 1..255 UTF-8
+ * bytes). 264 B. */
+#define IGGY_ID_NUMERIC 1u
+#define IGGY_ID_STRING 2u
+typedef struct iggy_identifier {
+    uint32_t kind;
+    uint32_t length;
+    uint8_t value[256];
+} iggy_identifier;
+
+/* WirePartitioning (primitives/partitioning.rs:24-140): kind 1 = balanced
+ * (length 0), 2 = partition id (length 4, u32 LE), 3 = messages key (1..255 B). */
+#define IGGY_PART_BALANCED 1u
+#define IGGY_PART_PARTITION_ID 2u
+#define IGGY_PART_MESSAGES_KEY 3u
+typedef struct iggy_partitioning {
+    uint32_t kind;
+    uint32_t length;
+    uint8_t value[256];
+} iggy_partitioning;
+
+/* SendMessagesHeader (requests/messages/send_messages.rs:189-195). */
+typedef struct iggy_send_messages_header {
+    iggy_identifier stream_id;
+    iggy_identifier topic_id;
+    iggy_partitioning partitioning;
+    uint32_t messages_count;
+    uint32_t _pad;
+} iggy_send_messages_header;
+
+/* SendMessagesHeader::metadata_length / WireEncode::encode (send_messages.rs:197-220):
+ * the metadata fields without the u32 length prefix. IGGY_ERR_INVALID_ARGUMENT for an
+ * identifier or partitioning that its Rust constructor would refuse (a numeric id
+ * not 4 bytes long, an empty or > 255-byte name or key, an unknown kind). */
+int iggy_send_messages_header_encode(const iggy_send_messages_header *h, uint8_t *out, uint64_t cap,
+                                     uint64_t *out_len);
+/* WireDecode for SendMessagesHeader (send_messages.rs:222-241), with the
+ * identifier / partitioning decode errors of identifier.rs:194-231 and
+ * partitioning.rs:106-140 (UnexpectedEof offsets relative to the field being
+ * decoded, as the Rust sub-slice decode reports them). *consumed = bytes used. */
+int iggy_send_messages_header_decode(const uint8_t *buf, uint64_t len, iggy_send_messages_header *out,
+                                     uint64_t *consumed, iggy_wire_error *err);
+/* SendMessagesEncoder::encoded_size (send_messages.rs:69-79). */
+uint64_t iggy_send_messages_encoded_size(const iggy_send_messages_header *h, const iggy_raw_messages *msgs);
+/* SendMessagesEncoder::encode (send_messages.rs:89-181), the whole body:
+ * [metadata_length u32][stream_id][topic_id][partitioning][messages_count u32][batch],
+ * the batch section encoded on the GPU (h->messages_count is ignored: the count is
+ * msgs->count, as the encoder takes it from the slice). */
+int iggy_codec_send_messages_encode(iggy_codec_ctx *ctx, const iggy_send_messages_header *h,
+                                    const iggy_raw_messages *msgs, uint8_t *out, uint64_t cap,
+                                    uint64_t *out_len, iggy_wire_error *err);
+
+/* The PollMessages response prefix (polled_messages.rs:61-83). 16 B. */
+typedef struct iggy_polled_prefix {
+    uint32_t partition_id;
+    uint32_t count;
+    uint64_t current_offset;
+} iggy_polled_prefix;
+/* PolledMessages::from_bytes (common/src/types/message/polled_messages.rs:61-90):
+ * fewer than 16 bytes -> IGGY_ERR_INVALID_NUMBER_ENCODING; then the records after the
+ * prefix as iggy_codec_poll_decode(IGGY_POLL_MODE_SDK) walks them. payload_pos /
+ * user_headers_pos are offsets into `bytes` (prefix included). */
+int iggy_codec_polled_messages_from_bytes(iggy_codec_ctx *ctx, const uint8_t *bytes, uint64_t len,
+                                          iggy_polled_prefix *prefix, iggy_polled_message *out,
+                                          uint64_t cap, uint64_t *n, iggy_wire_error *err);
+
+/* ------------------------------------------ SDK producer batching */
+/* The producer's buffering in front of the encoder: the background shard buffer
+ * (core/sdk/src/clients/producer_sharding.rs:136-247: one entry per send call,
+ * flush when entries >= batch_length or buffered bytes >= batch_size, consecutive
+ * same-destination entries merged into one request) and direct sends
+ * (producer.rs:406-470: each call split into chunks of batch_length messages,
+ * MAX_BATCH_LENGTH = 1 000 000 when 0, clients/mod.rs:41; a failed chunk fails the
+ * rest of its call). Message bytes are appended into pinned host staging, so the
+ * flush's H2D copies are DMA; every request body is encoded on the GPU through the
+ * context's asynchronous slots (up to 8 in flight). */
+#define IGGY_MAX_BATCH_LENGTH 1000000ull
+typedef struct iggy_producer_config {
+    uint64_t batch_length;  /* background: entries that trigger a flush (0 = none); direct: chunk size */
+    uint64_t batch_size;    /* background: buffered bytes that trigger a flush (0 = none) */
+    uint32_t direct;        /* 1 = direct sends, 0 = background shard buffer */
+    uint32_t _pad;
+    uint64_t _reserved;
+} iggy_producer_config;
+
+/* One request body written by iggy_producer_flush. 72 B. */
+typedef struct iggy_producer_request {
+    uint64_t offset, length;          /* the SendMessages body at out[offset, offset + length) */
+    uint64_t first_message, messages; /* its messages, indices in append order since the last flush */
+    uint32_t entry;                   /* the (first) append call it came from */
+    uint32_t sent;                    /* 0: not encoded (an earlier chunk of its direct call failed) */
+    iggy_wire_error error;            /* the encoder's verdict for this body */
+} iggy_producer_request;
+
+typedef struct iggy_producer iggy_producer;
+int iggy_producer_create(iggy_codec_ctx *ctx, const iggy_producer_config *cfg, iggy_producer **out);
+void iggy_producer_destroy(iggy_producer *p);
+/* One send call (a ShardMessage, producer_sharding.rs:91-109): the messages are
+ * copied into the staging; *flush_due = the background trigger fired (direct mode:
+ * always 1). */
+int iggy_producer_append(iggy_producer *p, const iggy_identifier *stream_id, const iggy_identifier *topic_id,
+                         const iggy_partitioning *partitioning, const iggy_raw_messages *msgs, int *flush_due);
+/* Buffered entries / bytes (ShardMessage::get_size_bytes, producer_sharding.rs:99-109:
+ * 2 + identifier length for stream and topic, 64 + payload + user headers per message). */
+int iggy_producer_pending(const iggy_producer *p, uint64_t *entries, uint64_t *bytes, uint64_t *messages);
+/* flush_buffer (producer_sharding.rs:215-247) / send_internal's chunking
+ * (producer.rs:433-455): every request body is encoded into `out` (cap bytes; register
+ * it with iggy_codec_host_register for asynchronous copies) and described in reqs
+ * (max_reqs). Returns 0 when every body was written (each carries its own verdict in
+ * reqs[k].error), IGGY_ERR_CAPACITY (err->a = bytes or requests needed) when out or
+ * reqs is too small (nothing is flushed then). The buffer is empty afterwards. */
+int iggy_producer_flush(iggy_producer *p, uint8_t *out, uint64_t cap, iggy_producer_request *reqs,
+                        uint64_t max_reqs, uint64_t *nreqs, iggy_wire_error *err);
 
 /* ------------------------------------------------------------- profiling */
 /* When enabled, the context brackets the dominant kernel of every decode /
