@@ -301,7 +301,9 @@ __device__ __forceinline__ void word_contrib(uint64_t m, uint64_t v, uint64_t &x
 // contiguous ranges per group, or a wave's groups claiming its frames as they
 // finish, cut the slowest group's 17 % lead over the mean but made the mean 12-16 %
 // slower -- the chip-wide front of consecutive frames is worth more; hashing the
-// <= 240 B frames inside the loop pushed the kernel past 256 VGPRs and spilled.)
+// <= 240 B frames inside the loop pushed the kernel past 256 VGPRs and spilled;
+// the last 25 % of the frames claimed one per group from a counter took the loop
+// from 0.53 to 1.57 ms: 16 K groups' claims on one address serialise in L2.)
 // Lane group fg (8 lanes) of verify wave vw hashes frames
 // f = 8 vw + fg + j * 8 nvw, j = 0, 1, ... at its own pace: every wave step
 // each group hashes one 1024-B block of its current frame while the next block
@@ -381,7 +383,6 @@ __device__ inline void verify_frames(const uint8_t *blob, const GeneralScratch &
     const uint64_t last0 = kSecretLast[2 * m], last1 = kSecretLast[2 * m + 1];
     const uint64_t mrg0 = kSecretMerge[2 * m], mrg1 = kSecretMerge[2 * m + 1];
     const uint64_t stride = 8ull * nvw;
-
     VFrame cur = vframe(gs, 8ull * vw + fg, nwalk);
     VFrame nxt = vframe(gs, cur.f + stride, nwalk);
     uint32_t b = 0;
@@ -456,12 +457,28 @@ __device__ inline void verify_frames(const uint8_t *blob, const GeneralScratch &
         atomicMax((unsigned long long *)&vstat[0], (unsigned long long)d);
         atomicAdd((unsigned long long *)&vstat[1], (unsigned long long)d);
     }
-    // frames of <= 240 hashed bytes: one lane each, after the streaming loop
-    const uint64_t tid = 64ull * vw + lane, nth = 64ull * nvw;
-    for (uint64_t f = tid; f < nwalk; f += nth) {
-        const uint64_t L = gs.flen[f];
-        if (L <= 240 && xxh3_64_lane(blob + gs.fpos[f] + 8, L) != gs.cs[f])
-            atomicMax((unsigned long long *)&gs.misc[2], (unsigned long long)~f);
+    // frames of <= 240 hashed bytes: one lane each, after the streaming loop, in
+    // chunks claimed from a counter, so that the waves whose loop ended early (the
+    // mean loop end is ~10 % before the slowest) do them while the slowest still stream
+    constexpr uint64_t kShortChunk = 256;
+    while (true) {
+        uint64_t c = 0;
+        if (lane == 0) c = atomicAdd((unsigned long long *)&gs.misc[6], 1ull);
+        c = __shfl(c, 0);
+        const uint64_t f0 = c * kShortChunk;
+        if (f0 >= nwalk) break;
+        uint64_t L[kShortChunk / 64];
+#pragma unroll
+        for (int k = 0; k < (int)(kShortChunk / 64); ++k) {
+            const uint64_t f = f0 + 64 * k + lane;
+            L[k] = f < nwalk ? gs.flen[f] : ~0ull;
+        }
+#pragma unroll
+        for (int k = 0; k < (int)(kShortChunk / 64); ++k) {
+            const uint64_t f = f0 + 64 * k + lane;
+            if (L[k] <= 240 && xxh3_64_lane(blob + gs.fpos[f] + 8, L[k]) != gs.cs[f])
+                atomicMax((unsigned long long *)&gs.misc[2], (unsigned long long)~f);
+        }
     }
     if (lane == 0) atomicMax((unsigned long long *)&vstat[2], (unsigned long long)(rt_now() - t0));  // [16]
 }
@@ -500,12 +517,19 @@ __global__ __launch_bounds__(kGenThreads) void k_decode_general(const uint8_t *_
     const uint64_t gthreads = (uint64_t)nwg * blockDim.x;
     const int lane = threadIdx.x & 63;
     const uint32_t wave = threadIdx.x >> 6;
-    const uint64_t wid = gtid >> 6, nwaves = gthreads >> 6;
+    const uint64_t nwaves = gthreads >> 6;
+    // wave ids interleaved across workgroups (wave-major): a phase with fewer work
+    // items than lanes (locate: 68 K tiles for C3 against 131 K lanes) spreads over
+    // every CU, one wave per SIMD first, instead of filling half the CUs two deep
+    const uint64_t wid = (uint64_t)wave * nwg + member;
     uint32_t phase = 0;
     bool ok = true;
 
     // ---------------- A: locate
-    for (uint64_t t = gtid; t < ntiles; t += gthreads) {
+    // (misc[6], the short-frame chunk counter of phase D+F, is re-armed here: the
+    // barriers in between order it before any claim)
+    if (member == 0 && threadIdx.x == 0) __hip_atomic_store(&gs.misc[6], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (uint64_t t = 64 * wid + lane; t < ntiles; t += gthreads) {
         const uint64_t lo = t << sh, hi = min(lo + T, bl);
         uint32_t *list = gs.tile_list + t * lcap;
         uint64_t s = kNoStart, x = kNoStart;

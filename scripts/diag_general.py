@@ -16,7 +16,7 @@ sys.path.insert(0, ROOT)
 from iggy_amd import abi  # noqa: E402
 from iggy_amd import codec as _codec  # noqa: E402
 
-_codec.use_library(_codec.DIAG_LIB_PATH)  # ablation bits live only in the diagnostic build
+_codec.use_library(os.environ.get("IGGY_DIAG_LIB", _codec.DIAG_LIB_PATH))  # ablation bits live only in the diagnostic build
 from iggy_amd.codec import Codec  # noqa: E402
 
 
