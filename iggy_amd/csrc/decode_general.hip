@@ -283,7 +283,9 @@ __device__ inline void pick_start(const uint8_t *blob, uint64_t bl, uint64_t lo,
     if (pick == kNoStart) pick = clean_p != kNoStart ? clean_p : first_valid;
     uint64_t x = kNoStart;
     uint32_t cnt = 0;
+#ifndef IGGY_DIAG_LOCATE_PICK_ONLY
     if (pick != kNoStart) cnt = walk(blob, bl, pick, hi, &x, list, lo);
+#endif
     *s_out = pick;
     *x_out = x;
     *cnt_out = cnt;

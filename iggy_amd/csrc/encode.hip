@@ -322,19 +322,20 @@ __global__ __launch_bounds__(256) void k_enc_frames(iggy_raw_messages m, EncScra
 // that runs past its payload reads (and discards) the next one's bytes; only
 // the buffer's last 15 bytes need a clamped, realigned load.
 struct EFrame {
-    uint64_t i, po, pl;  // i >= count: none
+    // i >= count: none. The payload offset is kept as its two loaded halves and added
+    // where it is used (the next step): adding them here made the compiler wait for
+    // every outstanding load and store (vmcnt(0)) at each frame switch
+    uint64_t i, tp, lp, pl;
+    __device__ __forceinline__ uint64_t po() const { return tp + lp; }
 };
 __device__ __forceinline__ EFrame eframe(const iggy_raw_messages &m, const EncScratch &es, uint64_t i,
                                          uint64_t n) {
     EFrame f;
     f.i = i < n ? i : ~0ull;  // past this launch's range: none
-    if (i < n) {
-        f.po = es.tile_pl[i / kEncTile] + es.pl_local[i];
-        f.pl = m.payload_lengths[i];
-    } else {
-        f.po = 0;
-        f.pl = 0;
-    }
+    const uint64_t k = i < n ? i : 0;
+    f.tp = es.tile_pl[k / kEncTile];
+    f.lp = es.pl_local[k];
+    f.pl = m.payload_lengths[k];
     return f;
 }
 // 128-bit little-endian value (lo, hi) moved down by d bytes (0 <= d < 16)
@@ -353,28 +354,53 @@ struct EStep {
     uint4 v[8];    // raw 16-B payload loads of the 8 pieces
     uint4 last;    // last-stripe piece (long frames, first step only)
     uint64_t id0, id1, ots;  // header inputs (first step only)
+    bool clamped;  // the pieces took the clamped form (some lane near the payload area's end)
+    uint64_t ntp, nlp, npl;  // the record of the frame that becomes `nxt` at the next switch
 };
 // the loads of frame f's block b (fixed count: unneeded ones read the buffer start)
-__device__ __forceinline__ void eissue(const iggy_raw_messages &m, const EFrame &f, uint32_t b, uint32_t poff,
-                                       uint32_t mm, uint64_t ptot, EStep &st) {
+__device__ __forceinline__ void eissue(const iggy_raw_messages &m, const EncScratch &es, const EFrame &f,
+                                       uint32_t b, uint32_t poff, uint32_t mm, uint64_t ptot, uint64_t nrec,
+                                       EStep &st) {
     const bool live = f.i < m.count;
     const uint64_t L = 40 + f.pl;
     const uint8_t *P = m.payloads;
+    const uint64_t blk = (uint64_t)(b << 10);  // b < 2^22 (frames < 4 GiB): 32-bit shift
+    // Common form: every piece of the block lies inside the payload area (the block
+    // ends >= 16 B before it), so the 8 loads are one base + constant offsets, with
+    // no per-piece select. Pieces past the frame read the next message's payload,
+    // which the neighbouring lane group of the same wave reads at the same time.
+    const bool near_lane = live ? f.po() + blk + 984 > ptot : ptot < 1024;
+    st.clamped = __ballot(near_lane) != 0;
+    if (!st.clamped) {
+        const uint8_t *base = live ? P + f.po() + blk + poff - 40 : P;
+        // piece 0 of block 0: the header pieces (poff 0, 16: value unused) and the
+        // reserved | payload[0..8) piece (poff 32) read from the payload start
+        const uint8_t *a0 = live ? ((b == 0 && poff <= 32) ? P + f.po() : base) : P;
+        st.v[0] = ld128_any(a0);
+        const uint64_t rem = live && L > blk + poff ? L - blk - poff : 0;  // stream bytes from piece 0 on
 #pragma unroll
-    for (int q = 0; q < 8; ++q) {
-        const uint64_t sp = 1024ull * b + 128 * q + poff;  // stream position of the piece
-        // payload index of the piece's first byte (the s == 32 piece starts 8 B early)
-        const uint64_t px = f.po + (sp >= 40 ? sp - 40 : 0);
-        const bool need = live && sp + 16 > 32 && sp < L;
-        const uint64_t a = (px + 16 <= ptot) ? px : ptot - 16;  // clamp: realigned at use
-        st.v[q] = ld128_any(P + (need ? a : 0));
+        for (int q = 1; q < 8; ++q) st.v[q] = ld128_any(rem > 128 * q ? base + 128 * q : P);
+    } else {
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            const uint64_t sp = blk + 128 * q + poff;  // stream position of the piece
+            // payload index of the piece's first byte (the s == 32 piece starts 8 B early)
+            const uint64_t px = f.po() + (sp >= 40 ? sp - 40 : 0);
+            const bool need = live && sp + 16 > 32 && sp < L;
+            const uint64_t a = (px + 16 <= ptot) ? px : ptot - 16;  // clamp: realigned at use
+            st.v[q] = ld128_any(P + (need ? a : 0));
+        }
     }
     const bool lng = live && L > 240 && b == 0;
-    st.last = ld128_any(P + (lng ? f.po + (L - 64 + 16 * mm) - 40 : 0));
+    st.last = ld128_any(P + (lng ? f.po() + (L - 64 + 16 * mm) - 40 : 0));
     const uint64_t i = live && b == 0 ? f.i : 0;
     st.id0 = m.ids[2 * i];
     st.id1 = m.ids[2 * i + 1];
     st.ots = m.origin_timestamps[i];
+    const uint64_t k = nrec < m.count ? nrec : 0;
+    st.ntp = es.tile_pl[k / kEncTile];
+    st.nlp = es.pl_local[k];
+    st.npl = m.payload_lengths[k];
 }
 
 __global__ __launch_bounds__(256, 2) void k_enc_lanes(iggy_raw_messages m, EncScratch es, uint8_t *out,
@@ -402,6 +428,16 @@ __global__ __launch_bounds__(256, 2) void k_enc_lanes(iggy_raw_messages m, EncSc
 
     EFrame cur = eframe(m, es, f_lo + 8ull * vw + fg, n);
     EFrame nxt = eframe(m, es, cur.i == ~0ull ? ~0ull : cur.i + stride, n);
+    // The record of the frame after `nxt` travels with each step's load set (Y.n*),
+    // so that a frame switch only moves registers whose loads the step already
+    // waited for: a record loaded at the (divergent) switch itself was merged by
+    // register moves right after its load, a vmcnt(0) that drained every
+    // outstanding load and store of the wave at each frame switch.
+    auto rec_after = [&](uint64_t c, bool sw) -> uint64_t {  // frame after nxt once the next step is done
+        if (c == ~0ull) return ~0ull;
+        const uint64_t r = c + (sw ? 3 : 2) * stride;
+        return r < n ? r : ~0ull;
+    };
     uint32_t b = 0;
     uint64_t a0 = init0, a1 = init1;
     uint64_t h0 = 0, h1 = 0, h2 = 0, h3 = 0;  // header words of the current frame
@@ -415,8 +451,7 @@ __global__ __launch_bounds__(256, 2) void k_enc_lanes(iggy_raw_messages m, EncSc
         const uint64_t ns = lng ? ((L - 1) - 1024 * nbF) / 64 : 0;
         const uint32_t nblk = (uint32_t)((L + 1023) / 1024);
         const bool fin = b + 1 == nblk;
-        if (!fin) eissue(m, cur, b + 1, poff, mm, ptot, Y);
-        else eissue(m, nxt, 0, poff, mm, ptot, Y);
+        eissue(m, es, fin ? nxt : cur, fin ? 0u : b + 1, poff, mm, ptot, rec_after(cur.i, fin), Y);
         if (b == 0) {
             const uint64_t delta = X.ots - origin;
             if (delta > IGGY_MAX_TIMESTAMP_DELTA_MICROS && l == 0)
@@ -427,16 +462,16 @@ __global__ __launch_bounds__(256, 2) void k_enc_lanes(iggy_raw_messages m, EncSc
             h3 = cur.pl << 32;  // user_headers_len 0 | payload_len
             lastp = X.last;
         }
-        uint8_t *F = out + 256 + 48 * cur.i + cur.po;  // frame start
+        uint8_t *F = out + 256 + 48 * cur.i + cur.po();  // frame start
         uint64_t p0[4] = {0, 0, 0, 0}, p1[4] = {0, 0, 0, 0};
         uint64_t tw0 = 0, tw1 = 0, tsp = ~0ull;
 #pragma unroll
         for (int q = 0; q < 8; ++q) {
-            const uint64_t sp = 1024ull * b + 128 * q + poff;
+            const uint64_t sp = (uint64_t)((b << 10) + 128 * q + poff);
             uint64_t w0 = (uint64_t)X.v[q].x | ((uint64_t)X.v[q].y << 32);
             uint64_t w1 = (uint64_t)X.v[q].z | ((uint64_t)X.v[q].w << 32);
-            {  // a load clamped to the payload area's last 16 B: realign it
-                const uint64_t px = cur.po + (sp >= 40 ? sp - 40 : 0);
+            if (X.clamped) {  // a load clamped to the payload area's last 16 B: realign it
+                const uint64_t px = cur.po() + (sp >= 40 ? sp - 40 : 0);
                 if (px + 16 > ptot) shr_bytes(w0, w1, (uint32_t)(px + 16 - ptot));
             }
             if (sp < 40) {
@@ -460,10 +495,25 @@ __global__ __launch_bounds__(256, 2) void k_enc_lanes(iggy_raw_messages m, EncSc
                 }
             }
         }
-        if (tsp != ~0ull) {
+        if (tsp != ~0ull) {  // 1..15 bytes: at most one 8-, 4-, 2- and 1-byte store each
             uint8_t *d = F + 8 + tsp;
             const uint32_t rem = (uint32_t)(L - tsp);
-            for (uint32_t k = 0; k < rem; ++k) d[k] = (uint8_t)((k < 8 ? tw0 : tw1) >> (8 * (k & 7)));
+            if (rem & 8) {
+                st64_any(d, tw0);
+                d += 8;
+                tw0 = tw1;
+            }
+            if (rem & 4) {
+                *(u32_ua *)d = (uint32_t)tw0;
+                d += 4;
+                tw0 >>= 32;
+            }
+            if (rem & 2) {
+                *(u16_ua *)d = (uint16_t)tw0;
+                d += 2;
+                tw0 >>= 16;
+            }
+            if (rem & 1) *d = (uint8_t)tw0;
         }
         uint64_t hsh = 0;
         if (lng) {
@@ -492,7 +542,12 @@ __global__ __launch_bounds__(256, 2) void k_enc_lanes(iggy_raw_messages m, EncSc
                 es.cs[cur.i] = hsh;
             }
             cur = nxt;
-            nxt = eframe(m, es, cur.i == ~0ull ? ~0ull : cur.i + stride, n);
+            // X carries the record of the frame after nxt (issued a step ago)
+            const uint64_t ni = cur.i == ~0ull || cur.i + stride >= n ? ~0ull : cur.i + stride;
+            nxt.i = ni;
+            nxt.tp = X.ntp;
+            nxt.lp = X.nlp;
+            nxt.pl = X.npl;
             b = 0;
             a0 = init0;
             a1 = init1;
@@ -502,7 +557,7 @@ __global__ __launch_bounds__(256, 2) void k_enc_lanes(iggy_raw_messages m, EncSc
     };
     // ping-pong over two load sets (no register copy of in-flight loads)
     EStep A, B;
-    eissue(m, cur, 0, poff, mm, ptot, A);
+    eissue(m, es, cur, 0, poff, mm, ptot, rec_after(cur.i, false), A);
     while (__ballot(cur.i < n)) {
         step(A, B);
         if (!__ballot(cur.i < n)) break;

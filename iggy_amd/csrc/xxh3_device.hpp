@@ -142,6 +142,7 @@ __device__ __forceinline__ uint64_t scramble1(uint64_t x, uint64_t key) {
 // to single global_load_dword{,x2,x4} instructions.
 typedef uint64_t __attribute__((aligned(1))) u64_ua;
 typedef uint32_t __attribute__((aligned(1))) u32_ua;
+typedef uint16_t __attribute__((aligned(1))) u16_ua;
 typedef uint4 __attribute__((aligned(1))) u128_ua;
 __device__ __forceinline__ uint64_t ld64_any(const uint8_t *p) { return *(const u64_ua *)p; }
 __device__ __forceinline__ uint32_t ld32_any(const uint8_t *p) { return *(const u32_ua *)p; }
