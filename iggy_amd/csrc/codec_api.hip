@@ -108,7 +108,7 @@ struct iggy_codec_ctx {
     uint64_t dec_cap_len = 0;
     DevBuf dsync;    // exited | first_bad | spec_fail | bar[4] | misc[16] | small[512]
     DevBuf dsums, derr;
-    DevBuf gtiles_s, gtiles_x, gtiles_cnt, gtiles_pre, gtiles_list, gtiles_e, gtiles_base, ggrp, gfpos, gcs, gflen, gbsums;
+    DevBuf gtiles_s, gtiles_x, gtiles_cnt, gtiles_pre, gtiles_list, gtiles_e, gtiles_base, ggrp, gfpos, gcs, gtiles_lcs, gbsums;
     int gen_grid = 0;  // WGs of k_decode_general (the ones that get a CU join its barriers)
     // encode: the batch-checksum chain of earlier frame segments runs on `side`
     // while later segments are encoded on the call's stream
@@ -186,7 +186,7 @@ int ensure_decode_scratch(iggy_codec_ctx *c, uint64_t len) {
     r |= c->gtiles_base.ensure(ntiles * 8);
     r |= c->gfpos.ensure(max_frames * 8);
     r |= c->gcs.ensure(max_frames * 8);
-    r |= c->gflen.ensure(max_frames * 8);
+    r |= c->gtiles_lcs.ensure(tile_list_words(L) * 8);
     r |= c->gbsums.ensure(max_blocks * 64);
     if (r) return IGGY_ERR_DEVICE;
     c->dec_cap_len = L;
@@ -219,7 +219,7 @@ GeneralScratch gscratch(iggy_codec_ctx *c) {
     g.tile_base = c->gtiles_base.as<uint64_t>();
     g.fpos = c->gfpos.as<uint64_t>();
     g.cs = c->gcs.as<uint64_t>();
-    g.flen = c->gflen.as<uint64_t>();
+    g.tile_lcs = c->gtiles_lcs.as<uint64_t>();
     g.bsums = c->gbsums.as<uint64_t>();
     g.misc = c->dsync.as<uint64_t>(kSyncMisc);
     g.bar = c->dsync.as<uint32_t>(kSyncBar);
@@ -455,7 +455,7 @@ void iggy_codec_destroy(iggy_codec_ctx *c) {
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     DevBuf *bufs[] = {&c->dsync, &c->dsums, &c->derr, &c->gtiles_s, &c->gtiles_x,
-                      &c->gtiles_cnt, &c->gtiles_pre, &c->gtiles_list, &c->gtiles_e, &c->gtiles_base, &c->ggrp, &c->gfpos, &c->gcs, &c->gflen,
+                      &c->gtiles_cnt, &c->gtiles_pre, &c->gtiles_list, &c->gtiles_e, &c->gtiles_base, &c->ggrp, &c->gfpos, &c->gcs, &c->gtiles_lcs,
                       &c->gbsums, &c->dresult, &c->din, &c->dpos, &c->dout, &c->epl, &c->euh,
                       &c->etile, &c->ecs, &c->emisc, &c->eids, &c->eots, &c->epay, &c->eplen,
                       &c->euhb, &c->euhl, &c->hbsums, &c->ppos, &c->pmsgs, &c->pres, &c->cwk, &c->sl, &c->slres, &c->cr};

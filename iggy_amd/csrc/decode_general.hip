@@ -22,8 +22,8 @@
 //               skipped, entries re-walked and re-listed). The result is exactly
 //               the reference walk: true frame starts are always candidates and
 //               the first non-candidate ends the walk.
-//   C  scatter: one lane per accepted tile copies its list to walk order:
-//               frame positions, stored checksums, hashed lengths.
+//   C  scatter: sixteen lanes per accepted tile copy its lists to walk order:
+//               frame positions and the stored checksums locate read beside them.
 //   E  sums   : XXH3 stripe sums of the batch-checksum input, one wave / block.
 //   D + F     : wave 0 of WG 0 runs the serial scramble chain over the block
 //               sums while every other wave verifies frames (8 lanes per frame,
@@ -59,9 +59,10 @@ struct GeneralScratch {
     uint64_t *tile_e;    // [ntiles] repaired groups: true entry (~0: no frame starts here)
     uint64_t *tile_base; // [ntiles] repaired groups: frames before the tile
     uint64_t *grp;       // [ngroups * kGrpWords]
-    uint64_t *fpos;      // [max_frames] frame starts in walk order
+    uint64_t *tile_lcs;  // [ntiles * tile_list_cap(sh)] stored checksum of each listed frame
+    uint64_t *fpos;      // [max_frames] frame starts in walk order (hashed length of frame f:
+                         // fpos[f+1] - fpos[f] - 8, the last frame's from the walk end)
     uint64_t *cs;        // [max_frames] stored checksums in walk order
-    uint64_t *flen;      // [max_frames] hashed lengths (frame size - 8) in walk order
     uint64_t *bsums;     // [max_blocks * 8]
     uint64_t *misc;      // [16]: 0 nwalk, 1 end (with stop bit), 2 first_bad enc
     uint32_t *bar;       // [4]: 0 barrier arrivals, 2 registration (count | kRegClosed), 3 members
@@ -155,21 +156,25 @@ __device__ __forceinline__ uint32_t tile_shift(uint64_t bl, uint32_t message_cou
 }
 
 // walk the candidate chain from p while p < hi (hi <= bl); with a list, every
-// frame's offset from lo is recorded
+// frame's offset from lo and its stored checksum are recorded (the checksum load
+// goes out in the same round as the header test: the scatter phase then copies
+// lists instead of re-reading one random header line per frame)
 __device__ inline uint32_t walk(const uint8_t *blob, uint64_t bl, uint64_t p, uint64_t hi,
-                                uint64_t *x_out, uint32_t *list = nullptr, uint64_t lo = 0) {
+                                uint64_t *x_out, uint32_t *list = nullptr, uint64_t lo = 0,
+                                uint64_t *lcs = nullptr) {
     uint32_t cnt = 0;
     while (p < hi) {
-        uint64_t e;
-        if (!candidate(blob, bl, p, &e)) {
-            *x_out = p | kStopBit;
-            return cnt;
-        }
+        if (p >= bl || bl - p < kFrameHdr) break;
+        const uint4 w = ld128_any(blob + p + 32);  // lengths at +32/+36, reserved at +40
+        const uint64_t c = lcs ? ld64_any(blob + p) : 0;
+        const uint64_t e = p + kFrameHdr + (uint64_t)w.x + w.y;
+        if ((w.z | w.w) != 0 || e > bl) break;
         if (list) list[cnt] = (uint32_t)(p - lo);
+        if (lcs) lcs[cnt] = c;
         ++cnt;
         p = e;
     }
-    *x_out = p;  // >= hi (== bl: clean end)
+    *x_out = p < hi ? (p | kStopBit) : p;  // >= hi: left the tile (== bl: clean end)
     return cnt;
 }
 
@@ -246,7 +251,8 @@ __device__ inline int window_candidates(const uint8_t *blob, uint64_t bl, uint64
 // re-walks any tile whose pick disagrees with the true entry.
 constexpr int kPickWindows = 4;
 __device__ inline void pick_start(const uint8_t *blob, uint64_t bl, uint64_t lo, uint64_t hi,
-                                  uint32_t *list, uint64_t *s_out, uint64_t *x_out, uint32_t *cnt_out) {
+                                  uint32_t *list, uint64_t *lcs, uint64_t *s_out, uint64_t *x_out,
+                                  uint32_t *cnt_out) {
     uint64_t pick = kNoStart, clean_p = kNoStart, clean_x = kNoStart, first_valid = kNoStart;
     uint64_t from = lo;
     for (int w = 0; w < kPickWindows && pick == kNoStart; ++w) {
@@ -284,7 +290,7 @@ __device__ inline void pick_start(const uint8_t *blob, uint64_t bl, uint64_t lo,
     uint64_t x = kNoStart;
     uint32_t cnt = 0;
 #ifndef IGGY_DIAG_LOCATE_PICK_ONLY
-    if (pick != kNoStart) cnt = walk(blob, bl, pick, hi, &x, list, lo);
+    if (pick != kNoStart) cnt = walk(blob, bl, pick, hi, &x, list, lo, lcs);
 #endif
     *s_out = pick;
     *x_out = x;
@@ -311,8 +317,9 @@ __device__ __forceinline__ void word_contrib(uint64_t m, uint64_t v, uint64_t &x
 // each group hashes one 1024-B block of its current frame while the next block
 // (or the next frame's first block and last stripe) is loading into the other
 // of two register sets (ping-pong: in-flight loads are never copied, which
-// would make the wave wait for them). Positions, lengths and stored checksums
-// come from the scatter phase's arrays, one frame ahead. Lane l = (m, par) owns
+// would make the wave wait for them). Positions and stored checksums come from
+// the scatter phase's arrays, one frame ahead (a length is the distance to the
+// next frame's start). Lane l = (m, par) owns
 // accumulators 2m, 2m+1 for the stripes of parity par: in every block it reads
 // the 16 B at 128q + 16(m + 4 par), q = 0..7 (stripe 2q+par, words 2m, 2m+1);
 // the pair of parity lanes is folded before each scramble; the last stripe and
@@ -321,13 +328,13 @@ __device__ __forceinline__ void word_contrib(uint64_t m, uint64_t v, uint64_t &x
 struct VFrame {
     uint64_t f, p, stored, L;
 };
-__device__ __forceinline__ VFrame vframe(const GeneralScratch &gs, uint64_t f, uint64_t nwalk) {
+__device__ __forceinline__ VFrame vframe(const GeneralScratch &gs, uint64_t f, uint64_t nwalk, uint64_t wend) {
     VFrame v;
     v.f = f;
     if (f < nwalk) {
         v.p = gs.fpos[f];
         v.stored = gs.cs[f];
-        v.L = gs.flen[f];
+        v.L = (f + 1 < nwalk ? gs.fpos[f + 1] : wend) - v.p - 8;  // frames tile the walk
     } else {
         v.p = 0; v.stored = 0; v.L = 0;
     }
@@ -371,7 +378,7 @@ __device__ __forceinline__ void vissue(const uint8_t *blob, const VFrame &v, uin
 }
 
 __device__ inline void verify_frames(const uint8_t *blob, const GeneralScratch &gs, uint64_t nwalk,
-                                     uint32_t vw, uint32_t nvw, int lane, uint64_t t0) {
+                                     uint64_t wend, uint32_t vw, uint32_t nvw, int lane, uint64_t t0) {
     const uint32_t l = lane & 7, m = l >> 1, par = l & 1, fg = (uint32_t)lane >> 3;
     const uint32_t poff = 16 * (m + 4 * par);
     uint64_t s0[8], s1[8];
@@ -385,8 +392,8 @@ __device__ inline void verify_frames(const uint8_t *blob, const GeneralScratch &
     const uint64_t last0 = kSecretLast[2 * m], last1 = kSecretLast[2 * m + 1];
     const uint64_t mrg0 = kSecretMerge[2 * m], mrg1 = kSecretMerge[2 * m + 1];
     const uint64_t stride = 8ull * nvw;
-    VFrame cur = vframe(gs, 8ull * vw + fg, nwalk);
-    VFrame nxt = vframe(gs, cur.f + stride, nwalk);
+    VFrame cur = vframe(gs, 8ull * vw + fg, nwalk, wend);
+    VFrame nxt = vframe(gs, cur.f + stride, nwalk, wend);
     uint32_t b = 0;
     uint64_t a0 = init0, a1 = init1;
     uint4 lastp = make_uint4(0, 0, 0, 0);
@@ -437,7 +444,7 @@ __device__ inline void verify_frames(const uint8_t *blob, const GeneralScratch &
         }
         if (fin) {
             cur = nxt;
-            nxt = vframe(gs, cur.f + stride, nwalk);
+            nxt = vframe(gs, cur.f + stride, nwalk, wend);
             b = 0;
             a0 = init0;
             a1 = init1;
@@ -473,7 +480,7 @@ __device__ inline void verify_frames(const uint8_t *blob, const GeneralScratch &
 #pragma unroll
         for (int k = 0; k < (int)(kShortChunk / 64); ++k) {
             const uint64_t f = f0 + 64 * k + lane;
-            L[k] = f < nwalk ? gs.flen[f] : ~0ull;
+            L[k] = f < nwalk ? (f + 1 < nwalk ? gs.fpos[f + 1] : wend) - gs.fpos[f] - 8 : ~0ull;
         }
 #pragma unroll
         for (int k = 0; k < (int)(kShortChunk / 64); ++k) {
@@ -534,13 +541,14 @@ __global__ __launch_bounds__(kGenThreads) void k_decode_general(const uint8_t *_
     for (uint64_t t = 64 * wid + lane; t < ntiles; t += gthreads) {
         const uint64_t lo = t << sh, hi = min(lo + T, bl);
         uint32_t *list = gs.tile_list + t * lcap;
+        uint64_t *lcs = VERIFY ? gs.tile_lcs + t * lcap : nullptr;
         uint64_t s = kNoStart, x = kNoStart;
         uint32_t cnt = 0;
         if (t == 0) {
             s = 0;
-            cnt = walk(blob, bl, 0, hi, &x, list, 0);
+            cnt = walk(blob, bl, 0, hi, &x, list, 0, lcs);
         } else {
-            pick_start(blob, bl, lo, hi, list, &s, &x, &cnt);
+            pick_start(blob, bl, lo, hi, list, lcs, &s, &x, &cnt);
         }
         gs.tile_s[t] = s;
         gs.tile_cnt[t] = cnt;
@@ -829,11 +837,21 @@ __global__ __launch_bounds__(kGenThreads) void k_decode_general(const uint8_t *_
                 const uint64_t lo = t << sh, hi = min(lo + T, bl);
                 uint64_t x2 = 0;
                 uint32_t c2 = 0;
+#ifdef IGGY_CODEC_DIAG
+                if (lane == 0 && nrep < 2) {  // what the first repairs re-walked (scripts/diag_general.py)
+                    uint64_t *st = (uint64_t *)(gs.small + 512) + 20 + 6 * nrep;
+                    st[0] = t; st[1] = eb - lo; st[2] = gs.tile_s[t] - lo;
+                    st[3] = gs.tile_cnt[t]; st[4] = gs.tile_x[t] - lo;
+                }
+#endif
                 if (lane == 0) {
-                    c2 = walk(blob, bl, eb, hi, &x2, gs.tile_list + t * lcap, lo);
+                    c2 = walk(blob, bl, eb, hi, &x2, gs.tile_list + t * lcap, lo, VERIFY ? gs.tile_lcs + t * lcap : nullptr);
                     gs.tile_cnt[t] = c2;
                     gs.tile_e[t] = eb;
                     gs.tile_base[t] = total;
+#ifdef IGGY_CODEC_DIAG
+                    if (nrep < 2) ((uint64_t *)(gs.small + 512))[25 + 6 * nrep] = c2 | ((x2 - lo) << 32);
+#endif
                 }
                 x2 = __shfl(x2, 0);
                 c2 = (uint32_t)__shfl((int)c2, 0);
@@ -864,40 +882,74 @@ __global__ __launch_bounds__(kGenThreads) void k_decode_general(const uint8_t *_
     gstamp(gs, member, 3, rt_now() - t0);
 
     const uint64_t nwalk = __hip_atomic_load(&gs.misc[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    // ---------------- C: scatter the accepted tiles' lists (walk order). Sixteen lanes per
-    // tile, four tiles per wave: a tile's list entries are spread over its lanes so that one
-    // round of header loads serves up to sixteen frames (a lane-per-tile loop paid one
-    // dependent load round per frame).
+    // ---------------- C: scatter the accepted tiles' lists (walk order): frame positions
+    // and the stored checksums locate listed beside them. Sixteen lanes per tile, four
+    // tiles per wave; each pass takes kScatU tile quads and issues each load round
+    // (group word -> tile prefix and count -> list entries) for all of them together,
+    // since the phase is a chain of dependent load rounds.
     {
+        constexpr int kScatU = 4, kScatK = 2;  // quads per pass; list entries per lane before the remainder loop
         const uint32_t sub = (uint32_t)lane >> 4, k0 = (uint32_t)lane & 15;
-        for (uint64_t t4 = wid; t4 * 4 < ntiles; t4 += nwaves) {
-            const uint64_t t = t4 * 4 + sub;
-            uint64_t base = 0;
-            bool live = false;
-            if (t < ntiles) {
-                const uint64_t *q = gs.grp + kGrpWords * (t / kGrpTiles);
-                const uint64_t mode = q[5];
-                if (mode == 1) {
-                    const uint32_t pre = gs.tile_pre[t];
-                    live = pre != kNotLive;
-                    base = q[4] + pre;
-                } else if (mode == 2) {
-                    live = gs.tile_e[t] != ~0ull;
-                    base = gs.tile_base[t];
-                }
+        const uint64_t nquads = (ntiles + 3) / 4;
+        for (uint64_t q0 = wid; q0 < nquads; q0 += (uint64_t)kScatU * nwaves) {
+            uint64_t t[kScatU], mode[kScatU], g4[kScatU], base[kScatU], te[kScatU], tb[kScatU];
+            uint32_t pre[kScatU], cnt[kScatU];
+#pragma unroll
+            for (int u = 0; u < kScatU; ++u) {
+                t[u] = (q0 + (uint64_t)u * nwaves) * 4 + sub;
+                const uint64_t tt = t[u] < ntiles ? t[u] : 0;
+                const uint64_t *q = gs.grp + kGrpWords * (tt / kGrpTiles);
+                mode[u] = t[u] < ntiles ? q[5] : 0;
+                g4[u] = q[4];
+                pre[u] = gs.tile_pre[tt];
+                te[u] = gs.tile_e[tt];  // (read for every mode, used by repaired groups only)
+                tb[u] = gs.tile_base[tt];
+                cnt[u] = gs.tile_cnt[tt];
             }
-            const uint32_t cnt = live ? gs.tile_cnt[t] : 0;
-            const uint32_t *list = gs.tile_list + t * lcap;
-            const uint64_t lo = t << sh;
-            for (uint32_t k = k0; k < cnt; k += 16) {
-                const uint64_t p = lo + list[k], i = base + k;
-                gs.fpos[i] = p;
-                if (VERIFY) {
-                    gs.cs[i] = ld64_any(blob + p);
-                    const uint64_t ln = ld64_any(blob + p + 32);
-                    gs.flen[i] = 40 + (uint64_t)(uint32_t)ln + (ln >> 32);
+#pragma unroll
+            for (int u = 0; u < kScatU; ++u) {
+                bool live = false;
+                base[u] = 0;
+                if (mode[u] == 1) {
+                    live = pre[u] != kNotLive;
+                    base[u] = g4[u] + pre[u];
+                } else if (mode[u] == 2) {
+                    live = te[u] != ~0ull;
+                    base[u] = tb[u];
                 }
-                if (frame_pos && i < cap) frame_pos[i] = p;
+                if (!live) cnt[u] = 0;
+            }
+            uint32_t off[kScatU][kScatK];
+            uint64_t lc[kScatU][kScatK];
+#pragma unroll
+            for (int u = 0; u < kScatU; ++u)
+#pragma unroll
+                for (int j = 0; j < kScatK; ++j) {
+                    const uint32_t k = k0 + 16 * j;
+                    const uint64_t li = k < cnt[u] ? t[u] * lcap + k : 0;
+                    off[u][j] = gs.tile_list[li];
+                    lc[u][j] = VERIFY ? gs.tile_lcs[li] : 0;
+                }
+#pragma unroll
+            for (int u = 0; u < kScatU; ++u) {
+                const uint64_t lo = t[u] << sh;
+#pragma unroll
+                for (int j = 0; j < kScatK; ++j) {
+                    const uint32_t k = k0 + 16 * j;
+                    if (k >= cnt[u]) continue;
+                    const uint64_t p = lo + off[u][j], i = base[u] + k;
+                    gs.fpos[i] = p;
+                    if (VERIFY) gs.cs[i] = lc[u][j];
+                    if (frame_pos && i < cap) frame_pos[i] = p;
+                }
+                // tiles of more than 16 * kScatK frames (small frames): the rest a round at a time
+                for (uint32_t k = k0 + 16 * kScatK; k < cnt[u]; k += 16) {
+                    const uint64_t li = t[u] * lcap + k;
+                    const uint64_t p = lo + gs.tile_list[li], i = base[u] + k;
+                    gs.fpos[i] = p;
+                    if (VERIFY) gs.cs[i] = gs.tile_lcs[li];
+                    if (frame_pos && i < cap) frame_pos[i] = p;
+                }
             }
         }
     }
@@ -976,7 +1028,8 @@ __global__ __launch_bounds__(kGenThreads) void k_decode_general(const uint8_t *_
         const uint32_t vw = member * (blockDim.x >> 6) + wave - 1;
         const uint32_t nvw = nwg * (blockDim.x >> 6) - 1;
         if (vw == 0 && lane == 0) ((uint64_t *)(gs.small + 512))[17] = nvw;
-        verify_frames(blob, gs, nwalk, vw, nvw, lane, t0);
+        const uint64_t wend = __hip_atomic_load(&gs.misc[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & ~kStopBit;
+        verify_frames(blob, gs, nwalk, wend, vw, nvw, lane, t0);
     }
     ok &= grid_barrier(gs.bar, nwg * ++phase, t0);
     gstamp(gs, member, 6, rt_now() - t0);

@@ -61,6 +61,11 @@ def main():
                 "fast_steps": st[8], "summary_groups": st[9], "span_groups": st[10], "repaired_groups": st[11],
                 "ntiles": st[12], "tile_shift": st[13],
                 "verify_loop_end_max_us": round(st[14] / 100, 1), "verify_short_end_max_us": round(st[16] / 100, 1)}
+        rep = list(buf[84:96])
+        line["repairs"] = [{"tile": rep[6 * k], "true_entry": rep[6 * k + 1], "pick": rep[6 * k + 2],
+                            "old_cnt": rep[6 * k + 3], "old_exit": rep[6 * k + 4],
+                            "new_cnt": rep[6 * k + 5] & 0xFFFFFFFF, "new_exit": rep[6 * k + 5] >> 32}
+                           for k in range(min(2, st[11]))]
         nvw = st[17]
         if nvw:
             line["verify_loop_end_mean_us"] = round(st[15] / nvw / 100, 1)
