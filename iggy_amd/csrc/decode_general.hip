@@ -271,15 +271,28 @@ __device__ inline void pick_start(const uint8_t *blob, uint64_t bl, uint64_t lo,
             val[k] = k < nc && cp[k] + kFrameHdr <= bl && (hv[k].z | hv[k].w) == 0 && e[k] <= bl;
             sv[k] = ld128_any(blob + ((val[k] && e[k] < hi && e[k] + kFrameHdr <= bl) ? e[k] + 32 : 0));
         }
+        // Zero runs of a true header make false candidates 1-2 B BEFORE its start, whose
+        // "payload length" is the true one shifted left a byte; for small payloads that
+        // lands inside the tile and, now and then, on another header's zero run, so the
+        // false chain is confirmed too (C3: ~2 tiles per decode, each a serial re-walk
+        // in the link phase). So a confirmed pick moves to a later confirmed candidate
+        // of the same cluster (each within 16 B of the one before).
+        bool done = false;
+        uint64_t last_c = 0;
 #pragma unroll
         for (int k = 0; k < kPickBatch; ++k) {
-            if (!val[k] || pick != kNoStart) continue;
+            if (!val[k] || done) continue;
+            if (pick != kNoStart && cp[k] > last_c + 16) {
+                done = true;
+                continue;
+            }
+            last_c = cp[k];
             if (first_valid == kNoStart) first_valid = cp[k];
             if (e[k] < hi) {
                 const bool conf = e[k] + kFrameHdr <= bl && (sv[k].z | sv[k].w) == 0 &&
                                   e[k] + kFrameHdr + (uint64_t)sv[k].x + sv[k].y <= bl;
                 if (conf) pick = cp[k];
-            } else if (e[k] < clean_x) {
+            } else if (pick == kNoStart && e[k] < clean_x) {
                 clean_p = cp[k];
                 clean_x = e[k];
             }
@@ -324,7 +337,7 @@ __device__ __forceinline__ void word_contrib(uint64_t m, uint64_t v, uint64_t &x
 // the 16 B at 128q + 16(m + 4 par), q = 0..7 (stripe 2q+par, words 2m, 2m+1);
 // the pair of parity lanes is folded before each scramble; the last stripe and
 // merge follow the XXH3 long form (> 240 B). Frames of <= 240 hashed bytes are
-// checked after the loop, one lane each.
+// checked before the loop, one lane each.
 struct VFrame {
     uint64_t f, p, stored, L;
 };
@@ -378,7 +391,8 @@ __device__ __forceinline__ void vissue(const uint8_t *blob, const VFrame &v, uin
 }
 
 __device__ inline void verify_frames(const uint8_t *blob, const GeneralScratch &gs, uint64_t nwalk,
-                                     uint64_t wend, uint32_t vw, uint32_t nvw, int lane, uint64_t t0) {
+                                     uint64_t wend, uint32_t vw, uint32_t nvw, uint32_t member, uint32_t nwg,
+                                     uint32_t *s_claim, int lane, uint64_t t0) {
     const uint32_t l = lane & 7, m = l >> 1, par = l & 1, fg = (uint32_t)lane >> 3;
     const uint32_t poff = 16 * (m + 4 * par);
     uint64_t s0[8], s1[8];
@@ -392,8 +406,24 @@ __device__ inline void verify_frames(const uint8_t *blob, const GeneralScratch &
     const uint64_t last0 = kSecretLast[2 * m], last1 = kSecretLast[2 * m + 1];
     const uint64_t mrg0 = kSecretMerge[2 * m], mrg1 = kSecretMerge[2 * m + 1];
     const uint64_t stride = 8ull * nvw;
-    VFrame cur = vframe(gs, 8ull * vw + fg, nwalk, wend);
-    VFrame nxt = vframe(gs, cur.f + stride, nwalk, wend);
+    // Frames below fdyn follow the static stride (the chip-wide front). The last
+    // eighth is split over the workgroups (member m: fdyn + m + k * nwg) and claimed
+    // frame by frame from an LDS counter, so lane groups that drew light frames take
+    // more and the loop ends near the workgroup's mean group load, not its heaviest
+    // wave's (C3: loop end mean ~465 us vs max ~550 us with the stride alone). An
+    // LDS claim waits on lgkmcnt, never on the in-flight frame loads (vmcnt).
+    // (same-box A/B on C3, loop end mean / max: static only 734-760 / 802-830 us,
+    // last quarter claimed 766-771 / 804-818, last eighth 755-761 / 804-807)
+    const uint64_t fdyn = nwalk - nwalk / 8;
+    auto next_f = [&](uint64_t f) -> uint64_t {  // f: the static successor
+        if (f < fdyn) return f;
+        uint32_t k = 0;
+        if (l == 0) k = atomicAdd(s_claim, 1u);
+        k = (uint32_t)__shfl((int)k, lane & ~7);
+        return fdyn + member + (uint64_t)nwg * k;  // >= nwalk: none left
+    };
+    VFrame cur = vframe(gs, next_f(8ull * vw + fg), nwalk, wend);
+    VFrame nxt = vframe(gs, cur.f < nwalk ? next_f(cur.f < fdyn ? cur.f + stride : fdyn) : nwalk, nwalk, wend);
     uint32_t b = 0;
     uint64_t a0 = init0, a1 = init1;
     uint4 lastp = make_uint4(0, 0, 0, 0);
@@ -444,7 +474,7 @@ __device__ inline void verify_frames(const uint8_t *blob, const GeneralScratch &
         }
         if (fin) {
             cur = nxt;
-            nxt = vframe(gs, cur.f + stride, nwalk, wend);
+            nxt = vframe(gs, cur.f < nwalk ? next_f(cur.f < fdyn ? cur.f + stride : fdyn) : nwalk, nwalk, wend);
             b = 0;
             a0 = init0;
             a1 = init1;
@@ -452,6 +482,19 @@ __device__ inline void verify_frames(const uint8_t *blob, const GeneralScratch &
             ++b;
         }
     };
+    // frames of <= 240 hashed bytes: one lane each, a contiguous slice per wave, before
+    // the streaming loop (chunks claimed from one counter after the loop serialised
+    // ~4 K claims once the balanced tail made every wave finish together: +40 us on C3)
+    {
+        const uint64_t C = (nwalk + nvw - 1) / nvw;
+        const uint64_t f1 = min((uint64_t)(vw + 1) * C, nwalk);
+        for (uint64_t f = (uint64_t)vw * C + lane; f < f1; f += 64) {
+            const uint64_t p = gs.fpos[f];
+            const uint64_t L = (f + 1 < nwalk ? gs.fpos[f + 1] : wend) - p - 8;
+            if (L <= 240 && xxh3_64_lane(blob + p + 8, L) != gs.cs[f])
+                atomicMax((unsigned long long *)&gs.misc[2], (unsigned long long)~f);
+        }
+    }
     VStep A, B;
     vissue(blob, cur, nwalk, 0, par, poff, m, A);
     while (__ballot(cur.f < nwalk)) {
@@ -465,29 +508,6 @@ __device__ inline void verify_frames(const uint8_t *blob, const GeneralScratch &
         const uint64_t d = rt_now() - t0;
         atomicMax((unsigned long long *)&vstat[0], (unsigned long long)d);
         atomicAdd((unsigned long long *)&vstat[1], (unsigned long long)d);
-    }
-    // frames of <= 240 hashed bytes: one lane each, after the streaming loop, in
-    // chunks claimed from a counter, so that the waves whose loop ended early (the
-    // mean loop end is ~10 % before the slowest) do them while the slowest still stream
-    constexpr uint64_t kShortChunk = 256;
-    while (true) {
-        uint64_t c = 0;
-        if (lane == 0) c = atomicAdd((unsigned long long *)&gs.misc[6], 1ull);
-        c = __shfl(c, 0);
-        const uint64_t f0 = c * kShortChunk;
-        if (f0 >= nwalk) break;
-        uint64_t L[kShortChunk / 64];
-#pragma unroll
-        for (int k = 0; k < (int)(kShortChunk / 64); ++k) {
-            const uint64_t f = f0 + 64 * k + lane;
-            L[k] = f < nwalk ? (f + 1 < nwalk ? gs.fpos[f + 1] : wend) - gs.fpos[f] - 8 : ~0ull;
-        }
-#pragma unroll
-        for (int k = 0; k < (int)(kShortChunk / 64); ++k) {
-            const uint64_t f = f0 + 64 * k + lane;
-            if (L[k] <= 240 && xxh3_64_lane(blob + gs.fpos[f] + 8, L[k]) != gs.cs[f])
-                atomicMax((unsigned long long *)&gs.misc[2], (unsigned long long)~f);
-        }
     }
     if (lane == 0) atomicMax((unsigned long long *)&vstat[2], (unsigned long long)(rt_now() - t0));  // [16]
 }
@@ -509,7 +529,7 @@ __global__ __launch_bounds__(kGenThreads) void k_decode_general(const uint8_t *_
         kStatusNeedGeneral)
         return;
     const uint64_t t0 = rt_now();
-    __shared__ uint32_t s_mem[2];
+    __shared__ uint32_t s_mem[3];
     join_members(gs, t0, s_mem);
     const uint32_t member = s_mem[0];
     if (member == kNotMember) return;  // registered after the close: the members do the work
@@ -535,9 +555,7 @@ __global__ __launch_bounds__(kGenThreads) void k_decode_general(const uint8_t *_
     bool ok = true;
 
     // ---------------- A: locate
-    // (misc[6], the short-frame chunk counter of phase D+F, is re-armed here: the
-    // barriers in between order it before any claim)
-    if (member == 0 && threadIdx.x == 0) __hip_atomic_store(&gs.misc[6], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (threadIdx.x == 0) s_mem[2] = 0;  // the verify tail's claim counter (ordered by the barriers)
     for (uint64_t t = 64 * wid + lane; t < ntiles; t += gthreads) {
         const uint64_t lo = t << sh, hi = min(lo + T, bl);
         uint32_t *list = gs.tile_list + t * lcap;
@@ -991,6 +1009,8 @@ __global__ __launch_bounds__(kGenThreads) void k_decode_general(const uint8_t *_
             if (lane < 8) gs.bsums[b * 8 + lane] = t8;
         }
     }
+    // (a grid barrier, not a block-sum count only the chain wave waits for: with the
+    // verify waves going straight on, the C3 decode measured 15-25 us slower)
     ok &= grid_barrier(gs.bar, nwg * ++phase, t0);
     gstamp(gs, member, 5, rt_now() - t0);
 
@@ -1029,7 +1049,7 @@ __global__ __launch_bounds__(kGenThreads) void k_decode_general(const uint8_t *_
         const uint32_t nvw = nwg * (blockDim.x >> 6) - 1;
         if (vw == 0 && lane == 0) ((uint64_t *)(gs.small + 512))[17] = nvw;
         const uint64_t wend = __hip_atomic_load(&gs.misc[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & ~kStopBit;
-        verify_frames(blob, gs, nwalk, wend, vw, nvw, lane, t0);
+        verify_frames(blob, gs, nwalk, wend, vw, nvw, member, nwg, &s_mem[2], lane, t0);
     }
     ok &= grid_barrier(gs.bar, nwg * ++phase, t0);
     gstamp(gs, member, 6, rt_now() - t0);
