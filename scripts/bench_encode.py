@@ -20,6 +20,10 @@ import torch
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 from iggy_amd import abi  # noqa: E402
+from iggy_amd import codec as _codec  # noqa: E402
+
+if os.environ.get("IGGY_DIAG_LIB"):  # ablation bits (IGGY_CODEC_DBG) live only in the diagnostic build
+    _codec.use_library(os.environ["IGGY_DIAG_LIB"])
 from iggy_amd.codec import Codec  # noqa: E402
 
 
