@@ -58,7 +58,12 @@ constexpr uint32_t kLdsBytes = kSideOff + 4 * 64 * kSideLane;  // 155648
 // filled by kGatherWaves gatherer waves, drained by the chain wave
 constexpr uint32_t kBatch = 64;
 constexpr uint32_t kRing = 8;
-constexpr uint32_t kGatherWaves = 4;  // consumer WG waves 1..4; wave 0 runs the chain at raised priority
+// consumer WG waves 1..2 gather; wave 0 runs the chain at raised priority. Waves 3, 4
+// idle, so only the chain wave issues on its SIMD: with 4 gatherers one shared it, and
+// C2 decodes measured 0.2363-0.2402 ms against 0.2296-0.2314 ms (same box, with the
+// poll-free passes below); 2 gatherers still outpace the chain when it is the bound
+// (8 M x 64 B records: 1.43 ms either way)
+constexpr uint32_t kGatherWaves = 2;
 constexpr uint32_t kUniformThreads = 320;  // 4 producer waves + 1 publisher wave per WG (consumer: chain + 4 gatherers)
 constexpr uint32_t kCtlOff = kRing * kBatch * 16 * 8;  // 64 KiB
 struct ChainCtl {
@@ -947,8 +952,8 @@ constexpr int kAuxSc1 = 16;  // buffer-load cache policy: sc1 (agent-coherent, a
 // Lane c of a batch loads the block records of blocks 2c and 2c + 1 (256 B) and
 // stages their 16 accumulator sums, completed by the blocks' last words.
 __device__ __forceinline__ void gather(const uint8_t *blob, const UPlan &pl, const DecodeScratch &sc,
-                                       uint32_t epoch, uint32_t gw, uint8_t *smem, uint64_t t_start,
-                                       uint32_t dbg) {
+                                       uint32_t epoch, uint32_t gw, uint32_t ngw, uint8_t *smem,
+                                       uint64_t t_start, uint32_t dbg) {
     const int lane = threadIdx.x & 63;
     ChainCtl *ctl = (ChainCtl *)(smem + kCtlOff);
     uint64_t *ring = (uint64_t *)smem;
@@ -959,8 +964,8 @@ __device__ __forceinline__ void gather(const uint8_t *blob, const UPlan &pl, con
                rt_now() - t_start > kSpinLimitTicks;
     };
     const uint32_t tag = epoch << 8;  // high dword of a granule: spare8 | tag24 << 8
-    uint64_t npass = 0, npoll = 0, twait = 0;  // diagnostics (dbg 512)
-    for (uint64_t bi = gw; bi < nbatch; bi += kGatherWaves) {
+    uint64_t npass = 0, npoll = 0, twait = 0;  // diagnostics (dbg 512; npoll stays 0)
+    for (uint64_t bi = gw; bi < nbatch; bi += ngw) {
         const uint32_t slot = (uint32_t)(bi % kRing);
         bool abort = false;
         const uint64_t tw0 = rt_now();
@@ -983,28 +988,15 @@ __device__ __forceinline__ void gather(const uint8_t *blob, const UPlan &pl, con
         // (and lane 63 the next batch's first block's 4 spare-carrying granules),
         // stages the chunks whose tags (and the next chunk's) all match, and publishes
         // how many LEADING chunks of the batch are staged, so the chain starts on
-        // chunk 0 as soon as its 2 blocks are published. Between passes it polls the
-        // last granule of each block of the lowest unstaged chunk.
+        // chunk 0 as soon as its 2 blocks are published.
         bool staged = !live;
         uint32_t published = 0;
         for (bool first = true; !abort; first = false) {
             if (dbg & 512) ++npass;
-            if (!first) {
-                while (!abort) {
-                    if (dbg & 512) ++npoll;
-                    bool ok = true;
-                    if (!staged) {
-                        const g4 a = __builtin_amdgcn_raw_buffer_load_b128(rs, (uint32_t)lane * 256u + 112u, 0, kAuxSc1);
-                        const g4 b = __builtin_amdgcn_raw_buffer_load_b128(rs, (uint32_t)lane * 256u + 240u, 0, kAuxSc1);
-                        ok = (a.w >> 8) == epoch && (b.w >> 8) == epoch;
-                    }
-                    const uint64_t pend = __ballot(!staged);
-                    const uint64_t bad = __ballot(!ok);
-                    if (!(bad & (pend & (~pend + 1)))) break;  // the lowest unstaged chunk is ready
-                    __builtin_amdgcn_s_sleep(2);
-                    if (give_up()) abort = true;
-                }
-                if (abort) break;
+            if (!first) {  // the next full pass after a short sleep (a separate 2-granule poll
+                           // first cost one more round trip per staged batch)
+                __builtin_amdgcn_s_sleep(1);
+                if (give_up()) { abort = true; break; }
             }
             g4 r[16];
 #pragma unroll
@@ -1130,7 +1122,7 @@ __device__ __forceinline__ void consumer(const uint8_t *body, const HeaderInfo &
         __syncthreads();
     }
     if (wave != 0) {  // gatherer waves feed the chain wave through the LDS ring
-        if (chain && wave <= kGatherWaves) gather(blob, pl, sc, epoch, wave - 1, smem, t_start, dbg);
+        if (chain && wave <= kGatherWaves) gather(blob, pl, sc, epoch, wave - 1, kGatherWaves, smem, t_start, dbg);
         return;
     }
     if (chain) {
