@@ -237,15 +237,80 @@ __global__ __launch_bounds__(256) void k_bsum_blocks_range(const iggy_batch_head
 
 // full blocks [b_lo, min(b_hi, nb)) of the chain; state[8] carries the
 // accumulators between segments (b_lo == 0 starts from the XXH3 init)
-__global__ __launch_bounds__(64) void k_chain_partial(const uint64_t *nframes_p, const uint64_t *bsums,
-                                                      uint64_t *state, uint64_t b_lo, uint64_t b_hi) {
+// Blocks [b_lo, b_hi) of the chain, carried in `state` (8 words). Beside a
+// streaming kernel the chain wave's global loads come back after microseconds, so
+// three register groups of prefetch (48 blocks, ~1.5 us of chain) starved it: a
+// segment chain beside k_enc_lanes took 70-130 ns per step. Here waves 1..3 stage
+// chunks of kChainChunk block sums into an LDS double buffer, one chunk ahead of
+// wave 0, which chains from LDS (two register groups in flight).
+constexpr uint32_t kChainChunk = 512;  // blocks per staged chunk (32 KiB)
+__global__ __launch_bounds__(256) void k_chain_partial(const uint64_t *nframes_p, const uint64_t *bsums,
+                                                       uint64_t *state, uint64_t b_lo, uint64_t b_hi) {
     const CsPlan pl = cs_plan(*nframes_p);
     if (!pl.long_cs) return;
-    const int lane = threadIdx.x & 63;
     const uint64_t hi = b_hi < pl.nb ? b_hi : pl.nb;
     if (b_lo >= hi) return;
-    const uint64_t acc = chain_blocks(bsums + 8 * b_lo, hi - b_lo, lane, b_lo ? state : nullptr);
-    if (lane < 8) state[lane] = acc;
+    __shared__ uint4 buf[2][kChainChunk * 4];  // 8 u64 (4 x 16 B) per block
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint64_t nbk = hi - b_lo;
+    const uint64_t nch = (nbk + kChainChunk - 1) / kChainChunk;
+    const uint4 *src = (const uint4 *)(bsums + 8 * b_lo);
+    auto stage = [&](uint64_t c, uint32_t t0, uint32_t nt) {  // chunk c by threads t0.. (nt of them)
+        const uint64_t q0 = 4 * kChainChunk * c, q1 = min(q0 + 4 * kChainChunk, 4 * nbk);
+        constexpr int kU = 11;  // ceil(4 * kChainChunk / 192): every load of a chunk in flight at once
+        uint4 r[kU];
+#pragma unroll
+        for (int u = 0; u < kU; ++u) {
+            const uint64_t q = q0 + threadIdx.x - t0 + (uint64_t)u * nt;
+            r[u] = q < q1 ? src[q] : make_uint4(0, 0, 0, 0);
+        }
+#pragma unroll
+        for (int u = 0; u < kU; ++u) {
+            const uint64_t q = q0 + threadIdx.x - t0 + (uint64_t)u * nt;
+            if (q < q1) buf[c & 1][q - q0] = r[u];
+        }
+    };
+    if (threadIdx.x >= 64) stage(0, 64, 192);
+    __syncthreads();
+    const int j = lane & 7;
+    uint64_t acc = b_lo ? state[j] : kAccInit[j];
+    const uint64_t key = kSecretW8[16 + j];
+    const uint32_t klo = (uint32_t)key, khi = (uint32_t)(key >> 32);
+    for (uint64_t c = 0; c < nch; ++c) {
+        if (wave != 0) {
+            if (c + 1 < nch) stage(c + 1, 64, 192);
+        } else {
+            const uint64_t *b = (const uint64_t *)buf[c & 1];
+            const uint32_t kend = (uint32_t)min<uint64_t>(kChainChunk, nbk - kChainChunk * c);
+            uint32_t k = 0;
+            uint64_t va[16], vb[16];
+            if (kend >= 16) {
+#pragma unroll
+                for (int x = 0; x < 16; ++x) va[x] = b[8 * x + j];
+                while (true) {
+                    const bool more = k + 32 <= kend;
+                    if (more) {
+#pragma unroll
+                        for (int x = 0; x < 16; ++x) vb[x] = b[8 * (k + 16 + x) + j];
+                    }
+                    acc = chain_run16(acc, va, klo, khi);
+                    k += 16;
+                    if (!more) break;
+                    const bool more2 = k + 32 <= kend;
+                    if (more2) {
+#pragma unroll
+                        for (int x = 0; x < 16; ++x) va[x] = b[8 * (k + 16 + x) + j];
+                    }
+                    acc = chain_run16(acc, vb, klo, khi);
+                    k += 16;
+                    if (!more2) break;
+                }
+            }
+            for (; k < kend; ++k) acc = scramble_fast(acc + b[8 * k + j], klo, khi);
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x < 8) state[threadIdx.x] = acc;
 }
 
 // last partial block, last stripe and merge after the segments (or the whole

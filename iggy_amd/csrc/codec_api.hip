@@ -1115,12 +1115,18 @@ static int enqueue_encode(iggy_codec_ctx *c, const iggy_raw_messages *dm, uint64
             hipLaunchKernelGGL(k_enc_short, sgrid, dim3(256), 0, s, m, es, d_out);
         }
         // one resident round of lane-group waves (2 WGs of 256 per CU at 240 VGPRs)
-        const uint64_t lwg = std::min<uint64_t>((n + 31) / 32, (uint64_t)c->ncu * ((diag_bits(c) & 2048) ? 8 : 2));
+        // segmented: one CU stays free of lane-group waves, so the side stream's
+        // single-wave chain (k_chain_partial) issues on a SIMD of its own (sharing one
+        // with lane-group waves it ran 132 ns/step instead of ~31)
+        const uint64_t lcu = (segmented && !(diag_bits(c) & 16384)) ? (uint64_t)c->ncu - 1 : (uint64_t)c->ncu;
+        const uint64_t lwg = std::min<uint64_t>((n + 31) / 32, lcu * ((diag_bits(c) & 2048) ? 8 : 2));
         uint64_t *state = c->emisc.as<uint64_t>(512);
         for (int k = 0; k < nseg; ++k) {
             // blocks [B_k, B_k+1) need frames up to 128 B_k+1 - 6: segment k encodes
             // frames [F_k, F_k+1), F_k = 128 B_k - 5
             // uneven segments: the last one (whose chain cannot overlap) is ~6 % of the blocks
+            // (same box: 60 / 30 / 8 / 2 % measured no better once the segment chains
+            // stopped starving: 1.383-1.389 vs 1.376-1.386 ms)
             static const uint32_t kSegPermille[kEncSegs + 1] = {0, 400, 750, 940, 1000};
             auto bound = [&](int q) {
                 if (nseg == 1) return q ? nb : (uint64_t)0;
@@ -1137,7 +1143,7 @@ static int enqueue_encode(iggy_codec_ctx *c, const iggy_raw_messages *dm, uint64
                 hipLaunchKernelGGL(k_bsum_blocks_range, dim3(c->ncu / 2), dim3(256), 0, c->side,
                                    (const iggy_batch_header *)es.hdr, (const uint64_t *)&es.misc[3], src,
                                    c->gbsums.as<uint64_t>(), B0, B1);
-                hipLaunchKernelGGL(k_chain_partial, dim3(1), dim3(64), 0, c->side, (const uint64_t *)&es.misc[3],
+                hipLaunchKernelGGL(k_chain_partial, dim3(1), dim3(256), 0, c->side, (const uint64_t *)&es.misc[3],
                                    (const uint64_t *)c->gbsums.as<uint64_t>(), state, B0, B1);
             }
         }
@@ -1148,7 +1154,7 @@ static int enqueue_encode(iggy_codec_ctx *c, const iggy_raw_messages *dm, uint64
             HIP_OK(hipStreamWaitEvent(s, c->seg_ev[kEncSegs], 0));
             hipLaunchKernelGGL(k_bsum_blocks_range, dim3(c->ncu), dim3(256), 0, s, (const iggy_batch_header *)es.hdr,
                                (const uint64_t *)&es.misc[3], src, c->gbsums.as<uint64_t>(), Bl, nb + 1);
-            hipLaunchKernelGGL(k_chain_partial, dim3(1), dim3(64), 0, s, (const uint64_t *)&es.misc[3],
+            hipLaunchKernelGGL(k_chain_partial, dim3(1), dim3(256), 0, s, (const uint64_t *)&es.misc[3],
                                (const uint64_t *)c->gbsums.as<uint64_t>(), state, Bl, nb);
         }
     } else {
