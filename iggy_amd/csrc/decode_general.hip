@@ -574,7 +574,7 @@ __global__ __launch_bounds__(kGenThreads) void k_decode_general(const uint8_t *_
     }
     ok &= grid_barrier(gs.bar, nwg * ++phase, t0);
     gstamp(gs, member, 1, rt_now() - t0);
-    gstamp(gs, member, 14, 0); gstamp(gs, member, 15, 0); gstamp(gs, member, 16, 0);  // verify clock (below)
+    gstamp(gs, member, 14, 0); gstamp(gs, member, 15, 0); gstamp(gs, member, 16, 0); gstamp(gs, member, 18, 0);  // verify / chain clock (below)
 
     // ---------------- B1: group summaries (one wave per 256 tiles, 4 per lane)
     for (uint64_t g = wid; g < ngroups; g += nwaves) {
@@ -1033,6 +1033,7 @@ __global__ __launch_bounds__(kGenThreads) void k_decode_general(const uint8_t *_
             for (int i = 0; i < 4; ++i)
                 r += fold64(a[2 * i] ^ Secret::w(11 + 16 * i), a[2 * i + 1] ^ Secret::w(19 + 16 * i));
             computed = avalanche(r);
+            if (lane == 0) ((uint64_t *)(gs.small + 512))[18] = rt_now() - t0;  // phase clock: chain done
         } else if (VERIFY && lane == 0) {
             uint8_t *s = gs.small;
             const uint64_t w[5] = {h.partition_id, h.base_offset, h.base_timestamp,

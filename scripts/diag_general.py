@@ -60,7 +60,8 @@ def main():
                 "phase_us": [round(st[i] / 100, 1) for i in range(1, 7)],
                 "fast_steps": st[8], "summary_groups": st[9], "span_groups": st[10], "repaired_groups": st[11],
                 "ntiles": st[12], "tile_shift": st[13],
-                "verify_loop_end_max_us": round(st[14] / 100, 1), "verify_short_end_max_us": round(st[16] / 100, 1)}
+                "verify_loop_end_max_us": round(st[14] / 100, 1), "verify_short_end_max_us": round(st[16] / 100, 1),
+                "chain_done_us": round(buf[64 + 18] / 100, 1)}
         rep = list(buf[84:96])
         line["repairs"] = [{"tile": rep[6 * k], "true_entry": rep[6 * k + 1], "pick": rep[6 * k + 2],
                             "old_cnt": rep[6 * k + 3], "old_exit": rep[6 * k + 4],
