@@ -296,8 +296,14 @@ int enqueue_decode(iggy_codec_ctx *c, const uint8_t *d_body, uint64_t len, int i
     const bool verify = integrity == IGGY_INTEGRITY_VERIFY;
     DecodeScratch ds = dscratch(c);
     GeneralScratch gs = gscratch(c);
-    // one persistent grid: one WG per CU, block 0 the consumer (chain) WG
-    const uint32_t grid = (uint32_t)c->ugrid;
+    // one persistent grid: one WG per CU, block 0 the consumer (chain) WG. Small
+    // records get grids sized to their work (at most one producer WG per 128-frame
+    // block of 48-B frames; one general WG per 64 KiB): dispatching two full
+    // persistent grids dominated a 300-KB decode. Both kernels split their work
+    // over whatever grid they get.
+    const uint64_t ub_blocks = len / (48 * 128) + 2;
+    const uint32_t grid = (uint32_t)std::min<uint64_t>((uint64_t)c->ugrid, ub_blocks + 1);
+    const uint32_t ggrid = (uint32_t)std::min<uint64_t>((uint64_t)c->gen_grid, len / (64 << 10) + 2);
     const uint32_t au = (uint32_t)c->allow_unaligned;
     prof_begin(c, 0, s);
     if (verify)
@@ -309,10 +315,10 @@ int enqueue_decode(iggy_codec_ctx *c, const uint8_t *d_body, uint64_t len, int i
     prof_end(c, 0, s);
     HIP_OK(hipGetLastError());
     if (verify) {
-        hipLaunchKernelGGL(k_decode_general<true>, dim3(c->gen_grid), dim3(kGenThreads), 0, s, d_body, len, d_pos,
+        hipLaunchKernelGGL(k_decode_general<true>, dim3(ggrid), dim3(kGenThreads), 0, s, d_body, len, d_pos,
                            cap, d_res, gs);
     } else {
-        hipLaunchKernelGGL(k_decode_general<false>, dim3(c->gen_grid), dim3(kGenThreads), 0, s, d_body, len,
+        hipLaunchKernelGGL(k_decode_general<false>, dim3(ggrid), dim3(kGenThreads), 0, s, d_body, len,
                            d_pos, cap, d_res, gs);
     }
     HIP_OK(hipGetLastError());
