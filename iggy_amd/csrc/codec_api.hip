@@ -285,6 +285,13 @@ void prof_end(iggy_codec_ctx *c, int which, hipStream_t s) {
 }
 
 // launch the whole decode (uniform kernel + guarded general kernel)
+// k_bsum_blocks grid: one wave per 1024-B block of the checksum input (44 + 8 N
+// bytes, N <= max_frames), at most 4 WGs per CU; small inputs launch a small grid
+static uint32_t bsum_grid(const iggy_codec_ctx *c, uint64_t max_frames) {
+    const uint64_t blocks = (44 + 8 * max_frames) / 1024 + 1;
+    return (uint32_t)std::min<uint64_t>((uint64_t)c->ncu * 4, (blocks + 3) / 4);
+}
+
 int enqueue_decode(iggy_codec_ctx *c, const uint8_t *d_body, uint64_t len, int integrity,
                    uint64_t *d_pos, uint64_t cap, iggy_decode_result *d_res, hipStream_t s) {
     int r = ensure_decode_scratch(c, len);
@@ -624,7 +631,7 @@ static int checksum_of_walk(iggy_codec_ctx *c, const iggy_batch_header *hdr, uin
     uint64_t *d_n = c->dresult.as<uint64_t>(3096);
     hipLaunchKernelGGL(k_put_header, dim3(1), dim3(64), 0, s, *hdr, nframes, (const uint64_t *)nullptr, dh, d_n);
     CsSource src{nullptr, d_blob, d_pos};
-    hipLaunchKernelGGL(k_bsum_blocks, dim3(c->ncu * 4), dim3(256), 0, s, dh, d_n, src,
+    hipLaunchKernelGGL(k_bsum_blocks, dim3(bsum_grid(c, nframes)), dim3(256), 0, s, dh, d_n, src,
                        c->gbsums.as<uint64_t>(), nullptr);
     hipLaunchKernelGGL(k_bsum_chain, dim3(1), dim3(64), 0, s, dh, d_n, src,
                        (const uint64_t *)c->gbsums.as<uint64_t>(), c->dsync.as<uint8_t>(kSyncSmall), d_out,
@@ -651,7 +658,7 @@ static int enqueue_checksum_of_staged(iggy_codec_ctx *c, const iggy_batch_header
     hipLaunchKernelGGL(k_put_header, dim3(1), dim3(64), 0, c->stream, hdr, (uint64_t)0,
                        (const uint64_t *)&d_res->frame_count, dh, d_n);
     CsSource src{nullptr, c->din.as<uint8_t>(256), c->dpos.as<uint64_t>()};
-    hipLaunchKernelGGL(k_bsum_blocks, dim3(c->ncu * 4), dim3(256), 0, c->stream, dh, d_n, src,
+    hipLaunchKernelGGL(k_bsum_blocks, dim3(bsum_grid(c, cap)), dim3(256), 0, c->stream, dh, d_n, src,
                        c->gbsums.as<uint64_t>(), nullptr);
     hipLaunchKernelGGL(k_bsum_chain, dim3(1), dim3(64), 0, c->stream, dh, d_n, src,
                        (const uint64_t *)c->gbsums.as<uint64_t>(), c->dsync.as<uint8_t>(kSyncSmall), d_out, nullptr);
@@ -770,7 +777,7 @@ int iggy_codec_admit_batch(iggy_codec_ctx *c, const uint8_t *batch, uint64_t len
         hipLaunchKernelGGL(k_admit_header, dim3(1), dim3(64), 0, c->stream, (const iggy_decode_result *)d_res,
                            partition_id, dh, d_n);
         CsSource src{nullptr, c->din.as<uint8_t>(256), c->dpos.as<uint64_t>()};
-        hipLaunchKernelGGL(k_bsum_blocks, dim3(c->ncu * 4), dim3(256), 0, c->stream, dh, d_n, src,
+        hipLaunchKernelGGL(k_bsum_blocks, dim3(bsum_grid(c, pcap)), dim3(256), 0, c->stream, dh, d_n, src,
                            c->gbsums.as<uint64_t>(), nullptr);
         hipLaunchKernelGGL(k_bsum_chain, dim3(1), dim3(64), 0, c->stream, dh, d_n, src,
                            (const uint64_t *)c->gbsums.as<uint64_t>(), c->dsync.as<uint8_t>(kSyncSmall), d_cs,
@@ -1173,7 +1180,7 @@ static int enqueue_encode(iggy_codec_ctx *c, const iggy_raw_messages *dm, uint64
                            (const uint64_t *)&es.misc[3], src, (const uint64_t *)c->gbsums.as<uint64_t>(),
                            (const uint64_t *)c->emisc.as<uint64_t>(512), c->emisc.as<uint8_t>(320), dcs);
     } else {
-        hipLaunchKernelGGL(k_bsum_blocks, dim3(c->ncu * 4), dim3(256), 0, s, (const iggy_batch_header *)es.hdr,
+        hipLaunchKernelGGL(k_bsum_blocks, dim3(bsum_grid(c, n)), dim3(256), 0, s, (const iggy_batch_header *)es.hdr,
                            (const uint64_t *)&es.misc[3], src, c->gbsums.as<uint64_t>(), nullptr);
         hipLaunchKernelGGL(k_bsum_chain, dim3(1), dim3(64), 0, s, (const iggy_batch_header *)es.hdr,
                            (const uint64_t *)&es.misc[3], src, (const uint64_t *)c->gbsums.as<uint64_t>(),
@@ -1572,7 +1579,7 @@ int enqueue_crypt(iggy_codec_ctx *c, bool enc, const uint8_t *key, const uint8_t
     hipLaunchKernelGGL(k_crypt_checksums, dim3(c->ncu * 16), dim3(256), 0, s, d_out, cap, cs);
     hipLaunchKernelGGL(k_crypt_header, dim3(1), dim3(64), 0, s, cap, cs);
     CsSource src{nullptr, d_out + kHdr, cs.opos};
-    hipLaunchKernelGGL(k_bsum_blocks, dim3(c->ncu * 4), dim3(256), 0, s, cs.dh, cs.dn, src,
+    hipLaunchKernelGGL(k_bsum_blocks, dim3(bsum_grid(c, cap / 48 + 1)), dim3(256), 0, s, cs.dh, cs.dn, src,
                        c->gbsums.as<uint64_t>(), nullptr);
     hipLaunchKernelGGL(k_bsum_chain, dim3(1), dim3(64), 0, s, cs.dh, cs.dn, src,
                        (const uint64_t *)c->gbsums.as<uint64_t>(), c->dsync.as<uint8_t>(kSyncSmall), cs.dsum,
@@ -1626,7 +1633,7 @@ static int enqueue_select(iggy_codec_ctx *c, const uint8_t *d_record, const uint
     hipLaunchKernelGGL(k_slice_pick, dim3(1), dim3(256), 0, s, d_record, d_frame_pos, nframes, qq,
                        (const uint32_t *)ss.tile_cnt, ntiles, ss, d_out, gate, d_matched);
     CsSource src{nullptr, d_record + kHdr, d_frame_pos, ss.first};
-    hipLaunchKernelGGL(k_bsum_blocks, dim3(c->ncu * 4), dim3(256), 0, s, (const iggy_batch_header *)ss.hdr,
+    hipLaunchKernelGGL(k_bsum_blocks, dim3(bsum_grid(c, nframes)), dim3(256), 0, s, (const iggy_batch_header *)ss.hdr,
                        (const uint64_t *)ss.nsel, src, c->gbsums.as<uint64_t>(), (const uint32_t *)ss.skip);
     hipLaunchKernelGGL(k_bsum_chain, dim3(1), dim3(64), 0, s, (const iggy_batch_header *)ss.hdr,
                        (const uint64_t *)ss.nsel, src, (const uint64_t *)c->gbsums.as<uint64_t>(),
@@ -1783,7 +1790,7 @@ int iggy_codec_stamp_batch_device(iggy_codec_ctx *c, uint8_t *d_record, const ui
     hipLaunchKernelGGL(k_stamp_prep, dim3(1), dim3(64), 0, s, (const uint8_t *)d_record, base_offset, base_timestamp,
                        nframes, dh, dn);
     CsSource src{nullptr, d_record + kHdr, d_frame_pos};
-    hipLaunchKernelGGL(k_bsum_blocks, dim3(c->ncu * 4), dim3(256), 0, s, (const iggy_batch_header *)dh,
+    hipLaunchKernelGGL(k_bsum_blocks, dim3(bsum_grid(c, nframes)), dim3(256), 0, s, (const iggy_batch_header *)dh,
                        (const uint64_t *)dn, src, c->gbsums.as<uint64_t>(), nullptr);
     hipLaunchKernelGGL(k_bsum_chain, dim3(1), dim3(64), 0, s, (const iggy_batch_header *)dh, (const uint64_t *)dn,
                        src, (const uint64_t *)c->gbsums.as<uint64_t>(), c->sl.as<uint8_t>(128), dcs, nullptr);
