@@ -112,6 +112,87 @@ __device__ inline uint64_t chain_blocks(const uint64_t *bsums, uint64_t nb, int 
     return acc;
 }
 
+// The same chain handed between two waves of a workgroup whose other waves do
+// something else (the general decode's verify): the stager wave copies chunks of
+// kChainChunk block sums into an LDS double buffer, the chain wave consumes them.
+// Reading its sums straight from global memory beside the verify stream, the
+// chain wave waited microseconds per prefetch group (C3: 53-56 ns per step). LDS
+// flags: [0], [1] = chunk index + 1 staged in buffer 0 / 1, [2] = chunks consumed.
+// Every wait is bounded (the waiter gives up after kSpinLimitTicks).
+constexpr uint32_t kChainChunk = 512;  // blocks per staged chunk (32 KiB)
+__device__ inline void chain_stager(const uint64_t *bsums, uint64_t nb, uint64_t *buf, uint32_t *flags, int lane,
+                                    uint64_t t0) {
+    const uint64_t nch = (nb + kChainChunk - 1) / kChainChunk;
+    const uint4 *src = (const uint4 *)bsums;
+    for (uint64_t c = 0; c < nch; ++c) {
+        // buffer c & 1 is free once chunk c - 2 is consumed
+        while (c >= 2 && __hip_atomic_load(&flags[2], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) + 2 <= c) {
+            __builtin_amdgcn_s_sleep(1);
+            if (rt_now() - t0 > kSpinLimitTicks) return;
+        }
+        uint4 *dst = (uint4 *)(buf + (c & 1) * kChainChunk * 8);
+        const uint64_t q0 = 4 * kChainChunk * c, q1 = min(q0 + 4 * kChainChunk, 4 * nb);
+        for (uint32_t h = 0; h < 2; ++h) {  // two rounds of 16 loads per lane
+            uint4 r[16];
+#pragma unroll
+            for (int u = 0; u < 16; ++u) {
+                const uint64_t q = q0 + 1024u * h + lane + 64u * u;
+                r[u] = q < q1 ? src[q] : make_uint4(0, 0, 0, 0);
+            }
+#pragma unroll
+            for (int u = 0; u < 16; ++u) {
+                const uint64_t q = q0 + 1024u * h + lane + 64u * u;
+                if (q < q1) dst[q - q0] = r[u];
+            }
+        }
+        __hip_atomic_store(&flags[c & 1], (uint32_t)(c + 1), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+}
+// the chain over nb blocks from the stager's buffer (false: gave up waiting)
+__device__ inline bool chain_staged(uint64_t nb, const uint64_t *buf, uint32_t *flags, int lane, uint64_t t0,
+                                    uint64_t &acc) {
+    const int j = lane & 7;
+    acc = kAccInit[j];
+    const uint64_t key = kSecretW8[16 + j];
+    const uint32_t klo = (uint32_t)key, khi = (uint32_t)(key >> 32);
+    const uint64_t nch = (nb + kChainChunk - 1) / kChainChunk;
+    for (uint64_t c = 0; c < nch; ++c) {
+        while (__hip_atomic_load(&flags[c & 1], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != c + 1) {
+            __builtin_amdgcn_s_sleep(1);
+            if (rt_now() - t0 > kSpinLimitTicks) return false;
+        }
+        const uint64_t *b = buf + (c & 1) * kChainChunk * 8;
+        const uint32_t kend = (uint32_t)min<uint64_t>(kChainChunk, nb - kChainChunk * c);
+        uint32_t k = 0;
+        uint64_t va[16], vb[16];
+        if (kend >= 16) {
+#pragma unroll
+            for (int x = 0; x < 16; ++x) va[x] = b[8 * x + j];
+            while (true) {
+                const bool more = k + 32 <= kend;
+                if (more) {
+#pragma unroll
+                    for (int x = 0; x < 16; ++x) vb[x] = b[8 * (k + 16 + x) + j];
+                }
+                acc = chain_run16(acc, va, klo, khi);
+                k += 16;
+                if (!more) break;
+                const bool more2 = k + 32 <= kend;
+                if (more2) {
+#pragma unroll
+                    for (int x = 0; x < 16; ++x) va[x] = b[8 * (k + 16 + x) + j];
+                }
+                acc = chain_run16(acc, vb, klo, khi);
+                k += 16;
+                if (!more2) break;
+            }
+        }
+        for (; k < kend; ++k) acc = scramble_fast(acc + b[8 * k + j], klo, khi);
+        __hip_atomic_store(&flags[2], (uint32_t)(c + 1), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+    return true;
+}
+
 // Header fields (by value) and the frame count (by value, or from a device word an
 // earlier kernel on the stream wrote, e.g. a decode's frame_count) into the device
 // words the checksum kernels read: no host copy on the enqueue path.
@@ -243,7 +324,6 @@ __global__ __launch_bounds__(256) void k_bsum_blocks_range(const iggy_batch_head
 // segment chain beside k_enc_lanes took 70-130 ns per step. Here waves 1..3 stage
 // chunks of kChainChunk block sums into an LDS double buffer, one chunk ahead of
 // wave 0, which chains from LDS (two register groups in flight).
-constexpr uint32_t kChainChunk = 512;  // blocks per staged chunk (32 KiB)
 __global__ __launch_bounds__(256) void k_chain_partial(const uint64_t *nframes_p, const uint64_t *bsums,
                                                        uint64_t *state, uint64_t b_lo, uint64_t b_hi) {
     const CsPlan pl = cs_plan(*nframes_p);

@@ -530,6 +530,9 @@ __global__ __launch_bounds__(kGenThreads) void k_decode_general(const uint8_t *_
         return;
     const uint64_t t0 = rt_now();
     __shared__ uint32_t s_mem[3];
+    __shared__ uint64_t s_cbuf[2 * kChainChunk * 8];  // the chain's staged block sums (64 KiB)
+    __shared__ uint32_t s_cflags[3];
+    if (threadIdx.x < 3) s_cflags[threadIdx.x] = 0;  // (ordered by the barriers before phase D + F)
     join_members(gs, t0, s_mem);
     const uint32_t member = s_mem[0];
     if (member == kNotMember) return;  // registered after the close: the members do the work
@@ -1016,10 +1019,13 @@ __global__ __launch_bounds__(kGenThreads) void k_decode_general(const uint8_t *_
 
     // ---------------- D + F: chain (wave 0 of WG 0) beside frame verification
     uint64_t computed = 0;
+    // WG 0: wave 0 chains, wave 1 stages its block sums through LDS (chain_stager);
+    // every other wave verifies
     if (member == 0 && wave == 0) {
         if (long_cs) {
             const int j = lane & 7;
-            uint64_t acc = chain_blocks(gs.bsums, nb, lane);
+            uint64_t acc = 0;
+            if (!chain_staged(nb, s_cbuf, s_cflags, lane, t0, acc)) ok = false;
             acc += gs.bsums[nb * 8 + j];
             const uint64_t v = gs.cs[nwalk - 8 + j];
             const uint64_t vx = __shfl_xor(v, 1);
@@ -1045,9 +1051,12 @@ __global__ __launch_bounds__(kGenThreads) void k_decode_general(const uint8_t *_
                 for (int k = 0; k < 8; ++k) s[44 + 8 * i + k] = (uint8_t)(gs.cs[i] >> (8 * k));
             computed = xxh3_64_lane(s, n);
         }
+    } else if (member == 0 && wave == 1 && long_cs) {
+        chain_stager(gs.bsums, nb, s_cbuf, s_cflags, lane, t0);
     } else if (VERIFY) {
-        const uint32_t vw = member * (blockDim.x >> 6) + wave - 1;
-        const uint32_t nvw = nwg * (blockDim.x >> 6) - 1;
+        const uint32_t ws = long_cs ? 2 : 1;  // WG 0's waves below ws chain (and stage)
+        const uint32_t vw = member * (blockDim.x >> 6) + wave - ws;
+        const uint32_t nvw = nwg * (blockDim.x >> 6) - ws;
         if (vw == 0 && lane == 0) ((uint64_t *)(gs.small + 512))[17] = nvw;
         const uint64_t wend = __hip_atomic_load(&gs.misc[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & ~kStopBit;
         verify_frames(blob, gs, nwalk, wend, vw, nvw, member, nwg, &s_mem[2], lane, t0);
