@@ -4,8 +4,8 @@
 //
 // The input is 44 + 8N bytes; as XXH3 "long" input it is 1024-B blocks whose
 // 16 stripe contributions commute (computed in parallel, one wave per block,
-// k_bsum_blocks) chained by one scramble per block (k_bsum_chain, one wave,
-// lane j carries accumulator j). Word m of the input (8 bytes at 8m):
+// k_bsum_blocks) chained by one scramble per block (k_bsum_chain: one wave chains,
+// lane j carries accumulator j; a second wave stages its sums through LDS). Word m of the input (8 bytes at 8m):
 //   m < 5  : partition_id, base_offset, base_timestamp, origin_timestamp, batch_length
 //   m == 5 : message_count | lo32(cs_0) << 32
 //   m >= 6 : hi32(cs_{m-6}) | lo32(cs_{m-5}) << 32
@@ -251,19 +251,30 @@ __global__ __launch_bounds__(256) void k_bsum_blocks(const iggy_batch_header *hp
 }
 
 // one wave: out[0] = batch checksum. `small` >= 240 B scratch for short inputs.
-__global__ __launch_bounds__(64) void k_bsum_chain(const iggy_batch_header *hp,
-                                                   const uint64_t *nframes_p, CsSource src,
-                                                   const uint64_t *bsums, uint8_t *small,
-                                                   uint64_t *out, const uint32_t *skip) {
+// two waves: wave 0 chains, wave 1 stages the block sums through LDS (chain_stager)
+__global__ __launch_bounds__(128) void k_bsum_chain(const iggy_batch_header *hp,
+                                                    const uint64_t *nframes_p, CsSource src,
+                                                    const uint64_t *bsums, uint8_t *small,
+                                                    uint64_t *out, const uint32_t *skip) {
     if (skip && *skip) return;
     const iggy_batch_header h = *hp;
     const uint64_t N = *nframes_p;
     if (src.first) src.fpos += *src.first;
     const CsPlan pl = cs_plan(N);
     const int lane = threadIdx.x & 63;
+    __shared__ uint64_t s_cbuf[2 * kChainChunk * 8];
+    __shared__ uint32_t s_cflags[3];
+    if (threadIdx.x < 3) s_cflags[threadIdx.x] = 0;
+    __syncthreads();
+    const uint64_t t0 = rt_now();
+    if (threadIdx.x >= 64) {
+        if (pl.long_cs) chain_stager(bsums, pl.nb, s_cbuf, s_cflags, lane, t0);
+        return;
+    }
     if (pl.long_cs) {
         const int j = lane & 7;
-        uint64_t acc = chain_blocks(bsums, pl.nb, lane);
+        uint64_t acc = 0;
+        if (!chain_staged(pl.nb, s_cbuf, s_cflags, lane, t0, acc)) acc = 0;  // bug guard (4 s): a wrong checksum
         acc += bsums[pl.nb * 8 + j];
         const uint64_t v = src(N - 8 + j);
         acc += __shfl_xor(v, 1);

@@ -633,7 +633,7 @@ static int checksum_of_walk(iggy_codec_ctx *c, const iggy_batch_header *hdr, uin
     CsSource src{nullptr, d_blob, d_pos};
     hipLaunchKernelGGL(k_bsum_blocks, dim3(bsum_grid(c, nframes)), dim3(256), 0, s, dh, d_n, src,
                        c->gbsums.as<uint64_t>(), nullptr);
-    hipLaunchKernelGGL(k_bsum_chain, dim3(1), dim3(64), 0, s, dh, d_n, src,
+    hipLaunchKernelGGL(k_bsum_chain, dim3(1), dim3(128), 0, s, dh, d_n, src,
                        (const uint64_t *)c->gbsums.as<uint64_t>(), c->dsync.as<uint8_t>(kSyncSmall), d_out,
                        nullptr);
     HIP_OK(hipGetLastError());
@@ -660,7 +660,7 @@ static int enqueue_checksum_of_staged(iggy_codec_ctx *c, const iggy_batch_header
     CsSource src{nullptr, c->din.as<uint8_t>(256), c->dpos.as<uint64_t>()};
     hipLaunchKernelGGL(k_bsum_blocks, dim3(bsum_grid(c, cap)), dim3(256), 0, c->stream, dh, d_n, src,
                        c->gbsums.as<uint64_t>(), nullptr);
-    hipLaunchKernelGGL(k_bsum_chain, dim3(1), dim3(64), 0, c->stream, dh, d_n, src,
+    hipLaunchKernelGGL(k_bsum_chain, dim3(1), dim3(128), 0, c->stream, dh, d_n, src,
                        (const uint64_t *)c->gbsums.as<uint64_t>(), c->dsync.as<uint8_t>(kSyncSmall), d_out, nullptr);
     HIP_OK(hipGetLastError());
     return 0;
@@ -779,7 +779,7 @@ int iggy_codec_admit_batch(iggy_codec_ctx *c, const uint8_t *batch, uint64_t len
         CsSource src{nullptr, c->din.as<uint8_t>(256), c->dpos.as<uint64_t>()};
         hipLaunchKernelGGL(k_bsum_blocks, dim3(bsum_grid(c, pcap)), dim3(256), 0, c->stream, dh, d_n, src,
                            c->gbsums.as<uint64_t>(), nullptr);
-        hipLaunchKernelGGL(k_bsum_chain, dim3(1), dim3(64), 0, c->stream, dh, d_n, src,
+        hipLaunchKernelGGL(k_bsum_chain, dim3(1), dim3(128), 0, c->stream, dh, d_n, src,
                            (const uint64_t *)c->gbsums.as<uint64_t>(), c->dsync.as<uint8_t>(kSyncSmall), d_cs,
                            nullptr);
         HIP_OK(hipGetLastError());
@@ -1182,7 +1182,7 @@ static int enqueue_encode(iggy_codec_ctx *c, const iggy_raw_messages *dm, uint64
     } else {
         hipLaunchKernelGGL(k_bsum_blocks, dim3(bsum_grid(c, n)), dim3(256), 0, s, (const iggy_batch_header *)es.hdr,
                            (const uint64_t *)&es.misc[3], src, c->gbsums.as<uint64_t>(), nullptr);
-        hipLaunchKernelGGL(k_bsum_chain, dim3(1), dim3(64), 0, s, (const iggy_batch_header *)es.hdr,
+        hipLaunchKernelGGL(k_bsum_chain, dim3(1), dim3(128), 0, s, (const iggy_batch_header *)es.hdr,
                            (const uint64_t *)&es.misc[3], src, (const uint64_t *)c->gbsums.as<uint64_t>(),
                            c->emisc.as<uint8_t>(320) /* 192 B of small */, dcs, nullptr);
     }
@@ -1581,7 +1581,7 @@ int enqueue_crypt(iggy_codec_ctx *c, bool enc, const uint8_t *key, const uint8_t
     CsSource src{nullptr, d_out + kHdr, cs.opos};
     hipLaunchKernelGGL(k_bsum_blocks, dim3(bsum_grid(c, cap / 48 + 1)), dim3(256), 0, s, cs.dh, cs.dn, src,
                        c->gbsums.as<uint64_t>(), nullptr);
-    hipLaunchKernelGGL(k_bsum_chain, dim3(1), dim3(64), 0, s, cs.dh, cs.dn, src,
+    hipLaunchKernelGGL(k_bsum_chain, dim3(1), dim3(128), 0, s, cs.dh, cs.dn, src,
                        (const uint64_t *)c->gbsums.as<uint64_t>(), c->dsync.as<uint8_t>(kSyncSmall), cs.dsum,
                        nullptr);
     if (enc) {
@@ -1635,7 +1635,7 @@ static int enqueue_select(iggy_codec_ctx *c, const uint8_t *d_record, const uint
     CsSource src{nullptr, d_record + kHdr, d_frame_pos, ss.first};
     hipLaunchKernelGGL(k_bsum_blocks, dim3(bsum_grid(c, nframes)), dim3(256), 0, s, (const iggy_batch_header *)ss.hdr,
                        (const uint64_t *)ss.nsel, src, c->gbsums.as<uint64_t>(), (const uint32_t *)ss.skip);
-    hipLaunchKernelGGL(k_bsum_chain, dim3(1), dim3(64), 0, s, (const iggy_batch_header *)ss.hdr,
+    hipLaunchKernelGGL(k_bsum_chain, dim3(1), dim3(128), 0, s, (const iggy_batch_header *)ss.hdr,
                        (const uint64_t *)ss.nsel, src, (const uint64_t *)c->gbsums.as<uint64_t>(),
                        c->sl.as<uint8_t>(128), ss.computed, (const uint32_t *)ss.skip);
     hipLaunchKernelGGL(k_slice_finish, dim3(1), dim3(64), 0, s, d_record, ss, d_out, d_header_out);
@@ -1792,7 +1792,7 @@ int iggy_codec_stamp_batch_device(iggy_codec_ctx *c, uint8_t *d_record, const ui
     CsSource src{nullptr, d_record + kHdr, d_frame_pos};
     hipLaunchKernelGGL(k_bsum_blocks, dim3(bsum_grid(c, nframes)), dim3(256), 0, s, (const iggy_batch_header *)dh,
                        (const uint64_t *)dn, src, c->gbsums.as<uint64_t>(), nullptr);
-    hipLaunchKernelGGL(k_bsum_chain, dim3(1), dim3(64), 0, s, (const iggy_batch_header *)dh, (const uint64_t *)dn,
+    hipLaunchKernelGGL(k_bsum_chain, dim3(1), dim3(128), 0, s, (const iggy_batch_header *)dh, (const uint64_t *)dn,
                        src, (const uint64_t *)c->gbsums.as<uint64_t>(), c->sl.as<uint8_t>(128), dcs, nullptr);
     hipLaunchKernelGGL(k_stamp_finish, dim3(1), dim3(64), 0, s, d_record, (const iggy_batch_header *)dh,
                        (const uint64_t *)dcs, d_header);

@@ -256,7 +256,10 @@ def _raw_from_arrays(n, pls, uhl, rng):
                                              # clamped, realigned last piece), the 240-B short/long boundary,
                                              # a payload area under 16 B (fallback kernel)
                                              (300, 0, 20, False), (64, 0, 3, False), (5, 1, 2, False),
-                                             (1000, 195, 206, False), (777, 1015, 1033, False)])
+                                             (1000, 195, 206, False), (777, 1015, 1033, False),
+                                             # unsegmented (< 2^18 messages) with a checksum chain of
+                                             # 1 172 blocks: three chunks through k_bsum_chain's LDS stager
+                                             (150_000, 0, 200, False)])
 @pytest.mark.parametrize("partition_id", [0, 3])
 def test_encode_matches_oracle(cx, n, lo, hi, with_uh, partition_id):
     from iggy_amd.codec import raw_messages
