@@ -17,7 +17,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from iggy_amd import abi  # noqa: E402
 from iggy_amd import codec as _codec  # noqa: E402
 
-_codec.use_library(_codec.DIAG_LIB_PATH)  # ablation bits live only in the diagnostic build
+_codec.use_library(os.environ.get("IGGY_DIAG_LIB", _codec.DIAG_LIB_PATH))  # ablation bits: diagnostic build only
 from iggy_amd.codec import Codec  # noqa: E402
 import bench  # noqa: E402
 
