@@ -1096,8 +1096,8 @@ static int enqueue_encode(iggy_codec_ctx *c, const iggy_raw_messages *dm, uint64
     es.hdr = c->emisc.as<iggy_batch_header>(128);
     iggy_raw_messages m = *dm;
     prof_begin(c, 1, s);
-    hipLaunchKernelGGL(k_enc_prep, dim3(ntiles), dim3(256), 0, s, m, es);
-    hipLaunchKernelGGL(k_enc_scan, dim3(1), dim3(256), 0, s, ntiles, n, partition_id, cap, es);
+    hipLaunchKernelGGL(k_enc_prep, dim3(ntiles), dim3(256), 0, s, m, es, partition_id, cap, (uint32_t)(ntiles == 1));
+    if (ntiles != 1) hipLaunchKernelGGL(k_enc_scan, dim3(1), dim3(256), 0, s, ntiles, n, partition_id, cap, es);
     const uint64_t waves = std::min<uint64_t>(n, (uint64_t)c->ncu * 32);
     CsSource src{es.cs, nullptr, nullptr};
     // checksum blocks: 44 + 8n bytes; full blocks nb (the chain), then the last one
@@ -1175,6 +1175,12 @@ static int enqueue_encode(iggy_codec_ctx *c, const iggy_raw_messages *dm, uint64
     }
     prof_end(c, 1, s);
     uint64_t *dcs = c->emisc.as<uint64_t>(256);
+    if (!segmented && nb + 1 <= kEncTailBlocks) {  // small batch: sums, chain and finish in one launch
+        hipLaunchKernelGGL(k_enc_tail_small, dim3(1), dim3(256), 0, s, m, es, partition_id, cap,
+                           c->emisc.as<uint8_t>(320), d_out, d_res);
+        HIP_OK(hipGetLastError());
+        return 0;
+    }
     if (segmented) {
         hipLaunchKernelGGL(k_chain_finish, dim3(1), dim3(64), 0, s, (const iggy_batch_header *)es.hdr,
                            (const uint64_t *)&es.misc[3], src, (const uint64_t *)c->gbsums.as<uint64_t>(),

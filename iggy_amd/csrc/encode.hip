@@ -33,7 +33,31 @@ struct EncScratch {
     iggy_batch_header *hdr;  // header being built
 };
 
-__global__ __launch_bounds__(256) void k_enc_prep(iggy_raw_messages m, EncScratch es) {
+// the scan's result: origin, blob bytes, capacity verdict and the header being built
+__device__ inline void enc_scan_result(EncScratch es, uint64_t n, uint64_t partition_id, uint64_t cap,
+                                       uint64_t tot_pl, uint64_t tot_uh, uint64_t mn) {
+    const uint64_t origin = (n == 0) ? 0 : mn;
+    es.misc[0] = origin;
+    es.misc[1] = 48 * n + tot_pl + tot_uh;
+    es.misc[2] = 0;
+    es.misc[3] = n;
+    es.misc[4] = tot_pl;  // total payload bytes (bounds the lane-group kernel's loads)
+    es.misc[5] = 256 + es.misc[1] > cap ? 1 : 0;
+    iggy_batch_header h{};
+    h.partition_id = partition_id;
+    h.base_offset = 0;
+    h.base_timestamp = 0;
+    h.origin_timestamp = origin;
+    h.batch_length = 256 + es.misc[1];
+    h.batch_checksum = 0;
+    h.message_count = (uint32_t)n;
+    *es.hdr = h;
+}
+
+// single: the batch is one tile (n <= kEncTile), and this launch also does
+// k_enc_scan's work (one launch less for small batches)
+__global__ __launch_bounds__(256) void k_enc_prep(iggy_raw_messages m, EncScratch es, uint64_t partition_id,
+                                                  uint64_t cap, uint32_t single) {
     __shared__ uint64_t s_pl[256], s_uh[256], s_min[256];
     const uint64_t n = m.count;
     const uint64_t t = blockIdx.x;
@@ -78,9 +102,16 @@ __global__ __launch_bounds__(256) void k_enc_prep(iggy_raw_messages m, EncScratc
         ouh += uh[k];
     }
     if (tid == 255) {
-        es.tile_pl[t] = s_pl[255];
-        es.tile_uh[t] = s_uh[255];
-        es.tile_min[t] = s_min[255];
+        if (single) {  // the tile's offsets are 0; the totals are the scan's
+            es.tile_pl[t] = 0;
+            es.tile_uh[t] = 0;
+            es.tile_min[t] = s_min[255];
+            enc_scan_result(es, n, partition_id, cap, s_pl[255], s_uh[255], s_min[255]);
+        } else {
+            es.tile_pl[t] = s_pl[255];
+            es.tile_uh[t] = s_uh[255];
+            es.tile_min[t] = s_min[255];
+        }
     }
 }
 
@@ -122,24 +153,7 @@ __global__ __launch_bounds__(256) void k_enc_scan(uint64_t ntiles, uint64_t n, u
         }
         __syncthreads();
     }
-    if (tid == 0) {
-        const uint64_t origin = (n == 0) ? 0 : carry_min;
-        es.misc[0] = origin;
-        es.misc[1] = 48 * n + carry_pl + carry_uh;
-        es.misc[2] = 0;
-        es.misc[3] = n;
-        es.misc[4] = carry_pl;  // total payload bytes (bounds the lane-group kernel's loads)
-        es.misc[5] = 256 + es.misc[1] > cap ? 1 : 0;
-        iggy_batch_header h{};
-        h.partition_id = partition_id;
-        h.base_offset = 0;
-        h.base_timestamp = 0;
-        h.origin_timestamp = origin;
-        h.batch_length = 256 + es.misc[1];
-        h.batch_checksum = 0;
-        h.message_count = (uint32_t)n;
-        *es.hdr = h;
-    }
+    if (tid == 0) enc_scan_result(es, n, partition_id, cap, carry_pl, carry_uh, carry_min);
 }
 
 // bytes [s, s+8) of the hashed stream H(40) || P(pl) || U(uh), zero past the end
@@ -594,12 +608,11 @@ __global__ __launch_bounds__(256) void k_enc_short(iggy_raw_messages m, EncScrat
     }
 }
 
-// error precedence (send_messages.rs:131-174) and the 256-B header
-__global__ void k_enc_finish(iggy_raw_messages m, EncScratch es, uint64_t partition_id, uint64_t cap,
-                             const uint64_t *checksum, uint8_t *out, iggy_encode_result *res) {
-    const int t = threadIdx.x;
+// error precedence (send_messages.rs:131-174) and the 256-B header (64 threads)
+__device__ inline void enc_finish(const iggy_raw_messages &m, EncScratch es, uint64_t partition_id, uint64_t cap,
+                                  uint64_t checksum, uint8_t *out, iggy_encode_result *res, int t) {
     iggy_batch_header h = *es.hdr;
-    h.batch_checksum = *checksum;
+    h.batch_checksum = checksum;
     const uint64_t ts_enc = es.misc[2];
     const bool over = es.misc[5] != 0;
     uint32_t kind = IGGY_OK;
@@ -639,6 +652,74 @@ __global__ void k_enc_finish(iggy_raw_messages m, EncScratch es, uint64_t partit
         res->error.c = 0;
         res->batch_length = h.batch_length;
     }
+}
+__global__ void k_enc_finish(iggy_raw_messages m, EncScratch es, uint64_t partition_id, uint64_t cap,
+                             const uint64_t *checksum, uint8_t *out, iggy_encode_result *res) {
+    enc_finish(m, es, partition_id, cap, *checksum, out, res, threadIdx.x);
+}
+
+// Small unsegmented batches (at most kEncTailBlocks checksum blocks, ~8 K messages):
+// block sums (4 waves, into LDS), the chain and the finish in one launch instead of
+// k_bsum_blocks + k_bsum_chain + k_enc_finish.
+constexpr uint32_t kEncTailBlocks = 64;
+__global__ __launch_bounds__(256) void k_enc_tail_small(iggy_raw_messages m, EncScratch es, uint64_t partition_id,
+                                                        uint64_t cap, uint8_t *small, uint8_t *out,
+                                                        iggy_encode_result *res) {
+    __shared__ uint64_t s_bs[kEncTailBlocks * 8];
+    __shared__ uint64_t s_ck;
+    const iggy_batch_header h = *es.hdr;
+    const uint64_t N = es.misc[3];
+    const CsSource src{es.cs, nullptr, nullptr};
+    const CsPlan pl = cs_plan(N);
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    if (pl.long_cs) {
+        for (uint64_t b = wave; b <= pl.nb; b += 4) {  // as k_bsum_blocks
+            uint64_t x = 0, y = 0;
+#pragma unroll
+            for (int half = 0; half < 2; ++half) {
+                const uint64_t mw = 128 * b + 64 * half + lane;
+                if (mw < pl.Mreg) {
+                    const uint64_t v = cs_word(mw, h, src);
+                    y += v;
+                    x += mul32x32(v ^ kSecretW8[((mw >> 3) & 15) + (mw & 7)]);
+                }
+            }
+            x += __shfl_xor(x, 8); y += __shfl_xor(y, 8);
+            x += __shfl_xor(x, 16); y += __shfl_xor(y, 16);
+            x += __shfl_xor(x, 32); y += __shfl_xor(y, 32);
+            const uint64_t t8 = x + __shfl_xor(y, 1);
+            if (lane < 8) s_bs[b * 8 + lane] = t8;
+        }
+    }
+    __syncthreads();
+    if (wave != 0) return;
+    if (pl.long_cs) {  // as k_bsum_chain, from LDS
+        const int j = lane & 7;
+        const uint64_t key = kSecretW8[16 + j];
+        const uint32_t klo = (uint32_t)key, khi = (uint32_t)(key >> 32);
+        uint64_t acc = kAccInit[j];
+        for (uint64_t b = 0; b < pl.nb; ++b) acc = scramble_fast(acc + s_bs[8 * b + j], klo, khi);
+        acc += s_bs[pl.nb * 8 + j];
+        const uint64_t v = src(N - 8 + j);
+        acc += __shfl_xor(v, 1);
+        acc += mul32x32(v ^ kSecretLast[j]);
+        uint64_t a[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) a[i] = __shfl(acc, i);
+        uint64_t r = pl.n * P64_1;
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+            r += fold64(a[2 * i] ^ Secret::w(11 + 16 * i), a[2 * i + 1] ^ Secret::w(19 + 16 * i));
+        if (lane == 0) s_ck = avalanche(r);
+    } else if (lane == 0) {
+        for (uint64_t mw = 0; mw < 5; ++mw) st64_any(small + 8 * mw, cs_word(mw, h, src));
+        *(uint32_t *)(small + 40) = h.message_count;
+        for (uint64_t i = 0; i < N; ++i) st64_any(small + 44 + 8 * i, src(i));
+        s_ck = xxh3_64_lane(small, pl.n);
+    }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    enc_finish(m, es, partition_id, cap, s_ck, out, res, lane);
 }
 
 }  // namespace iggy
