@@ -1114,18 +1114,17 @@ static int enqueue_encode(iggy_codec_ctx *c, const iggy_raw_messages *dm, uint64
                 if (!ev) nseg = 1;
         }
         segmented = nseg > 1;
-        hipLaunchKernelGGL(k_enc_frames, dim3((waves + 3) / 4), dim3(256), 0, s, m, es, d_out, 1u);
         // frames of <= 240 hashed bytes (one lane each, latency-bound): segmented, they
         // run at the head of the side stream beside the first segment, ahead of every
         // block-sum range that reads their checksums; k_enc_lanes never writes their
-        // checksum words
-        const dim3 sgrid((uint32_t)std::min<uint64_t>((n + 255) / 256, (uint64_t)c->ncu * 4));
+        // checksum words. Unsegmented, the one k_enc_lanes launch hashes them after its
+        // loop and runs the < 16-B payload-area fallback itself (own_tail).
         if (segmented) {
+            hipLaunchKernelGGL(k_enc_frames, dim3((waves + 3) / 4), dim3(256), 0, s, m, es, d_out, 1u);
+            const dim3 sgrid((uint32_t)std::min<uint64_t>((n + 255) / 256, (uint64_t)c->ncu * 4));
             HIP_OK(hipEventRecord(c->seg_ev[kEncSegs + 1], s));
             HIP_OK(hipStreamWaitEvent(c->side, c->seg_ev[kEncSegs + 1], 0));
             hipLaunchKernelGGL(k_enc_short, sgrid, dim3(256), 0, c->side, m, es, d_out);
-        } else {
-            hipLaunchKernelGGL(k_enc_short, sgrid, dim3(256), 0, s, m, es, d_out);
         }
         // one resident round of lane-group waves (2 WGs of 256 per CU at 240 VGPRs)
         // segmented: one CU stays free of lane-group waves, so the side stream's
@@ -1149,7 +1148,10 @@ static int enqueue_encode(iggy_codec_ctx *c, const iggy_raw_messages *dm, uint64
             const uint64_t B0 = bound(k), B1 = bound(k + 1);
             const uint64_t F0 = k == 0 ? 0 : std::min<uint64_t>(n, 128 * B0 - 5);
             const uint64_t F1 = k == nseg - 1 ? n : std::min<uint64_t>(n, 128 * B1 - 5);
-            hipLaunchKernelGGL(k_enc_lanes, dim3(lwg), dim3(256), 0, s, m, es, d_out, F0, F1);
+            if (segmented)
+                hipLaunchKernelGGL(k_enc_lanes<false>, dim3(lwg), dim3(256), 0, s, m, es, d_out, F0, F1);
+            else
+                hipLaunchKernelGGL(k_enc_lanes<true>, dim3(lwg), dim3(256), 0, s, m, es, d_out, F0, F1);
             if (segmented && k < nseg - 1) {
                 HIP_OK(hipEventRecord(c->seg_ev[k], s));
                 HIP_OK(hipStreamWaitEvent(c->side, c->seg_ev[k], 0));

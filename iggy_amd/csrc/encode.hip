@@ -214,15 +214,12 @@ __device__ inline uint64_t xxh3_short_stream(const FrameStream &fs) {
     return avalanche(acc);
 }
 
-__global__ __launch_bounds__(256) void k_enc_frames(iggy_raw_messages m, EncScratch es,
-                                                    uint8_t *out, uint32_t fallback_only) {
-    // fallback_only: the lane-group kernel ran unless the payload area is < 16 B
-    if (es.misc[5] || (fallback_only && es.misc[4] >= 16)) return;
+// one wave per frame, frames wid, wid + nwaves, ... (any layout, user headers included)
+__device__ inline void enc_frames_body(const iggy_raw_messages &m, EncScratch es, uint8_t *out, uint64_t wid,
+                                       uint64_t nwaves) {
     const int lane = threadIdx.x & 63;
     const uint64_t n = m.count;
     const uint64_t origin = es.misc[0];
-    const uint64_t wid = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-    const uint64_t nwaves = ((uint64_t)gridDim.x * blockDim.x) >> 6;
     // lanes with equal (lane & 3) own accumulators j0 = 2(lane&3), j1 = j0 + 1
     const int q = lane & 3, j0 = 2 * q, j1 = j0 + 1;
     const uint64_t sec0 = kSecretW8[(lane >> 2) + j0];
@@ -319,6 +316,13 @@ __global__ __launch_bounds__(256) void k_enc_frames(iggy_raw_messages m, EncScra
             es.cs[i] = hsh;
         }
     }
+}
+__global__ __launch_bounds__(256) void k_enc_frames(iggy_raw_messages m, EncScratch es,
+                                                    uint8_t *out, uint32_t fallback_only) {
+    // fallback_only: the lane-group kernel ran unless the payload area is < 16 B
+    if (es.misc[5] || (fallback_only && es.misc[4] >= 16)) return;
+    enc_frames_body(m, es, out, ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6,
+                    ((uint64_t)gridDim.x * blockDim.x) >> 6);
 }
 
 // ---------------------------------------------------------------------------
@@ -417,10 +421,22 @@ __device__ __forceinline__ void eissue(const iggy_raw_messages &m, const EncScra
     st.npl = m.payload_lengths[k];
 }
 
+__device__ inline void enc_short_frame(const iggy_raw_messages &m, EncScratch es, uint8_t *out, uint64_t origin,
+                                       uint64_t i);
+// own_tail (unsegmented launches of small batches): this launch also runs the < 16-B
+// payload-area fallback and hashes the frames of <= 240 B (a slice per wave after its
+// loop) -- two launches fewer than k_enc_frames + k_enc_short
+// (a template parameter: the segmented launches keep the code without the tail)
+template <bool OWN_TAIL>
 __global__ __launch_bounds__(256, 2) void k_enc_lanes(iggy_raw_messages m, EncScratch es, uint8_t *out,
                                                        uint64_t f_lo, uint64_t f_hi) {
     const uint64_t ptot = es.misc[4];
-    if (ptot < 16 || es.misc[5]) return;  // tiny payload area: k_enc_frames (fallback) encodes it
+    if (ptot < 16 || es.misc[5]) {  // tiny payload area: the fallback (k_enc_frames' body) encodes it
+        if (OWN_TAIL && !es.misc[5])
+            enc_frames_body(m, es, out, ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6,
+                            ((uint64_t)gridDim.x * blockDim.x) >> 6);
+        return;
+    }
     const uint64_t n = f_hi < m.count ? f_hi : m.count;  // this launch: frames [f_lo, f_hi)
     const uint64_t origin = es.misc[0];
     const int lane = threadIdx.x & 63;
@@ -577,35 +593,43 @@ __global__ __launch_bounds__(256, 2) void k_enc_lanes(iggy_raw_messages m, EncSc
         if (!__ballot(cur.i < n)) break;
         step(B, A);
     }
+    if (OWN_TAIL) {  // frames of <= 240 hashed bytes: one lane each, a slice per wave
+        const uint64_t C = (n + nvw - 1) / nvw;
+        const uint64_t f1 = min((uint64_t)(vw + 1) * C, n);
+        for (uint64_t i = (uint64_t)vw * C + lane; i < f1; i += 64) enc_short_frame(m, es, out, origin, i);
+    }
 }
 
 // Frames of <= 240 hashed bytes of a lane-group encode: one lane each hashes the
 // stream (XXH3 17-128 / 129-240 paths) from the SoA input and backpatches.
+__device__ inline void enc_short_frame(const iggy_raw_messages &m, EncScratch es, uint8_t *out, uint64_t origin,
+                                       uint64_t i) {
+    const uint64_t pl = m.payload_lengths[i];
+    if (40 + pl > 240) return;
+    const uint64_t po = es.tile_pl[i / kEncTile] + es.pl_local[i];
+    FrameStream fs;
+    fs.pl = pl;
+    fs.uh = 0;
+    fs.L = 40 + pl;
+    fs.P = m.payloads + po;
+    fs.U = m.payloads;
+    const uint64_t delta = m.origin_timestamps[i] - origin;
+    fs.h[0] = m.ids[2 * i];
+    fs.h[1] = m.ids[2 * i + 1];
+    fs.h[2] = (i & 0xFFFFFFFFull) | ((delta & 0xFFFFFFFFull) << 32);
+    fs.h[3] = pl << 32;
+    fs.h[4] = 0;
+    const uint64_t hsh = xxh3_short_stream(fs);
+    st64_any(out + 256 + 48 * i + po, hsh);
+    es.cs[i] = hsh;
+}
 __global__ __launch_bounds__(256) void k_enc_short(iggy_raw_messages m, EncScratch es, uint8_t *out) {
     if (es.misc[4] < 16 || es.misc[5]) return;  // the fallback kernel encoded everything
     const uint64_t n = m.count;
     const uint64_t origin = es.misc[0];
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
-         i += (uint64_t)gridDim.x * blockDim.x) {
-        const uint64_t pl = m.payload_lengths[i];
-        if (40 + pl > 240) continue;
-        const uint64_t po = es.tile_pl[i / kEncTile] + es.pl_local[i];
-        FrameStream fs;
-        fs.pl = pl;
-        fs.uh = 0;
-        fs.L = 40 + pl;
-        fs.P = m.payloads + po;
-        fs.U = m.payloads;
-        const uint64_t delta = m.origin_timestamps[i] - origin;
-        fs.h[0] = m.ids[2 * i];
-        fs.h[1] = m.ids[2 * i + 1];
-        fs.h[2] = (i & 0xFFFFFFFFull) | ((delta & 0xFFFFFFFFull) << 32);
-        fs.h[3] = pl << 32;
-        fs.h[4] = 0;
-        const uint64_t hsh = xxh3_short_stream(fs);
-        st64_any(out + 256 + 48 * i + po, hsh);
-        es.cs[i] = hsh;
-    }
+         i += (uint64_t)gridDim.x * blockDim.x)
+        enc_short_frame(m, es, out, origin, i);
 }
 
 // error precedence (send_messages.rs:131-174) and the 256-B header (64 threads)
