@@ -74,14 +74,19 @@ def _check_decode(cx, rec):
 @pytest.mark.parametrize("n,pl", [(1, 0), (1, 200), (7, 1024), (24, 64), (25, 64), (120, 16),
                                   (122, 1024), (123, 1024), (250, 1024), (251, 1024), (506, 1024),
                                   (3000, 1024), (4097, 256), (20000, 1024), (1000, 256),
-                                  (300, 193), (301, 5000), (64, 1000)])
+                                  (300, 193), (301, 5000), (64, 1000),
+                                  # grids sized to small records (<= one producer WG per 128
+                                  # frames of 48 B): frames at or near that bound
+                                  (30000, 0), (70000, 8)])
 def test_uniform_random_batches(cx, n, pl):
     rec = O.synth_batch(n, pl, pl, 0, seed=0x16619E3779B97F4A ^ n)
     _check_decode(cx, rec)
 
 
 @pytest.mark.parametrize("n,lo,hi,uh", [(200, 64, 4096, 0), (1000, 0, 300, 7), (50, 5000, 70000, 0),
-                                        (5000, 64, 4096, 0), (333, 1, 2, 3)])
+                                        (5000, 64, 4096, 0), (333, 1, 2, 3),
+                                        # small variable frames: a general grid of one WG per 64 KiB
+                                        (40000, 0, 40, 0)])
 def test_variable_random_batches(cx, n, lo, hi, uh):
     rec = O.synth_batch(n, lo, hi, uh, seed=0xABCDEF ^ n)
     _check_decode(cx, rec)
