@@ -5,8 +5,8 @@
 // One persistent launch (bounded grid barriers over the workgroups that joined:
 // join_members) that returns immediately unless the uniform-stride kernel left
 // result->status == kStatusNeedGeneral. The blob is cut into tiles of
-// T = 2^sh bytes, sized from the header's message count to hold 8-16 frames
-// (4 KiB <= T <= 1 MiB); a group is 256 tiles, 4 per lane of one wave. Phases:
+// T bytes, 8-16 average frames (4 KiB <= T <= 1 MiB, tile_bytes); a group is 256
+// tiles, 4 per lane of one wave. Phases:
 //   A  locate : one lane per tile picks a speculative entry (a confirmed
 //               candidate frame start: 8 zero reserved bytes at +40, lengths
 //               inside the blob; 256-B vector scan for zero dwords) and walks
@@ -43,8 +43,8 @@ constexpr uint64_t kGrpOk = 1, kGrpTerm = 2;
 constexpr uint32_t kNotLive = ~0u;
 constexpr uint32_t kGenThreads = 512;  // one WG per CU: half the barrier arrivals of 2 x 256
 
-// list entries (u32 offsets from the tile start) per tile of 2^sh bytes
-__host__ __device__ __forceinline__ uint64_t tile_list_cap(uint32_t sh) { return ((1ull << sh) / 48) + 1; }
+// list entries (u32 offsets from the tile start) per tile of T bytes
+__host__ __device__ __forceinline__ uint64_t tile_list_cap(uint64_t T) { return T / 48 + 1; }
 // host sizing of the list area for a blob of up to L bytes (any tile size)
 __host__ __device__ __forceinline__ uint64_t tile_list_words(uint64_t L) {
     return L / 48 + L / kTileMin + (1ull << kTileShiftMax) / 48 + 64;
@@ -55,11 +55,11 @@ struct GeneralScratch {
     uint64_t *tile_x;    // [ntiles] exit position (| kStopBit when the walk stopped inside)
     uint32_t *tile_cnt;  // [ntiles] frames listed for the tile
     uint32_t *tile_pre;  // [ntiles] frames before the tile inside its group (kNotLive: none)
-    uint32_t *tile_list; // [ntiles * tile_list_cap(sh)] frame offsets from the tile start
+    uint32_t *tile_list; // [ntiles * tile_list_cap(T)] frame offsets from the tile start
     uint64_t *tile_e;    // [ntiles] repaired groups: true entry (~0: no frame starts here)
     uint64_t *tile_base; // [ntiles] repaired groups: frames before the tile
     uint64_t *grp;       // [ngroups * kGrpWords]
-    uint64_t *tile_lcs;  // [ntiles * tile_list_cap(sh)] stored checksum of each listed frame
+    uint64_t *tile_lcs;  // [ntiles * tile_list_cap(T)] stored checksum of each listed frame
     uint64_t *fpos;      // [max_frames] frame starts in walk order (hashed length of frame f:
                          // fpos[f+1] - fpos[f] - 8, the last frame's from the walk end)
     uint64_t *cs;        // [max_frames] stored checksums in walk order
@@ -147,12 +147,19 @@ __device__ inline void join_members(const GeneralScratch &gs, uint64_t t0, uint3
     __syncthreads();
 }
 
-// tile size: 8-16 frames of the header's average size, a power of two in range
-__device__ __forceinline__ uint32_t tile_shift(uint64_t bl, uint32_t message_count) {
-    const uint64_t want = 8 * (message_count ? bl / message_count : bl);
-    uint32_t sh = kTileShiftMin;
-    while (sh < kTileShiftMax && (1ull << sh) < want) ++sh;
-    return sh;
+// Tile size: the smallest power of two holding 8 frames of the header's average
+// size; when that holds fewer than 14, 16 frames (a multiple of 64 B) instead;
+// always inside [kTileMin, 2^kTileShiftMax]. Same-box phase clocks: C3 (2.1-KB
+// frames) 32-KiB tiles (15.4 frames) 0.85-0.88 ms against 0.86-0.90 ms for 31.9-
+// and 34.1-KB tiles (15 / 16 frames: locate 10-15 us slower) and 0.886-0.912 ms
+// for one 17-KB tile per locate lane; 4 M x U[64, 512] B: 4-KiB tiles (12 frames)
+// 1.42-1.47 ms, 5.1-KB (15) 1.38-1.42 ms, 5.4-KB (16) 1.35-1.39 ms.
+__device__ __forceinline__ uint64_t tile_bytes(uint64_t bl, uint32_t message_count) {
+    const uint64_t avg = message_count ? bl / message_count : bl;
+    uint64_t T = kTileMin;
+    while (T < (1ull << kTileShiftMax) && T < 8 * avg) T <<= 1;
+    if (T < 14 * avg) T = min(max((16 * avg + 63) & ~63ull, kTileMin), 1ull << kTileShiftMax);
+    return T;
 }
 
 // walk the candidate chain from p while p < hi (hi <= bl); with a list, every
@@ -540,13 +547,12 @@ __global__ __launch_bounds__(kGenThreads) void k_decode_general(const uint8_t *_
     const iggy_batch_header h = result->header;
     const uint8_t *blob = body + kHdr;
     const uint64_t bl = h.batch_length - kHdr;
-    const uint32_t sh = tile_shift(bl, h.message_count);
-    const uint64_t T = 1ull << sh;
-    const uint64_t ntiles = (bl + T - 1) >> sh;
-    const uint64_t ngroups = (ntiles + kGrpTiles - 1) / kGrpTiles;
-    const uint64_t lcap = tile_list_cap(sh);
     const uint64_t gtid = (uint64_t)member * blockDim.x + threadIdx.x;
     const uint64_t gthreads = (uint64_t)nwg * blockDim.x;
+    const uint64_t T = tile_bytes(bl, h.message_count);
+    const uint64_t ntiles = (bl + T - 1) / T;
+    const uint64_t ngroups = (ntiles + kGrpTiles - 1) / kGrpTiles;
+    const uint64_t lcap = tile_list_cap(T);
     const int lane = threadIdx.x & 63;
     const uint32_t wave = threadIdx.x >> 6;
     const uint64_t nwaves = gthreads >> 6;
@@ -560,7 +566,7 @@ __global__ __launch_bounds__(kGenThreads) void k_decode_general(const uint8_t *_
     // ---------------- A: locate
     if (threadIdx.x == 0) s_mem[2] = 0;  // the verify tail's claim counter (ordered by the barriers)
     for (uint64_t t = 64 * wid + lane; t < ntiles; t += gthreads) {
-        const uint64_t lo = t << sh, hi = min(lo + T, bl);
+        const uint64_t lo = t * T, hi = min(lo + T, bl);
         uint32_t *list = gs.tile_list + t * lcap;
         uint64_t *lcs = VERIFY ? gs.tile_lcs + t * lcap : nullptr;
         uint64_t s = kNoStart, x = kNoStart;
@@ -593,7 +599,7 @@ __global__ __launch_bounds__(kGenThreads) void k_decode_general(const uint8_t *_
             if (t >= ntiles || lterm) continue;
             const uint64_t s = gs.tile_s[t], x = gs.tile_x[t];
             const uint32_t c = gs.tile_cnt[t];
-            const uint64_t hi_t = min((t + 1) << sh, bl);
+            const uint64_t hi_t = min((t + 1) * T, bl);
             lhi = hi_t;
             if (s != kNoStart && !(lhas && lx >= hi_t)) {  // else spanned by the running frame
                 if (lhas) lok &= s == lx;
@@ -671,7 +677,7 @@ __global__ __launch_bounds__(kGenThreads) void k_decode_general(const uint8_t *_
             const uint64_t S = in ? q[0] : kNoStart, X = in ? q[1] : 0, CNT = in ? q[2] : 0;
             const uint64_t flags = in ? q[3] : 0;
             const bool has = S != kNoStart;
-            const uint64_t ghi = min(min((uint64_t)kGrpTiles * (g + 1), ntiles) << sh, bl);
+            const uint64_t ghi = min(min((uint64_t)kGrpTiles * (g + 1), ntiles) * T, bl);
             const uint64_t termmask = __ballot(in && has && (flags & kGrpTerm));
             const int last = termmask ? __builtin_ctzll(termmask) : 63;
             uint64_t pm = (in && has && lane <= last) ? X : 0;
@@ -763,7 +769,7 @@ __global__ __launch_bounds__(kGenThreads) void k_decode_general(const uint8_t *_
                     const uint32_t k = 4 * lane + i;
                     const uint64_t t = gt0 + k;
                     if (k < k0 || t >= ntiles || lterm || ts[i] == kNoStart) continue;
-                    const uint64_t hi = min((t + 1) << sh, bl);
+                    const uint64_t hi = min((t + 1) * T, bl);
                     if (seen && lx >= hi) continue;  // spanned
                     seen = true;
                     lx = tx[i];
@@ -791,7 +797,7 @@ __global__ __launch_bounds__(kGenThreads) void k_decode_general(const uint8_t *_
                     const uint32_t k = 4 * lane + i;
                     const uint64_t t = gt0 + k;
                     if (k < k0 || t >= ntiles || stop || kbad != kGrpTiles || lane > tl) continue;
-                    const uint64_t hi = min((t + 1) << sh, bl);
+                    const uint64_t hi = min((t + 1) * T, bl);
                     const bool has = ts[i] != kNoStart;
                     const bool assumed = has && (!aseen || ax < hi);
                     bool fail;
@@ -855,7 +861,7 @@ __global__ __launch_bounds__(kGenThreads) void k_decode_general(const uint8_t *_
                 const uint32_t owner = kb >> 2;
                 const uint64_t eb = __shfl(ebad, (int)owner);
                 const uint64_t t = gt0 + kb;
-                const uint64_t lo = t << sh, hi = min(lo + T, bl);
+                const uint64_t lo = t * T, hi = min(lo + T, bl);
                 uint64_t x2 = 0;
                 uint32_t c2 = 0;
 #ifdef IGGY_CODEC_DIAG
@@ -894,7 +900,7 @@ __global__ __launch_bounds__(kGenThreads) void k_decode_general(const uint8_t *_
         }
         if (lane == 0) {
             uint64_t *st = (uint64_t *)(gs.small + 512);
-            st[8] = nfast; st[9] = nsum; st[10] = nspan; st[11] = nrep; st[12] = ntiles; st[13] = sh;
+            st[8] = nfast; st[9] = nsum; st[10] = nspan; st[11] = nrep; st[12] = ntiles; st[13] = T;
             __hip_atomic_store(&gs.misc[0], total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             __hip_atomic_store(&gs.misc[1], e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
@@ -953,7 +959,7 @@ __global__ __launch_bounds__(kGenThreads) void k_decode_general(const uint8_t *_
                 }
 #pragma unroll
             for (int u = 0; u < kScatU; ++u) {
-                const uint64_t lo = t[u] << sh;
+                const uint64_t lo = t[u] * T;
 #pragma unroll
                 for (int j = 0; j < kScatK; ++j) {
                     const uint32_t k = k0 + 16 * j;

@@ -59,7 +59,7 @@ def main():
         line = {"iter": it, "host_ms": round(ms, 3), "err": dr.error.kind, "frames": dr.frame_count,
                 "phase_us": [round(st[i] / 100, 1) for i in range(1, 7)],
                 "fast_steps": st[8], "summary_groups": st[9], "span_groups": st[10], "repaired_groups": st[11],
-                "ntiles": st[12], "tile_shift": st[13],
+                "ntiles": st[12], "tile_bytes": st[13],
                 "verify_loop_end_max_us": round(st[14] / 100, 1), "verify_short_end_max_us": round(st[16] / 100, 1),
                 "chain_done_us": round(buf[64 + 18] / 100, 1)}
         rep = list(buf[84:96])
