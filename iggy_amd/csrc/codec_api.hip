@@ -106,7 +106,7 @@ struct iggy_codec_ctx {
     hipEvent_t order_ev = nullptr;
     // decode scratch
     uint64_t dec_cap_len = 0;
-    DevBuf dsync;    // exited | first_bad | spec_fail | bar[4] | misc[16] | small[512]
+    DevBuf dsync;    // exited | first_bad | spec_fail | bar[4] | misc[16] | small[512] | bar2 (128-B stride)
     DevBuf dsums, derr;
     DevBuf gtiles_s, gtiles_x, gtiles_cnt, gtiles_pre, gtiles_list, gtiles_e, gtiles_base, ggrp, gfpos, gcs, gtiles_lcs, gbsums;
     int gen_grid = 0;  // WGs of k_decode_general (the ones that get a CU join its barriers)
@@ -155,7 +155,8 @@ struct iggy_codec_ctx {
 namespace {
 
 constexpr size_t kSyncExited = 0, kSyncFirstBad = 8, kSyncSpecFail = 16, kSyncBar = 32,
-                 kSyncMisc = 64, kSyncSmall = 256, kSyncBytes = 1024;
+                 kSyncMisc = 64, kSyncSmall = 256, kSyncBar2 = 1024,  // + kBar2Words u32 at 128-B stride
+                 kSyncBytes = kSyncBar2 + kBar2Words * 128;
 
 int ensure_decode_scratch(iggy_codec_ctx *c, uint64_t len) {
     if (len <= c->dec_cap_len && c->dsync.p) return 0;
@@ -202,6 +203,7 @@ DecodeScratch dscratch(iggy_codec_ctx *c) {
     s.errslot = c->derr.as<uint64_t>();
     s.small = c->dsync.as<uint8_t>(kSyncSmall);
     s.gbar = c->dsync.as<uint32_t>(kSyncBar);
+    s.gbar2 = c->dsync.as<uint32_t>(kSyncBar2);
     s.gmisc = c->dsync.as<uint64_t>(kSyncMisc);
     s.max_chunks = (c->dsums.cap - 64) / (kChunkSumWords * 8);
     return s;
@@ -223,6 +225,7 @@ GeneralScratch gscratch(iggy_codec_ctx *c) {
     g.bsums = c->gbsums.as<uint64_t>();
     g.misc = c->dsync.as<uint64_t>(kSyncMisc);
     g.bar = c->dsync.as<uint32_t>(kSyncBar);
+    g.bar2 = c->dsync.as<uint32_t>(kSyncBar2);
     g.u_exited = c->dsync.as<uint32_t>(kSyncExited);
     g.u_first_bad = c->dsync.as<uint64_t>(kSyncFirstBad);
     g.u_spec_fail = c->dsync.as<uint64_t>(kSyncSpecFail);

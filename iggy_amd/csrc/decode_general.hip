@@ -42,6 +42,7 @@ constexpr uint32_t kGrpWords = 6;    // S, X, CNT, flags | base, mode
 constexpr uint64_t kGrpOk = 1, kGrpTerm = 2;
 constexpr uint32_t kNotLive = ~0u;
 constexpr uint32_t kGenThreads = 512;  // one WG per CU: half the barrier arrivals of 2 x 256
+constexpr uint32_t kBar2Groups = 8, kBar2Words = kBar2Groups + 1;  // grid_barrier2 counters + top
 
 // list entries (u32 offsets from the tile start) per tile of T bytes
 __host__ __device__ __forceinline__ uint64_t tile_list_cap(uint64_t T) { return T / 48 + 1; }
@@ -65,7 +66,8 @@ struct GeneralScratch {
     uint64_t *cs;        // [max_frames] stored checksums in walk order
     uint64_t *bsums;     // [max_blocks * 8]
     uint64_t *misc;      // [16]: 0 nwalk, 1 end (with stop bit), 2 first_bad enc
-    uint32_t *bar;       // [4]: 0 barrier arrivals, 2 registration (count | kRegClosed), 3 members
+    uint32_t *bar2;      // [kBar2Words * 32]: two-level barrier counters, 128 B apart (grid_barrier2)
+    uint32_t *bar;       // [4]: 2 registration (count | kRegClosed), 3 members
                          // (all re-armed by k_decode_uniform, which always runs first on the stream)
     uint32_t *u_exited;  // the uniform kernel's sync words, re-armed here for the next decode
     uint64_t *u_first_bad, *u_spec_fail;
@@ -85,16 +87,25 @@ __device__ __forceinline__ bool candidate(const uint8_t *blob, uint64_t bl, uint
     return true;
 }
 
-// grid barrier: monotonic arrive counter, agent release/acquire, bounded
-__device__ bool grid_barrier(uint32_t *bar, uint32_t target, uint64_t t0) {
+// Two-level grid barrier: members arrive on one of kBar2Groups counters (member % 8),
+// the last arrival of a counter's phase adds one to the top counter, and everyone
+// waits for the top counter. A single counter took all ~256 workgroups' arrivals on
+// one address, serialised at the memory side. Monotonic: phase p (1-based) is done
+// when the top counter reaches min(nwg, kBar2Groups) * p. Bounded like grid_barrier.
+__device__ bool grid_barrier2(uint32_t *bar2, uint32_t member, uint32_t nwg, uint32_t p, uint64_t t0) {
     __syncthreads();
     bool ok = true;
     if (threadIdx.x == 0) {
+        const uint32_t g = member % kBar2Groups;
+        const uint32_t nsub = (nwg - 1 - g) / kBar2Groups + 1;  // members on counter g (member < nwg)
+        const uint32_t ngrp = nwg < kBar2Groups ? nwg : kBar2Groups;
+        uint32_t *top = bar2 + 32 * kBar2Groups;
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __hip_atomic_fetch_add(bar, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        while (__hip_atomic_load(bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
-            __builtin_amdgcn_s_sleep(2);
+        const uint32_t old = __hip_atomic_fetch_add(bar2 + 32 * g, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (old + 1 == nsub * p) __hip_atomic_fetch_add(top, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        while (__hip_atomic_load(top, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < ngrp * p) {
+            __builtin_amdgcn_s_sleep(1);
             if (rt_now() - t0 > kSpinLimitTicks) { ok = false; break; }
         }
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
@@ -581,7 +592,7 @@ __global__ __launch_bounds__(kGenThreads) void k_decode_general(const uint8_t *_
         gs.tile_cnt[t] = cnt;
         gs.tile_x[t] = x;
     }
-    ok &= grid_barrier(gs.bar, nwg * ++phase, t0);
+    ok &= grid_barrier2(gs.bar2, member, nwg, ++phase, t0);
     gstamp(gs, member, 1, rt_now() - t0);
     gstamp(gs, member, 14, 0); gstamp(gs, member, 15, 0); gstamp(gs, member, 16, 0); gstamp(gs, member, 18, 0);  // verify / chain clock (below)
 
@@ -655,7 +666,7 @@ __global__ __launch_bounds__(kGenThreads) void k_decode_general(const uint8_t *_
             q[0] = S; q[1] = X; q[2] = CNT; q[3] = flags;
         }
     }
-    ok &= grid_barrier(gs.bar, nwg * ++phase, t0);
+    ok &= grid_barrier2(gs.bar2, member, nwg, ++phase, t0);
     gstamp(gs, member, 2, rt_now() - t0);
 
     // ---------------- B2: link (one wave)
@@ -905,7 +916,7 @@ __global__ __launch_bounds__(kGenThreads) void k_decode_general(const uint8_t *_
             __hip_atomic_store(&gs.misc[1], e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
     }
-    ok &= grid_barrier(gs.bar, nwg * ++phase, t0);
+    ok &= grid_barrier2(gs.bar2, member, nwg, ++phase, t0);
     gstamp(gs, member, 3, rt_now() - t0);
 
     const uint64_t nwalk = __hip_atomic_load(&gs.misc[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -980,7 +991,7 @@ __global__ __launch_bounds__(kGenThreads) void k_decode_general(const uint8_t *_
             }
         }
     }
-    ok &= grid_barrier(gs.bar, nwg * ++phase, t0);
+    ok &= grid_barrier2(gs.bar2, member, nwg, ++phase, t0);
     gstamp(gs, member, 4, rt_now() - t0);
 
     // ---------------- E: checksum-input block sums (one wave per block)
@@ -1020,7 +1031,7 @@ __global__ __launch_bounds__(kGenThreads) void k_decode_general(const uint8_t *_
     }
     // (a grid barrier, not a block-sum count only the chain wave waits for: with the
     // verify waves going straight on, the C3 decode measured 15-25 us slower)
-    ok &= grid_barrier(gs.bar, nwg * ++phase, t0);
+    ok &= grid_barrier2(gs.bar2, member, nwg, ++phase, t0);
     gstamp(gs, member, 5, rt_now() - t0);
 
     // ---------------- D + F: chain (wave 0 of WG 0) beside frame verification
@@ -1067,7 +1078,7 @@ __global__ __launch_bounds__(kGenThreads) void k_decode_general(const uint8_t *_
         const uint64_t wend = __hip_atomic_load(&gs.misc[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & ~kStopBit;
         verify_frames(blob, gs, nwalk, wend, vw, nvw, member, nwg, &s_mem[2], lane, t0);
     }
-    ok &= grid_barrier(gs.bar, nwg * ++phase, t0);
+    ok &= grid_barrier2(gs.bar2, member, nwg, ++phase, t0);
     gstamp(gs, member, 6, rt_now() - t0);
 
     // ---------------- resolution (wave 0 of WG 0)

@@ -44,6 +44,7 @@ struct DecodeScratch {
                           // (half | epoch << 32); see publish_unit_sums
     uint64_t *errslot;    // [max_chunks*32][2] (stored, computed) of the first mismatch per 8-frame group
     uint8_t *small;       // >= 512 B: short batch-checksum inputs
+    uint32_t *gbar2;      // the general kernel's two-level barrier counters (kBar2Words, 128-B stride)
     uint32_t *gbar;       // the general kernel's barrier / registration words and its
     uint64_t *gmisc;      // first-bad slot: re-armed here (see k_decode_general)
     uint64_t max_chunks;
@@ -1334,6 +1335,8 @@ __global__ __launch_bounds__(kUniformThreads, 1) void k_decode_uniform(const uin
         __hip_atomic_store(&sc.gbar[3], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(&sc.gmisc[2], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
+    if (blockIdx.x == 0 && threadIdx.x < kBar2Words)
+        __hip_atomic_store(&sc.gbar2[32 * threadIdx.x], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     HeaderInfo hi;
     parse_header(body, len, hi);
     UPlan pl;
