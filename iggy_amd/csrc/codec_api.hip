@@ -86,6 +86,7 @@ struct Slot {
     }
 };
 
+constexpr size_t kCrTabBytesHost = (size_t)kGhPowers * 32 * 8;  // GHASH tables (= kCrTabBytes below)
 constexpr int kEncSegs = 4;                   // encode segments (checksum chain overlap); bounds below
 constexpr uint64_t kEncSegMinFrames = 1 << 18;  // below this one segment
 
@@ -95,7 +96,8 @@ struct iggy_codec_ctx {
     int ncu = 256;
     // uniform decode grid: one WG per CU but one. A pipelined decode's consumer WG
     // (the previous batch's chain tail) then never holds back one of the next
-    // decode's producer WGs. IGGY_CODEC_UNIFORM_GRID overrides (tuning).
+    // decode's producer WGs. IGGY_CODEC_UNIFORM_GRID overrides it in the diagnostic
+    // build only.
     int ugrid = 255;
     uint32_t epoch = 0;
     int allow_unaligned = 0;
@@ -134,7 +136,9 @@ struct iggy_codec_ctx {
     // [256,384) decode result, [1024, +16 KiB) GHASH tables, then sizes / positions / tile sums
     DevBuf cr;
     void *cr_pinned = nullptr;   // host staging of the GHASH tables
-    uint8_t cr_key[32] = {};     // the key whose tables are on the device
+    // fingerprint of the key whose tables are on the device: E_K(0) || E_K(1), never the
+    // key itself (the reference keeps the key only inside its Aes256Gcm cipher object)
+    uint8_t cr_fp[32] = {};
     bool cr_key_set = false;
     // pinned host mirror of results
     void *h_pinned = nullptr;
@@ -400,12 +404,13 @@ int iggy_codec_create(int device, iggy_codec_ctx **out) {
     c->device = device;
     c->ncu = prop.multiProcessorCount;
     c->ugrid = std::max(2, c->ncu - 1);
-    if (const char *g = getenv("IGGY_CODEC_UNIFORM_GRID")) {
-        const long v = strtol(g, nullptr, 0);
-        if (v >= 2 && v <= c->ncu) c->ugrid = (int)v;
-    }
-    if (kDiagMask)  // diagnostic build only
+    if (kDiagMask) {  // diagnostic build only: tuning / ablation knobs never reach the product
         if (const char *d = getenv("IGGY_CODEC_DBG")) c->dbg = (uint32_t)strtoul(d, nullptr, 0);
+        if (const char *g = getenv("IGGY_CODEC_UNIFORM_GRID")) {
+            const long v = strtol(g, nullptr, 0);
+            if (v >= 2 && v <= c->ncu) c->ugrid = (int)v;
+        }
+    }
     if (hipSetDevice(device) != hipSuccess ||
         hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
         hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking) != hipSuccess) {
@@ -485,7 +490,15 @@ void iggy_codec_destroy(iggy_codec_ctx *c) {
         if (ev) (void)hipEventDestroy(ev);
     if (c->order_ev) (void)hipEventDestroy(c->order_ev);
     if (c->wstage) (void)hipHostFree(c->wstage);
-    if (c->cr_pinned) (void)hipHostFree(c->cr_pinned);
+    if (c->cr_pinned) {  // GHASH tables of the key: cleared before the pages go back
+        volatile uint8_t *z = (volatile uint8_t *)c->cr_pinned;
+        for (size_t i = 0; i < kCrTabBytesHost; ++i) z[i] = 0;
+        (void)hipHostFree(c->cr_pinned);
+    }
+    {
+        volatile uint8_t *z = c->cr_fp;
+        for (int i = 0; i < 32; ++i) z[i] = 0;
+    }
     for (auto &ev : c->wev)
         if (ev) (void)hipEventDestroy(ev);
     for (Slot &sl : c->slots) sl.release();
@@ -1537,7 +1550,11 @@ int enqueue_crypt(iggy_codec_ctx *c, bool enc, const uint8_t *key, const uint8_t
     }
     CryptKey ck;
     aes256_key_schedule(key, ck.rk);
-    if (!c->cr_key_set || memcmp(c->cr_key, key, 32) != 0) {
+    uint8_t fp[32] = {};
+    fp[16 + 15] = 1;
+    aes256_block_host(ck.rk, fp, fp);            // E_K(0)
+    aes256_block_host(ck.rk, fp + 16, fp + 16);  // E_K(1)
+    if (!c->cr_key_set || memcmp(c->cr_fp, fp, 32) != 0) {
         // new key: H = E_K(0), tables of H^1 .. H^64 (the staging buffer is rewritten
         // only after every earlier upload on this stream order has run)
         HIP_OK(hipStreamSynchronize(s));
@@ -1554,7 +1571,7 @@ int enqueue_crypt(iggy_codec_ctx *c, bool enc, const uint8_t *key, const uint8_t
             ph = nh; pl = nl;
         }
         HIP_OK(hipMemcpyAsync(c->cr.as<uint8_t>(kCrTab), c->cr_pinned, kCrTabBytes, hipMemcpyHostToDevice, s));
-        memcpy(c->cr_key, key, 32);
+        memcpy(c->cr_fp, fp, 32);
         c->cr_key_set = true;
     }
     CryptScratch cs;

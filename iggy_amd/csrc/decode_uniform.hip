@@ -9,27 +9,33 @@
 // stops there (result still exact) or continues with another size (status
 // kStatusNeedGeneral: the general walk in decode_general.hip takes over).
 //
-// Work layout (MI355X: 256 CUs, wave64, 160 KiB LDS):
-//  * grid = 1 consumer WG + NPROD producer WGs (one per CU, 256 threads,
-//    152 KiB LDS). Producer g handles chunks g, g+NPROD, ... statically.
-//  * a chunk = 256 consecutive frames [256c-6, 256c+250); the -6 aligns the
-//    chunk with two 1024-B blocks of the batch-checksum input
-//    (44 header bytes + 8 bytes per frame => checksum word m = frame + 6).
-//  * each wave owns 64 frames (one per lane) and runs independently (no
-//    workgroup barrier anywhere in the producer): it streams its frames
-//    through a 4-slot LDS ring with global_load_lds_dwordx4, three phases of
-//    8 x 16 B per lane in flight (24 KiB per wave, 96 KiB per CU). One
-//    wave-instruction moves 8 frames x 128 contiguous bytes (full lines); the
-//    image is XOR-swizzled so the per-lane ds_read_b128 are bank-balanced.
-//    Short frames (S <= 248) use 2 slots of 16 chunks (whole frame per slot).
-//  * XXH3 per lane: stripe words accumulate in registers, scramble at block
-//    ends, last stripe from a per-lane side copy, merge.
-//  * batch checksum: each wave reduces its 63 interior checksum-input words to
-//    8 accumulator partial sums and publishes them (write-through sc1 stores,
-//    then a per-wave flag once its vmcnt covers the stores). The consumer WG's
-//    single wave gathers 64 chunks at a time (partials + wave-boundary words),
-//    stages them in LDS and runs the serial 1-scramble-per-block chain while
-//    the next 64 chunks' loads are in flight.
+// Work layout (MI355X: 256 CUs in 8 XCDs, wave64, 160 KiB LDS per CU):
+//  * one persistent grid of ncu - 1 WGs of 320 threads (one CU stays free for a
+//    pipelined decode's chain). Block 0 is the consumer WG; blocks 1.. produce.
+//  * checksum blocks: 128 consecutive frames [128b - 6, 128b + 122) cover exactly
+//    the 1024-B block b of the batch-checksum input (44 header bytes + 8 bytes per
+//    frame => checksum word m = frame + 6); a 32-frame "unit" is a quarter block.
+//  * Long frames under Verify (hashed length > 240 B, the C2 path): 4 lane-group
+//    producer waves + 1 publisher wave per WG. Producer WG g sweeps blocks g,
+//    g + NP, ...; at step j its wave w takes 8-frame group w of unit j & 3 of its
+//    block j >> 2. 8 lanes per frame, 8 frames per wave-instruction: each step is
+//    exactly 9 global_load_lds_dwordx4 (8 pieces of a 1-KiB block, then the last-
+//    stripe piece in even lanes / the stored checksum in odd lanes) into a 4-slot
+//    LDS ring per wave with a constant vmcnt (3 steps in flight). XXH3 accumulator
+//    pairs stay lane-local, folded by DPP at block ends. The producers deposit each
+//    group's 8 stored checksums in LDS; the publisher wave reduces each block's
+//    127 interior checksum words to 8 accumulator sums and stores ONE epoch-tagged
+//    128-B block record (no flag, no fence).
+//  * Short frames (hashed <= 240 B) and LayoutOnly: LDS-staged producers (waves
+//    0-3, 64 frames per wave per 256-frame chunk, XOR-swizzled rings, bank-balanced
+//    ds_read_b128); odd/even wave pairs join their halves of a block in LDS and the
+//    even wave publishes the same block record.
+//  * Consumer WG: 2 gatherer waves load block records (coherent sc1 buffer loads,
+//    tags checked), add each block's last word and stage 16 sums per 256-frame
+//    chunk into a 64 KiB LDS ring; the chain wave (raised priority, a SIMD of its
+//    own) runs the serial one-scramble-per-block batch-checksum chain beside the
+//    producers, then resolves precedence (batch.rs:395-421, 461-506).
+//  DESIGN.md section 4.1 has the measurements behind each choice.
 #include "codec_common.hpp"
 
 #include <utility>
@@ -40,8 +46,8 @@ struct DecodeScratch {
     uint32_t *exited;     // producer waves that finished (reset by consumer)
     uint64_t *first_bad;  // ~index of first checksum mismatch (max-encoded), 0 = none
     uint64_t *spec_fail;  // ~index of first frame whose header breaks the stride
-    uint64_t *sums;       // [max_chunks][8 units][32] epoch-tagged 32-bit halves (256 B per unit)
-                          // (half | epoch << 32); see publish_unit_sums
+    uint64_t *sums;       // block records: one 128-B line (16 epoch-tagged granules) per
+                          // 128-frame checksum block, 2 per chunk; see publish_block
     uint64_t *errslot;    // [max_chunks*32][2] (stored, computed) of the first mismatch per 8-frame group
     uint8_t *small;       // >= 512 B: short batch-checksum inputs
     uint32_t *gbar2;      // the general kernel's two-level barrier counters (kBar2Words, 128-B stride)

@@ -230,6 +230,61 @@ struct iggy_producer {
     bool any_uh = false;
 };
 
+namespace {
+
+// Remove messages [0, upto) (whole flushed requests) from the staging: the arrays
+// keep their tails, the entries are rebased, fully flushed entries disappear.
+void drop_flushed(iggy_producer *p, uint64_t upto) {
+    const uint64_t N = p->ids.n / 2;
+    if (upto >= N) {
+        p->entries.clear();
+        p->bytes = 0;
+        p->ids.n = p->ots.n = p->plen.n = p->uhl.n = p->pay.n = p->uh.n = 0;
+        p->any_uh = false;
+        return;
+    }
+    uint64_t pay_cut = 0, uh_cut = 0;
+    for (uint64_t i = 0; i < upto; ++i) {
+        pay_cut += p->plen.p[i];
+        uh_cut += p->uhl.p[i];
+    }
+    auto shift = [](auto &a, uint64_t cut) {
+        memmove(a.p, a.p + cut, (a.n - cut) * sizeof(*a.p));
+        a.n -= cut;
+    };
+    shift(p->ids, 2 * upto);
+    shift(p->ots, upto);
+    shift(p->plen, upto);
+    shift(p->uhl, upto);
+    shift(p->pay, pay_cut);
+    shift(p->uh, uh_cut);
+    std::vector<ProducerEntry> keep;
+    uint64_t bytes = 0;
+    for (ProducerEntry e : p->entries) {
+        if (e.m1 <= upto) continue;
+        const uint64_t m0 = std::max(e.m0, upto);
+        e.m0 = m0 - upto;
+        e.m1 -= upto;
+        uint64_t spl = 0, suh = 0;
+        for (uint64_t i = e.m0; i < e.m1; ++i) {
+            spl += p->plen.p[i];
+            suh += p->uhl.p[i];
+        }
+        bytes += (2 + (uint64_t)e.stream.length) + (2 + (uint64_t)e.topic.length) + 64 * (e.m1 - e.m0) + spl + suh;
+        keep.push_back(e);
+    }
+    uint64_t pay0 = 0, uh0 = 0, i = 0;
+    for (ProducerEntry &e : keep) {  // byte offsets of the kept entries
+        for (; i < e.m0; ++i) { pay0 += p->plen.p[i]; uh0 += p->uhl.p[i]; }
+        e.pay0 = pay0;
+        e.uh0 = uh0;
+    }
+    p->entries.swap(keep);
+    p->bytes = bytes;
+}
+
+}  // namespace
+
 extern "C" {
 
 int iggy_send_messages_header_encode(const iggy_send_messages_header *h, uint8_t *out, uint64_t cap,
@@ -375,17 +430,23 @@ int iggy_producer_append(iggy_producer *p, const iggy_identifier *stream_id, con
     e.m1 = e.m0 + n;
     e.pay0 = p->pay.n;
     e.uh0 = p->uh.n;
-    bool ok = p->ids.append(m->ids, 2 * n) && p->ots.append(m->origin_timestamps, n) &&
-              p->plen.append(m->payload_lengths, n) && p->pay.append(m->payloads, spl);
-    if (ok) {
-        if (m->user_headers_lengths) {
-            ok = p->uhl.append(m->user_headers_lengths, n) && p->uh.append(m->user_headers, suh);
-            p->any_uh = p->any_uh || suh > 0;
-        } else {
-            ok = p->uhl.append_zero(n);
-        }
+    // every staging array is grown first; the entry is appended only once all six
+    // reservations succeeded, so a failed allocation leaves the buffer as it was
+    const bool has_uh = m->user_headers_lengths != nullptr;
+    if (!p->ids.reserve(p->ids.n + 2 * n) || !p->ots.reserve(p->ots.n + n) || !p->plen.reserve(p->plen.n + n) ||
+        !p->pay.reserve(p->pay.n + spl) || !p->uhl.reserve(p->uhl.n + n) || !p->uh.reserve(p->uh.n + suh))
+        return IGGY_ERR_DEVICE;
+    p->ids.append(m->ids, 2 * n);
+    p->ots.append(m->origin_timestamps, n);
+    p->plen.append(m->payload_lengths, n);
+    p->pay.append(m->payloads, spl);
+    if (has_uh) {
+        p->uhl.append(m->user_headers_lengths, n);
+        p->uh.append(m->user_headers, suh);
+        p->any_uh = p->any_uh || suh > 0;
+    } else {
+        p->uhl.append_zero(n);
     }
-    if (!ok) return IGGY_ERR_DEVICE;
     p->entries.push_back(e);
     // ShardMessage::get_size_bytes (producer_sharding.rs:99-109; Identifier: length + 2,
     // common/src/types/identifier/mod.rs:206-210; IggyMessage: 64 + payload + user headers,
@@ -511,7 +572,9 @@ int iggy_producer_flush(iggy_producer *p, uint8_t *out, uint64_t cap, iggy_produ
             const int s = iggy_codec_encode_submit(p->ctx, &m, 0, o, off[r + 1] - (uint64_t)(o - out), &tick[r]);
             if (s == IGGY_ERR_BUSY) {
                 while (oldest < r && !live[oldest]) ++oldest;
-                if (oldest >= r) { rc = IGGY_ERR_DEVICE; break; }
+                // every slot is held by other operations of the context: the caller's
+                // own submits must drain first (not a device failure)
+                if (oldest >= r) { rc = IGGY_ERR_BUSY; break; }
                 rc = retire(oldest++);
                 if (rc) break;
                 continue;
@@ -523,11 +586,14 @@ int iggy_producer_flush(iggy_producer *p, uint8_t *out, uint64_t cap, iggy_produ
         live[r] = 1;
         rq.sent = 1;
     }
-    for (size_t r = 0; r < sendable.size(); ++r)
+    size_t nsent = 0;  // requests encoded (a prefix: submission stops at the first failure)
+    for (size_t r = 0; r < sendable.size(); ++r) {
         if (live[r]) {
             const int w = retire(r);
             if (!rc) rc = w;
         }
+        if (reqs[r].sent) nsent = r + 1;
+    }
     // direct sends: the chunks after a failed one were never sent (producer.rs:446-452)
     if (!rc && p->cfg.direct)
         for (size_t r = 1; r < sendable.size(); ++r) {
@@ -537,12 +603,16 @@ int iggy_producer_flush(iggy_producer *p, uint8_t *out, uint64_t cap, iggy_produ
                 reqs[r].error = iggy_wire_error{};
             }
         }
-    if (rc) return rc;
+    if (rc) {
+        // A submit or wait failed part-way: reqs[0..nsent) are written (each with its
+        // own verdict) and must be sent by the caller; they leave the buffer, which keeps
+        // only the messages of the requests after them, so a retry never re-sends one.
+        if (nreqs) *nreqs = nsent;
+        if (nsent) drop_flushed(p, sendable[nsent - 1].m1);
+        return rc;
+    }
     if (nreqs) *nreqs = sendable.size();
-    p->entries.clear();
-    p->bytes = 0;
-    p->ids.n = p->ots.n = p->plen.n = p->uhl.n = p->pay.n = p->uh.n = 0;
-    p->any_uh = false;
+    drop_flushed(p, N);
     return 0;
 }
 

@@ -669,7 +669,13 @@ int iggy_producer_pending(const iggy_producer *p, uint64_t *entries, uint64_t *b
  * it with iggy_codec_host_register for asynchronous copies) and described in reqs
  * (max_reqs). Returns 0 when every body was written (each carries its own verdict in
  * reqs[k].error), IGGY_ERR_CAPACITY (err->a = bytes or requests needed) when out or
- * reqs is too small (nothing is flushed then). The buffer is empty afterwards. */
+ * reqs is too small (nothing is flushed then). The buffer is empty afterwards.
+ * When a submit or wait fails part-way (IGGY_ERR_DEVICE, or IGGY_ERR_BUSY when every
+ * slot of the context is held by operations the caller has not retired), *nreqs =
+ * the requests already written: reqs[0..*nreqs) are complete (each with its own
+ * verdict) and are the caller's to send; their messages leave the buffer, which keeps
+ * the rest, so a retry never re-sends a request. A failed append leaves the buffer
+ * unchanged. */
 int iggy_producer_flush(iggy_producer *p, uint8_t *out, uint64_t cap, iggy_producer_request *reqs,
                         uint64_t max_reqs, uint64_t *nreqs, iggy_wire_error *err);
 

@@ -93,13 +93,16 @@ def test_variable_random_batches(cx, n, lo, hi, uh):
 
 
 @pytest.mark.parametrize("shift", [1, 3, 8, 13])
-def test_unaligned_record(cx, shift):
+def test_unaligned_host_buffer(cx, shift):
+    """The host-buffer entry point reading a caller buffer at an odd host address
+    (the H2D copy's source alignment). Device-side misalignment of the record itself
+    is covered by test_robust_gpu.py::test_misaligned_device_records."""
     rec = O.synth_batch(700, 1024, 1024)
     buf = np.zeros(rec.size + shift, dtype=np.uint8)
     buf[shift:] = rec
-    # decode from an unaligned view (the C ABI copies into device memory at the same misalignment? no:
-    # the sync API stages at offset 0) -> use the device API below for real misalignment
-    _check_decode(cx, buf[shift:])
+    view = buf[shift:]
+    assert view.ctypes.data % 16 == shift % 16
+    _check_decode(cx, view)
 
 
 def test_corruption_sweep(cx):
