@@ -29,9 +29,13 @@ At N = 1 the line also carries, timed in the same run:
   c1                     BASELINE configs[0] shapes (10 batches x 1000 x 256 B):
                          cpu_ref encode/decode and the GPU's per-batch latency
                          (iggy-bench itself needs a Rust toolchain: not run);
+  c4                     BASELINE configs[3]: 262,144 x 1 KiB batches encode ->
+                         decode end to end through the asynchronous host API
+                         (pinned H2D/D2H included), PCIe share and overlap;
   cpu_baseline           the oracle's AVX2 restatement of the C2 decode on this
-                         host's cores (1, 8 and 16 threads; reported, not optimised
-                         against).
+                         host's cores (1, 8, 16 and nproc threads; reported, not
+                         optimised against). At N > 1 rank 0 adds a short sample
+                         (1 thread and one per rank).
 
 The synthetic batches are produced on the GPU by the codec's own encoder
 (SendMessagesEncoder semantics, server-twin form with partition_id = rank+1):
@@ -336,14 +340,118 @@ def c1_leg(cx, dev, seconds: float):
     }
 
 
-def cpu_baseline(seconds: float):
+def c4_leg(dev, batches: int):
+    """BASELINE configs[3] (C4): end-to-end encode -> decode including the pinned
+    host<->device copies, 262,144 x 1 KiB batches streamed back to back through the
+    product's asynchronous host API. A producer context encodes each batch from host
+    SoA input (iggy_codec_encode_submit: H2D of the SoA, the kernels, D2H of the wire
+    bytes into registered host memory -- the socket side), a server context decodes
+    every finished batch (iggy_codec_decode_submit: H2D of the wire bytes, Verify
+    decode, D2H of the frame positions -- the segment side); copy-in, kernels and
+    copy-out of different batches overlap. Reported beside it: the same batch's PCIe
+    copies and kernels timed alone (HIP events), the PCIe share of the isolated
+    batch, and the overlap factor (isolated sum / pipelined time per batch)."""
+    import torch
+    from iggy_amd import abi
+    from iggy_amd.codec import Codec, raw_messages
+
+    n, pl = 262_144, 1024
+    total = 256 + n * (48 + pl)
+    g = torch.Generator().manual_seed(0x16619E3779B97F4A)
+    t_ids = torch.randint(1, 2**62, (2 * n,), dtype=torch.int64, generator=g).pin_memory()
+    t_ots = (1_700_000_000_000_000 + torch.arange(n, dtype=torch.int64)).pin_memory()
+    t_pay = torch.randint(0, 256, (n * pl,), dtype=torch.uint8, generator=g).pin_memory()
+    t_pls = torch.full((n,), pl, dtype=torch.int32).pin_memory()
+    raw = raw_messages(t_ids.numpy().view(np.uint64), t_ots.numpy().view(np.uint64), t_pay.numpy(),
+                       t_pls.numpy().view(np.uint32))
+    wires = [torch.empty(total, dtype=torch.uint8).pin_memory() for _ in range(3)]
+    poss = [torch.empty(n, dtype=torch.int64).pin_memory() for _ in range(3)]
+    A, B = Codec(dev.index or 0), Codec(dev.index or 0)
+
+    def once():
+        te, td = {}, {}
+        for b in range(batches + 2):
+            if b < batches:
+                te[b] = A.encode_submit(raw, 1, wires[b % 3].numpy())
+            if 1 <= b <= batches:
+                c = A.wait(te[b - 1])
+                assert c.error.kind == 0 and c.bytes == total, c.error
+                td[b - 1] = B.decode_submit(wires[(b - 1) % 3].numpy(), abi.INTEGRITY_VERIFY,
+                                            poss[(b - 1) % 3].numpy().view(np.uint64))
+            if b >= 2:
+                c = B.wait(td[b - 2])
+                assert c.error.kind == 0 and c.frame_count == n, c.error
+        assert int(poss[0][1]) == 48 + pl
+
+    once()  # slots and scratch sized
+    t0 = time.perf_counter()
+    once()
+    wall = time.perf_counter() - t0
+    A.close()
+    B.close()
+    # the same batch's pieces alone on one stream: PCIe copies and device-resident kernels
+    cx = Codec(dev.index or 0)
+    s = torch.cuda.Stream(dev)
+    d_ids, d_ots, d_pay, d_pls = (t.to(dev) for t in (t_ids, t_ots, t_pay, t_pls))
+    d_wire = torch.empty(total, dtype=torch.uint8, device=dev)
+    d_pos = torch.empty(n, dtype=torch.int64, device=dev)
+    d_eres = torch.zeros(ctypes.sizeof(abi.EncodeResult), dtype=torch.uint8, device=dev)
+    d_dres = torch.zeros(ctypes.sizeof(abi.DecodeResult), dtype=torch.uint8, device=dev)
+    draw = abi.RawMessages(n, d_ids.data_ptr(), d_ots.data_ptr(), d_pay.data_ptr(), d_pls.data_ptr(), None, None)
+    torch.cuda.synchronize(dev)
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(7)]
+    ms = {}
+    for rep in range(3):
+        with torch.cuda.stream(s):
+            ev[0].record()
+            for dst, src in ((d_ids, t_ids), (d_ots, t_ots), (d_pay, t_pay), (d_pls, t_pls)):
+                dst.copy_(src, non_blocking=True)
+            ev[1].record()
+            assert cx.encode_device(draw, 1, d_wire.data_ptr(), total, d_eres.data_ptr(), s.cuda_stream) == 0
+            ev[2].record()
+            wires[0].copy_(d_wire, non_blocking=True)
+            ev[3].record()
+            d_wire.copy_(wires[0], non_blocking=True)
+            ev[4].record()
+            assert cx.decode_device(d_wire.data_ptr(), total, abi.INTEGRITY_VERIFY, d_pos.data_ptr(), n,
+                                    d_dres.data_ptr(), s.cuda_stream) == 0
+            ev[5].record()
+            poss[0].copy_(d_pos, non_blocking=True)
+            ev[6].record()
+        s.synchronize()
+        ms = {k: ev[i].elapsed_time(ev[i + 1]) for i, k in
+              enumerate(["h2d_soa", "encode", "d2h_wire", "h2d_wire", "decode", "d2h_positions"])}
+    cx.close()
+    dr = abi.DecodeResult.from_buffer_copy(d_dres.cpu().numpy().tobytes())
+    assert dr.error.kind == 0 and dr.frame_count == n, dr.error
+    soa = 16 * n + 8 * n + n * pl + 4 * n
+    pcie = soa + 2 * total + 8 * n + 2 * ctypes.sizeof(abi.DecodeResult)
+    copy_ms = ms["h2d_soa"] + ms["d2h_wire"] + ms["h2d_wire"] + ms["d2h_positions"]
+    iso_ms = sum(ms.values())
+    per = wall / batches
+    return {
+        "workload": "C4: SoA -> encode_submit -> wire bytes (host) -> decode_submit(Verify) -> positions (host), "
+                    f"{n} msgs x {pl} B per batch, {batches} batches back to back, registered host buffers",
+        "e2e_gib_s": round(total / per / 2**30, 3),
+        "ms_per_batch": round(per * 1e3, 3),
+        "batch_bytes": total,
+        "pcie_bytes_per_batch": pcie,
+        "pcie_gb_s": round(pcie / per / 1e9, 2),
+        "isolated_batch_ms": {k: round(v, 3) for k, v in ms.items()},
+        "pcie_share_isolated": round(copy_ms / iso_ms, 3),
+        "overlap_factor": round(iso_ms / (per * 1e3), 3),
+    }
+
+
+def cpu_baseline(seconds: float, threads=None):
     """The oracle's restatement of the same decode on host cores (bounded sample).
 
     The sample is a full C2-shaped record (not cache-resident: 1.05 GiB), each
     thread walking and verifying the whole record serially (the reference's
     execution model: one shard thread per batch); T threads decode independent
-    walks of it concurrently, T = 1, 8 (one per partition, C5) and 16 (this
-    process's CPU share on the GPU box)."""
+    walks of it concurrently, T = 1, 8 (one per partition, C5), 16 (this process's
+    CPU share on the GPU box) and nproc (the CPUs this process may run
+    on). `threads` overrides the counts (multi-GPU lines: a short sample)."""
     from oracle import oracle as O  # cpu_baseline leg: the only bench use of oracle/
 
     rec = O.synth_batch(N_MSG, PAYLOAD, PAYLOAD)
@@ -360,7 +468,13 @@ def cpu_baseline(seconds: float):
         return threads * total_reps * nbytes / total_secs / 2**30
 
     share = min(16, os.cpu_count() or 1)
-    rates = {t: rate(t) for t in sorted({1, min(8, share), share})}
+    try:
+        nproc = len(os.sched_getaffinity(0))
+    except AttributeError:
+        nproc = os.cpu_count() or 1
+    counts = threads or sorted({1, min(8, share), share, nproc})
+    rates = {t: rate(t) for t in counts}
+    share = min(share, max(counts))
     model = ""
     try:
         with open("/proc/cpuinfo") as f:
@@ -378,7 +492,9 @@ def cpu_baseline(seconds: float):
                   f"thread count; oracle C restatement with AVX2 XXH3",
         "by_threads_gib_s": {str(t): round(v, 3) for t, v in rates.items()},
         "single_thread_gib_s": round(rates[1], 3), "cpu_model": model,
-        "host_cpus_visible": os.cpu_count(),
+        "host_cpus_visible": os.cpu_count(), "nproc": nproc,
+        "note": "value = the 16-thread rate (this process's CPU share on the GPU box); T = nproc "
+                "threads share those cores with every other thread of the box",
         "avx2": bool(O.lib().oracle_has_avx2()),
     }
 
@@ -491,9 +607,13 @@ def run(args, world: int, rank: int, local: int, dist):
         torch.cuda.empty_cache()
         extra["c3_encode"], extra["c3_decode"] = c3_leg(lanes[0]["cx"], dev, max(5, args.steps // 2))
         extra["c1"] = c1_leg(lanes[0]["cx"], dev, args.cpu_seconds)
+        extra["c4"] = c4_leg(dev, 16)
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu:
-        cpu = cpu_baseline(args.cpu_seconds)
+    if rank == 0 and not args.no_cpu:
+        # N = 1: the full sample; N > 1: a short one (1 thread and one per rank) so the
+        # scaling lines carry the CPU axis too without lengthening the run much
+        cpu = cpu_baseline(args.cpu_seconds) if world == 1 else \
+            cpu_baseline(min(args.cpu_seconds, 1.5), threads=sorted({1, world}))
 
     traffic, traffic_src = pmc_traffic(n)
     value = whole_job_gib_s(world, L, args.steps, elapsed)

@@ -99,6 +99,7 @@ def load(path: str) -> ctypes.CDLL:
     L.iggy_codec_calculate_batch_checksum.argtypes = [vp, vp, vp, u64, vp]
     L.iggy_codec_encode_batch.argtypes = [vp, vp, u64, vp, u64, vp, vp]
     L.iggy_codec_poll_decode.argtypes = [vp, vp, u64, ci, vp, u64, vp, vp]
+    L.iggy_codec_decode_records.argtypes = [vp, vp, u64, vp, u64, ci, vp]
     L.iggy_codec_stamp_batch.argtypes = [vp, vp, u64, u64, u64, vp, vp]
     L.iggy_codec_decode_batch_device.argtypes = [vp, vp, u64, ci, vp, u64, vp, vp]
     L.iggy_codec_encode_batch_device.argtypes = [vp, vp, u64, vp, u64, vp, vp]
@@ -310,6 +311,16 @@ class Codec:
                                             checksum_mode, out.ctypes.data, out.size, ctypes.byref(h),
                                             ctypes.byref(e))
         return rc, e, h, (out[:a.size].tobytes() if rc == 0 else None)
+
+    def decode_records(self, buf, offsets, integrity: int = abi.INTEGRITY_VERIFY):
+        """decode_batch_slice_with of record k = buf[offsets[k]:] for every k, one launch
+        for the single-stride records -> (rc, [DecodeResult])."""
+        a = _np(buf)
+        offs = np.ascontiguousarray(offsets, dtype=np.uint64)
+        out = (abi.DecodeResult * max(offs.size, 1))()
+        rc = self._L.iggy_codec_decode_records(self._h, _addr(a), a.size, offs.ctypes.data if offs.size else None,
+                                               offs.size, integrity, out)
+        return rc, [out[i] for i in range(offs.size)]
 
     def recover_segment(self, messages, start_offset: int):
         """recover_segment_bounds' index-less walk (segment_recovery.rs:425-530)

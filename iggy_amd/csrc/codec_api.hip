@@ -22,6 +22,7 @@
 #include "batch_checksum.hip"
 #include "decode_general.hip"
 #include "decode_uniform.hip"
+#include "decode_records.hip"
 #include "encode.hip"
 #include "poll.hip"
 #include "slice.hip"
@@ -127,6 +128,12 @@ struct iggy_codec_ctx {
     // poll
     DevBuf ppos, pmsgs, pres;
     DevBuf cwk;  // disk-chunk walk: state, gates, per-batch slice results, fragments
+    // multi-record decode (decode_records.hip): tasks | states | wg map, block sums,
+    // results, and the pinned staging of the task table (uploaded in one copy)
+    DevBuf rtab, rbsums, rres, clinks;
+    void *rpin = nullptr, *cpin = nullptr;  // task table / chunk-walk candidates and results
+    size_t rpin_cap = 0, cpin_cap = 0;
+    uint32_t chunk_epoch = 0;  // k_chunk_walk link tags
     // segment writer: pinned staging halves and their copy events
     void *wstage = nullptr;
     hipEvent_t wev[2] = {nullptr, nullptr};
@@ -384,6 +391,161 @@ int decode_host(iggy_codec_ctx *c, const uint8_t *body, uint64_t len, int integr
     return 0;
 }
 
+
+// ------------------------------------------------------- multi-record decode
+// The walks over a sequence of batches (disk chunk, segment recovery, transferred
+// segment, poll body) decode every record in ONE launch of k_decode_records
+// (decode_records.hip). The host plans the launch from its own copy of the bytes
+// with the same stride speculation as make_plan: each single-stride record gets one
+// workgroup per 128-frame checksum block; a record that is not single-stride (or
+// is large enough to fill the chip on its own) takes the single-record path.
+struct RecIn {
+    uint64_t off, len;           // record start in the buffer, bytes available from there
+    uint64_t pos_base, pos_cap;  // frame positions (device buffer passed to enqueue_records)
+    uint64_t msg_base;           // polled messages (idem)
+};
+constexpr uint64_t kRecSingleBytes = 64ull << 20;  // larger records: the persistent single-record decode
+
+// -> workgroups of record [h, h + len) in k_decode_records (>= 1), 0 = single-record path
+uint64_t rec_plan(const uint8_t *h, uint64_t len, uint64_t *n_frames) {
+    *n_frames = 0;
+    if (len < kHdr) return 1;  // UnexpectedEof: resolved by the kernel from the header alone
+    uint64_t bl;
+    memcpy(&bl, h + 32, 8);
+    if (bl < kHdr) return 1;
+    for (uint32_t i = 52; i < kHdr; ++i)
+        if (h[i]) return 1;
+    if (len < bl) return 1;
+    const uint64_t blob = bl - kHdr;
+    if (blob == 0) return 1;
+    uint64_t resv;
+    if (blob < kFrameHdr) return 1;
+    memcpy(&resv, h + kHdr + 40, 8);
+    if (resv) return 1;
+    uint32_t uh, pl;
+    memcpy(&uh, h + kHdr + 32, 4);
+    memcpy(&pl, h + kHdr + 36, 4);
+    const uint64_t S = kFrameHdr + (uint64_t)uh + pl;
+    if (S > blob) return 1;
+    if (blob % S != 0 || S > (1u << 20) || bl > kRecSingleBytes) return 0;
+    *n_frames = blob / S;
+    return rec_blocks(blob / S);
+}
+
+// Enqueue the decode of K records of the device buffer d_base (h_base: the host
+// copy of the same bytes) on the context's stream: one k_decode_records launch for
+// every planned record, then the single-record decode of the others (appended to
+// *single). d_res[k] receives record k's verdict; a record left with status
+// kStatusNeedGeneral (its stride breaks mid-record) is re-decoded by redo_general.
+// n_frames[k] (nullable) = the planned frame count (0 for single-path records).
+int enqueue_records(iggy_codec_ctx *c, const uint8_t *d_base, const uint8_t *h_base, const RecIn *recs, size_t K,
+                    int integrity, uint64_t *d_pos, iggy_polled_message *d_msgs, iggy_decode_result *d_res,
+                    std::vector<size_t> *single, std::vector<uint64_t> *n_frames = nullptr) {
+    hipStream_t s = c->stream;
+    std::vector<RecTask> tasks(K);
+    std::vector<uint32_t> wgmap;
+    uint64_t nbs = 0, maxlen = 0;
+    if (n_frames) n_frames->assign(K, 0);
+    for (size_t k = 0; k < K; ++k) {
+        uint64_t nf = 0;
+        const uint64_t nw = rec_plan(h_base + recs[k].off, recs[k].len, &nf);
+        RecTask &t = tasks[k];
+        t.off = recs[k].off;
+        t.len = recs[k].len;
+        t.pos_base = recs[k].pos_base;
+        t.pos_cap = d_pos ? recs[k].pos_cap : 0;
+        t.msg_base = recs[k].msg_base;
+        t.bsum_base = nbs;
+        t.wg0 = (uint32_t)wgmap.size();
+        t.nwg = (uint32_t)nw;
+        if (!nw) {
+            single->push_back(k);
+            maxlen = std::max(maxlen, recs[k].len);
+            continue;
+        }
+        if (n_frames) (*n_frames)[k] = nf;
+        nbs += nw;
+        wgmap.insert(wgmap.end(), nw, (uint32_t)k);
+    }
+    const uint64_t W = wgmap.size();
+    if (W) {
+        const size_t tb = K * sizeof(RecTask), sb = K * sizeof(RecState), wb = W * 4;
+        const size_t bytes = tb + sb + wb;
+        if (c->rpin_cap < bytes) {
+            if (c->rpin) (void)hipHostFree(c->rpin);
+            c->rpin = nullptr;
+            c->rpin_cap = 0;
+            const size_t want = std::max<size_t>(bytes, 64 << 10);
+            if (hipHostMalloc(&c->rpin, want, hipHostMallocDefault) != hipSuccess) return IGGY_ERR_DEVICE;
+            c->rpin_cap = want;
+        }
+        int r = c->rtab.ensure(bytes);
+        r |= c->rbsums.ensure(nbs * 64 + 64);
+        if (r) return IGGY_ERR_DEVICE;
+        uint8_t *hp = (uint8_t *)c->rpin;
+        memcpy(hp, tasks.data(), tb);
+        memset(hp + tb, 0, sb);
+        memcpy(hp + tb + sb, wgmap.data(), wb);
+        HIP_OK(hipMemcpyAsync(c->rtab.p, hp, bytes, hipMemcpyHostToDevice, s));
+        const RecTask *dt = c->rtab.as<RecTask>();
+        RecState *ds = c->rtab.as<RecState>(tb);
+        const uint32_t *dw = c->rtab.as<uint32_t>(tb + sb);
+        if (integrity == IGGY_INTEGRITY_VERIFY)
+            hipLaunchKernelGGL(k_decode_records<true>, dim3((uint32_t)W), dim3(kRecThreads), 0, s, d_base, dt, dw, ds,
+                               c->rbsums.as<uint64_t>(), d_pos, d_msgs, d_res);
+        else
+            hipLaunchKernelGGL(k_decode_records<false>, dim3((uint32_t)W), dim3(kRecThreads), 0, s, d_base, dt, dw,
+                               ds, c->rbsums.as<uint64_t>(), d_pos, d_msgs, d_res);
+        HIP_OK(hipGetLastError());
+    }
+    if (!single->empty()) {
+        int r = ensure_decode_scratch(c, maxlen);
+        if (r) return r;
+        for (size_t k : *single) {
+            r = enqueue_decode(c, d_base + recs[k].off, recs[k].len, integrity,
+                               d_pos ? d_pos + recs[k].pos_base : nullptr, d_pos ? recs[k].pos_cap : 0, d_res + k, s);
+            if (r) return r;
+        }
+    }
+    return 0;
+}
+
+// After a sync: records the multi-record kernel left with status kStatusNeedGeneral
+// are decoded again by the single-record path (general walk); res (host) is
+// refreshed for them. Returns IGGY_ERR_TIMEOUT if a bug guard fired anywhere.
+int redo_general(iggy_codec_ctx *c, const uint8_t *d_base, const RecIn *recs, size_t K, int integrity,
+                 uint64_t *d_pos, iggy_decode_result *d_res, iggy_decode_result *res, std::vector<size_t> *redone) {
+    std::vector<size_t> redo;
+    uint64_t maxlen = 0;
+    for (size_t k = 0; k < K; ++k) {
+        if (res[k].error.kind == IGGY_ERR_TIMEOUT) {
+            reset_after_timeout(c);
+            return IGGY_ERR_TIMEOUT;
+        }
+        if (res[k].status == kStatusNeedGeneral) {
+            redo.push_back(k);
+            maxlen = std::max(maxlen, recs[k].len);
+        }
+    }
+    if (redo.empty()) return 0;
+    int r = ensure_decode_scratch(c, maxlen);
+    if (r) return r;
+    for (size_t k : redo) {
+        r = enqueue_decode(c, d_base + recs[k].off, recs[k].len, integrity, d_pos ? d_pos + recs[k].pos_base : nullptr,
+                           d_pos ? recs[k].pos_cap : 0, d_res + k, c->stream);
+        if (r) return r;
+        HIP_OK(hipMemcpyAsync(res + k, d_res + k, sizeof(iggy_decode_result), hipMemcpyDeviceToHost, c->stream));
+    }
+    HIP_OK(hipStreamSynchronize(c->stream));
+    for (size_t k : redo)
+        if (res[k].error.kind == IGGY_ERR_TIMEOUT) {
+            reset_after_timeout(c);
+            return IGGY_ERR_TIMEOUT;
+        }
+    if (redone) *redone = redo;
+    return 0;
+}
+
 }  // namespace
 
 // ===================================================================== ABI
@@ -479,7 +641,8 @@ void iggy_codec_destroy(iggy_codec_ctx *c) {
                       &c->gtiles_cnt, &c->gtiles_pre, &c->gtiles_list, &c->gtiles_e, &c->gtiles_base, &c->ggrp, &c->gfpos, &c->gcs, &c->gtiles_lcs,
                       &c->gbsums, &c->dresult, &c->din, &c->dpos, &c->dout, &c->epl, &c->euh,
                       &c->etile, &c->ecs, &c->emisc, &c->eids, &c->eots, &c->epay, &c->eplen,
-                      &c->euhb, &c->euhl, &c->hbsums, &c->ppos, &c->pmsgs, &c->pres, &c->cwk, &c->sl, &c->slres, &c->cr};
+                      &c->euhb, &c->euhl, &c->hbsums, &c->ppos, &c->pmsgs, &c->pres, &c->cwk, &c->sl, &c->slres, &c->cr,
+                      &c->rtab, &c->rbsums, &c->rres, &c->clinks};
     for (DevBuf *b : bufs) b->release();
     if (c->h_pinned) (void)hipHostFree(c->h_pinned);
     for (int w = 0; w < 2; ++w) {
@@ -490,6 +653,8 @@ void iggy_codec_destroy(iggy_codec_ctx *c) {
         if (ev) (void)hipEventDestroy(ev);
     if (c->order_ev) (void)hipEventDestroy(c->order_ev);
     if (c->wstage) (void)hipHostFree(c->wstage);
+    if (c->rpin) (void)hipHostFree(c->rpin);
+    if (c->cpin) (void)hipHostFree(c->cpin);
     if (c->cr_pinned) {  // GHASH tables of the key: cleared before the pages go back
         volatile uint8_t *z = (volatile uint8_t *)c->cr_pinned;
         for (size_t i = 0; i < kCrTabBytesHost; ++i) z[i] = 0;
@@ -831,6 +996,30 @@ int iggy_codec_admit_batch(iggy_codec_ctx *c, const uint8_t *batch, uint64_t len
     return 0;
 }
 
+int iggy_codec_decode_records(iggy_codec_ctx *c, const uint8_t *buf, uint64_t len, const uint64_t *offsets,
+                              uint64_t nrec, int integrity, iggy_decode_result *out) {
+    if (!c || (!buf && len) || (nrec && (!offsets || !out))) return IGGY_ERR_INVALID_ARGUMENT;
+    if (integrity != IGGY_INTEGRITY_VERIFY && integrity != IGGY_INTEGRITY_LAYOUT_ONLY) return IGGY_ERR_INVALID_ARGUMENT;
+    for (uint64_t k = 0; k < nrec; ++k)
+        if (offsets[k] > len) return IGGY_ERR_INVALID_ARGUMENT;
+    if (!nrec) return 0;
+    DevGuard dg(c->device);
+    bind(c, nullptr);
+    int r = c->din.ensure(len + 16);
+    r |= c->rres.ensure(nrec * sizeof(iggy_decode_result));
+    if (r) return IGGY_ERR_DEVICE;
+    if (len) HIP_OK(hipMemcpyAsync(c->din.p, buf, len, hipMemcpyHostToDevice, c->stream));
+    std::vector<RecIn> recs(nrec);
+    for (uint64_t k = 0; k < nrec; ++k) recs[k] = RecIn{offsets[k], len - offsets[k], 0, 0, 0};
+    iggy_decode_result *d_res = c->rres.as<iggy_decode_result>();
+    std::vector<size_t> single;
+    r = enqueue_records(c, c->din.as<uint8_t>(), buf, recs.data(), nrec, integrity, nullptr, nullptr, d_res, &single);
+    if (r) return r;
+    HIP_OK(hipMemcpyAsync(out, d_res, nrec * sizeof(iggy_decode_result), hipMemcpyDeviceToHost, c->stream));
+    HIP_OK(hipStreamSynchronize(c->stream));
+    return redo_general(c, c->din.as<uint8_t>(), recs.data(), nrec, integrity, nullptr, d_res, out, nullptr);
+}
+
 // recover_segment_bounds' index-less walk (core/partitions/src/segment_recovery.rs:425-530).
 // The chain of candidate batches depends on headers only (decode, extent, offset
 // contiguity), so the host walks it first; every candidate is then verified on the
@@ -859,30 +1048,30 @@ int iggy_codec_recover_segment(iggy_codec_ctx *c, const uint8_t *messages, uint6
     }
     size_t accepted = 0;
     if (!cand.empty()) {
+        // one copy of the file, every candidate verified in one multi-record launch
+        // (the single-record decode for the rest), one sync
         const uint64_t span = cand.back().pos + cand.back().h.batch_length;
+        const size_t K = cand.size();
         int r = c->din.ensure(span + 16);
-        r |= c->dout.ensure(cand.size() * sizeof(iggy_decode_result));
+        r |= c->rres.ensure(K * sizeof(iggy_decode_result));
         if (r) return IGGY_ERR_DEVICE;
-        r = ensure_decode_scratch(c, maxlen);
-        if (r) return r;
+        (void)maxlen;
         HIP_OK(hipMemcpyAsync(c->din.p, messages, span, hipMemcpyHostToDevice, c->stream));
-        iggy_decode_result *d_res = c->dout.as<iggy_decode_result>();
-        for (size_t k = 0; k < cand.size(); ++k) {
-            r = enqueue_decode(c, c->din.as<uint8_t>(cand[k].pos), cand[k].h.batch_length, IGGY_INTEGRITY_VERIFY,
-                               nullptr, 0, d_res + k, c->stream);
-            if (r) return r;
-        }
-        std::vector<iggy_decode_result> res(cand.size());
-        HIP_OK(hipMemcpyAsync(res.data(), d_res, res.size() * sizeof(iggy_decode_result), hipMemcpyDeviceToHost,
-                              c->stream));
+        std::vector<RecIn> recs(K);
+        for (size_t k = 0; k < K; ++k) recs[k] = RecIn{cand[k].pos, cand[k].h.batch_length, 0, 0, 0};
+        iggy_decode_result *d_res = c->rres.as<iggy_decode_result>();
+        std::vector<size_t> single;
+        r = enqueue_records(c, c->din.as<uint8_t>(), messages, recs.data(), K, IGGY_INTEGRITY_VERIFY, nullptr, nullptr,
+                            d_res, &single);
+        if (r) return r;
+        std::vector<iggy_decode_result> res(K);
+        HIP_OK(hipMemcpyAsync(res.data(), d_res, K * sizeof(iggy_decode_result), hipMemcpyDeviceToHost, c->stream));
         HIP_OK(hipStreamSynchronize(c->stream));
-        for (; accepted < cand.size(); ++accepted) {
-            if (res[accepted].error.kind == IGGY_ERR_TIMEOUT) {
-                reset_after_timeout(c);
-                return IGGY_ERR_TIMEOUT;
-            }
+        r = redo_general(c, c->din.as<uint8_t>(), recs.data(), K, IGGY_INTEGRITY_VERIFY, nullptr, d_res, res.data(),
+                         nullptr);
+        if (r) return r;
+        for (; accepted < K; ++accepted)
             if (res[accepted].error.kind != IGGY_OK) break;
-        }
     }
     uint64_t end_offset = start_offset, end_ts = 0, start_ts = 0, walked = 0;
     bool have_start = false;
@@ -928,20 +1117,26 @@ int iggy_codec_walk_segment_payload(iggy_codec_ctx *c, const uint8_t *bytes, uin
     }
     std::vector<iggy_decode_result> res(cand.size());
     if (!cand.empty()) {
+        // one copy, every batch in one multi-record launch (single-record decode for the
+        // rest), one sync
+        const size_t K = cand.size();
         int r = c->din.ensure(len + 16);
-        r |= c->pres.ensure(cand.size() * sizeof(iggy_decode_result));
-        if (!r) r = ensure_decode_scratch(c, maxlen);
-        if (r) return r ? r : IGGY_ERR_DEVICE;
+        r |= c->rres.ensure(K * sizeof(iggy_decode_result));
+        if (r) return IGGY_ERR_DEVICE;
+        (void)maxlen;
         HIP_OK(hipMemcpyAsync(c->din.p, bytes, len, hipMemcpyHostToDevice, c->stream));
-        iggy_decode_result *d_res = c->pres.as<iggy_decode_result>();
-        for (size_t k = 0; k < cand.size(); ++k) {
-            r = enqueue_decode(c, c->din.as<uint8_t>(cand[k].pos), len - cand[k].pos, IGGY_INTEGRITY_VERIFY, nullptr,
-                               0, d_res + k, c->stream);
-            if (r) return r;
-        }
-        HIP_OK(hipMemcpyAsync(res.data(), d_res, res.size() * sizeof(iggy_decode_result), hipMemcpyDeviceToHost,
-                              c->stream));
+        std::vector<RecIn> recs(K);
+        for (size_t k = 0; k < K; ++k) recs[k] = RecIn{cand[k].pos, len - cand[k].pos, 0, 0, 0};
+        iggy_decode_result *d_res = c->rres.as<iggy_decode_result>();
+        std::vector<size_t> single;
+        r = enqueue_records(c, c->din.as<uint8_t>(), bytes, recs.data(), K, IGGY_INTEGRITY_VERIFY, nullptr, nullptr,
+                            d_res, &single);
+        if (r) return r;
+        HIP_OK(hipMemcpyAsync(res.data(), d_res, K * sizeof(iggy_decode_result), hipMemcpyDeviceToHost, c->stream));
         HIP_OK(hipStreamSynchronize(c->stream));
+        r = redo_general(c, c->din.as<uint8_t>(), recs.data(), K, IGGY_INTEGRITY_VERIFY, nullptr, d_res, res.data(),
+                         nullptr);
+        if (r) return r;
     }
     uint64_t next_offset = base_offset, indexed = 0, nidx = 0;
     bool have_stats = false, have_index = false;
@@ -1331,35 +1526,55 @@ int iggy_codec_poll_decode(iggy_codec_ctx *c, const uint8_t *buf, uint64_t len, 
         if (h.batch_length > len - position) break;  // its decode reports the EOF
         position += h.batch_length;
     }
-    // 2. every record's frame walk (LayoutOnly), back to back on the device: one
-    //    copy of the body, one enqueue per record, one sync
+    // 2. every record's frame walk (LayoutOnly) in ONE multi-record launch, which also
+    //    writes the message descriptors of the single-stride records; the others take
+    //    the single-record decode and k_poll_fill. Descriptor slots: record k's planned
+    //    frame count, consecutive, so a body of well-formed records comes back in one
+    //    copy; single-path and re-walked records fill a tail area instead.
     const size_t K = recs.size();
+    std::vector<RecIn> rin(K);
+    std::vector<uint64_t> slot(K), tailb(K);
+    uint64_t nslots = 0;
+    for (size_t k = 0; k < K; ++k) {
+        const uint64_t avail = std::min<uint64_t>(recs[k].bl, len - recs[k].pos);
+        uint64_t nf = 0;
+        const uint64_t nw = rec_plan(buf + recs[k].pos, len - recs[k].pos, &nf);
+        slot[k] = nslots;
+        nslots += nw ? nf : 0;
+        rin[k] = RecIn{recs[k].pos, len - recs[k].pos, recs[k].pbase, avail / 48 + 1, slot[k]};
+    }
+    for (size_t k = 0; k < K; ++k) tailb[k] = nslots + recs[k].pbase;
     int r = c->din.ensure(len + 16);
     r |= c->ppos.ensure((pwords + 1) * 8);
     r |= c->pres.ensure((K + 1) * sizeof(iggy_decode_result));
-    r |= c->pmsgs.ensure((len / 48 + 2) * sizeof(iggy_polled_message));
+    r |= c->pmsgs.ensure((nslots + pwords + 1) * sizeof(iggy_polled_message));
     if (r) return IGGY_ERR_DEVICE;
     if (len) HIP_OK(hipMemcpyAsync(c->din.p, buf, len, hipMemcpyHostToDevice, c->stream));
     iggy_decode_result *d_res = c->pres.as<iggy_decode_result>();
-    for (size_t k = 0; k < K; ++k) {
-        r = enqueue_decode(c, c->din.as<uint8_t>(recs[k].pos), len - recs[k].pos, IGGY_INTEGRITY_LAYOUT_ONLY,
-                           c->ppos.as<uint64_t>(8 * recs[k].pbase), std::min<uint64_t>(recs[k].bl, len - recs[k].pos) / 48 + 1,
-                           d_res + k, c->stream);
-        if (r) return r;
-    }
+    iggy_polled_message *d_msgs = c->pmsgs.as<iggy_polled_message>();
+    std::vector<size_t> single, redone;
+    r = enqueue_records(c, c->din.as<uint8_t>(), buf, rin.data(), K, IGGY_INTEGRITY_LAYOUT_ONLY, c->ppos.as<uint64_t>(),
+                        d_msgs, d_res, &single);
+    if (r) return r;
     std::vector<iggy_decode_result> res(K);
     if (K) HIP_OK(hipMemcpyAsync(res.data(), d_res, K * sizeof(iggy_decode_result), hipMemcpyDeviceToHost, c->stream));
     HIP_OK(hipStreamSynchronize(c->stream));
-    // 3. verdicts in record order; messages expanded on the device, one more sync
+    r = redo_general(c, c->din.as<uint8_t>(), rin.data(), K, IGGY_INTEGRITY_LAYOUT_ONLY, c->ppos.as<uint64_t>(), d_res,
+                     res.data(), &redone);
+    if (r) {
+        if (r == IGGY_ERR_TIMEOUT) set_err(err, IGGY_ERR_TIMEOUT);
+        return r;
+    }
+    std::vector<uint8_t> in_tail(K, 0);
+    for (size_t k : single) in_tail[k] = 1;
+    for (size_t k : redone) in_tail[k] = 1;
+    // 3. verdicts in record order; descriptors of tail records expanded, one copy out
     uint64_t n = 0;
     int rc = 0;
+    struct Span { uint64_t src, n; };
+    std::vector<Span> spans;
     for (size_t k = 0; k < K && !rc; ++k) {
         const iggy_decode_result &rs = res[k];
-        if (rs.error.kind == IGGY_ERR_TIMEOUT) {
-            reset_after_timeout(c);
-            fill_err(err, rs.error);
-            return IGGY_ERR_TIMEOUT;
-        }
         if (mode == IGGY_POLL_MODE_SDK) {
             // the SDK walk only needs the frames to tile the record (no count check)
             if (rs.covered != recs[k].bl - 256) {
@@ -1378,10 +1593,16 @@ int iggy_codec_poll_decode(iggy_codec_ctx *c, const uint8_t *buf, uint64_t len, 
             break;
         }
         if (nf) {
-            hipLaunchKernelGGL(k_poll_fill, dim3((uint32_t)std::min<uint64_t>((nf + 255) / 256, 65535)), dim3(256), 0,
-                               c->stream, c->din.as<uint8_t>(), recs[k].pos, c->ppos.as<uint64_t>(8 * recs[k].pbase),
-                               nf, c->pmsgs.as<iggy_polled_message>(n * sizeof(iggy_polled_message)));
-            HIP_OK(hipGetLastError());
+            uint64_t src = slot[k];
+            if (in_tail[k]) {
+                src = tailb[k];
+                hipLaunchKernelGGL(k_poll_fill, dim3((uint32_t)std::min<uint64_t>((nf + 255) / 256, 65535)), dim3(256),
+                                   0, c->stream, c->din.as<uint8_t>(), recs[k].pos,
+                                   c->ppos.as<uint64_t>(8 * recs[k].pbase), nf, d_msgs + src);
+                HIP_OK(hipGetLastError());
+            }
+            if (!spans.empty() && spans.back().src + spans.back().n == src) spans.back().n += nf;
+            else spans.push_back({src, nf});
         }
         n += nf;
     }
@@ -1389,7 +1610,12 @@ int iggy_codec_poll_decode(iggy_codec_ctx *c, const uint8_t *buf, uint64_t len, 
         fill_err(err, stop_err);
         rc = stop_rc;
     }
-    if (n) HIP_OK(hipMemcpyAsync(out, c->pmsgs.p, n * sizeof(iggy_polled_message), hipMemcpyDeviceToHost, c->stream));
+    uint64_t o = 0;
+    for (const Span &sp : spans) {
+        HIP_OK(hipMemcpyAsync(out + o, d_msgs + sp.src, sp.n * sizeof(iggy_polled_message), hipMemcpyDeviceToHost,
+                              c->stream));
+        o += sp.n;
+    }
     HIP_OK(hipStreamSynchronize(c->stream));
     if (n_out) *n_out = n;
     return rc;
@@ -1681,13 +1907,13 @@ int iggy_codec_select_slice_device(iggy_codec_ctx *c, const uint8_t *d_record, c
     return enqueue_select(c, d_record, d_frame_pos, nframes, *q, d_out, d_header_out, s);
 }
 
-int iggy_codec_walk_disk_chunk(iggy_codec_ctx *c, const uint8_t *chunk, uint64_t len, const iggy_slice_query *q,
-                               int integrity, iggy_chunk_fragment *frags, uint8_t *headers, uint64_t cap,
-                               iggy_chunk_walk *out) {
-    if (!c || !q || !out || (!chunk && len) || (cap && !frags)) return IGGY_ERR_INVALID_ARGUMENT;
-    if (q->kind != IGGY_LOOKUP_OFFSET && q->kind != IGGY_LOOKUP_TIMESTAMP) return IGGY_ERR_INVALID_ARGUMENT;
-    DevGuard dg(c->device);
-    bind(c, nullptr);
+// The per-batch form of the chunk walk: every batch's decode, gate, selection and
+// fragment push enqueued one after the other (~11 stream operations per batch). Used
+// for chunks holding a batch that is not single-stride, or that the one-launch form
+// (below) found to need the general walk.
+static int walk_chunk_per_batch(iggy_codec_ctx *c, const uint8_t *chunk, uint64_t len, const iggy_slice_query *q,
+                                int integrity, iggy_chunk_fragment *frags, uint8_t *headers, uint64_t cap,
+                                iggy_chunk_walk *out) {
     memset(out, 0, sizeof(*out));
     // the batch extents follow from the 256-B headers alone (host); a header that does
     // not decode or a batch that does not fit is the last candidate (its decode fails)
@@ -1753,6 +1979,118 @@ int iggy_codec_walk_disk_chunk(iggy_codec_ctx *c, const uint8_t *chunk, uint64_t
     if (hs.error.kind == IGGY_ERR_TIMEOUT) {  // a bug guard fired, not a verdict on the chunk
         reset_after_timeout(c);
         return IGGY_ERR_TIMEOUT;
+    }
+    out->consumed = std::min<uint64_t>(hs.consumed, len);
+    out->corrupt = hs.corrupt;
+    out->matched = hs.matched;
+    out->last_matching_offset = hs.last_matching_offset;
+    out->has_last_matching_offset = (uint32_t)hs.has_last;
+    out->fragments = hs.nfrag;
+    out->error = hs.error;
+    out->batches = hs.batches;
+    return hs.nfrag > cap ? IGGY_ERR_CAPACITY : 0;
+}
+
+int iggy_codec_walk_disk_chunk(iggy_codec_ctx *c, const uint8_t *chunk, uint64_t len, const iggy_slice_query *q,
+                               int integrity, iggy_chunk_fragment *frags, uint8_t *headers, uint64_t cap,
+                               iggy_chunk_walk *out) {
+    if (!c || !q || !out || (!chunk && len) || (cap && !frags)) return IGGY_ERR_INVALID_ARGUMENT;
+    if (q->kind != IGGY_LOOKUP_OFFSET && q->kind != IGGY_LOOKUP_TIMESTAMP) return IGGY_ERR_INVALID_ARGUMENT;
+    DevGuard dg(c->device);
+    bind(c, nullptr);
+    memset(out, 0, sizeof(*out));
+    // the batch extents follow from the 256-B headers alone (host); a header that does
+    // not decode or a batch that does not fit is the last candidate (its decode fails)
+    std::vector<ChunkCand> cand;
+    uint64_t cursor = 0, pwords = 0, nbb = 0;
+    bool one_launch = true;
+    while (cursor + 256 <= len) {
+        iggy_batch_header h;
+        iggy_wire_error he;
+        const bool ok = iggy_batch_header_decode(chunk + cursor, len - cursor, &h, &he) == 0;
+        const bool fits = ok && h.batch_length <= len - cursor;
+        uint64_t nfp = 0;
+        if (!rec_plan(chunk + cursor, len - cursor, &nfp)) one_launch = false;
+        const uint64_t nf = fits ? (h.batch_length - 256) / 48 + 1 : 1;
+        cand.push_back({cursor, fits ? h.batch_length : 0, pwords, nbb});
+        pwords += nf;
+        nbb += rec_blocks(nfp) + 2;
+        if (!fits) break;
+        cursor += h.batch_length;
+    }
+    const uint64_t K = cand.size();
+    if (K == 0) {  // no header fits: the loop does not run (poll_plan.rs:963)
+        out->matched = q->already_matched;
+        return 0;
+    }
+    if (!one_launch) return walk_chunk_per_batch(c, chunk, len, q, integrity, frags, headers, cap, out);
+    // One copy of the chunk, ONE multi-record decode launch, ONE k_chunk_walk launch
+    // (one workgroup per batch: gate, selection, partial checksum, fragment push, the
+    // match count handed batch to batch), one copy back, one sync.
+    const uint64_t capk = std::min<uint64_t>(cap, K);  // at most one fragment per batch
+    const size_t res_bytes = 256 + capk * (sizeof(iggy_chunk_fragment) + 256);
+    const size_t cand_bytes = K * sizeof(ChunkCand), link_bytes = K * sizeof(ChunkLink);
+    int r = c->din.ensure(len + 16);
+    r |= c->dpos.ensure((pwords + 1) * 8);
+    r |= c->pres.ensure((K + 1) * sizeof(iggy_decode_result));
+    r |= c->cwk.ensure(res_bytes + cand_bytes + 64);
+    r |= c->sl.ensure(nbb * 64 + 64);
+    // the links live in a buffer of their own that only ever holds links: a stale one
+    // carries an older epoch, never the current one (zeroed whenever it is new)
+    const size_t links_cap_before = c->clinks.cap;
+    r |= c->clinks.ensure(link_bytes);
+    if (r) return IGGY_ERR_DEVICE;
+    const size_t pin_need = ((cand_bytes + 255) & ~(size_t)255) + res_bytes;
+    if (c->cpin_cap < pin_need) {
+        if (c->cpin) (void)hipHostFree(c->cpin);
+        c->cpin = nullptr;
+        c->cpin_cap = 0;
+        const size_t want = std::max<size_t>(pin_need, 64 << 10);
+        if (hipHostMalloc(&c->cpin, want, hipHostMallocDefault) != hipSuccess) return IGGY_ERR_DEVICE;
+        c->cpin_cap = want;
+    }
+    hipStream_t s = c->stream;
+    HIP_OK(hipMemcpyAsync(c->din.p, chunk, len, hipMemcpyHostToDevice, s));
+    std::vector<RecIn> rin(K);
+    for (uint64_t k = 0; k < K; ++k)
+        rin[k] = RecIn{cand[k].pos, len - cand[k].pos, cand[k].pbase, cand[k].bl ? (cand[k].bl - 256) / 48 + 1 : 0, 0};
+    iggy_decode_result *d_res = c->pres.as<iggy_decode_result>();
+    std::vector<size_t> single;
+    r = enqueue_records(c, c->din.as<uint8_t>(), chunk, rin.data(), K, integrity, c->dpos.as<uint64_t>(), nullptr,
+                        d_res, &single);
+    if (r) return r;
+    uint8_t *pin = (uint8_t *)c->cpin;
+    uint8_t *pin_res = pin + ((cand_bytes + 255) & ~(size_t)255);
+    memcpy(pin, cand.data(), cand_bytes);
+    ChunkState *d_state = c->cwk.as<ChunkState>(0);
+    iggy_chunk_fragment *d_frags = c->cwk.as<iggy_chunk_fragment>(256);
+    uint8_t *d_hdrs = c->cwk.as<uint8_t>(256 + capk * sizeof(iggy_chunk_fragment));
+    ChunkLink *d_links = c->clinks.as<ChunkLink>();
+    ChunkCand *d_cand = c->cwk.as<ChunkCand>(res_bytes);
+    HIP_OK(hipMemcpyAsync(d_cand, pin, cand_bytes, hipMemcpyHostToDevice, s));
+    if (++c->chunk_epoch == 0 || c->clinks.cap != links_cap_before) {  // new buffer or wrapped tags
+        if (c->chunk_epoch == 0) c->chunk_epoch = 1;
+        HIP_OK(hipMemsetAsync(c->clinks.p, 0, c->clinks.cap, s));
+    }
+    hipLaunchKernelGGL(k_chunk_walk, dim3((uint32_t)K), dim3(kChunkThreads), 0, s, (const uint8_t *)c->din.p,
+                       (const ChunkCand *)d_cand, (uint32_t)K, (const iggy_decode_result *)d_res,
+                       (const uint64_t *)c->dpos.as<uint64_t>(), *q, c->chunk_epoch, d_links, d_state, d_frags,
+                       headers ? d_hdrs : nullptr, capk, c->sl.as<uint64_t>());
+    HIP_OK(hipGetLastError());
+    HIP_OK(hipMemcpyAsync(pin_res, c->cwk.p, res_bytes, hipMemcpyDeviceToHost, s));
+    HIP_OK(hipStreamSynchronize(s));
+    ChunkState hs;
+    memcpy(&hs, pin_res, sizeof(hs));
+    if (hs.error.kind == IGGY_ERR_PENDING)  // a batch needs the general walk: the per-batch form
+        return walk_chunk_per_batch(c, chunk, len, q, integrity, frags, headers, cap, out);
+    if (hs.error.kind == IGGY_ERR_TIMEOUT) {  // a bug guard fired, not a verdict on the chunk
+        reset_after_timeout(c);
+        return IGGY_ERR_TIMEOUT;
+    }
+    const uint64_t nf = std::min<uint64_t>(hs.nfrag, capk);
+    if (nf) {
+        memcpy(frags, pin_res + 256, nf * sizeof(iggy_chunk_fragment));
+        if (headers) memcpy(headers, pin_res + 256 + capk * sizeof(iggy_chunk_fragment), nf * 256);
     }
     out->consumed = std::min<uint64_t>(hs.consumed, len);
     out->corrupt = hs.corrupt;

@@ -1,0 +1,358 @@
+// decode_records.hip — decode_batch_slice_with (core/binary_protocol/src/batch.rs:391-506)
+// over MANY records in ONE launch: the walks that visit a sequence of batches (a
+// 1 MiB disk-poll chunk, poll_plan.rs:484/950-1011; boot recovery of a segment,
+// segment_recovery.rs:425-530; a transferred segment, state_transfer.rs:715-833;
+// a poll response body, poll_messages.rs:95-165 / polled_messages.rs:95-150)
+// mostly carry C1-sized batches (1 000 x 256 B = 304 KB, core/bench
+// defaults.rs:33). The persistent single-record decode (decode_uniform.hip) sizes a
+// whole-chip grid per record; here every record's 128-frame checksum blocks are
+// workgroups of ONE grid, so a chunk or a segment of small batches fills the chip
+// with one dispatch.
+//
+// Per record (uniform stride S taken from frame 0, as decode_uniform.hip
+// speculates and proves): WG (record, b) checks and hashes frames
+// [128b - 6, 128b + 122) -- exactly the frames whose stored checksums form words
+// 128b .. 128b + 127 of the batch-checksum input -- and stores that block's 8
+// XXH3 accumulator sums. 8 lanes per frame (lane-group XXH3, 16-B pieces, pairs
+// folded by DPP) for hashed lengths > 240 B; one lane per frame otherwise and
+// under LayoutOnly. The LAST workgroup of a record to finish (a per-record
+// counter after a release fence) runs the record's serial scramble chain over its
+// block sums and resolves precedence exactly as the uniform kernel's consumer
+// does. A record whose stride speculation breaks without the walk stopping is
+// left with status kStatusNeedGeneral; the host re-decodes it with the general
+// walk (decode_general.hip).
+//
+// Optional fused outputs (both written speculatively by the block workgroups,
+// valid when the record decodes):
+//  * frame positions at frame_pos[pos_base + i];
+//  * polled message descriptors (poll.hip's k_poll_fill) at msgs[msg_base + i].
+#include "codec_common.hpp"
+
+namespace iggy {
+
+struct RecTask {
+    uint64_t off, len;            // record start in the device buffer, bytes available from there
+    uint64_t pos_base, pos_cap;   // frame positions: frame_pos[pos_base + i], i < pos_cap
+    uint64_t msg_base;            // polled messages: msgs[msg_base + i] (when msgs != nullptr)
+    uint64_t bsum_base;           // block sums of this record: bsums[8 * (bsum_base + b) + j]
+    uint32_t wg0, nwg;            // its workgroups in the grid
+};
+struct RecState {  // zeroed by the host before the launch
+    uint64_t first_bad;  // ~min index of a frame whose checksum mismatches (max-encoded), 0 = none
+    uint64_t spec_fail;  // ~min index of a frame that breaks the stride
+    uint32_t done;       // block workgroups finished
+    uint32_t _pad;
+};
+
+constexpr uint32_t kRecThreads = 256;
+constexpr uint32_t kRecFrames = 128;  // frames per workgroup: one checksum block
+
+__host__ __device__ __forceinline__ uint64_t rec_blocks(uint64_t N) { return (N + 5) / kRecFrames + 1; }
+
+__device__ __forceinline__ void rec_fill_msg(const uint8_t *rec, uint64_t rec_off, uint64_t p, uint64_t base_offset,
+                                             uint64_t base_ts, uint64_t origin, iggy_polled_message *out) {
+    const uint8_t *f = rec + kHdr + p;
+    iggy_polled_message m;
+    m.checksum = ld64_any(f);
+    m.id_lo = ld64_any(f + 8);
+    m.id_hi = ld64_any(f + 16);
+    m.offset = base_offset + ld32_any(f + 24);  // wrapping, as in release Rust
+    m.timestamp = base_ts;                      // flat per batch
+    m.origin_timestamp = origin + ld32_any(f + 28);
+    m.user_headers_length = ld32_any(f + 32);
+    m.payload_length = ld32_any(f + 36);
+    m.payload_pos = rec_off + kHdr + p + kFrameHdr;
+    m.user_headers_pos = m.payload_pos + m.payload_length;
+    m._pad = 0;
+    *out = m;
+}
+
+// min over the WG of per-thread candidates (~0 = none), via wave minima in LDS
+__device__ __forceinline__ uint64_t wg_min(uint64_t v, uint64_t *s4) {
+    for (int d = 32; d; d >>= 1) {
+        const uint64_t o = __shfl_xor(v, d);
+        v = o < v ? o : v;
+    }
+    if ((threadIdx.x & 63) == 0) s4[threadIdx.x >> 6] = v;
+    __syncthreads();
+    uint64_t m = s4[0];
+#pragma unroll
+    for (int w = 1; w < (int)(kRecThreads / 64); ++w) m = s4[w] < m ? s4[w] : m;
+    __syncthreads();
+    return m;
+}
+
+template <bool VERIFY>
+__global__ __launch_bounds__(kRecThreads) void k_decode_records(const uint8_t *__restrict__ base,
+                                                                const RecTask *__restrict__ tasks,
+                                                                const uint32_t *__restrict__ wg_task,
+                                                                RecState *st, uint64_t *bsums, uint64_t *frame_pos,
+                                                                iggy_polled_message *msgs,
+                                                                iggy_decode_result *results) {
+    __shared__ uint64_t s_cs[kRecFrames + 2];  // stored checksums of frames 128b - 6 + k
+    __shared__ uint64_t s_min[4];
+    __shared__ uint32_t s_last;
+    __shared__ uint8_t s_small[256];  // short checksum inputs (N <= 24): 44 + 8 N bytes
+    const uint32_t t = wg_task[blockIdx.x];
+    const RecTask tk = tasks[t];
+    const uint32_t blk = blockIdx.x - tk.wg0;
+    const uint8_t *body = base + tk.off;
+    const uint8_t *blob = body + kHdr;
+    const int lane = threadIdx.x & 63;
+    const uint32_t wave = threadIdx.x >> 6;
+    HeaderInfo hi;
+    parse_header(body, tk.len, hi);
+    UPlan pl;
+    make_plan(hi, blob, tk.len, VERIFY, ~0ull, true, pl);
+    iggy_decode_result *res = results + t;
+
+    if (pl.state != 0 || tk.nwg < rec_blocks(pl.N)) {
+        // result known without the frames (header errors, empty record, broken first
+        // frame), or not a single-stride record: the general walk (host re-decodes)
+        if (blk != 0 || wave != 0) return;
+        uint32_t kind = pl.ekind, reason = pl.ereason, status = kStatusDone;
+        uint64_t a = pl.ea, b = pl.eb, c = pl.ec, computed = 0;
+        if (pl.state != 1) {
+            status = kStatusNeedGeneral;
+        } else if (kind == IGGY_OK && VERIFY && lane == 0) {
+            // zero frames: the checksum over the 44 header bytes (batch.rs:452-458)
+            const uint64_t w[5] = {hi.h.partition_id, hi.h.base_offset, hi.h.base_timestamp,
+                                   hi.h.origin_timestamp, hi.h.batch_length};
+            for (int i = 0; i < 5; ++i) st64_any(s_small + 8 * i, w[i]);
+            *(u32_ua *)(s_small + 40) = hi.h.message_count;
+            computed = xxh3_64_lane(s_small, 44);
+            if (computed != hi.h.batch_checksum) {
+                kind = IGGY_ERR_INVALID_BATCH_CHECKSUM; reason = 0;
+                a = hi.h.batch_checksum; b = computed; c = hi.h.base_offset;
+            }
+        }
+        if (lane == 0) write_result(res, hi, kind, reason, a, b, c, 0, computed, 1, status, 0);
+        return;
+    }
+    const uint64_t S = pl.S, N = pl.N, L = pl.L;
+    const uint64_t nblk = rec_blocks(N);
+    if (blk >= nblk) return;
+    const int64_t i0 = (int64_t)kRecFrames * blk - 6;
+    const uint64_t base_offset = hi.h.base_offset, base_ts = hi.h.base_timestamp, origin = hi.h.origin_timestamp;
+    uint64_t mybad = ~0ull, mysf = ~0ull;
+
+    if (VERIFY && pl.long_frames) {
+        // lane groups: group g = 8 wave + (lane >> 3) takes frames i0 + g + 32 k, k = 0..3
+        const uint32_t l = lane & 7, m = l >> 1, par = l & 1, g = 8 * wave + ((uint32_t)lane >> 3);
+        const uint32_t poff = 16 * (m + 4 * par);
+        uint64_t s0[8], s1[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            s0[q] = kSecretW8[2 * q + par + 2 * m];
+            s1[q] = kSecretW8[2 * q + par + 2 * m + 1];
+        }
+        const uint64_t key0 = kSecretW8[16 + 2 * m], key1 = kSecretW8[17 + 2 * m];
+        const uint64_t init0 = par ? 0 : kAccInit[2 * m], init1 = par ? 0 : kAccInit[2 * m + 1];
+        const uint64_t last0 = kSecretLast[2 * m], last1 = kSecretLast[2 * m + 1];
+        const uint64_t mrg0 = kSecretMerge[2 * m], mrg1 = kSecretMerge[2 * m + 1];
+        const uint64_t nbF = pl.nbF, ns = pl.ns;
+#pragma unroll 1
+        for (uint32_t k = 0; k < kRecFrames / 32; ++k) {
+            const int64_t i = i0 + g + 32 * k;
+            const bool valid = i >= 0 && (uint64_t)i < N;
+            const uint8_t *fb = blob + (valid ? (uint64_t)i : 0) * S;
+            const uint8_t *hb = fb + 8 + poff;
+            uint4 hdr = make_uint4(0, 0, 0, 0);
+            uint64_t stored = 0;
+            if (l == 0) {
+                hdr = ld128_any(fb + 32);  // user_headers_length, payload_length, reserved
+                stored = ld64_any(fb);
+            }
+            uint64_t a0 = init0, a1 = init1;
+            for (uint64_t b = 0; b < nbF; ++b) {
+                uint4 pc[8];
+#pragma unroll
+                for (int q = 0; q < 8; ++q) pc[q] = ld128_any(hb + 1024 * b + 128 * q);
+                uint64_t p0[4] = {0, 0, 0, 0}, p1[4] = {0, 0, 0, 0};
+#pragma unroll
+                for (int q = 0; q < 8; ++q) piece(p0[q & 3], p1[q & 3], pc[q], s0[q], s1[q]);
+                a0 += (p0[0] + p0[1]) + (p0[2] + p0[3]);
+                a1 += (p1[0] + p1[1]) + (p1[2] + p1[3]);
+                a0 += gdpp64<0xB1>(a0);
+                a1 += gdpp64<0xB1>(a1);
+                a0 = scramble1(a0, key0);
+                a1 = scramble1(a1, key1);
+                if (par) { a0 = 0; a1 = 0; }
+            }
+            {
+                uint4 pc[8];
+#pragma unroll
+                for (int q = 0; q < 8; ++q)
+                    pc[q] = (2 * (uint64_t)q + par < ns) ? ld128_any(hb + 1024 * nbF + 128 * q) : make_uint4(0, 0, 0, 0);
+                const uint4 lastp = par ? make_uint4(0, 0, 0, 0) : ld128_any(fb + 8 + L - 64 + 16 * m);
+#pragma unroll
+                for (int q = 0; q < 8; ++q)
+                    if (2 * (uint64_t)q + par < ns) piece(a0, a1, pc[q], s0[q], s1[q]);
+                a0 += gdpp64<0xB1>(a0);
+                a1 += gdpp64<0xB1>(a1);
+                piece(a0, a1, lastp, last0, last1);  // odd lanes: never used
+            }
+            uint64_t tt = fold64(a0 ^ mrg0, a1 ^ mrg1);
+            tt += gdpp64<0x4E>(tt);
+            tt += gswz_xor4(tt);
+            const uint64_t h = avalanche(L * P64_1 + tt);
+            if (l == 0) {
+                if (valid) {
+                    if (hdr.z | hdr.w || (uint64_t)kFrameHdr + hdr.x + hdr.y != S) mysf = min(mysf, (uint64_t)i);
+                    if (h != stored) mybad = min(mybad, (uint64_t)i);
+                    if (frame_pos && (uint64_t)i < tk.pos_cap) frame_pos[tk.pos_base + i] = (uint64_t)i * S;
+                }
+                s_cs[g + 32 * k] = valid ? stored : 0;
+            }
+        }
+    } else if (threadIdx.x < kRecFrames) {
+        // one lane per frame: header checks, short-frame hashes (<= 240 B), positions
+        const uint32_t k = threadIdx.x;
+        const int64_t i = i0 + k;
+        const bool valid = i >= 0 && (uint64_t)i < N;
+        uint64_t stored = 0;
+        if (valid) {
+            const uint8_t *fb = blob + (uint64_t)i * S;
+            const uint4 hdr = ld128_any(fb + 32);
+            stored = ld64_any(fb);
+            if (hdr.z | hdr.w || (uint64_t)kFrameHdr + hdr.x + hdr.y != S) mysf = (uint64_t)i;
+            if (VERIFY && xxh3_64_lane(fb + 8, L) != stored) mybad = (uint64_t)i;
+            if (frame_pos && (uint64_t)i < tk.pos_cap) frame_pos[tk.pos_base + i] = (uint64_t)i * S;
+        }
+        s_cs[k] = stored;
+    }
+    if (msgs) {  // poll-side descriptors (poll.hip), written whether or not the record decodes
+        for (uint32_t k = threadIdx.x; k < kRecFrames; k += kRecThreads) {
+            const int64_t i = i0 + k;
+            if (i >= 0 && (uint64_t)i < N)
+                rec_fill_msg(body, tk.off, (uint64_t)i * S, base_offset, base_ts, origin, msgs + tk.msg_base + i);
+        }
+    }
+    if (threadIdx.x == 0) {  // frame 128b + 122: its low half closes word 128b + 127
+        const int64_t i = i0 + kRecFrames;
+        s_cs[kRecFrames] = (i >= 0 && (uint64_t)i < N) ? ld64_any(blob + (uint64_t)i * S) : 0;
+    }
+    const uint64_t wbad = wg_min(mybad, s_min);  // (its barriers also publish s_cs)
+    const uint64_t wsf = wg_min(mysf, s_min);
+    if (threadIdx.x == 0) {
+        if (wbad != ~0ull) atomicMax((unsigned long long *)&st[t].first_bad, (unsigned long long)~wbad);
+        if (wsf != ~0ull) atomicMax((unsigned long long *)&st[t].spec_fail, (unsigned long long)~wsf);
+    }
+    if (VERIFY && pl.long_cs && wave == 0) {
+        // words m = 128b + j of the checksum input, j = lane, lane + 64
+        const uint64_t mb = (uint64_t)kRecFrames * blk;
+        uint64_t x = 0, y = 0;
+        word_contrib(pl.Mreg, mb + lane, s_cs[lane], s_cs[lane + 1], true, x, y);
+        word_contrib(pl.Mreg, mb + 64 + lane, s_cs[64 + lane], s_cs[65 + lane], true, x, y);
+        const uint64_t t8 = reduce_acc8(x, y);
+        if (lane < 8) bsums[8 * (tk.bsum_base + blk) + lane] = t8;
+    }
+    // the last block workgroup of the record resolves it
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __threadfence();  // release: this WG's block sums, positions and atomics
+        const uint32_t old = atomicAdd(&st[t].done, 1u);
+        s_last = old + 1 == (uint32_t)nblk;
+    }
+    __syncthreads();
+    if (!s_last || wave != 0) return;
+    __threadfence();  // acquire: every block workgroup's stores of this record
+
+    uint64_t computed = 0;
+    if (VERIFY && pl.long_cs) {
+        const int j = lane & 7;
+        uint64_t acc = kAccInit[j];
+        const uint64_t key = kSecretW8[16 + j];
+        const uint32_t klo = (uint32_t)key, khi = (uint32_t)(key >> 32);
+        {  // words 0..5: header fields, then count | lo32(cs_0)
+            const uint64_t cs0 = ld64_any(blob);
+            const uint64_t w6[6] = {hi.h.partition_id, hi.h.base_offset, hi.h.base_timestamp,
+                                    hi.h.origin_timestamp, hi.h.batch_length,
+                                    (uint64_t)hi.h.message_count | (cs0 << 32)};
+#pragma unroll
+            for (int mm = 0; mm < 6; ++mm) {
+                if (j == (mm ^ 1)) acc += w6[mm];
+                if (j == mm) acc += mul32x32(w6[mm] ^ Secret::w(8 * mm));
+            }
+        }
+        // y = acc + S_0; y = scramble(y) + S_b for b = 1 .. nb (the partial block nb only adds)
+        const uint64_t *src = bsums + 8 * tk.bsum_base + j;
+        uint64_t y = acc + src[0];
+        const uint64_t nb = pl.nb;
+        uint64_t b = 1;
+        uint64_t v[16];
+        for (; b + 16 <= nb + 1; b += 16) {
+#pragma unroll
+            for (int q = 0; q < 16; ++q) v[q] = src[8 * (b + q)];
+#pragma unroll
+            for (int q = 0; q < 16; ++q) y = chain_step(y, v[q], klo, khi);
+        }
+        for (; b <= nb; ++b) y = chain_step(y, src[8 * b], klo, khi);
+        acc = y;
+        // last stripe = stored checksums of frames N-8 .. N-1 (secret offset 121)
+        const uint64_t lv = ld64_any(blob + (N - 8 + j) * S);
+        acc += __shfl_xor(lv, 1);
+        acc += mul32x32(lv ^ kSecretLast[j]);
+        uint64_t a[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) a[i] = __shfl(acc, i);
+        uint64_t r = pl.n * P64_1;
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+            r += fold64(a[2 * i] ^ Secret::w(11 + 16 * i), a[2 * i + 1] ^ Secret::w(19 + 16 * i));
+        computed = avalanche(r);
+    } else if (VERIFY && lane == 0) {
+        // short checksum input (N <= 24): hash it directly
+        const uint64_t w[5] = {hi.h.partition_id, hi.h.base_offset, hi.h.base_timestamp, hi.h.origin_timestamp,
+                               hi.h.batch_length};
+        for (int i = 0; i < 5; ++i) st64_any(s_small + 8 * i, w[i]);
+        *(u32_ua *)(s_small + 40) = hi.h.message_count;
+        for (uint64_t i = 0; i < N; ++i) st64_any(s_small + 44 + 8 * i, ld64_any(blob + i * S));
+        computed = xxh3_64_lane(s_small, pl.n);
+    }
+    if (lane != 0) return;
+    // precedence, as the uniform kernel's consumer (batch.rs:395-421, 461-506)
+    const uint64_t fb_enc = __hip_atomic_load(&st[t].first_bad, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint64_t sf_enc = __hip_atomic_load(&st[t].spec_fail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const bool has_fb = fb_enc != 0, has_sf = sf_enc != 0;
+    const uint64_t fbi = ~fb_enc, sf = ~sf_enc;
+    uint32_t kind = IGGY_OK, reason = 0, status = kStatusDone;
+    uint64_t a = 0, b = 0, c = 0, nframes = N;
+    auto msg_err = [&](uint64_t idx) {
+        const uint8_t *f = blob + idx * S;
+        kind = IGGY_ERR_INVALID_MESSAGE_CHECKSUM;
+        a = ld64_any(f);
+        b = xxh3_64_lane(f + 8, L);
+        c = sat_add(hi.h.base_offset, ld32_any(f + 24));
+    };
+    if (has_sf) {
+        // the true walk reaches frame sf at sf*S (all earlier frames have size S)
+        const uint64_t pos = sf * S, bl = hi.blob_len;
+        bool stops = (bl - pos < kFrameHdr) || ld64_any(blob + pos + 40) != 0;
+        if (!stops) {
+            const uint64_t end = pos + kFrameHdr + ld32_any(blob + pos + 36) + ld32_any(blob + pos + 32);
+            stops = end > bl;
+        }
+        nframes = sf;
+        if (!stops) status = kStatusNeedGeneral;
+        else if (VERIFY && has_fb && fbi < sf) msg_err(fbi);
+        else { kind = IGGY_ERR_VALIDATION; reason = IGGY_V_FRAMES_DO_NOT_TILE; }
+    } else if (VERIFY && has_fb) {
+        msg_err(fbi);
+    } else if (N != (uint64_t)hi.h.message_count) {
+        kind = IGGY_ERR_VALIDATION; reason = IGGY_V_FRAMES_DO_NOT_TILE;
+    } else if (VERIFY && computed != hi.h.batch_checksum) {
+        kind = IGGY_ERR_INVALID_BATCH_CHECKSUM;
+        a = hi.h.batch_checksum; b = computed; c = hi.h.base_offset;
+    }
+    write_result(res, hi, kind, reason, a, b, c, nframes, computed, 1, status, nframes * S);
+}
+
+template __global__ void k_decode_records<true>(const uint8_t *__restrict__, const RecTask *__restrict__,
+                                                const uint32_t *__restrict__, RecState *, uint64_t *, uint64_t *,
+                                                iggy_polled_message *, iggy_decode_result *);
+template __global__ void k_decode_records<false>(const uint8_t *__restrict__, const RecTask *__restrict__,
+                                                 const uint32_t *__restrict__, RecState *, uint64_t *, uint64_t *,
+                                                 iggy_polled_message *, iggy_decode_result *);
+
+}  // namespace iggy

@@ -331,4 +331,245 @@ __global__ void k_chunk_after(const iggy_slice_result *sr, const uint8_t *hdr_by
     }
 }
 
+
+// ---- walk_disk_chunk in ONE launch after the chunk's batches are decoded by
+// k_decode_records (decode_records.hip): one workgroup per batch. Each computes
+// what it can alone (the ceiling stop and the selected-frame counts), then takes
+// the walk state after batch k - 1 from its predecessor (decoupled look-back on a
+// published, epoch-tagged link: workgroups are dispatched in order, so the one
+// waited on is always resident or done), applies the loop condition and the
+// decode verdict (poll_plan.rs:963-988), selects (journal.rs:1025-1086),
+// recomputes a partial selection's batch checksum (batch.rs:439-450 via
+// checksum_for_blob), pushes the fragment (journal.rs:1096-1137) and publishes
+// the walk state after batch k.
+struct ChunkCand {
+    uint64_t pos;    // chunk offset of the batch header
+    uint64_t bl;     // batch_length (0: the header did not decode or the batch does not fit)
+    uint64_t pbase;  // its frame positions: pos_all[pbase + i]
+    uint64_t bbase;  // its block-sum scratch: bsums[8 * (bbase + b) + j]
+};
+struct ChunkLink {
+    ChunkState st;  // the walk state after this batch
+    uint32_t ready; // == epoch once st is published
+    uint32_t _pad[7];
+};
+constexpr uint32_t kChunkThreads = 256;
+
+__global__ __launch_bounds__(kChunkThreads) void k_chunk_walk(const uint8_t *__restrict__ chunk,
+                                                              const ChunkCand *__restrict__ cands, uint32_t K,
+                                                              const iggy_decode_result *__restrict__ dres,
+                                                              const uint64_t *__restrict__ pos_all,
+                                                              iggy_slice_query q, uint32_t epoch, ChunkLink *links,
+                                                              ChunkState *out_state, iggy_chunk_fragment *frags,
+                                                              uint8_t *headers, uint64_t cap, uint64_t *bsums_all) {
+    __shared__ uint64_t s_red[kChunkThreads / 64];
+    __shared__ uint32_t s_cnt[kChunkThreads];
+    __shared__ ChunkState s_st;
+    __shared__ uint64_t s_sel[4];  // first, last, matched, selected
+    __shared__ uint8_t s_small[256];
+    const uint32_t k = blockIdx.x;
+    const uint32_t tid = threadIdx.x;
+    const int lane = tid & 63;
+    const ChunkCand cd = cands[k];
+    const iggy_decode_result res = dres[k];
+    const bool ok = res.error.kind == IGGY_OK && res.status == kStatusDone && cd.bl != 0;
+    const uint8_t *rec = chunk + cd.pos;
+    const uint8_t *blob = rec + kHdr;
+    const uint64_t *pos = pos_all + cd.pbase;
+    const uint64_t nf = ok ? res.frame_count : 0;
+    const iggy_batch_header h = res.header;
+    auto wmin = [&](uint64_t v) -> uint64_t {
+        for (int d = 32; d; d >>= 1) {
+            const uint64_t o = __shfl_xor(v, d);
+            v = o < v ? o : v;
+        }
+        if (lane == 0) s_red[tid >> 6] = v;
+        __syncthreads();
+        uint64_t m = s_red[0];
+        for (uint32_t w = 1; w < kChunkThreads / 64; ++w) m = s_red[w] < m ? s_red[w] : m;
+        __syncthreads();
+        return m;
+    };
+    // 1. alone: the first frame above the ceiling (the walk breaks there, journal.rs:1048-1050)
+    //    and the selected frames before it, a contiguous range per thread
+    uint64_t mine = ~0ull;
+    for (uint64_t i = tid; i < nf; i += kChunkThreads)
+        if (slice_offset(blob, pos, h.base_offset, i) > q.ceiling) { mine = i; break; }
+    const uint64_t stop = wmin(mine);
+    const uint64_t lim = stop < nf ? stop : nf;
+    const uint64_t F = (lim + kChunkThreads - 1) / kChunkThreads;
+    const uint64_t r0 = min((uint64_t)tid * F, lim), r1 = min(r0 + F, lim);
+    uint32_t c = 0;
+    for (uint64_t i = r0; i < r1; ++i) c += slice_selected(q, slice_offset(blob, pos, h.base_offset, i), h.base_timestamp);
+    s_cnt[tid] = c;
+    __syncthreads();
+    for (uint32_t d = 1; d < kChunkThreads; d <<= 1) {  // inclusive scan of the per-thread counts
+        const uint32_t v = tid >= d ? s_cnt[tid - d] : 0;
+        __syncthreads();
+        s_cnt[tid] += v;
+        __syncthreads();
+    }
+    const uint32_t incl = s_cnt[tid], excl = incl - c, total = s_cnt[kChunkThreads - 1];
+    // 2. the walk state after batch k - 1
+    if (tid == 0) {
+        ChunkState st{};
+        if (k == 0) {
+            st.matched = q.already_matched;
+        } else {
+            const uint64_t t0 = rt_now();
+            bool timed_out = false;
+            while (__hip_atomic_load(&links[k - 1].ready, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) != epoch) {
+                __builtin_amdgcn_s_sleep(1);
+                if (rt_now() - t0 > kSpinLimitTicks) { timed_out = true; break; }
+            }
+            if (timed_out) {
+                st.stopped = 1;
+                st.error.kind = IGGY_ERR_TIMEOUT;
+            } else {
+                st = links[k - 1].st;
+            }
+        }
+        s_st = st;
+    }
+    __syncthreads();
+    ChunkState st = s_st;
+    bool sel_live = false;
+    uint32_t remaining = 0;
+    if (!st.stopped) {  // the loop condition and the decode verdict (poll_plan.rs:963-988)
+        if (st.matched >= q.count) {
+            st.stopped = 1;
+            st.consumed = cd.pos;
+        } else if (!ok) {
+            st.stopped = 1;
+            st.consumed = cd.pos;
+            st.corrupt = res.error.kind == IGGY_ERR_INVALID_BATCH_CHECKSUM ? 1u : 0u;
+            st.error = res.error;
+            if (res.status != kStatusDone) st.error.kind = IGGY_ERR_PENDING;  // host re-walks (general record)
+        } else {
+            remaining = q.count > st.matched ? q.count - st.matched : 0;  // journal.rs:1030
+            sel_live = remaining != 0 && h.message_count != 0 && total != 0;  // :1032-1034, `start?`
+        }
+    }
+    // 3. selection: the first selected frame and the min(remaining, total)-th
+    if (tid == 0) s_sel[3] = 0;
+    __syncthreads();
+    if (sel_live) {
+        const uint32_t need = remaining < total ? remaining : total;
+        if (c && excl == 0) {  // the first selected frame
+            for (uint64_t i = r0; i < r1; ++i)
+                if (slice_selected(q, slice_offset(blob, pos, h.base_offset, i), h.base_timestamp)) { s_sel[0] = i; break; }
+        }
+        if (c && excl < need && need <= incl) {
+            uint32_t r = excl;
+            for (uint64_t i = r0; i < r1; ++i)
+                if (slice_selected(q, slice_offset(blob, pos, h.base_offset, i), h.base_timestamp) && ++r == need) {
+                    s_sel[1] = i;
+                    break;
+                }
+        }
+        if (tid == 0) { s_sel[2] = need; s_sel[3] = 1; }
+    }
+    __syncthreads();
+    iggy_chunk_fragment fr{};
+    bool pushed = false;
+    iggy_batch_header w = h;
+    if (s_sel[3]) {
+        const uint64_t first = s_sel[0], last = s_sel[1];
+        const uint64_t start = pos[first], lp = pos[last];
+        const uint64_t end = lp + kFrameHdr + ld32_any(blob + lp + 36) + ld32_any(blob + lp + 32);
+        const uint64_t blob_len = h.batch_length - kHdr;
+        const bool full = start == 0 && end == blob_len;  // journal.rs:1105
+        if (!full) {  // journal.rs:1114-1124: clamped length and count, checksum over the slice
+            w.batch_length = kHdr + (end - start);
+            w.message_count = (uint32_t)s_sel[2];
+            const uint64_t nsel = last - first + 1;
+            const CsSource src{nullptr, blob, pos + first};
+            const CsPlan cp = cs_plan(nsel);
+            uint64_t computed = 0;
+            if (cp.long_cs) {
+                uint64_t *bs = bsums_all + 8 * cd.bbase;
+                for (uint64_t b = tid >> 6; b <= cp.nb; b += kChunkThreads / 64) {
+                    uint64_t x = 0, y = 0;
+#pragma unroll
+                    for (int half = 0; half < 2; ++half) {
+                        const uint64_t m = 128 * b + 64 * half + lane;
+                        if (m < cp.Mreg) {
+                            const uint64_t v = cs_word(m, w, src);
+                            y += v;
+                            x += mul32x32(v ^ kSecretW8[((m >> 3) & 15) + (m & 7)]);
+                        }
+                    }
+                    x += __shfl_xor(x, 8); y += __shfl_xor(y, 8);
+                    x += __shfl_xor(x, 16); y += __shfl_xor(y, 16);
+                    x += __shfl_xor(x, 32); y += __shfl_xor(y, 32);
+                    const uint64_t t8 = x + __shfl_xor(y, 1);
+                    if (lane < 8) bs[b * 8 + lane] = t8;
+                }
+                __syncthreads();  // (workgroup-scope fence: the block sums are visible to wave 0)
+                if (tid < 64) {
+                    const int j = lane & 7;
+                    uint64_t acc = chain_blocks(bs, cp.nb, lane);
+                    acc += bs[cp.nb * 8 + j];
+                    const uint64_t v = src(nsel - 8 + j);
+                    acc += __shfl_xor(v, 1);
+                    acc += mul32x32(v ^ kSecretLast[j]);
+                    uint64_t a[8];
+#pragma unroll
+                    for (int i = 0; i < 8; ++i) a[i] = __shfl(acc, i);
+                    uint64_t r = cp.n * P64_1;
+#pragma unroll
+                    for (int i = 0; i < 4; ++i)
+                        r += fold64(a[2 * i] ^ Secret::w(11 + 16 * i), a[2 * i + 1] ^ Secret::w(19 + 16 * i));
+                    computed = avalanche(r);
+                }
+            } else if (tid == 0) {
+                for (uint64_t m = 0; m < 5; ++m) st64_any(s_small + 8 * m, cs_word(m, w, src));
+                *(u32_ua *)(s_small + 40) = w.message_count;
+                for (uint64_t i = 0; i < nsel; ++i) st64_any(s_small + 44 + 8 * i, src(i));
+                computed = xxh3_64_lane(s_small, cp.n);
+            }
+            w.batch_checksum = computed;  // (thread 0's value is the one used below)
+        }
+        fr.batch_pos = cd.pos;
+        fr.full_body = full ? 1u : 0u;
+        fr.matched_messages = (uint32_t)s_sel[2];
+        fr.body_start = full ? cd.pos : cd.pos + kHdr + start;
+        fr.body_end = full ? cd.pos + h.batch_length : cd.pos + kHdr + end;
+        fr.last_matching_offset = slice_offset(blob, pos, h.base_offset, last);
+        pushed = true;
+        // the header bytes served with the fragment: the record's own (full body) or rewritten
+        const uint32_t idx = st.nfrag;
+        if (headers && idx < cap && tid < 64) {
+            const uint64_t wcs = __shfl(w.batch_checksum, 0);
+            uint32_t word;
+            const uint32_t off = 4 * tid;
+            if (full) {
+                word = ld32_any(rec + off);
+            } else {
+                word = 0;
+                const uint64_t f[6] = {w.partition_id, w.base_offset, w.base_timestamp,
+                                       w.origin_timestamp, w.batch_length, wcs};
+                if (off < 48) word = (off & 4) ? (uint32_t)(f[off / 8] >> 32) : (uint32_t)f[off / 8];
+                else if (off == 48) word = w.message_count;
+            }
+            *(u32_ua *)(headers + 256ull * idx + off) = word;
+        }
+    }
+    if (tid != 0) return;
+    if (!st.stopped) {  // push_selected_batch_fragments and the cursor advance (:1003)
+        if (pushed) {
+            if (st.nfrag < cap) frags[st.nfrag] = fr;
+            st.nfrag += 1;
+            st.matched += fr.matched_messages;
+            st.last_matching_offset = fr.last_matching_offset;
+            st.has_last = 1;
+        }
+        st.consumed = cd.pos + cd.bl;
+        st.batches += 1;
+    }
+    links[k].st = st;
+    __hip_atomic_store(&links[k].ready, epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    if (k + 1 == K) *out_state = st;
+}
+
 }  // namespace iggy

@@ -446,6 +446,17 @@ int iggy_codec_admit_batch(iggy_codec_ctx *ctx, const uint8_t *batch, uint64_t l
                            uint32_t metadata_messages_count, uint64_t partition_id, int checksum_mode,
                            uint8_t *out, uint64_t cap, iggy_batch_header *hdr_out, iggy_wire_error *err);
 
+/* decode_batch_slice_with (batch.rs:391-422) of many records of one host buffer in
+ * one call: record k is buf[offsets[k] .. len) (trailing bytes allowed, as the walks
+ * over a disk chunk, a segment or a poll body pass each batch; poll_plan.rs:964,
+ * segment_recovery.rs:529, state_transfer.rs:751, poll_messages.rs:132). One copy of
+ * the buffer, ONE launch for every single-stride record (one workgroup per
+ * 128-frame checksum block, decode_records.hip), the single-record decode for the
+ * rest, one sync. out[k] receives record k's verdict exactly as
+ * iggy_codec_decode_batch_device writes it. */
+int iggy_codec_decode_records(iggy_codec_ctx *ctx, const uint8_t *buf, uint64_t len, const uint64_t *offsets,
+                              uint64_t nrec, int integrity, iggy_decode_result *out);
+
 /* -------------------------------------------------------- segment recovery */
 /* recover_segment_bounds' index-less arm (core/partitions/src/segment_recovery.rs:425-488,
  * batch_verifies :518-530): walk the batches of one segment's messages file from
