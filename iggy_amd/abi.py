@@ -17,6 +17,8 @@ ERR_PAYLOAD_TOO_LARGE = 6
 ERR_INVALID_NUMBER_ENCODING = 20
 ERR_INVALID_MESSAGE_PAYLOAD_LENGTH = 21
 ERR_INVALID_COMMAND = 22  # IggyError::InvalidCommand (server_common batch_error)
+ERR_CONNECTION_CLOSED = 25  # IggyError::ConnectionClosed (message_bus framing.rs:165-171)
+ERR_TCP_ERROR = 26
 ERR_DEVICE = 100
 ERR_INVALID_ARGUMENT = 101
 ERR_CAPACITY = 102

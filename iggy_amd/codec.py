@@ -100,6 +100,8 @@ def load(path: str) -> ctypes.CDLL:
     L.iggy_codec_encode_batch.argtypes = [vp, vp, u64, vp, u64, vp, vp]
     L.iggy_codec_poll_decode.argtypes = [vp, vp, u64, ci, vp, u64, vp, vp]
     L.iggy_codec_decode_records.argtypes = [vp, vp, u64, vp, u64, ci, vp]
+    L.iggy_frame_read.argtypes = [ci, vp, u64, u64, vp, vp]
+    L.iggy_codec_convert_request.argtypes = [vp, vp, u64, u64, ci, vp, u64, vp, vp, vp]
     L.iggy_codec_stamp_batch.argtypes = [vp, vp, u64, u64, u64, vp, vp]
     L.iggy_codec_decode_batch_device.argtypes = [vp, vp, u64, ci, vp, u64, vp, vp]
     L.iggy_codec_encode_batch_device.argtypes = [vp, vp, u64, vp, u64, vp, vp]
@@ -150,6 +152,19 @@ def _np(buf) -> np.ndarray:
 
 def _addr(a: np.ndarray):
     return a.ctypes.data if a.size else None
+
+
+def frame_read(fd: int, cap: int, max_message_size: int = 64 << 20):
+    """read_message (message_bus/src/framing.rs:107-164) on a blocking socket fd
+    -> (rc, WireError, frame bytes as a numpy view of a 4096-aligned buffer)."""
+    raw = np.zeros(cap + 4096, dtype=np.uint8)
+    off = (-raw.ctypes.data) % 4096
+    buf = raw[off: off + cap]
+    n = u64(0)
+    e = WireError()
+    rc = lib().iggy_frame_read(fd, buf.ctypes.data if cap else None, cap, max_message_size, ctypes.byref(n),
+                               ctypes.byref(e))
+    return rc, e, buf[: n.value]
 
 
 def send_messages_header_encode(h: SendMessagesHeader) -> bytes:
@@ -321,6 +336,20 @@ class Codec:
         rc = self._L.iggy_codec_decode_records(self._h, _addr(a), a.size, offs.ctypes.data if offs.size else None,
                                                offs.size, integrity, out)
         return rc, [out[i] for i in range(offs.size)]
+
+    def convert_request(self, frame, partition_id: int, checksum_mode: int = 0, cap: int | None = None):
+        """convert_request_message + admit_wire_request (server_common/src/send_messages.rs:459-540)
+        on one [RoutedRequestHeader][body] frame -> (rc, WireError, BatchHeader, output bytes)."""
+        a = _np(frame)
+        cap = a.size + 256 if cap is None else cap
+        out = np.zeros(max(cap, 1), dtype=np.uint8)
+        n = u64(0)
+        h = BatchHeader()
+        e = WireError()
+        rc = self._L.iggy_codec_convert_request(self._h, _addr(a), a.size, partition_id, checksum_mode,
+                                                out.ctypes.data, cap, ctypes.byref(n), ctypes.byref(h),
+                                                ctypes.byref(e))
+        return rc, e, h, out[: n.value].tobytes()
 
     def recover_segment(self, messages, start_offset: int):
         """recover_segment_bounds' index-less walk (segment_recovery.rs:425-530)

@@ -231,6 +231,7 @@ __global__ __launch_bounds__(256) void k_bsum_blocks(const iggy_batch_header *hp
     const int lane = threadIdx.x & 63;
     const uint64_t wid = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     const uint64_t nwaves = ((uint64_t)gridDim.x * blockDim.x) >> 6;
+    const uint64_t sec[2] = {block_word_secret(0, lane), block_word_secret(1, lane)};
     for (uint64_t b = wid; b <= pl.nb; b += nwaves) {
         uint64_t x = 0, y = 0;
 #pragma unroll
@@ -239,7 +240,7 @@ __global__ __launch_bounds__(256) void k_bsum_blocks(const iggy_batch_header *hp
             if (m < pl.Mreg) {
                 const uint64_t v = cs_word(m, h, src);
                 y += v;
-                x += mul32x32(v ^ kSecretW8[((m >> 3) & 15) + (m & 7)]);
+                x += mul32x32(v ^ sec[half]);
             }
         }
         x += __shfl_xor(x, 8); y += __shfl_xor(y, 8);
@@ -308,6 +309,7 @@ __global__ __launch_bounds__(256) void k_bsum_blocks_range(const iggy_batch_head
     const uint64_t wid = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     const uint64_t nwaves = ((uint64_t)gridDim.x * blockDim.x) >> 6;
     const uint64_t hi = b_hi < pl.nb + 1 ? b_hi : pl.nb + 1;
+    const uint64_t sec[2] = {block_word_secret(0, lane), block_word_secret(1, lane)};
     for (uint64_t b = b_lo + wid; b < hi; b += nwaves) {
         uint64_t x = 0, y = 0;
 #pragma unroll
@@ -316,7 +318,7 @@ __global__ __launch_bounds__(256) void k_bsum_blocks_range(const iggy_batch_head
             if (m < pl.Mreg) {
                 const uint64_t v = cs_word(m, h, src);
                 y += v;
-                x += mul32x32(v ^ kSecretW8[((m >> 3) & 15) + (m & 7)]);
+                x += mul32x32(v ^ sec[half]);
             }
         }
         x += __shfl_xor(x, 8); y += __shfl_xor(y, 8);
@@ -456,6 +458,7 @@ __global__ __launch_bounds__(256) void k_xxh3_big_blocks(const uint8_t *p, uint6
     const uint64_t Mreg = 8 * (16 * nb + ns);
     const uint64_t wid = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     const uint64_t nwaves = ((uint64_t)gridDim.x * blockDim.x) >> 6;
+    const uint64_t sec[2] = {block_word_secret(0, lane), block_word_secret(1, lane)};
     for (uint64_t b = wid; b <= nb; b += nwaves) {
         uint64_t x = 0, y = 0;
 #pragma unroll
@@ -464,7 +467,7 @@ __global__ __launch_bounds__(256) void k_xxh3_big_blocks(const uint8_t *p, uint6
             if (m < Mreg) {
                 const uint64_t v = ld64_any(p + 8 * m);
                 y += v;
-                x += mul32x32(v ^ kSecretW8[((m >> 3) & 15) + (m & 7)]);
+                x += mul32x32(v ^ sec[half]);
             }
         }
         x += __shfl_xor(x, 8); y += __shfl_xor(y, 8);

@@ -66,6 +66,37 @@ struct DevBuf {
     }
 };
 
+// Mapped, coherent pinned host memory that kernels read and write directly (small
+// tables in, results / positions / flags out): no copy operation on the stream.
+struct HostMap {
+    void *h = nullptr;
+    uint8_t *d = nullptr;  // the device's address of the same bytes
+    size_t cap = 0;
+    int ensure(size_t n) {
+        if (n <= cap) return 0;
+        release();
+        const size_t want = std::max<size_t>(n, 64 << 10);
+        if (hipHostMalloc(&h, want, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess) {
+            h = nullptr;
+            return IGGY_ERR_DEVICE;
+        }
+        if (hipHostGetDevicePointer((void **)&d, h, 0) != hipSuccess) {
+            release();
+            return IGGY_ERR_DEVICE;
+        }
+        cap = want;
+        return 0;
+    }
+    template <class T> T *hp(size_t off = 0) { return (T *)((uint8_t *)h + off); }
+    template <class T> T *dp(size_t off = 0) { return (T *)(d + off); }
+    void release() {
+        if (h) (void)hipHostFree(h);
+        h = nullptr;
+        d = nullptr;
+        cap = 0;
+    }
+};
+
 }  // namespace
 
 // one asynchronous host-buffer operation in flight (iggy_codec_*_submit / iggy_codec_poll)
@@ -130,9 +161,11 @@ struct iggy_codec_ctx {
     DevBuf cwk;  // disk-chunk walk: state, gates, per-batch slice results, fragments
     // multi-record decode (decode_records.hip): tasks | states | wg map, block sums,
     // results, and the pinned staging of the task table (uploaded in one copy)
-    DevBuf rtab, rbsums, rres, clinks;
-    void *rpin = nullptr, *cpin = nullptr;  // task table / chunk-walk candidates and results
-    size_t rpin_cap = 0, cpin_cap = 0;
+    DevBuf rtab, rbsums, rres, clinks, rstate, rcount;
+    HostMap rmap;  // task table + workgroup map (read by the kernel in place when small)
+    HostMap cmap;  // chunk-walk candidates (read in place)
+    HostMap omap;  // [0, 64): completion flag; then results / positions / chunk-walk outputs
+    uint32_t hseq = 0;  // completion flag values
     uint32_t chunk_epoch = 0;  // k_chunk_walk link tags
     // segment writer: pinned staging halves and their copy events
     void *wstage = nullptr;
@@ -366,9 +399,14 @@ int reset_after_timeout(iggy_codec_ctx *c) {
 }
 
 // synchronous decode of a host buffer; also used by stamp / checksum helpers
+constexpr uint64_t kHostFastBytes = 16ull << 20;
+int decode_host_fast(iggy_codec_ctx *c, const uint8_t *body, uint64_t len, int integrity,
+                     iggy_decode_result *res_out, uint64_t *frame_pos, uint64_t cap, bool *done);
 int decode_host(iggy_codec_ctx *c, const uint8_t *body, uint64_t len, int integrity,
                 iggy_decode_result *res_out, uint64_t *frame_pos, uint64_t cap, bool keep_on_device) {
-    int r = 0;
+    bool done = false;
+    int r = decode_host_fast(c, body, len, integrity, res_out, frame_pos, cap, &done);
+    if (r || done) return r;
     r |= c->din.ensure(len + 16);
     const uint64_t pcap = frame_pos ? std::min<uint64_t>(cap, len / 48 + 1) : 0;
     r |= c->dpos.ensure((pcap + 1) * 8);
@@ -435,12 +473,18 @@ uint64_t rec_plan(const uint8_t *h, uint64_t len, uint64_t *n_frames) {
 // Enqueue the decode of K records of the device buffer d_base (h_base: the host
 // copy of the same bytes) on the context's stream: one k_decode_records launch for
 // every planned record, then the single-record decode of the others (appended to
-// *single). d_res[k] receives record k's verdict; a record left with status
-// kStatusNeedGeneral (its stride breaks mid-record) is re-decoded by redo_general.
-// n_frames[k] (nullable) = the planned frame count (0 for single-path records).
+// *single). d_res[k] receives record k's verdict (device or host-mapped memory when
+// no record takes the single path); a record left with status kStatusNeedGeneral
+// (its stride breaks mid-record) is re-decoded by redo_general. host_flag (device
+// address of host-mapped memory, nullable): raised to flag_value when the launch is
+// complete. n_frames[k] (nullable) = the planned frame count (0 for single-path
+// records).
+constexpr uint64_t kRecZeroCopyWgs = 4096;  // larger launches upload their tables (H2D)
+
 int enqueue_records(iggy_codec_ctx *c, const uint8_t *d_base, const uint8_t *h_base, const RecIn *recs, size_t K,
                     int integrity, uint64_t *d_pos, iggy_polled_message *d_msgs, iggy_decode_result *d_res,
-                    std::vector<size_t> *single, std::vector<uint64_t> *n_frames = nullptr) {
+                    std::vector<size_t> *single, std::vector<uint64_t> *n_frames = nullptr,
+                    uint32_t *host_flag = nullptr, uint32_t flag_value = 0) {
     hipStream_t s = c->stream;
     std::vector<RecTask> tasks(K);
     std::vector<uint32_t> wgmap;
@@ -469,33 +513,39 @@ int enqueue_records(iggy_codec_ctx *c, const uint8_t *d_base, const uint8_t *h_b
     }
     const uint64_t W = wgmap.size();
     if (W) {
-        const size_t tb = K * sizeof(RecTask), sb = K * sizeof(RecState), wb = W * 4;
-        const size_t bytes = tb + sb + wb;
-        if (c->rpin_cap < bytes) {
-            if (c->rpin) (void)hipHostFree(c->rpin);
-            c->rpin = nullptr;
-            c->rpin_cap = 0;
-            const size_t want = std::max<size_t>(bytes, 64 << 10);
-            if (hipHostMalloc(&c->rpin, want, hipHostMallocDefault) != hipSuccess) return IGGY_ERR_DEVICE;
-            c->rpin_cap = want;
-        }
-        int r = c->rtab.ensure(bytes);
+        const size_t tb = K * sizeof(RecTask), wb = W * 4;
+        int r = c->rmap.ensure(tb + wb);
         r |= c->rbsums.ensure(nbs * 64 + 64);
+        const size_t st_before = c->rstate.cap;
+        r |= c->rstate.ensure(K * sizeof(RecState));
+        if (!c->rcount.p) {
+            r |= c->rcount.ensure(64);
+            if (!r) HIP_OK(hipMemsetAsync(c->rcount.p, 0, c->rcount.cap, s));
+        }
         if (r) return IGGY_ERR_DEVICE;
-        uint8_t *hp = (uint8_t *)c->rpin;
-        memcpy(hp, tasks.data(), tb);
-        memset(hp + tb, 0, sb);
-        memcpy(hp + tb + sb, wgmap.data(), wb);
-        HIP_OK(hipMemcpyAsync(c->rtab.p, hp, bytes, hipMemcpyHostToDevice, s));
-        const RecTask *dt = c->rtab.as<RecTask>();
-        RecState *ds = c->rtab.as<RecState>(tb);
-        const uint32_t *dw = c->rtab.as<uint32_t>(tb + sb);
+        if (c->rstate.cap != st_before)  // fresh state: zero (the resolvers keep it zero after)
+            HIP_OK(hipMemsetAsync(c->rstate.p, 0, c->rstate.cap, s));
+        memcpy(c->rmap.hp<uint8_t>(), tasks.data(), tb);
+        memcpy(c->rmap.hp<uint8_t>(tb), wgmap.data(), wb);
+        const RecTask *dt = c->rmap.dp<RecTask>();
+        const uint32_t *dw = c->rmap.dp<uint32_t>(tb);
+        if (W > kRecZeroCopyWgs) {  // a big launch: every workgroup would read its task over PCIe
+            r = c->rtab.ensure(tb + wb);
+            if (r) return IGGY_ERR_DEVICE;
+            HIP_OK(hipMemcpyAsync(c->rtab.p, c->rmap.h, tb + wb, hipMemcpyHostToDevice, s));
+            dt = c->rtab.as<RecTask>();
+            dw = c->rtab.as<uint32_t>(tb);
+        }
+        RecState *ds = c->rstate.as<RecState>();
+        uint32_t *flag = single->empty() ? host_flag : nullptr;
         if (integrity == IGGY_INTEGRITY_VERIFY)
             hipLaunchKernelGGL(k_decode_records<true>, dim3((uint32_t)W), dim3(kRecThreads), 0, s, d_base, dt, dw, ds,
-                               c->rbsums.as<uint64_t>(), d_pos, d_msgs, d_res);
+                               c->rbsums.as<uint64_t>(), d_pos, d_msgs, d_res, c->rcount.as<uint32_t>(), flag,
+                               flag_value);
         else
             hipLaunchKernelGGL(k_decode_records<false>, dim3((uint32_t)W), dim3(kRecThreads), 0, s, d_base, dt, dw,
-                               ds, c->rbsums.as<uint64_t>(), d_pos, d_msgs, d_res);
+                               ds, c->rbsums.as<uint64_t>(), d_pos, d_msgs, d_res, c->rcount.as<uint32_t>(), flag,
+                               flag_value);
         HIP_OK(hipGetLastError());
     }
     if (!single->empty()) {
@@ -510,11 +560,42 @@ int enqueue_records(iggy_codec_ctx *c, const uint8_t *d_base, const uint8_t *h_b
     return 0;
 }
 
-// After a sync: records the multi-record kernel left with status kStatusNeedGeneral
-// are decoded again by the single-record path (general walk); res (host) is
-// refreshed for them. Returns IGGY_ERR_TIMEOUT if a bug guard fired anywhere.
+// true when every record goes to the multi-record kernel (the launch can raise the
+// host flag: results straight into host-mapped memory, no copy, no stream sync)
+bool records_all_planned(const uint8_t *h_base, const RecIn *recs, size_t K) {
+    for (size_t k = 0; k < K; ++k) {
+        uint64_t nf;
+        if (!rec_plan(h_base + recs[k].off, recs[k].len, &nf)) return false;
+    }
+    return true;
+}
+
+// Wait for a kernel to raise the host-mapped completion flag (a spin: the host
+// round trip of a stream sync or a result copy is what small host-buffer calls pay
+// most for). If the stream drains without the flag, the launch failed.
+int wait_host_flag(iggy_codec_ctx *c, uint32_t v) {
+    volatile uint32_t *flag = c->omap.hp<volatile uint32_t>();
+    for (uint64_t i = 1;; ++i) {
+        if (__atomic_load_n(flag, __ATOMIC_ACQUIRE) == v) return 0;
+        if ((i & 1023) == 0) {
+            const hipError_t q = hipStreamQuery(c->stream);
+            if (q == hipSuccess) return __atomic_load_n(flag, __ATOMIC_ACQUIRE) == v ? 0 : IGGY_ERR_DEVICE;
+            if (q != hipErrorNotReady) return IGGY_ERR_DEVICE;
+        }
+        __builtin_ia32_pause();
+    }
+}
+uint32_t next_flag(iggy_codec_ctx *c) {
+    if (++c->hseq == 0) c->hseq = 1;
+    return c->hseq;
+}
+
+// After the launch: records the multi-record kernel left with status
+// kStatusNeedGeneral are decoded again by the single-record path (general walk, into
+// the device results buffer) and res (host) is refreshed for them. Returns
+// IGGY_ERR_TIMEOUT if a bug guard fired anywhere.
 int redo_general(iggy_codec_ctx *c, const uint8_t *d_base, const RecIn *recs, size_t K, int integrity,
-                 uint64_t *d_pos, iggy_decode_result *d_res, iggy_decode_result *res, std::vector<size_t> *redone) {
+                 uint64_t *d_pos, iggy_decode_result *res, std::vector<size_t> *redone) {
     std::vector<size_t> redo;
     uint64_t maxlen = 0;
     for (size_t k = 0; k < K; ++k) {
@@ -529,7 +610,9 @@ int redo_general(iggy_codec_ctx *c, const uint8_t *d_base, const RecIn *recs, si
     }
     if (redo.empty()) return 0;
     int r = ensure_decode_scratch(c, maxlen);
-    if (r) return r;
+    r |= c->rres.ensure(K * sizeof(iggy_decode_result));
+    if (r) return r ? r : IGGY_ERR_DEVICE;
+    iggy_decode_result *d_res = c->rres.as<iggy_decode_result>();
     for (size_t k : redo) {
         r = enqueue_decode(c, d_base + recs[k].off, recs[k].len, integrity, d_pos ? d_pos + recs[k].pos_base : nullptr,
                            d_pos ? recs[k].pos_cap : 0, d_res + k, c->stream);
@@ -543,6 +626,67 @@ int redo_general(iggy_codec_ctx *c, const uint8_t *d_base, const RecIn *recs, si
             return IGGY_ERR_TIMEOUT;
         }
     if (redone) *redone = redo;
+    return 0;
+}
+
+// Every record of the device buffer d_base decoded, the verdicts in res (host): one
+// launch; when every record is planned for the multi-record kernel its results land
+// in host-mapped memory and the host spins on the completion flag, otherwise device
+// results, one copy and a stream sync; then the general re-walks, if any.
+int decode_records_to_host(iggy_codec_ctx *c, const uint8_t *d_base, const uint8_t *h_base, const RecIn *recs,
+                           size_t K, int integrity, iggy_decode_result *res) {
+    std::vector<size_t> single;
+    const size_t rb = K * sizeof(iggy_decode_result);
+    if (records_all_planned(h_base, recs, K)) {
+        if (c->omap.ensure(64 + rb)) return IGGY_ERR_DEVICE;
+        const uint32_t v = next_flag(c);
+        int r = enqueue_records(c, d_base, h_base, recs, K, integrity, nullptr, nullptr,
+                                c->omap.dp<iggy_decode_result>(64), &single, nullptr, c->omap.dp<uint32_t>(), v);
+        if (r) return r;
+        r = wait_host_flag(c, v);
+        if (r) return r;
+        memcpy(res, c->omap.hp<uint8_t>(64), rb);
+    } else {
+        if (c->rres.ensure(rb)) return IGGY_ERR_DEVICE;
+        iggy_decode_result *d_res = c->rres.as<iggy_decode_result>();
+        int r = enqueue_records(c, d_base, h_base, recs, K, integrity, nullptr, nullptr, d_res, &single);
+        if (r) return r;
+        HIP_OK(hipMemcpyAsync(res, d_res, rb, hipMemcpyDeviceToHost, c->stream));
+        HIP_OK(hipStreamSynchronize(c->stream));
+    }
+    return redo_general(c, d_base, recs, K, integrity, nullptr, res, nullptr);
+}
+
+// A small single-stride record from host memory (iggy_codec_decode_batch and the
+// host entry points built on it): one H2D copy and ONE k_decode_records launch that
+// writes the verdict and the frame positions straight into host-mapped memory, the
+// host spinning on its completion flag -- two stream operations instead of the
+// persistent pair's five (H2D, two kernels, two copies back, a sync). *done = false
+// leaves the record to the persistent path (not single-stride, too large, or the
+// stride broke mid-record).
+int decode_host_fast(iggy_codec_ctx *c, const uint8_t *body, uint64_t len, int integrity,
+                     iggy_decode_result *res_out, uint64_t *frame_pos, uint64_t cap, bool *done) {
+    *done = false;
+    uint64_t nf = 0;
+    if (len > kHostFastBytes || !rec_plan(body, len, &nf)) return 0;
+    const uint64_t pcap = frame_pos ? std::min<uint64_t>(cap, len / 48 + 1) : 0;
+    if (c->din.ensure(len + 16) || c->omap.ensure(64 + 128 + pcap * 8)) return IGGY_ERR_DEVICE;
+    if (len) HIP_OK(hipMemcpyAsync(c->din.p, body, len, hipMemcpyHostToDevice, c->stream));
+    const RecIn rec{0, len, 0, pcap, 0};
+    std::vector<size_t> single;
+    const uint32_t v = next_flag(c);
+    int r = enqueue_records(c, c->din.as<uint8_t>(), body, &rec, 1, integrity,
+                            pcap ? c->omap.dp<uint64_t>(192) : nullptr, nullptr, c->omap.dp<iggy_decode_result>(64),
+                            &single, nullptr, c->omap.dp<uint32_t>(), v);
+    if (r) return r;
+    r = wait_host_flag(c, v);
+    if (r) return r;
+    const iggy_decode_result res = *c->omap.hp<iggy_decode_result>(64);
+    if (res.status == kStatusNeedGeneral) return 0;
+    *res_out = res;
+    if (frame_pos && pcap && res.error.kind == IGGY_OK)
+        memcpy(frame_pos, c->omap.hp<uint64_t>(192), std::min<uint64_t>(res.frame_count, pcap) * 8);
+    *done = true;
     return 0;
 }
 
@@ -642,7 +786,7 @@ void iggy_codec_destroy(iggy_codec_ctx *c) {
                       &c->gbsums, &c->dresult, &c->din, &c->dpos, &c->dout, &c->epl, &c->euh,
                       &c->etile, &c->ecs, &c->emisc, &c->eids, &c->eots, &c->epay, &c->eplen,
                       &c->euhb, &c->euhl, &c->hbsums, &c->ppos, &c->pmsgs, &c->pres, &c->cwk, &c->sl, &c->slres, &c->cr,
-                      &c->rtab, &c->rbsums, &c->rres, &c->clinks};
+                      &c->rtab, &c->rbsums, &c->rres, &c->clinks, &c->rstate, &c->rcount};
     for (DevBuf *b : bufs) b->release();
     if (c->h_pinned) (void)hipHostFree(c->h_pinned);
     for (int w = 0; w < 2; ++w) {
@@ -653,8 +797,9 @@ void iggy_codec_destroy(iggy_codec_ctx *c) {
         if (ev) (void)hipEventDestroy(ev);
     if (c->order_ev) (void)hipEventDestroy(c->order_ev);
     if (c->wstage) (void)hipHostFree(c->wstage);
-    if (c->rpin) (void)hipHostFree(c->rpin);
-    if (c->cpin) (void)hipHostFree(c->cpin);
+    c->rmap.release();
+    c->cmap.release();
+    c->omap.release();
     if (c->cr_pinned) {  // GHASH tables of the key: cleared before the pages go back
         volatile uint8_t *z = (volatile uint8_t *)c->cr_pinned;
         for (size_t i = 0; i < kCrTabBytesHost; ++i) z[i] = 0;
@@ -1005,19 +1150,11 @@ int iggy_codec_decode_records(iggy_codec_ctx *c, const uint8_t *buf, uint64_t le
     if (!nrec) return 0;
     DevGuard dg(c->device);
     bind(c, nullptr);
-    int r = c->din.ensure(len + 16);
-    r |= c->rres.ensure(nrec * sizeof(iggy_decode_result));
-    if (r) return IGGY_ERR_DEVICE;
+    if (c->din.ensure(len + 16)) return IGGY_ERR_DEVICE;
     if (len) HIP_OK(hipMemcpyAsync(c->din.p, buf, len, hipMemcpyHostToDevice, c->stream));
     std::vector<RecIn> recs(nrec);
     for (uint64_t k = 0; k < nrec; ++k) recs[k] = RecIn{offsets[k], len - offsets[k], 0, 0, 0};
-    iggy_decode_result *d_res = c->rres.as<iggy_decode_result>();
-    std::vector<size_t> single;
-    r = enqueue_records(c, c->din.as<uint8_t>(), buf, recs.data(), nrec, integrity, nullptr, nullptr, d_res, &single);
-    if (r) return r;
-    HIP_OK(hipMemcpyAsync(out, d_res, nrec * sizeof(iggy_decode_result), hipMemcpyDeviceToHost, c->stream));
-    HIP_OK(hipStreamSynchronize(c->stream));
-    return redo_general(c, c->din.as<uint8_t>(), recs.data(), nrec, integrity, nullptr, d_res, out, nullptr);
+    return decode_records_to_host(c, c->din.as<uint8_t>(), buf, recs.data(), nrec, integrity, out);
 }
 
 // recover_segment_bounds' index-less walk (core/partitions/src/segment_recovery.rs:425-530).
@@ -1052,23 +1189,14 @@ int iggy_codec_recover_segment(iggy_codec_ctx *c, const uint8_t *messages, uint6
         // (the single-record decode for the rest), one sync
         const uint64_t span = cand.back().pos + cand.back().h.batch_length;
         const size_t K = cand.size();
-        int r = c->din.ensure(span + 16);
-        r |= c->rres.ensure(K * sizeof(iggy_decode_result));
-        if (r) return IGGY_ERR_DEVICE;
+        if (c->din.ensure(span + 16)) return IGGY_ERR_DEVICE;
         (void)maxlen;
         HIP_OK(hipMemcpyAsync(c->din.p, messages, span, hipMemcpyHostToDevice, c->stream));
         std::vector<RecIn> recs(K);
         for (size_t k = 0; k < K; ++k) recs[k] = RecIn{cand[k].pos, cand[k].h.batch_length, 0, 0, 0};
-        iggy_decode_result *d_res = c->rres.as<iggy_decode_result>();
-        std::vector<size_t> single;
-        r = enqueue_records(c, c->din.as<uint8_t>(), messages, recs.data(), K, IGGY_INTEGRITY_VERIFY, nullptr, nullptr,
-                            d_res, &single);
-        if (r) return r;
         std::vector<iggy_decode_result> res(K);
-        HIP_OK(hipMemcpyAsync(res.data(), d_res, K * sizeof(iggy_decode_result), hipMemcpyDeviceToHost, c->stream));
-        HIP_OK(hipStreamSynchronize(c->stream));
-        r = redo_general(c, c->din.as<uint8_t>(), recs.data(), K, IGGY_INTEGRITY_VERIFY, nullptr, d_res, res.data(),
-                         nullptr);
+        int r = decode_records_to_host(c, c->din.as<uint8_t>(), messages, recs.data(), K, IGGY_INTEGRITY_VERIFY,
+                                       res.data());
         if (r) return r;
         for (; accepted < K; ++accepted)
             if (res[accepted].error.kind != IGGY_OK) break;
@@ -1120,22 +1248,13 @@ int iggy_codec_walk_segment_payload(iggy_codec_ctx *c, const uint8_t *bytes, uin
         // one copy, every batch in one multi-record launch (single-record decode for the
         // rest), one sync
         const size_t K = cand.size();
-        int r = c->din.ensure(len + 16);
-        r |= c->rres.ensure(K * sizeof(iggy_decode_result));
-        if (r) return IGGY_ERR_DEVICE;
+        if (c->din.ensure(len + 16)) return IGGY_ERR_DEVICE;
         (void)maxlen;
         HIP_OK(hipMemcpyAsync(c->din.p, bytes, len, hipMemcpyHostToDevice, c->stream));
         std::vector<RecIn> recs(K);
         for (size_t k = 0; k < K; ++k) recs[k] = RecIn{cand[k].pos, len - cand[k].pos, 0, 0, 0};
-        iggy_decode_result *d_res = c->rres.as<iggy_decode_result>();
-        std::vector<size_t> single;
-        r = enqueue_records(c, c->din.as<uint8_t>(), bytes, recs.data(), K, IGGY_INTEGRITY_VERIFY, nullptr, nullptr,
-                            d_res, &single);
-        if (r) return r;
-        HIP_OK(hipMemcpyAsync(res.data(), d_res, K * sizeof(iggy_decode_result), hipMemcpyDeviceToHost, c->stream));
-        HIP_OK(hipStreamSynchronize(c->stream));
-        r = redo_general(c, c->din.as<uint8_t>(), recs.data(), K, IGGY_INTEGRITY_VERIFY, nullptr, d_res, res.data(),
-                         nullptr);
+        int r = decode_records_to_host(c, c->din.as<uint8_t>(), bytes, recs.data(), K, IGGY_INTEGRITY_VERIFY,
+                                       res.data());
         if (r) return r;
     }
     uint64_t next_offset = base_offset, indexed = 0, nidx = 0;
@@ -1559,7 +1678,7 @@ int iggy_codec_poll_decode(iggy_codec_ctx *c, const uint8_t *buf, uint64_t len, 
     std::vector<iggy_decode_result> res(K);
     if (K) HIP_OK(hipMemcpyAsync(res.data(), d_res, K * sizeof(iggy_decode_result), hipMemcpyDeviceToHost, c->stream));
     HIP_OK(hipStreamSynchronize(c->stream));
-    r = redo_general(c, c->din.as<uint8_t>(), rin.data(), K, IGGY_INTEGRITY_LAYOUT_ONLY, c->ppos.as<uint64_t>(), d_res,
+    r = redo_general(c, c->din.as<uint8_t>(), rin.data(), K, IGGY_INTEGRITY_LAYOUT_ONLY, c->ppos.as<uint64_t>(),
                      res.data(), &redone);
     if (r) {
         if (r == IGGY_ERR_TIMEOUT) set_err(err, IGGY_ERR_TIMEOUT);
@@ -2026,29 +2145,22 @@ int iggy_codec_walk_disk_chunk(iggy_codec_ctx *c, const uint8_t *chunk, uint64_t
     if (!one_launch) return walk_chunk_per_batch(c, chunk, len, q, integrity, frags, headers, cap, out);
     // One copy of the chunk, ONE multi-record decode launch, ONE k_chunk_walk launch
     // (one workgroup per batch: gate, selection, partial checksum, fragment push, the
-    // match count handed batch to batch), one copy back, one sync.
+    // match count handed batch to batch). The tables are read and the outputs written
+    // by the kernels in host-mapped memory; the host spins on the completion flag.
     const uint64_t capk = std::min<uint64_t>(cap, K);  // at most one fragment per batch
     const size_t res_bytes = 256 + capk * (sizeof(iggy_chunk_fragment) + 256);
     const size_t cand_bytes = K * sizeof(ChunkCand), link_bytes = K * sizeof(ChunkLink);
     int r = c->din.ensure(len + 16);
     r |= c->dpos.ensure((pwords + 1) * 8);
     r |= c->pres.ensure((K + 1) * sizeof(iggy_decode_result));
-    r |= c->cwk.ensure(res_bytes + cand_bytes + 64);
     r |= c->sl.ensure(nbb * 64 + 64);
+    r |= c->cmap.ensure(cand_bytes);
+    r |= c->omap.ensure(64 + res_bytes);
     // the links live in a buffer of their own that only ever holds links: a stale one
     // carries an older epoch, never the current one (zeroed whenever it is new)
     const size_t links_cap_before = c->clinks.cap;
     r |= c->clinks.ensure(link_bytes);
     if (r) return IGGY_ERR_DEVICE;
-    const size_t pin_need = ((cand_bytes + 255) & ~(size_t)255) + res_bytes;
-    if (c->cpin_cap < pin_need) {
-        if (c->cpin) (void)hipHostFree(c->cpin);
-        c->cpin = nullptr;
-        c->cpin_cap = 0;
-        const size_t want = std::max<size_t>(pin_need, 64 << 10);
-        if (hipHostMalloc(&c->cpin, want, hipHostMallocDefault) != hipSuccess) return IGGY_ERR_DEVICE;
-        c->cpin_cap = want;
-    }
     hipStream_t s = c->stream;
     HIP_OK(hipMemcpyAsync(c->din.p, chunk, len, hipMemcpyHostToDevice, s));
     std::vector<RecIn> rin(K);
@@ -2059,26 +2171,24 @@ int iggy_codec_walk_disk_chunk(iggy_codec_ctx *c, const uint8_t *chunk, uint64_t
     r = enqueue_records(c, c->din.as<uint8_t>(), chunk, rin.data(), K, integrity, c->dpos.as<uint64_t>(), nullptr,
                         d_res, &single);
     if (r) return r;
-    uint8_t *pin = (uint8_t *)c->cpin;
-    uint8_t *pin_res = pin + ((cand_bytes + 255) & ~(size_t)255);
-    memcpy(pin, cand.data(), cand_bytes);
-    ChunkState *d_state = c->cwk.as<ChunkState>(0);
-    iggy_chunk_fragment *d_frags = c->cwk.as<iggy_chunk_fragment>(256);
-    uint8_t *d_hdrs = c->cwk.as<uint8_t>(256 + capk * sizeof(iggy_chunk_fragment));
+    memcpy(c->cmap.h, cand.data(), cand_bytes);
+    uint8_t *pin_res = c->omap.hp<uint8_t>(64);
+    ChunkState *d_state = c->omap.dp<ChunkState>(64);
+    iggy_chunk_fragment *d_frags = c->omap.dp<iggy_chunk_fragment>(64 + 256);
+    uint8_t *d_hdrs = c->omap.dp<uint8_t>(64 + 256 + capk * sizeof(iggy_chunk_fragment));
     ChunkLink *d_links = c->clinks.as<ChunkLink>();
-    ChunkCand *d_cand = c->cwk.as<ChunkCand>(res_bytes);
-    HIP_OK(hipMemcpyAsync(d_cand, pin, cand_bytes, hipMemcpyHostToDevice, s));
     if (++c->chunk_epoch == 0 || c->clinks.cap != links_cap_before) {  // new buffer or wrapped tags
         if (c->chunk_epoch == 0) c->chunk_epoch = 1;
         HIP_OK(hipMemsetAsync(c->clinks.p, 0, c->clinks.cap, s));
     }
+    const uint32_t v = next_flag(c);
     hipLaunchKernelGGL(k_chunk_walk, dim3((uint32_t)K), dim3(kChunkThreads), 0, s, (const uint8_t *)c->din.p,
-                       (const ChunkCand *)d_cand, (uint32_t)K, (const iggy_decode_result *)d_res,
+                       c->cmap.dp<const ChunkCand>(), (uint32_t)K, (const iggy_decode_result *)d_res,
                        (const uint64_t *)c->dpos.as<uint64_t>(), *q, c->chunk_epoch, d_links, d_state, d_frags,
-                       headers ? d_hdrs : nullptr, capk, c->sl.as<uint64_t>());
+                       headers ? d_hdrs : nullptr, capk, c->sl.as<uint64_t>(), c->omap.dp<uint32_t>(), v);
     HIP_OK(hipGetLastError());
-    HIP_OK(hipMemcpyAsync(pin_res, c->cwk.p, res_bytes, hipMemcpyDeviceToHost, s));
-    HIP_OK(hipStreamSynchronize(s));
+    r = wait_host_flag(c, v);
+    if (r) return r;
     ChunkState hs;
     memcpy(&hs, pin_res, sizeof(hs));
     if (hs.error.kind == IGGY_ERR_PENDING)  // a batch needs the general walk: the per-batch form

@@ -1002,6 +1002,7 @@ __global__ __launch_bounds__(kGenThreads) void k_decode_general(const uint8_t *_
         nb = (n - 1) / 1024;
         const uint64_t ns = ((n - 1) - 1024 * nb) / 64;
         Mreg = 8 * (16 * nb + ns);
+        const uint64_t sec[2] = {block_word_secret(0, lane), block_word_secret(1, lane)};
         for (uint64_t b = wid; b <= nb; b += nwaves) {
             uint64_t x = 0, y = 0;
             for (int half = 0; half < 2; ++half) {
@@ -1016,10 +1017,8 @@ __global__ __launch_bounds__(kGenThreads) void k_decode_general(const uint8_t *_
                     } else {
                         v = (gs.cs[mw - 6] >> 32) | (gs.cs[mw - 5] << 32);
                     }
-                    uint64_t xx, yy;
-                    word_contrib(mw, v, xx, yy);
-                    x += xx;
-                    y += yy;
+                    y += v;
+                    x += mul32x32(v ^ sec[half]);
                 }
             }
             x += __shfl_xor(x, 8); y += __shfl_xor(y, 8);

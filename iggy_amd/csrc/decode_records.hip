@@ -37,7 +37,7 @@ struct RecTask {
     uint64_t bsum_base;           // block sums of this record: bsums[8 * (bsum_base + b) + j]
     uint32_t wg0, nwg;            // its workgroups in the grid
 };
-struct RecState {  // zeroed by the host before the launch
+struct RecState {  // zero between launches: zeroed when allocated, reset by the record's resolver
     uint64_t first_bad;  // ~min index of a frame whose checksum mismatches (max-encoded), 0 = none
     uint64_t spec_fail;  // ~min index of a frame that breaks the stride
     uint32_t done;       // block workgroups finished
@@ -82,13 +82,29 @@ __device__ __forceinline__ uint64_t wg_min(uint64_t v, uint64_t *s4) {
     return m;
 }
 
+// Launch completion for host callers that spin instead of synchronising the stream:
+// every workgroup arrives on a device counter once its writes are fenced at system
+// scope; the last one re-arms the counter and stores `value` into the host-mapped
+// flag (a plain launch boundary would otherwise need a stream sync, ~3 us more, or
+// a D2H copy of the results, ~5 us more; scripts/latency_micro.cpp).
+__device__ __forceinline__ void launch_done(uint32_t *counter, uint32_t *host_flag, uint32_t value) {
+    if (!host_flag) return;
+    __threadfence_system();  // every wave: its own host-visible writes (a fence orders only its wave's)
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        if (atomicAdd(counter, 1u) == gridDim.x - 1) {
+            __hip_atomic_store(counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __threadfence_system();
+            __hip_atomic_store(host_flag, value, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+    }
+}
+
 template <bool VERIFY>
-__global__ __launch_bounds__(kRecThreads) void k_decode_records(const uint8_t *__restrict__ base,
-                                                                const RecTask *__restrict__ tasks,
-                                                                const uint32_t *__restrict__ wg_task,
-                                                                RecState *st, uint64_t *bsums, uint64_t *frame_pos,
-                                                                iggy_polled_message *msgs,
-                                                                iggy_decode_result *results) {
+__device__ __forceinline__ void decode_record_block(const uint8_t *__restrict__ base, const RecTask *__restrict__ tasks,
+                                                    const uint32_t *__restrict__ wg_task, RecState *st,
+                                                    uint64_t *bsums, uint64_t *frame_pos, iggy_polled_message *msgs,
+                                                    iggy_decode_result *results) {
     __shared__ uint64_t s_cs[kRecFrames + 2];  // stored checksums of frames 128b - 6 + k
     __shared__ uint64_t s_min[4];
     __shared__ uint32_t s_last;
@@ -242,8 +258,9 @@ __global__ __launch_bounds__(kRecThreads) void k_decode_records(const uint8_t *_
         // words m = 128b + j of the checksum input, j = lane, lane + 64
         const uint64_t mb = (uint64_t)kRecFrames * blk;
         uint64_t x = 0, y = 0;
-        word_contrib(pl.Mreg, mb + lane, s_cs[lane], s_cs[lane + 1], true, x, y);
-        word_contrib(pl.Mreg, mb + 64 + lane, s_cs[64 + lane], s_cs[65 + lane], true, x, y);
+        word_contrib_s(pl.Mreg, mb + lane, s_cs[lane], s_cs[lane + 1], true, kSecretW8[(lane >> 3) + (lane & 7)], x, y);
+        word_contrib_s(pl.Mreg, mb + 64 + lane, s_cs[64 + lane], s_cs[65 + lane], true,
+                       kSecretW8[8 + (lane >> 3) + (lane & 7)], x, y);
         const uint64_t t8 = reduce_acc8(x, y);
         if (lane < 8) bsums[8 * (tk.bsum_base + blk) + lane] = t8;
     }
@@ -314,6 +331,10 @@ __global__ __launch_bounds__(kRecThreads) void k_decode_records(const uint8_t *_
     // precedence, as the uniform kernel's consumer (batch.rs:395-421, 461-506)
     const uint64_t fb_enc = __hip_atomic_load(&st[t].first_bad, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const uint64_t sf_enc = __hip_atomic_load(&st[t].spec_fail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // every block workgroup of the record has arrived: re-arm its state for the next launch
+    __hip_atomic_store(&st[t].first_bad, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(&st[t].spec_fail, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(&st[t].done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const bool has_fb = fb_enc != 0, has_sf = sf_enc != 0;
     const uint64_t fbi = ~fb_enc, sf = ~sf_enc;
     uint32_t kind = IGGY_OK, reason = 0, status = kStatusDone;
@@ -348,11 +369,27 @@ __global__ __launch_bounds__(kRecThreads) void k_decode_records(const uint8_t *_
     write_result(res, hi, kind, reason, a, b, c, nframes, computed, 1, status, nframes * S);
 }
 
+// tasks / wg_task may live in host-mapped pinned memory (read once per workgroup);
+// results and frame_pos may too (plain stores); st, bsums and counter are device memory.
+template <bool VERIFY>
+__global__ __launch_bounds__(kRecThreads) void k_decode_records(const uint8_t *__restrict__ base,
+                                                                const RecTask *__restrict__ tasks,
+                                                                const uint32_t *__restrict__ wg_task,
+                                                                RecState *st, uint64_t *bsums, uint64_t *frame_pos,
+                                                                iggy_polled_message *msgs,
+                                                                iggy_decode_result *results, uint32_t *counter,
+                                                                uint32_t *host_flag, uint32_t flag_value) {
+    decode_record_block<VERIFY>(base, tasks, wg_task, st, bsums, frame_pos, msgs, results);
+    launch_done(counter, host_flag, flag_value);
+}
+
 template __global__ void k_decode_records<true>(const uint8_t *__restrict__, const RecTask *__restrict__,
                                                 const uint32_t *__restrict__, RecState *, uint64_t *, uint64_t *,
-                                                iggy_polled_message *, iggy_decode_result *);
+                                                iggy_polled_message *, iggy_decode_result *, uint32_t *, uint32_t *,
+                                                uint32_t);
 template __global__ void k_decode_records<false>(const uint8_t *__restrict__, const RecTask *__restrict__,
                                                  const uint32_t *__restrict__, RecState *, uint64_t *, uint64_t *,
-                                                 iggy_polled_message *, iggy_decode_result *);
+                                                 iggy_polled_message *, iggy_decode_result *, uint32_t *, uint32_t *,
+                                                 uint32_t);
 
 }  // namespace iggy

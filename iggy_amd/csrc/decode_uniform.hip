@@ -415,6 +415,15 @@ __device__ __forceinline__ void word_contrib(uint64_t Mreg, uint64_t m, uint64_t
         x += mul32x32(v ^ kSecretW8[((m >> 3) & 15) + (m & 7)]);
     }
 }
+// the same with the word's secret already in a register
+__device__ __forceinline__ void word_contrib_s(uint64_t Mreg, uint64_t m, uint64_t cur, uint64_t nxt, bool use,
+                                               uint64_t sec, uint64_t &x, uint64_t &y) {
+    if (use && m >= 6 && m < Mreg) {
+        const uint64_t v = (cur >> 32) | (nxt << 32);
+        y += v;
+        x += mul32x32(v ^ sec);
+    }
+}
 // lanes hold words with m & 7 == lane & 7: returns acc[j] on lanes j < 8
 __device__ __forceinline__ uint64_t reduce_acc8(uint64_t x, uint64_t y) {
     x += __shfl_xor(x, 8); y += __shfl_xor(y, 8);
@@ -450,7 +459,10 @@ __device__ __forceinline__ void produce(const uint8_t *blob, const UPlan &pl, ui
     const uint32_t ring = wave * kWaveRing;
     uint8_t *side = smem + kSideOff + wave * 64 * kSideLane + (uint32_t)lane * kSideLane;
     const uint32_t tid = wave * 64 + (uint32_t)lane;
+    // secret words of this wave's checksum words m = 256 c + 64 wave + lane (any chunk
+    // c) and of its joining word m = 256 c + 64 wave + 63: wave and lane only
     const uint64_t cs_sec = kSecretW8[((tid >> 3) & 15) + (tid & 7)];
+    const uint64_t join_sec = kSecretW8[((8 * wave + 7) & 15) + 7];
 
     // flat stream of steps (chunk, phase) issued DEPTH ahead of the compute side
     uint64_t ic = g;
@@ -534,7 +546,7 @@ __device__ __forceinline__ void produce(const uint8_t *blob, const UPlan &pl, ui
             // wave's is the block's last word, added by the gatherer)
             const uint64_t m = (uint64_t)(i + 6);
             uint64_t x = 0, y = 0;
-            word_contrib(pl.Mreg, m, stored, __shfl_down(stored, 1), lane < 63, x, y);
+            word_contrib_s(pl.Mreg, m, stored, __shfl_down(stored, 1), lane < 63, cs_sec, x, y);
             uint64_t t8 = reduce_acc8(x, y);
             const uint32_t first_lo = (uint32_t)__shfl(stored, 0);
             const uint32_t last_hi = (uint32_t)(__shfl(stored, 63) >> 32);
@@ -562,7 +574,7 @@ __device__ __forceinline__ void produce(const uint8_t *blob, const UPlan &pl, ui
                 if (lane == 0) __hip_atomic_store(taken, it + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                 // the word joining the halves: hi32 of this wave's last frame, lo32 of the odd wave's first
                 uint64_t bx = 0, by = 0;
-                word_contrib(pl.Mreg, m - lane + 63, (uint64_t)last_hi << 32, pfl, true, bx, by);
+                word_contrib_s(pl.Mreg, m - lane + 63, (uint64_t)last_hi << 32, pfl, true, join_sec, bx, by);
                 t8 += pt8 + (lane == 7 ? bx : 0) + (lane == 6 ? by : 0);
                 if (ok) publish_block(sc, epoch, 2 * c + k, lane, t8, first_lo, (uint32_t)(pfl >> 32));
             }
@@ -817,6 +829,13 @@ __device__ __forceinline__ void lg_deposit(uint8_t *smem, const LgLane &c, uint6
 __device__ __forceinline__ void lg_publisher(uint8_t *smem, const LgPlan &pl, const DecodeScratch &sc,
                                              uint32_t epoch, uint32_t g, uint32_t np, int lane, uint32_t dbg) {
     const uint64_t t_start = rt_now();
+    // the secret word of checksum word m = 128b + lane (and + 64) depends on the lane
+    // only: (m >> 3) & 15 = lane >> 3 (+ 8), m & 7 = lane & 7. Loaded once here: a
+    // runtime-indexed table read per block is a vector-memory load that waits behind
+    // the producers' whole read stream, and a publisher that falls behind stalls the
+    // producers on the unit slots.
+    const uint64_t sec_lo = kSecretW8[(lane >> 3) + (lane & 7)];
+    const uint64_t sec_hi = kSecretW8[8 + (lane >> 3) + (lane & 7)];
     const uint64_t blocks = 2 * pl.nchunks;
     if (g >= blocks) return;
     const uint64_t mine = (blocks - g + np - 1) / np;
@@ -845,8 +864,8 @@ __device__ __forceinline__ void lg_publisher(uint8_t *smem, const LgPlan &pl, co
         if (!pl.long_cs || pl.nopub) continue;
         const uint64_t b = g + jb * np;
         uint64_t x = 0, y = 0;
-        word_contrib(pl.Mreg, 128 * b + lane, c0, n0, true, x, y);
-        word_contrib(pl.Mreg, 128 * b + 64 + lane, c1, n1, lane < 63, x, y);
+        word_contrib_s(pl.Mreg, 128 * b + lane, c0, n0, true, sec_lo, x, y);
+        word_contrib_s(pl.Mreg, 128 * b + 64 + lane, c1, n1, lane < 63, sec_hi, x, y);
         publish_block(sc, epoch, b, lane, reduce_acc8(x, y), first_lo, last_hi);
         if ((dbg & 512) && b < 2 && lane == 0) ((uint64_t *)(sc.small + 256))[11 + b] = rt_now();
     }

@@ -697,6 +697,7 @@ __global__ __launch_bounds__(256) void k_enc_tail_small(iggy_raw_messages m, Enc
     const CsPlan pl = cs_plan(N);
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     if (pl.long_cs) {
+        const uint64_t sec[2] = {block_word_secret(0, lane), block_word_secret(1, lane)};
         for (uint64_t b = wave; b <= pl.nb; b += 4) {  // as k_bsum_blocks
             uint64_t x = 0, y = 0;
 #pragma unroll
@@ -705,7 +706,7 @@ __global__ __launch_bounds__(256) void k_enc_tail_small(iggy_raw_messages m, Enc
                 if (mw < pl.Mreg) {
                     const uint64_t v = cs_word(mw, h, src);
                     y += v;
-                    x += mul32x32(v ^ kSecretW8[((mw >> 3) & 15) + (mw & 7)]);
+                    x += mul32x32(v ^ sec[half]);
                 }
             }
             x += __shfl_xor(x, 8); y += __shfl_xor(y, 8);

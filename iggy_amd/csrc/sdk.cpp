@@ -10,7 +10,12 @@
 //   core/binary_protocol/src/requests/messages/send_messages.rs:65-241
 //   core/common/src/types/message/polled_messages.rs:53-90
 //   core/sdk/src/clients/producer_sharding.rs:91-293, producer.rs:406-470
+//   core/message_bus/src/framing.rs:107-171 (socket framing)
+//   core/server_common/src/send_messages.rs:459-540 (convert_request_message)
 #include <hip/hip_runtime.h>
+
+#include <errno.h>
+#include <unistd.h>
 
 #include <algorithm>
 #include <cstdint>
@@ -613,6 +618,126 @@ int iggy_producer_flush(iggy_producer *p, uint8_t *out, uint64_t cap, iggy_produ
     }
     if (nreqs) *nreqs = sendable.size();
     drop_flushed(p, N);
+    return 0;
+}
+
+
+// ---------------------------------------------------------- server socket side
+// read_exact on a blocking stream socket (compio's read_exact: EOF before the
+// requested bytes -> UnexpectedEof)
+static int read_exact_fd(int fd, uint8_t *p, uint64_t n) {
+    uint64_t got = 0;
+    while (got < n) {
+        const ssize_t r = read(fd, p + got, n - got);
+        if (r > 0) {
+            got += (uint64_t)r;
+            continue;
+        }
+        if (r == 0) return IGGY_ERR_CONNECTION_CLOSED;  // framing.rs:165-171 to_read_error
+        if (errno == EINTR) continue;
+        return IGGY_ERR_TCP_ERROR;
+    }
+    return 0;
+}
+
+int iggy_frame_read(int fd, uint8_t *buf, uint64_t cap, uint64_t max_message_size, uint64_t *total_size,
+                    iggy_wire_error *err) {
+    if (fd < 0 || !buf || !total_size) return IGGY_ERR_INVALID_ARGUMENT;
+    seterr(err, IGGY_OK);
+    *total_size = 0;
+    if (cap < IGGY_FRAME_HEADER_BYTES) {
+        seterr(err, IGGY_ERR_CAPACITY, 0, IGGY_FRAME_HEADER_BYTES);
+        return IGGY_ERR_CAPACITY;
+    }
+    // stage 1: the fixed header (framing.rs:114-116)
+    int r = read_exact_fd(fd, buf, IGGY_FRAME_HEADER_BYTES);
+    if (r) {
+        seterr(err, (uint32_t)r);
+        return r;
+    }
+    uint32_t size;  // read_size_field (consensus/header.rs:73-78)
+    memcpy(&size, buf + IGGY_FRAME_SIZE_OFFSET, 4);
+    if (size < IGGY_FRAME_HEADER_BYTES || size > max_message_size) {  // framing.rs:120-122
+        seterr(err, IGGY_ERR_INVALID_COMMAND);
+        return IGGY_ERR_INVALID_COMMAND;
+    }
+    if (size > cap) {  // the reference grows its Owned buffer in place; ours is the caller's
+        seterr(err, IGGY_ERR_CAPACITY, 0, size, cap);
+        return IGGY_ERR_CAPACITY;
+    }
+    // stage 2: the body into the tail of the same buffer (framing.rs:128-160)
+    if (size > IGGY_FRAME_HEADER_BYTES) {
+        r = read_exact_fd(fd, buf + IGGY_FRAME_HEADER_BYTES, size - IGGY_FRAME_HEADER_BYTES);
+        if (r) {
+            seterr(err, (uint32_t)r);
+            return r;
+        }
+    }
+    *total_size = size;
+    return 0;
+}
+
+int iggy_codec_convert_request(iggy_codec_ctx *ctx, const uint8_t *frame, uint64_t len, uint64_t partition_id,
+                               int checksum_mode, uint8_t *out, uint64_t cap, uint64_t *out_len,
+                               iggy_batch_header *hdr_out, iggy_wire_error *err) {
+    if (!ctx || !frame || !out || !out_len) return IGGY_ERR_INVALID_ARGUMENT;
+    seterr(err, IGGY_OK);
+    *out_len = 0;
+    const uint64_t hs = IGGY_FRAME_HEADER_BYTES;
+    auto invalid = [&]() {
+        seterr(err, IGGY_ERR_INVALID_COMMAND);
+        return IGGY_ERR_INVALID_COMMAND;
+    };
+    if (len < hs) return invalid();
+    uint32_t total;
+    memcpy(&total, frame + IGGY_FRAME_SIZE_OFFSET, 4);
+    if (total < hs || total > len) return invalid();  // a Message's size never exceeds its buffer
+    const uint8_t *body = frame + hs;
+    const uint64_t blen = total - hs;
+    // 1. a body that already IS one canonical batch (send_messages.rs:466-476): the
+    //    checksum-verified decode decides; any failure falls through to the wire form
+    iggy_batch_header h;
+    iggy_wire_error e;
+    if (iggy_batch_header_decode(body, blen, &h, &e) == 0 && h.batch_length <= blen &&
+        iggy_codec_decode_batch(ctx, body, blen, IGGY_INTEGRITY_VERIFY, &h, nullptr, 0, nullptr, &e) == 0) {
+        if (h.message_count == 0 || blen != h.batch_length || h.partition_id != partition_id) return invalid();
+        if (cap < total) {
+            seterr(err, IGGY_ERR_CAPACITY, 0, total, cap);
+            return IGGY_ERR_CAPACITY;
+        }
+        if (out != frame) memcpy(out, frame, total);
+        *out_len = total;
+        if (hdr_out) *hdr_out = h;
+        return 0;
+    }
+    // 2. admit_wire_request (send_messages.rs:480-540)
+    if (blen < 4) return invalid();
+    uint32_t mlen;
+    memcpy(&mlen, body, 4);
+    const uint64_t batch_start = 4 + (uint64_t)mlen;
+    if (blen < batch_start) return invalid();
+    iggy_send_messages_header meta;
+    uint64_t consumed = 0;
+    if (iggy_send_messages_header_decode(body + 4, mlen, &meta, &consumed, &e) != 0 || consumed != mlen)
+        return invalid();
+    const uint8_t *batch = body + batch_start;
+    const uint64_t batch_len = blen - batch_start;
+    if (cap < hs) {
+        seterr(err, IGGY_ERR_CAPACITY, 0, hs + batch_len, cap);
+        return IGGY_ERR_CAPACITY;
+    }
+    iggy_batch_header ah;
+    const int r = iggy_codec_admit_batch(ctx, batch, batch_len, meta.messages_count, partition_id, checksum_mode,
+                                         out + hs, cap - hs, &ah, err);
+    if (r) return r;
+    // the request header with the pipeline form's size (:523-528)
+    memcpy(out, frame, hs);
+    const uint64_t new_total = hs + ah.batch_length;
+    if (new_total > 0xFFFFFFFFull) return invalid();
+    const uint32_t nt = (uint32_t)new_total;
+    memcpy(out + IGGY_FRAME_SIZE_OFFSET, &nt, 4);
+    *out_len = new_total;
+    if (hdr_out) *hdr_out = ah;
     return 0;
 }
 

@@ -354,6 +354,9 @@ struct ChunkLink {
     uint32_t _pad[7];
 };
 constexpr uint32_t kChunkThreads = 256;
+// Host callers may pass cands in host-mapped memory and frags / headers / out_state
+// there too; the last batch's workgroup then raises host_flag (launch completion
+// without a stream sync or a D2H copy).
 
 __global__ __launch_bounds__(kChunkThreads) void k_chunk_walk(const uint8_t *__restrict__ chunk,
                                                               const ChunkCand *__restrict__ cands, uint32_t K,
@@ -361,7 +364,8 @@ __global__ __launch_bounds__(kChunkThreads) void k_chunk_walk(const uint8_t *__r
                                                               const uint64_t *__restrict__ pos_all,
                                                               iggy_slice_query q, uint32_t epoch, ChunkLink *links,
                                                               ChunkState *out_state, iggy_chunk_fragment *frags,
-                                                              uint8_t *headers, uint64_t cap, uint64_t *bsums_all) {
+                                                              uint8_t *headers, uint64_t cap, uint64_t *bsums_all,
+                                                              uint32_t *host_flag, uint32_t flag_value) {
     __shared__ uint64_t s_red[kChunkThreads / 64];
     __shared__ uint32_t s_cnt[kChunkThreads];
     __shared__ ChunkState s_st;
@@ -488,6 +492,7 @@ __global__ __launch_bounds__(kChunkThreads) void k_chunk_walk(const uint8_t *__r
             uint64_t computed = 0;
             if (cp.long_cs) {
                 uint64_t *bs = bsums_all + 8 * cd.bbase;
+                const uint64_t sec[2] = {block_word_secret(0, lane), block_word_secret(1, lane)};
                 for (uint64_t b = tid >> 6; b <= cp.nb; b += kChunkThreads / 64) {
                     uint64_t x = 0, y = 0;
 #pragma unroll
@@ -496,7 +501,7 @@ __global__ __launch_bounds__(kChunkThreads) void k_chunk_walk(const uint8_t *__r
                         if (m < cp.Mreg) {
                             const uint64_t v = cs_word(m, w, src);
                             y += v;
-                            x += mul32x32(v ^ kSecretW8[((m >> 3) & 15) + (m & 7)]);
+                            x += mul32x32(v ^ sec[half]);
                         }
                     }
                     x += __shfl_xor(x, 8); y += __shfl_xor(y, 8);
@@ -555,6 +560,8 @@ __global__ __launch_bounds__(kChunkThreads) void k_chunk_walk(const uint8_t *__r
             *(u32_ua *)(headers + 256ull * idx + off) = word;
         }
     }
+    if (host_flag) __threadfence_system();  // every wave's header bytes, before thread 0 publishes
+    __syncthreads();
     if (tid != 0) return;
     if (!st.stopped) {  // push_selected_batch_fragments and the cursor advance (:1003)
         if (pushed) {
@@ -568,8 +575,17 @@ __global__ __launch_bounds__(kChunkThreads) void k_chunk_walk(const uint8_t *__r
         st.batches += 1;
     }
     links[k].st = st;
+    // frags / headers / out_state may be host-mapped memory: system scope before the
+    // link, so the last workgroup's flag covers every earlier workgroup's writes
+    if (host_flag) __threadfence_system();
     __hip_atomic_store(&links[k].ready, epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-    if (k + 1 == K) *out_state = st;
+    if (k + 1 == K) {
+        *out_state = st;
+        if (host_flag) {
+            __threadfence_system();
+            __hip_atomic_store(host_flag, flag_value, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+    }
 }
 
 }  // namespace iggy

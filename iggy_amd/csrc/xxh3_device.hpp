@@ -71,6 +71,13 @@ __constant__ static const uint64_t kSecretMerge[8] = {
 __constant__ static const uint64_t kAccInit[8] = {P32_3, P64_1, P64_2, P64_3,
                                                   P64_4, P32_2, P64_5, P32_1};
 
+// Secret word of word m = 128 b + 64 half + lane of a 1024-B block (any b): it depends
+// on (half, lane) only -- (m >> 3) & 15 = 8 half + (lane >> 3), m & 7 = lane & 7 -- so
+// block loops load it once instead of a runtime-indexed table read per block.
+__device__ __forceinline__ uint64_t block_word_secret(int half, int lane) {
+    return kSecretW8[8 * half + (lane >> 3) + (lane & 7)];
+}
+
 __device__ __forceinline__ uint64_t mul32x32(uint64_t k) {
     return (uint64_t)(uint32_t)k * (uint64_t)(uint32_t)(k >> 32);
 }

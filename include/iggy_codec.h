@@ -85,6 +85,10 @@ typedef enum iggy_error_kind {
      * headers) is shorter than nonce + tag or fails the GCM tag
      * (core/common/src/utils/crypto.rs:80-90, server_common/src/send_messages.rs:385-399) */
     IGGY_ERR_CANNOT_DECRYPT_DATA = 24,
+    /* IggyError::ConnectionClosed / TcpError of the socket framing
+     * (core/message_bus/src/framing.rs:165-171) */
+    IGGY_ERR_CONNECTION_CLOSED = 25,
+    IGGY_ERR_TCP_ERROR = 26,
     /* library-level failures (not wire errors) */
     IGGY_ERR_DEVICE = 100,
     IGGY_ERR_INVALID_ARGUMENT = 101,
@@ -635,6 +639,45 @@ typedef struct iggy_polled_prefix {
 int iggy_codec_polled_messages_from_bytes(iggy_codec_ctx *ctx, const uint8_t *bytes, uint64_t len,
                                           iggy_polled_prefix *prefix, iggy_polled_message *out,
                                           uint64_t cap, uint64_t *n, iggy_wire_error *err);
+
+/* ------------------------------------------ server socket side */
+/* The consensus frame header (core/binary_protocol/src/consensus/header.rs:49-78):
+ * 256 bytes, the frame's total size a u32 at byte 48. */
+#define IGGY_FRAME_HEADER_BYTES 256u
+#define IGGY_FRAME_SIZE_OFFSET 48u
+#define IGGY_MAX_MESSAGE_SIZE (64ull << 20) /* message_bus framing.rs:40 */
+
+/* read_message (core/message_bus/src/framing.rs:107-164) on a connected blocking
+ * stream socket: the 256-B header is read into buf, its size field checked against
+ * [256, max_message_size] (IGGY_ERR_INVALID_COMMAND otherwise), then the body is read
+ * into the tail of the SAME buffer -- one buffer per frame, no reassembly copy. buf
+ * is the caller's (the server's 4096-aligned Owned pool, iobuf.rs), registered once
+ * with iggy_codec_host_register so the codec's H2D copy of the frame is DMA. EOF
+ * before the frame is complete -> IGGY_ERR_CONNECTION_CLOSED, any other I/O error ->
+ * IGGY_ERR_TCP_ERROR, a frame larger than cap -> IGGY_ERR_CAPACITY (err->a = size).
+ * *total_size = the frame's size. (The consensus header's own field validation,
+ * Message::try_from, stays in Rust.) No device work. */
+int iggy_frame_read(int fd, uint8_t *buf, uint64_t cap, uint64_t max_message_size, uint64_t *total_size,
+                    iggy_wire_error *err);
+
+/* convert_request_message (core/server_common/src/send_messages.rs:459-478) fused
+ * with admit_wire_request (:480-540) on one framed SendMessages request
+ * [RoutedRequestHeader 256 B][body] of `len` bytes (as iggy_frame_read leaves it):
+ *  - a body that is ONE canonical batch (the encrypt ingest path re-entering) is
+ *    Verify-decoded on the GPU; it must carry messages, fill the body exactly and
+ *    carry this namespace's partition_id (else IGGY_ERR_INVALID_COMMAND); the frame
+ *    is kept as is (copied to out);
+ *  - otherwise the producer's wire form [u32 metadata_length][SendMessagesHeader]
+ *    [batch]: the metadata decoded (iggy_send_messages_header_decode, every failure
+ *    IGGY_ERR_INVALID_COMMAND, its length must match), then iggy_codec_admit_batch
+ *    with its messages_count (GPU Verify decode, partition stamped, batch checksum
+ *    recomputed or zeroed per checksum_mode); out = [the request header with size =
+ *    256 + batch_length][the admitted batch].
+ * Checksum failures keep their typed errors (batch_error). *out_len = bytes written;
+ * hdr_out (nullable) = the batch header of the output. */
+int iggy_codec_convert_request(iggy_codec_ctx *ctx, const uint8_t *frame, uint64_t len, uint64_t partition_id,
+                               int checksum_mode, uint8_t *out, uint64_t cap, uint64_t *out_len,
+                               iggy_batch_header *hdr_out, iggy_wire_error *err);
 
 /* ------------------------------------------ SDK producer batching */
 /* The producer's buffering in front of the encoder: the background shard buffer

@@ -169,3 +169,43 @@ def plan_requests(entries, direct: bool, batch_length: int):
                 continue
             plan.append([k, m0, m1])
     return [tuple(p) for p in plan if p[2] > p[1]]
+
+
+# ---- server admission of a framed request: convert_request_message + admit_wire_request
+# (core/server_common/src/send_messages.rs:459-540); the batch checks come from the C
+# restatement (oracle.decode_batch_slice_with / oracle.admit_batch)
+ERR_INVALID_COMMAND = 22
+
+
+def convert_request(frame: bytes, partition_id: int, checksum_mode: int = 0):
+    """-> (rc, err tuple, output bytes)."""
+    from oracle import oracle as O
+
+    frame = bytes(frame)
+    inv = (ERR_INVALID_COMMAND, (ERR_INVALID_COMMAND, 0, 0, 0, 0), b"")
+    if len(frame) < 256:
+        return inv
+    total = struct.unpack_from("<I", frame, 48)[0]
+    if total < 256 or total > len(frame):
+        return inv
+    body = frame[256:total]
+    rc, e, h, _ = O.decode_batch_slice_with(body, 0, want_frames=False)  # decode_batch_slice (Verify)
+    if rc == 0:  # :466-476, the canonical-batch shape
+        if h.message_count == 0 or len(body) != h.batch_length or h.partition_id != partition_id:
+            return inv
+        return 0, (0, 0, 0, 0, 0), frame[:total]
+    if len(body) < 4:  # admit_wire_request :486-500
+        return inv
+    mlen = struct.unpack_from("<I", body, 0)[0]
+    start = 4 + mlen
+    if len(body) < start:
+        return inv
+    err, meta, consumed = decode_metadata(body[4:start])
+    if err or consumed != mlen:
+        return inv
+    rc, e, ah, admitted = O.admit_batch(body[start:], meta[3], partition_id, checksum_mode)
+    if rc:
+        return rc, tuple(e.astuple()), b""
+    hdr = bytearray(frame[:256])
+    struct.pack_into("<I", hdr, 48, 256 + ah.batch_length)
+    return 0, (0, 0, 0, 0, 0), bytes(hdr) + admitted
