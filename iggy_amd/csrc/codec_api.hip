@@ -1663,6 +1663,64 @@ int iggy_codec_poll_decode(iggy_codec_ctx *c, const uint8_t *buf, uint64_t len, 
         rin[k] = RecIn{recs[k].pos, len - recs[k].pos, recs[k].pbase, avail / 48 + 1, slot[k]};
     }
     for (size_t k = 0; k < K; ++k) tailb[k] = nslots + recs[k].pbase;
+    if (K && records_all_planned(buf, rin.data(), K)) {
+        // every record single-stride: descriptors and verdicts straight into host-mapped
+        // memory, the host spinning on the launch's completion flag (one H2D, one launch)
+        const size_t rb = K * sizeof(iggy_decode_result), mo = (64 + rb + 127) & ~(size_t)127;
+        if (c->din.ensure(len + 16) || c->omap.ensure(mo + (nslots + 1) * sizeof(iggy_polled_message)))
+            return IGGY_ERR_DEVICE;
+        if (len) HIP_OK(hipMemcpyAsync(c->din.p, buf, len, hipMemcpyHostToDevice, c->stream));
+        std::vector<size_t> single;
+        const uint32_t v = next_flag(c);
+        int r = enqueue_records(c, c->din.as<uint8_t>(), buf, rin.data(), K, IGGY_INTEGRITY_LAYOUT_ONLY, nullptr,
+                                c->omap.dp<iggy_polled_message>(mo), c->omap.dp<iggy_decode_result>(64), &single,
+                                nullptr, c->omap.dp<uint32_t>(), v);
+        if (r) return r;
+        r = wait_host_flag(c, v);
+        if (r) return r;
+        const iggy_decode_result *res = c->omap.hp<iggy_decode_result>(64);
+        bool general = false;
+        for (size_t k = 0; k < K; ++k) {
+            if (res[k].error.kind == IGGY_ERR_TIMEOUT) {
+                reset_after_timeout(c);
+                set_err(err, IGGY_ERR_TIMEOUT);
+                return IGGY_ERR_TIMEOUT;
+            }
+            general |= res[k].status == kStatusNeedGeneral;
+        }
+        if (!general) {  // (a stride that broke mid-record: the path below, from scratch)
+            const iggy_polled_message *msgs = c->omap.hp<iggy_polled_message>(mo);
+            uint64_t n = 0;
+            int rc = 0;
+            for (size_t k = 0; k < K && !rc; ++k) {
+                const iggy_decode_result &rs = res[k];
+                if (mode == IGGY_POLL_MODE_SDK) {
+                    if (rs.covered != recs[k].bl - 256) {
+                        set_err(err, IGGY_ERR_INVALID_MESSAGE_PAYLOAD_LENGTH);
+                        return IGGY_ERR_INVALID_MESSAGE_PAYLOAD_LENGTH;
+                    }
+                } else if (rs.error.kind != IGGY_OK) {
+                    fill_err(err, rs.error);
+                    rc = (int)rs.error.kind;
+                    break;
+                }
+                const uint64_t nf = rs.frame_count;
+                if (n + nf > cap) {
+                    set_err(err, IGGY_ERR_CAPACITY, 0, n + nf, cap);
+                    rc = IGGY_ERR_CAPACITY;
+                    break;
+                }
+                if (nf) memcpy(out + n, msgs + slot[k], nf * sizeof(iggy_polled_message));
+                n += nf;
+            }
+            if (!rc && stop_rc) {
+                fill_err(err, stop_err);
+                rc = stop_rc;
+            }
+            if (n_out) *n_out = n;
+            return rc;
+        }
+    }
     int r = c->din.ensure(len + 16);
     r |= c->ppos.ensure((pwords + 1) * 8);
     r |= c->pres.ensure((K + 1) * sizeof(iggy_decode_result));
