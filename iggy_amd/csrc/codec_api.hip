@@ -1424,6 +1424,7 @@ static int enqueue_encode(iggy_codec_ctx *c, const iggy_raw_messages *dm, uint64
     es.cs = c->ecs.as<uint64_t>();
     es.misc = c->emisc.as<uint64_t>();
     es.hdr = c->emisc.as<iggy_batch_header>(128);
+    es.dbg = diag_bits(c);
     iggy_raw_messages m = *dm;
     prof_begin(c, 1, s);
     hipLaunchKernelGGL(k_enc_prep, dim3(ntiles), dim3(256), 0, s, m, es, partition_id, cap, (uint32_t)(ntiles == 1));

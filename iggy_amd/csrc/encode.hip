@@ -31,6 +31,7 @@ struct EncScratch {
     uint64_t *misc;       // [8]: 0 min origin, 1 blob bytes, 2 ts-error (~index, max), 3 n, 4 payload bytes,
                           //      5 batch does not fit the output capacity (nothing is written)
     iggy_batch_header *hdr;  // header being built
+    uint32_t dbg;         // ablation bits (diagnostic build only; kDiagMask folds them out)
 };
 
 // the scan's result: origin, blob bytes, capacity verdict and the header being built
@@ -509,12 +510,16 @@ __global__ __launch_bounds__(256, 2) void k_enc_lanes(iggy_raw_messages m, EncSc
                 else if (sp == 16) { w0 = h2; w1 = h3; }
                 else { w1 = w0; w0 = 0; }  // reserved | payload[0..8)
             }
-            if (sp + 16 <= L) {
+            if (kDiagMask && (es.dbg & 0x30000)) {  // ablations: aligned destination / no stores
+                if (!(es.dbg & 0x20000) && sp + 16 <= L)
+                    *(uint4 *)(((uintptr_t)(F + 8) & ~(uintptr_t)15) + sp) =
+                        make_uint4((uint32_t)w0, (uint32_t)(w0 >> 32), (uint32_t)w1, (uint32_t)(w1 >> 32));
+            } else if (sp + 16 <= L) {
                 st128_any(F + 8 + sp, make_uint4((uint32_t)w0, (uint32_t)(w0 >> 32), (uint32_t)w1, (uint32_t)(w1 >> 32)));
             } else if (sp < L) {  // the frame's partial last piece (at most one per lane)
                 tw0 = w0; tw1 = w1; tsp = sp;
             }
-            if (lng) {
+            if (lng && !(kDiagMask && (es.dbg & 0x40000))) {  // (ablation: no hashing)
                 const uint64_t sa = s_sec[sbase + 2 * q], sb = s_sec[sbase + 2 * q + 1];
                 if (b < nbF) {
                     p0[q & 3] += mul32x32(w0 ^ sa) + w1;
