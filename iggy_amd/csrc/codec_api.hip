@@ -253,6 +253,9 @@ DecodeScratch dscratch(iggy_codec_ctx *c) {
     return s;
 }
 
+// diagnostic ablation bits, zero in the product build
+inline uint32_t diag_bits(const iggy_codec_ctx *c) { return c->dbg & kDiagMask; }
+
 GeneralScratch gscratch(iggy_codec_ctx *c) {
     GeneralScratch g;
     g.tile_s = c->gtiles_s.as<uint64_t>();
@@ -277,6 +280,7 @@ GeneralScratch gscratch(iggy_codec_ctx *c) {
     g.ntiles = c->gtiles_s.cap / 8;
     g.max_frames = c->gfpos.cap / 8;
     g.max_blocks = c->gbsums.cap / 64;
+    g.dbg = diag_bits(c);
     return g;
 }
 
@@ -309,8 +313,6 @@ struct DevGuard {
     }
 };
 
-// diagnostic ablation bits, zero in the product build
-inline uint32_t diag_bits(const iggy_codec_ctx *c) { return c->dbg & kDiagMask; }
 
 void prof_begin(iggy_codec_ctx *c, int which, hipStream_t s) {
     if (!c->profile) return;

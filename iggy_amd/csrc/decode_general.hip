@@ -73,6 +73,7 @@ struct GeneralScratch {
     uint64_t *u_first_bad, *u_spec_fail;
     uint8_t *small;      // >= 512 B
     uint64_t ntiles, max_frames, max_blocks;  // ntiles: capacity in kTileMin tiles
+    uint32_t dbg;        // ablation bits (diagnostic build only; kDiagMask folds them out)
 };
 
 // ---------------------------------------------------------------- helpers
@@ -388,7 +389,7 @@ __device__ __forceinline__ uint4 realign(uint4 w, uint32_t nb, uint32_t r) {
 // (only when the frame is misaligned; that dword holds a byte the hash needs, so
 // it never reaches past the 4-B word of a frame byte) and realigned in registers.
 __device__ __forceinline__ void vissue(const uint8_t *blob, const VFrame &v, uint64_t nwalk, uint32_t b,
-                                       uint32_t par, uint32_t poff, uint32_t m, VStep &st) {
+                                       uint32_t par, uint32_t poff, uint32_t m, VStep &st, uint32_t dbg = 0) {
     const bool lng = v.f < nwalk && v.L > 240;
     const uint64_t nbF = lng ? (v.L - 1) / 1024 : 0, ns = lng ? ((v.L - 1) - 1024 * nbF) / 64 : 0;
     const uint8_t *H = blob + v.p + 8;
@@ -398,7 +399,8 @@ __device__ __forceinline__ void vissue(const uint8_t *blob, const VFrame &v, uin
     for (int q = 0; q < 8; ++q) {
         const bool use = lng && (b < nbF || 2 * q + par < ns);
         st.v[q] = ld128_any(use ? hb + 128 * q : blob);
-        st.nx[q] = *(const uint32_t *)((use && r) ? hb + 128 * q + 16 : blob);
+        if (kDiagMask && (dbg & 0x80000)) st.nx[q] = 0;  // ablation: no realignment loads (hash wrong)
+        else st.nx[q] = *(const uint32_t *)((use && r) ? hb + 128 * q + 16 : blob);
     }
     const uint8_t *E = H + v.L;
     const uint32_t rl = (uint32_t)((uintptr_t)E & 3);
@@ -455,8 +457,8 @@ __device__ inline void verify_frames(const uint8_t *blob, const GeneralScratch &
         const uint64_t ns = lng ? ((L - 1) - 1024 * nbF) / 64 : 0;
         const uint32_t nsteps = lng ? (uint32_t)(nbF + (ns > 0)) : 1u;
         const bool fin = b + 1 == nsteps;
-        if (!fin) vissue(blob, cur, nwalk, b + 1, par, poff, m, Y);
-        else vissue(blob, nxt, nwalk, 0, par, poff, m, Y);
+        if (!fin) vissue(blob, cur, nwalk, b + 1, par, poff, m, Y, gs.dbg);
+        else vissue(blob, nxt, nwalk, 0, par, poff, m, Y, gs.dbg);
         const uint32_t r = (uint32_t)((uintptr_t)(blob + cur.p + 8) & 3);
         if (b == 0) lastp = realign(X.last, X.lnx, (uint32_t)((uintptr_t)(blob + cur.p + 8 + L) & 3));
         uint4 pc[8];
@@ -514,7 +516,7 @@ __device__ inline void verify_frames(const uint8_t *blob, const GeneralScratch &
         }
     }
     VStep A, B;
-    vissue(blob, cur, nwalk, 0, par, poff, m, A);
+    vissue(blob, cur, nwalk, 0, par, poff, m, A, gs.dbg);
     while (__ballot(cur.f < nwalk)) {
         step(A, B);
         if (!__ballot(cur.f < nwalk)) break;
