@@ -85,6 +85,10 @@ struct HostMap {
             return IGGY_ERR_DEVICE;
         }
         cap = want;
+        // the completion flag lives in the first word: pinned memory handed back by the
+        // allocator may still hold another context's flag values, one of which this
+        // context's sequence could reach before its kernel writes it
+        memset(h, 0, 256);
         return 0;
     }
     template <class T> T *hp(size_t off = 0) { return (T *)((uint8_t *)h + off); }

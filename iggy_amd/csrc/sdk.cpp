@@ -731,7 +731,7 @@ int iggy_codec_convert_request(iggy_codec_ctx *ctx, const uint8_t *frame, uint64
                                          out + hs, cap - hs, &ah, err);
     if (r) return r;
     // the request header with the pipeline form's size (:523-528)
-    memcpy(out, frame, hs);
+    if (out != frame) memcpy(out, frame, hs);
     const uint64_t new_total = hs + ah.batch_length;
     if (new_total > 0xFFFFFFFFull) return invalid();
     const uint32_t nt = (uint32_t)new_total;
