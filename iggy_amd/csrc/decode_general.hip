@@ -377,7 +377,20 @@ struct VStep {
     uint32_t nx[8];   // the dword after each chunk (the bytes the alignment shifted out)
     uint4 last;       // the frame's last-stripe chunk (first block only), aligned the same way
     uint32_t lnx;     // the dword after it
+    uint32_t nx7;     // (diagnostic neighbour form) the dword after the block, for lane k = 7
+    uint32_t clampm;  // (idem) bit q: chunk q was loaded 12 B early (a neighbour-only chunk at the blob end)
 };
+// Diagnostic form (dbg bit 0x100000, next-round candidate): the dword after each chunk
+// is the first dword of the chunk the next lane of the group loaded (poff order
+// k = m + 4 par: lanes l = 0..5 take lane l + 2, lane 6 lane 1, lane 7 lane 0 of the
+// next row), moved with DPP instead of loaded: 10 loads per step instead of 18.
+__device__ __forceinline__ uint32_t dpp_u32(uint32_t x, int ctrl) {
+    switch (ctrl) {
+        case 0: return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x102, 0xF, 0xF, false);  // row_shl:2
+        case 1: return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x115, 0xF, 0xF, false);  // row_shr:5
+        default: return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x117, 0xF, 0xF, false); // row_shr:7
+    }
+}
 // 16 bytes starting r bytes into (w.x, w.y, w.z, w.w, nb)
 __device__ __forceinline__ uint4 realign(uint4 w, uint32_t nb, uint32_t r) {
     return make_uint4(__builtin_amdgcn_alignbyte(w.y, w.x, r), __builtin_amdgcn_alignbyte(w.z, w.y, r),
@@ -389,12 +402,36 @@ __device__ __forceinline__ uint4 realign(uint4 w, uint32_t nb, uint32_t r) {
 // (only when the frame is misaligned; that dword holds a byte the hash needs, so
 // it never reaches past the 4-B word of a frame byte) and realigned in registers.
 __device__ __forceinline__ void vissue(const uint8_t *blob, const VFrame &v, uint64_t nwalk, uint32_t b,
-                                       uint32_t par, uint32_t poff, uint32_t m, VStep &st, uint32_t dbg = 0) {
+                                       uint32_t par, uint32_t poff, uint32_t m, VStep &st, uint32_t dbg = 0,
+                                       const uint8_t *blob_end = nullptr) {
     const bool lng = v.f < nwalk && v.L > 240;
     const uint64_t nbF = lng ? (v.L - 1) / 1024 : 0, ns = lng ? ((v.L - 1) - 1024 * nbF) / 64 : 0;
     const uint8_t *H = blob + v.p + 8;
     const uint32_t r = (uint32_t)((uintptr_t)H & 3);
     const uint8_t *hb = H - r + 1024ull * b + poff;
+    if (kDiagMask && (dbg & 0x100000)) {
+        // a chunk is loaded when its own piece is hashed, or (misaligned frames) when the
+        // piece before it in stream order is: its first dword completes that piece
+        const uint32_t k = m + 4 * par;
+        st.clampm = 0;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            const bool full = b < nbF;
+            const bool use = lng && (full || 2 * q + par < ns);
+            const uint64_t sprev = k == 0 ? (uint64_t)(2 * q) - 1 : 2 * q + (k - 1 >= 4 ? 1 : 0);
+            const bool prev_use = lng && (k != 0 || q != 0) && (full || sprev < ns);
+            const bool need = use || (r && prev_use);
+            const uint8_t *a = hb + 128 * q;
+            // a neighbour-only chunk of the record's last frame may run past the blob
+            // end: load the 16 B that end with its first dword instead
+            const bool clamp = need && !use && a + 16 > blob_end;
+            if (clamp) st.clampm |= 1u << q;
+            st.v[q] = ld128_any(need ? (clamp ? a - 12 : a) : blob);
+            st.nx[q] = 0;
+        }
+        const bool use77 = lng && (b < nbF || 15 < ns);  // piece (7, k = 7): stripe 15
+        st.nx7 = *(const uint32_t *)((k == 7 && use77 && r) ? hb + 128 * 7 + 16 : blob);
+    } else
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
         const bool use = lng && (b < nbF || 2 * q + par < ns);
@@ -412,7 +449,7 @@ __device__ __forceinline__ void vissue(const uint8_t *blob, const VFrame &v, uin
 
 __device__ inline void verify_frames(const uint8_t *blob, const GeneralScratch &gs, uint64_t nwalk,
                                      uint64_t wend, uint32_t vw, uint32_t nvw, uint32_t member, uint32_t nwg,
-                                     uint32_t *s_claim, int lane, uint64_t t0) {
+                                     uint32_t *s_claim, int lane, uint64_t t0, const uint8_t *blob_end) {
     const uint32_t l = lane & 7, m = l >> 1, par = l & 1, fg = (uint32_t)lane >> 3;
     const uint32_t poff = 16 * (m + 4 * par);
     uint64_t s0[8], s1[8];
@@ -457,13 +494,26 @@ __device__ inline void verify_frames(const uint8_t *blob, const GeneralScratch &
         const uint64_t ns = lng ? ((L - 1) - 1024 * nbF) / 64 : 0;
         const uint32_t nsteps = lng ? (uint32_t)(nbF + (ns > 0)) : 1u;
         const bool fin = b + 1 == nsteps;
-        if (!fin) vissue(blob, cur, nwalk, b + 1, par, poff, m, Y, gs.dbg);
-        else vissue(blob, nxt, nwalk, 0, par, poff, m, Y, gs.dbg);
+        if (!fin) vissue(blob, cur, nwalk, b + 1, par, poff, m, Y, gs.dbg, blob_end);
+        else vissue(blob, nxt, nwalk, 0, par, poff, m, Y, gs.dbg, blob_end);
         const uint32_t r = (uint32_t)((uintptr_t)(blob + cur.p + 8) & 3);
         if (b == 0) lastp = realign(X.last, X.lnx, (uint32_t)((uintptr_t)(blob + cur.p + 8 + L) & 3));
         uint4 pc[8];
+        if (kDiagMask && (gs.dbg & 0x100000)) {
+            uint32_t ex[8];
 #pragma unroll
-        for (int q = 0; q < 8; ++q) pc[q] = realign(X.v[q], X.nx[q], r);
+            for (int q = 0; q < 8; ++q) ex[q] = ((X.clampm >> q) & 1) ? X.v[q].w : X.v[q].x;
+#pragma unroll
+            for (int q = 0; q < 8; ++q) {
+                const uint32_t a = dpp_u32(ex[q], 0), bb = dpp_u32(ex[q], 1);
+                const uint32_t c = q < 7 ? dpp_u32(ex[q < 7 ? q + 1 : q], 2) : X.nx7;
+                const uint32_t nx = l <= 5 ? a : (l == 6 ? bb : c);
+                pc[q] = realign(X.v[q], nx, r);
+            }
+        } else {
+#pragma unroll
+            for (int q = 0; q < 8; ++q) pc[q] = realign(X.v[q], X.nx[q], r);
+        }
         if (lng) {
             if (b < nbF) {
                 uint64_t p0[4] = {0, 0, 0, 0}, p1[4] = {0, 0, 0, 0};
@@ -516,7 +566,7 @@ __device__ inline void verify_frames(const uint8_t *blob, const GeneralScratch &
         }
     }
     VStep A, B;
-    vissue(blob, cur, nwalk, 0, par, poff, m, A, gs.dbg);
+    vissue(blob, cur, nwalk, 0, par, poff, m, A, gs.dbg, blob_end);
     while (__ballot(cur.f < nwalk)) {
         step(A, B);
         if (!__ballot(cur.f < nwalk)) break;
@@ -1077,7 +1127,7 @@ __global__ __launch_bounds__(kGenThreads) void k_decode_general(const uint8_t *_
         const uint32_t nvw = nwg * (blockDim.x >> 6) - ws;
         if (vw == 0 && lane == 0) ((uint64_t *)(gs.small + 512))[17] = nvw;
         const uint64_t wend = __hip_atomic_load(&gs.misc[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & ~kStopBit;
-        verify_frames(blob, gs, nwalk, wend, vw, nvw, member, nwg, &s_mem[2], lane, t0);
+        verify_frames(blob, gs, nwalk, wend, vw, nvw, member, nwg, &s_mem[2], lane, t0, blob + bl);
     }
     ok &= grid_barrier2(gs.bar2, member, nwg, ++phase, t0);
     gstamp(gs, member, 6, rt_now() - t0);
