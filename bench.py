@@ -601,19 +601,34 @@ def run(args, world: int, rank: int, local: int, dist):
         for ln in lanes[1:]:  # free HBM held by the other lanes' records
             ln["batch"] = None
         torch.cuda.empty_cache()
-        extra["crypt_c2"] = crypt_leg(lanes[0]["cx"], dev, lanes[0]["batch"], n, max(5, args.steps // 4),
-                                      rank == 0 and not args.no_cpu)
+        # The side legs (other BASELINE configs) never take the headline line down with
+        # them: a leg that fails reports its error in its own field.
+        def leg(name, fn):
+            try:
+                return fn()
+            except Exception as ex:  # reported, not hidden: the field carries the failure
+                torch.cuda.synchronize()
+                return {"error": f"{type(ex).__name__}: {ex}"[:500]}
+
+        extra["crypt_c2"] = leg("crypt_c2", lambda: crypt_leg(lanes[0]["cx"], dev, lanes[0]["batch"], n,
+                                                              max(5, args.steps // 4), rank == 0 and not args.no_cpu))
         lanes[0]["batch"] = None
         torch.cuda.empty_cache()
-        extra["c3_encode"], extra["c3_decode"] = c3_leg(lanes[0]["cx"], dev, max(5, args.steps // 2))
-        extra["c1"] = c1_leg(lanes[0]["cx"], dev, args.cpu_seconds)
-        extra["c4"] = c4_leg(dev, 16)
+        c3 = leg("c3", lambda: c3_leg(lanes[0]["cx"], dev, max(5, args.steps // 2)))
+        extra["c3_encode"], extra["c3_decode"] = c3 if isinstance(c3, tuple) else (c3, c3)
+        torch.cuda.empty_cache()
+        extra["c1"] = leg("c1", lambda: c1_leg(lanes[0]["cx"], dev, args.cpu_seconds))
+        torch.cuda.empty_cache()
+        extra["c4"] = leg("c4", lambda: c4_leg(dev, 16))
     cpu = None
     if rank == 0 and not args.no_cpu:
         # N = 1: the full sample; N > 1: a short one (1 thread and one per rank) so the
         # scaling lines carry the CPU axis too without lengthening the run much
-        cpu = cpu_baseline(args.cpu_seconds) if world == 1 else \
-            cpu_baseline(min(args.cpu_seconds, 1.5), threads=sorted({1, world}))
+        try:
+            cpu = cpu_baseline(args.cpu_seconds) if world == 1 else \
+                cpu_baseline(min(args.cpu_seconds, 1.5), threads=sorted({1, world}))
+        except Exception as ex:  # reported in the line, never silently dropped
+            cpu = {"error": f"{type(ex).__name__}: {ex}"[:500]}
 
     traffic, traffic_src = pmc_traffic(n)
     value = whole_job_gib_s(world, L, args.steps, elapsed)
