@@ -101,6 +101,7 @@ def load(path: str) -> ctypes.CDLL:
     L.iggy_codec_poll_decode.argtypes = [vp, vp, u64, ci, vp, u64, vp, vp]
     L.iggy_codec_decode_records.argtypes = [vp, vp, u64, vp, u64, ci, vp]
     L.iggy_frame_read.argtypes = [ci, vp, u64, u64, vp, vp]
+    L.iggy_frame_read_rest.argtypes = [ci, vp, u64, vp]
     L.iggy_codec_convert_request.argtypes = [vp, vp, u64, u64, ci, vp, u64, vp, vp, vp]
     L.iggy_codec_stamp_batch.argtypes = [vp, vp, u64, u64, u64, vp, vp]
     L.iggy_codec_decode_batch_device.argtypes = [vp, vp, u64, ci, vp, u64, vp, vp]
@@ -154,9 +155,11 @@ def _addr(a: np.ndarray):
     return a.ctypes.data if a.size else None
 
 
-def frame_read(fd: int, cap: int, max_message_size: int = 64 << 20):
-    """read_message (message_bus/src/framing.rs:107-164) on a blocking socket fd
-    -> (rc, WireError, frame bytes as a numpy view of a 4096-aligned buffer)."""
+def frame_read(fd: int, cap: int, max_message_size: int = 64 << 20, grow: bool = False):
+    """read_message (message_bus/src/framing.rs:107-164) + Message::<GenericHeader>::
+    try_from on a blocking socket fd -> (rc, WireError, frame bytes as a numpy view of a
+    4096-aligned buffer). grow: a frame larger than cap continues in a larger buffer
+    (iggy_frame_read_rest) instead of returning IGGY_ERR_CAPACITY."""
     raw = np.zeros(cap + 4096, dtype=np.uint8)
     off = (-raw.ctypes.data) % 4096
     buf = raw[off: off + cap]
@@ -164,7 +167,16 @@ def frame_read(fd: int, cap: int, max_message_size: int = 64 << 20):
     e = WireError()
     rc = lib().iggy_frame_read(fd, buf.ctypes.data if cap else None, cap, max_message_size, ctypes.byref(n),
                                ctypes.byref(e))
-    return rc, e, buf[: n.value]
+    if rc == abi.ERR_CAPACITY and grow and n.value:
+        # the reference grows its buffer in place (framing.rs:150-160): a larger aligned
+        # buffer takes the header and the rest of the frame is read into it
+        big = np.zeros(n.value + 4096, dtype=np.uint8)
+        off = (-big.ctypes.data) % 4096
+        nb = big[off: off + n.value]
+        nb[:256] = buf[:256]
+        rc = lib().iggy_frame_read_rest(fd, nb.ctypes.data, n.value, ctypes.byref(e))
+        return rc, e, nb if rc == 0 else nb[:0]
+    return rc, e, buf[: n.value] if rc == 0 else buf[:0]
 
 
 def send_messages_header_encode(h: SendMessagesHeader) -> bytes:
@@ -540,11 +552,13 @@ class Producer:
         self._L.iggy_producer_pending(self._h, ctypes.byref(e), ctypes.byref(b), ctypes.byref(m))
         return e.value, b.value, m.value
 
-    def flush(self, cap: int, max_reqs: int = 4096, out: np.ndarray | None = None):
-        """-> (rc, WireError, out bytes, [ProducerRequest])."""
+    def flush(self, cap: int, max_reqs: int = 4096, out: np.ndarray | None = None, reqs=None):
+        """-> (rc, WireError, out bytes, [ProducerRequest]). `reqs`: a caller-owned
+        (ProducerRequest * max_reqs) array reused across flushes (the C caller's form)."""
         if out is None:
             out = np.zeros(max(cap, 1), dtype=np.uint8)
-        reqs = (ProducerRequest * max(max_reqs, 1))()
+        if reqs is None:
+            reqs = (ProducerRequest * max(max_reqs, 1))()
         n = u64(0)
         e = WireError()
         rc = self._L.iggy_producer_flush(self._h, out.ctypes.data, cap, reqs, max_reqs, ctypes.byref(n),

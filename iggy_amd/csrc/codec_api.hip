@@ -823,7 +823,14 @@ int iggy_codec_create(int device, iggy_codec_ctx **out) {
 void iggy_codec_destroy(iggy_codec_ctx *c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
+    // every stream that may still run this context's work (the caller's last stream,
+    // the side stream of segmented encodes, the copy streams of the asynchronous host
+    // operations) drains before any buffer it reads or writes goes back to the allocator
     if (c->stream) (void)hipStreamSynchronize(c->stream);
+    if (c->last && c->last != c->stream) (void)hipStreamSynchronize(c->last);
+    if (c->side) (void)hipStreamSynchronize(c->side);
+    if (c->h2d) (void)hipStreamSynchronize(c->h2d);
+    if (c->d2h) (void)hipStreamSynchronize(c->d2h);
     DevBuf *bufs[] = {&c->dsync, &c->dsums, &c->derr, &c->gtiles_s, &c->gtiles_x,
                       &c->gtiles_cnt, &c->gtiles_pre, &c->gtiles_list, &c->gtiles_e, &c->gtiles_base, &c->ggrp, &c->gfpos, &c->gcs, &c->gtiles_lcs,
                       &c->gbsums, &c->dresult, &c->din, &c->dpos, &c->dout, &c->epl, &c->euh,
@@ -879,57 +886,8 @@ int iggy_codec_synchronize(iggy_codec_ctx *c) {
     return 0;
 }
 
-// ---------------------------------------------------------------- host pure
-int iggy_batch_header_decode(const uint8_t *b, uint64_t len, iggy_batch_header *h,
-                             iggy_wire_error *err) {
-    set_err(err, IGGY_OK);
-    if (!b && len) return IGGY_ERR_INVALID_ARGUMENT;
-    if (len < 256) {
-        set_err(err, IGGY_ERR_UNEXPECTED_EOF, 0, 0, 256, len);
-        return IGGY_ERR_UNEXPECTED_EOF;
-    }
-    uint64_t bl;
-    memcpy(&bl, b + 32, 8);
-    if (bl < 256) {
-        set_err(err, IGGY_ERR_VALIDATION, IGGY_V_BATCH_LENGTH_SHORT);
-        return IGGY_ERR_VALIDATION;
-    }
-    for (int i = 52; i < 256; ++i)
-        if (b[i]) {
-            set_err(err, IGGY_ERR_VALIDATION, IGGY_V_BATCH_RESERVED);
-            return IGGY_ERR_VALIDATION;
-        }
-    if (h) {
-        memset(h, 0, sizeof(*h));
-        memcpy(&h->partition_id, b + 0, 8);
-        memcpy(&h->base_offset, b + 8, 8);
-        memcpy(&h->base_timestamp, b + 16, 8);
-        memcpy(&h->origin_timestamp, b + 24, 8);
-        h->batch_length = bl;
-        memcpy(&h->batch_checksum, b + 40, 8);
-        memcpy(&h->message_count, b + 48, 4);
-    }
-    return 0;
-}
-
-void iggy_batch_header_encode(const iggy_batch_header *h, uint8_t out[256]) {
-    memset(out, 0, 256);
-    memcpy(out + 0, &h->partition_id, 8);
-    memcpy(out + 8, &h->base_offset, 8);
-    memcpy(out + 16, &h->base_timestamp, 8);
-    memcpy(out + 24, &h->origin_timestamp, 8);
-    memcpy(out + 32, &h->batch_length, 8);
-    memcpy(out + 40, &h->batch_checksum, 8);
-    memcpy(out + 48, &h->message_count, 4);
-}
-
-uint64_t iggy_encoded_batch_size(const iggy_raw_messages *m) {
-    if (!m) return 0;
-    uint64_t t = 256;
-    for (uint64_t i = 0; i < m->count; ++i)
-        t += 48 + (uint64_t)m->payload_lengths[i] + (m->user_headers_lengths ? m->user_headers_lengths[i] : 0);
-    return t;
-}
+// iggy_batch_header_decode / _encode and iggy_encoded_batch_size (host pure) live in
+// sdk.cpp, which also builds alone for the host sanitizer run (tests/fuzz/).
 
 // ------------------------------------------------------------ synchronous
 int iggy_codec_decode_batch(iggy_codec_ctx *c, const uint8_t *body, uint64_t len, int integrity,

@@ -12,9 +12,17 @@
 //   core/sdk/src/clients/producer_sharding.rs:91-293, producer.rs:406-470
 //   core/message_bus/src/framing.rs:107-171 (socket framing)
 //   core/server_common/src/send_messages.rs:459-540 (convert_request_message)
+//   core/binary_protocol/src/batch.rs:98-150 (BatchHeader decode / encode_into)
+//
+// -DIGGY_HOST_ONLY builds the host-pure half alone (no HIP, no codec entry points:
+// the functions that call the device are left out, staging memory is plain malloc)
+// for the host sanitizer run of tests/test_sdk_fuzz_cpu.py (-fsanitize=address,undefined).
+#ifndef IGGY_HOST_ONLY
 #include <hip/hip_runtime.h>
+#endif
 
 #include <errno.h>
+#include <stdlib.h>
 #include <unistd.h>
 
 #include <algorithm>
@@ -185,17 +193,26 @@ template <class T>
 struct Pinned {
     T *p = nullptr;
     uint64_t n = 0, cap = 0;
-    ~Pinned() {
-        if (p) (void)hipHostFree(p);
+    ~Pinned() { release(p); }
+    static void release(void *q) {
+#ifdef IGGY_HOST_ONLY
+        free(q);
+#else
+        if (q) (void)hipHostFree(q);
+#endif
     }
     bool reserve(uint64_t want) {
         if (want <= cap) return true;
         uint64_t nc = cap ? cap : 4096 / sizeof(T) + 1;
         while (nc < want) nc *= 2;
         void *q = nullptr;
+#ifdef IGGY_HOST_ONLY
+        if (!(q = malloc(nc * sizeof(T)))) return false;
+#else
         if (hipHostMalloc(&q, nc * sizeof(T), hipHostMallocDefault) != hipSuccess) return false;
+#endif
         if (n) memcpy(q, p, n * sizeof(T));
-        if (p) (void)hipHostFree(p);
+        release(p);
         p = (T *)q;
         cap = nc;
         return true;
@@ -292,6 +309,60 @@ void drop_flushed(iggy_producer *p, uint64_t upto) {
 
 extern "C" {
 
+// ------------------------------------------------------------ batch header (host pure)
+// BatchHeader::decode (batch.rs:98-134): EOF below 256 B, batch_length < 256 before
+// the reserved bytes 52..256 (which must be zero)
+int iggy_batch_header_decode(const uint8_t *b, uint64_t len, iggy_batch_header *h, iggy_wire_error *err) {
+    seterr(err, IGGY_OK);
+    if (!b && len) return IGGY_ERR_INVALID_ARGUMENT;
+    if (len < 256) {
+        seterr(err, IGGY_ERR_UNEXPECTED_EOF, 0, 0, 256, len);
+        return IGGY_ERR_UNEXPECTED_EOF;
+    }
+    uint64_t bl;
+    memcpy(&bl, b + 32, 8);
+    if (bl < 256) {
+        seterr(err, IGGY_ERR_VALIDATION, IGGY_V_BATCH_LENGTH_SHORT);
+        return IGGY_ERR_VALIDATION;
+    }
+    for (int i = 52; i < 256; ++i)
+        if (b[i]) {
+            seterr(err, IGGY_ERR_VALIDATION, IGGY_V_BATCH_RESERVED);
+            return IGGY_ERR_VALIDATION;
+        }
+    if (h) {
+        memset(h, 0, sizeof(*h));
+        memcpy(&h->partition_id, b + 0, 8);
+        memcpy(&h->base_offset, b + 8, 8);
+        memcpy(&h->base_timestamp, b + 16, 8);
+        memcpy(&h->origin_timestamp, b + 24, 8);
+        h->batch_length = bl;
+        memcpy(&h->batch_checksum, b + 40, 8);
+        memcpy(&h->message_count, b + 48, 4);
+    }
+    return 0;
+}
+
+// BatchHeader::encode_into (batch.rs:138-150)
+void iggy_batch_header_encode(const iggy_batch_header *h, uint8_t out[256]) {
+    memset(out, 0, 256);
+    memcpy(out + 0, &h->partition_id, 8);
+    memcpy(out + 8, &h->base_offset, 8);
+    memcpy(out + 16, &h->base_timestamp, 8);
+    memcpy(out + 24, &h->origin_timestamp, 8);
+    memcpy(out + 32, &h->batch_length, 8);
+    memcpy(out + 40, &h->batch_checksum, 8);
+    memcpy(out + 48, &h->message_count, 4);
+}
+
+uint64_t iggy_encoded_batch_size(const iggy_raw_messages *m) {
+    if (!m) return 0;
+    uint64_t t = 256;
+    for (uint64_t i = 0; i < m->count; ++i)
+        t += 48 + (uint64_t)m->payload_lengths[i] + (m->user_headers_lengths ? m->user_headers_lengths[i] : 0);
+    return t;
+}
+
 int iggy_send_messages_header_encode(const iggy_send_messages_header *h, uint8_t *out, uint64_t cap,
                                      uint64_t *out_len) {
     if (!h || !id_valid(h->stream_id) || !id_valid(h->topic_id) || !part_valid(h->partitioning))
@@ -338,6 +409,7 @@ uint64_t iggy_send_messages_encoded_size(const iggy_send_messages_header *h, con
     return 4 + metadata_length(*h) + iggy_encoded_batch_size(m);
 }
 
+#ifndef IGGY_HOST_ONLY
 int iggy_codec_send_messages_encode(iggy_codec_ctx *ctx, const iggy_send_messages_header *h,
                                     const iggy_raw_messages *m, uint8_t *out, uint64_t cap, uint64_t *out_len,
                                     iggy_wire_error *err) {
@@ -393,6 +465,8 @@ int iggy_codec_polled_messages_from_bytes(iggy_codec_ctx *ctx, const uint8_t *by
     if (n) *n = k;
     return r;
 }
+
+#endif  // IGGY_HOST_ONLY
 
 // ------------------------------------------------------------------- producer
 int iggy_producer_create(iggy_codec_ctx *ctx, const iggy_producer_config *cfg, iggy_producer **out) {
@@ -469,6 +543,7 @@ int iggy_producer_append(iggy_producer *p, const iggy_identifier *stream_id, con
     return 0;
 }
 
+#ifndef IGGY_HOST_ONLY
 int iggy_producer_flush(iggy_producer *p, uint8_t *out, uint64_t cap, iggy_producer_request *reqs,
                         uint64_t max_reqs, uint64_t *nreqs, iggy_wire_error *err) {
     if (!p || (!out && cap) || (!reqs && max_reqs)) return IGGY_ERR_INVALID_ARGUMENT;
@@ -538,13 +613,19 @@ int iggy_producer_flush(iggy_producer *p, uint8_t *out, uint64_t cap, iggy_produ
     //    flight; a full set retires its oldest request)
     std::vector<iggy_ticket> tick(sendable.size(), 0);
     std::vector<uint8_t> live(sendable.size(), 0);
+    // every request slot this flush may report is cleared first: a caller reusing its
+    // array from an earlier flush must not see a stale `sent` past a failure
+    memset(reqs, 0, sendable.size() * sizeof(iggy_producer_request));
     size_t oldest = 0;
     int rc = 0;
     auto retire = [&](size_t r) -> int {
         iggy_completion c;
         const int w = iggy_codec_wait(p->ctx, tick[r], &c);
         live[r] = 0;
-        if (w) return w;
+        if (w) {
+            reqs[r].sent = 0;  // no verdict: the request is not complete and is not reported
+            return w;
+        }
         reqs[r].error = c.error;
         return 0;
     };
@@ -591,14 +672,16 @@ int iggy_producer_flush(iggy_producer *p, uint8_t *out, uint64_t cap, iggy_produ
         live[r] = 1;
         rq.sent = 1;
     }
-    size_t nsent = 0;  // requests encoded (a prefix: submission stops at the first failure)
     for (size_t r = 0; r < sendable.size(); ++r) {
         if (live[r]) {
             const int w = retire(r);
             if (!rc) rc = w;
         }
-        if (reqs[r].sent) nsent = r + 1;
     }
+    // requests encoded AND retired with a verdict: the prefix up to the first that is
+    // not (submission stops at the first failure; a failed wait clears its request)
+    size_t nsent = 0;
+    while (nsent < sendable.size() && reqs[nsent].sent) ++nsent;
     // direct sends: the chunks after a failed one were never sent (producer.rs:446-452)
     if (!rc && p->cfg.direct)
         for (size_t r = 1; r < sendable.size(); ++r) {
@@ -612,6 +695,7 @@ int iggy_producer_flush(iggy_producer *p, uint8_t *out, uint64_t cap, iggy_produ
         // A submit or wait failed part-way: reqs[0..nsent) are written (each with its
         // own verdict) and must be sent by the caller; they leave the buffer, which keeps
         // only the messages of the requests after them, so a retry never re-sends one.
+        for (size_t r = nsent; r < sendable.size(); ++r) reqs[r].sent = 0;  // staged again, not reported
         if (nreqs) *nreqs = nsent;
         if (nsent) drop_flushed(p, sendable[nsent - 1].m1);
         return rc;
@@ -620,6 +704,8 @@ int iggy_producer_flush(iggy_producer *p, uint8_t *out, uint64_t cap, iggy_produ
     drop_flushed(p, N);
     return 0;
 }
+
+#endif  // IGGY_HOST_ONLY
 
 
 // ---------------------------------------------------------- server socket side
@@ -662,21 +748,40 @@ int iggy_frame_read(int fd, uint8_t *buf, uint64_t cap, uint64_t max_message_siz
         return IGGY_ERR_INVALID_COMMAND;
     }
     if (size > cap) {  // the reference grows its Owned buffer in place; ours is the caller's
+        *total_size = size;  // the caller resumes with iggy_frame_read_rest
         seterr(err, IGGY_ERR_CAPACITY, 0, size, cap);
         return IGGY_ERR_CAPACITY;
     }
+    r = iggy_frame_read_rest(fd, buf, size, err);
+    if (r == IGGY_ERR_INVALID_COMMAND) *total_size = size;  // consumed whole: the stream stays in sync
+    if (r) return r;
+    *total_size = size;
+    return 0;
+}
+
+int iggy_frame_read_rest(int fd, uint8_t *buf, uint64_t size, iggy_wire_error *err) {
+    if (fd < 0 || !buf || size < IGGY_FRAME_HEADER_BYTES) return IGGY_ERR_INVALID_ARGUMENT;
+    seterr(err, IGGY_OK);
     // stage 2: the body into the tail of the same buffer (framing.rs:128-160)
     if (size > IGGY_FRAME_HEADER_BYTES) {
-        r = read_exact_fd(fd, buf + IGGY_FRAME_HEADER_BYTES, size - IGGY_FRAME_HEADER_BYTES);
+        const int r = read_exact_fd(fd, buf + IGGY_FRAME_HEADER_BYTES, size - IGGY_FRAME_HEADER_BYTES);
         if (r) {
             seterr(err, (uint32_t)r);
             return r;
         }
     }
-    *total_size = size;
+    // Message::<GenericHeader>::try_from (consensus_message.rs:468-500): the checked bit
+    // pattern of the header (only `command` has invalid patterns, command.rs:90-95),
+    // validate() (always Ok for GenericHeader), size >= 256 and <= the bytes read
+    // (both hold by construction here)
+    if (buf[IGGY_FRAME_COMMAND_OFFSET] > IGGY_FRAME_COMMAND_MAX) {
+        seterr(err, IGGY_ERR_INVALID_COMMAND);
+        return IGGY_ERR_INVALID_COMMAND;
+    }
     return 0;
 }
 
+#ifndef IGGY_HOST_ONLY
 int iggy_codec_convert_request(iggy_codec_ctx *ctx, const uint8_t *frame, uint64_t len, uint64_t partition_id,
                                int checksum_mode, uint8_t *out, uint64_t cap, uint64_t *out_len,
                                iggy_batch_header *hdr_out, iggy_wire_error *err) {
@@ -740,5 +845,7 @@ int iggy_codec_convert_request(iggy_codec_ctx *ctx, const uint8_t *frame, uint64
     if (hdr_out) *hdr_out = ah;
     return 0;
 }
+
+#endif  // IGGY_HOST_ONLY
 
 }  // extern "C"

@@ -646,6 +646,11 @@ int iggy_codec_polled_messages_from_bytes(iggy_codec_ctx *ctx, const uint8_t *by
 #define IGGY_FRAME_HEADER_BYTES 256u
 #define IGGY_FRAME_SIZE_OFFSET 48u
 #define IGGY_MAX_MESSAGE_SIZE (64ull << 20) /* message_bus framing.rs:40 */
+/* GenericHeader.command (consensus/header.rs:201-212: offset 16+16+16+4+4+4 = 60), a
+ * #[repr(u8)] Command whose CheckedBitPattern admits 0..=ForwardLogoutResult (29)
+ * (consensus/command.rs:24-95) */
+#define IGGY_FRAME_COMMAND_OFFSET 60u
+#define IGGY_FRAME_COMMAND_MAX 29u
 
 /* read_message (core/message_bus/src/framing.rs:107-164) on a connected blocking
  * stream socket: the 256-B header is read into buf, its size field checked against
@@ -654,11 +659,24 @@ int iggy_codec_polled_messages_from_bytes(iggy_codec_ctx *ctx, const uint8_t *by
  * is the caller's (the server's 4096-aligned Owned pool, iobuf.rs), registered once
  * with iggy_codec_host_register so the codec's H2D copy of the frame is DMA. EOF
  * before the frame is complete -> IGGY_ERR_CONNECTION_CLOSED, any other I/O error ->
- * IGGY_ERR_TCP_ERROR, a frame larger than cap -> IGGY_ERR_CAPACITY (err->a = size).
- * *total_size = the frame's size. (The consensus header's own field validation,
- * Message::try_from, stays in Rust.) No device work. */
+ * IGGY_ERR_TCP_ERROR. Then Message::<GenericHeader>::try_from (consensus_message.rs:
+ * 468-500): the header's checked bit pattern (the command byte at 60 must be a Command
+ * discriminant, <= 29; every other GenericHeader field is a plain integer or byte
+ * array) and GenericHeader::validate (header.rs:246-248: always Ok) -> a bad command is
+ * IGGY_ERR_INVALID_COMMAND, reported, as in the reference, after the body has been
+ * consumed (the stream stays in sync; *total_size = the bytes consumed, 0 when the
+ * size field itself was refused). *total_size = the frame's size.
+ * A frame larger than cap -> IGGY_ERR_CAPACITY (err->a = size, *total_size = size):
+ * the 256-B header is in buf and the body is still on the socket. The reference grows
+ * its buffer in place (framing.rs:150-160); here the caller takes a buffer of >= size
+ * bytes, copies the header into it and finishes the frame with iggy_frame_read_rest.
+ * No device work. */
 int iggy_frame_read(int fd, uint8_t *buf, uint64_t cap, uint64_t max_message_size, uint64_t *total_size,
                     iggy_wire_error *err);
+/* the rest of a frame iggy_frame_read left at IGGY_ERR_CAPACITY: buf[0..256) holds its
+ * header (copied by the caller), size = the *total_size it reported; the body is read
+ * into buf[256..size) and the header validated as above. */
+int iggy_frame_read_rest(int fd, uint8_t *buf, uint64_t size, iggy_wire_error *err);
 
 /* convert_request_message (core/server_common/src/send_messages.rs:459-478) fused
  * with admit_wire_request (:480-540) on one framed SendMessages request

@@ -160,11 +160,25 @@ typedef struct {
     int (*update)(void *, unsigned char *, int *, const unsigned char *, int);
     int (*final)(void *, unsigned char *, int *);
     int (*ctrl)(void *, int, int, void *);
+    /* OpenSSL 3: a cipher fetched per worker (EVP_CIPHER_fetch), so the workers share
+     * no reference-counted cipher object; NULL -> the legacy EVP_aes_256_gcm() */
+    void *(*fetch)(void *, const char *, const char *);
+    void (*cipher_free)(void *);
 } evp_t;
 typedef struct {
     const evp_t *e;
     int nsec, secsize, ok;
+    /* timed form: every worker starts at the barrier and seals until the shared
+     * deadline; done = sections sealed */
+    pthread_barrier_t *start;
+    const struct timespec *deadline;
+    long long done;
 } gcm_job_t;
+static int past(const struct timespec *d) {
+    struct timespec now;
+    clock_gettime(CLOCK_MONOTONIC, &now);
+    return now.tv_sec > d->tv_sec || (now.tv_sec == d->tv_sec && now.tv_nsec >= d->tv_nsec);
+}
 static void *gcm_worker(void *arg) {
     gcm_job_t *j = (gcm_job_t *)arg;
     unsigned char key[32], iv[12], tag[16];
@@ -176,8 +190,12 @@ static void *gcm_worker(void *arg) {
     j->ok = c != NULL;
     /* the key schedule once per thread (as a long-lived Aes256GcmEncryptor), a fresh
      * nonce per section */
-    if (j->ok) j->ok &= j->e->init(c, j->e->cipher(), NULL, key, NULL) == 1;
-    for (int s = 0; s < j->nsec && j->ok; ++s) {
+    void *own = j->e->fetch ? j->e->fetch(NULL, "AES-256-GCM", NULL) : NULL;
+    if (j->ok) j->ok &= j->e->init(c, own ? own : j->e->cipher(), NULL, key, NULL) == 1;
+    if (j->start) pthread_barrier_wait(j->start);
+    for (long long s = 0; j->ok; ++s) {
+        if (j->deadline ? ((s & 63) == 0 && past(j->deadline)) : s >= j->nsec) break;
+        j->done = s + 1;
         int ol = 0, fl = 0;
         iv[0] = (unsigned char)s; iv[1] = (unsigned char)(s >> 8); iv[2] = (unsigned char)(s >> 16);
         j->ok &= j->e->init(c, NULL, NULL, NULL, iv) == 1;
@@ -186,34 +204,44 @@ static void *gcm_worker(void *arg) {
         j->ok &= j->e->ctrl(c, 0x10 /* EVP_CTRL_GCM_GET_TAG */, 16, tag) == 1;
     }
     if (c) j->e->ctx_free(c);
+    if (own && j->e->cipher_free) j->e->cipher_free(own);
     free(in);
     free(out);
     return NULL;
 }
-double oracle_cpu_gcm_bench(int threads, int nsec, int secsize) {
-    static evp_t e;
+static evp_t gcm_evp;
+static int gcm_load(void) {
     static int loaded = 0;
+    evp_t *e = &gcm_evp;
     if (!loaded) {
         void *h = dlopen("libcrypto.so.3", RTLD_NOW | RTLD_LOCAL);
-        if (!h) return -1.0;
-        e.ctx_new = (void *(*)(void))dlsym(h, "EVP_CIPHER_CTX_new");
-        e.ctx_free = (void (*)(void *))dlsym(h, "EVP_CIPHER_CTX_free");
-        e.cipher = (const void *(*)(void))dlsym(h, "EVP_aes_256_gcm");
-        e.init = (int (*)(void *, const void *, void *, const unsigned char *, const unsigned char *))dlsym(
+        if (!h) return 0;
+        e->ctx_new = (void *(*)(void))dlsym(h, "EVP_CIPHER_CTX_new");
+        e->ctx_free = (void (*)(void *))dlsym(h, "EVP_CIPHER_CTX_free");
+        e->cipher = (const void *(*)(void))dlsym(h, "EVP_aes_256_gcm");
+        e->init = (int (*)(void *, const void *, void *, const unsigned char *, const unsigned char *))dlsym(
             h, "EVP_EncryptInit_ex");
-        e.update = (int (*)(void *, unsigned char *, int *, const unsigned char *, int))dlsym(h, "EVP_EncryptUpdate");
-        e.final = (int (*)(void *, unsigned char *, int *))dlsym(h, "EVP_EncryptFinal_ex");
-        e.ctrl = (int (*)(void *, int, int, void *))dlsym(h, "EVP_CIPHER_CTX_ctrl");
-        if (!e.ctx_new || !e.ctx_free || !e.cipher || !e.init || !e.update || !e.final || !e.ctrl) return -1.0;
+        e->update = (int (*)(void *, unsigned char *, int *, const unsigned char *, int))dlsym(h, "EVP_EncryptUpdate");
+        e->final = (int (*)(void *, unsigned char *, int *))dlsym(h, "EVP_EncryptFinal_ex");
+        e->ctrl = (int (*)(void *, int, int, void *))dlsym(h, "EVP_CIPHER_CTX_ctrl");
+        e->fetch = (void *(*)(void *, const char *, const char *))dlsym(h, "EVP_CIPHER_fetch");
+        e->cipher_free = (void (*)(void *))dlsym(h, "EVP_CIPHER_free");
+        if (!e->ctx_new || !e->ctx_free || !e->cipher || !e->init || !e->update || !e->final || !e->ctrl) return 0;
         loaded = 1;
     }
+    return 1;
+}
+
+/* threads x nsec seals; returns seconds (spawn included), -1 when unavailable */
+double oracle_cpu_gcm_bench(int threads, int nsec, int secsize) {
+    if (!gcm_load()) return -1.0;
     if (threads < 1) threads = 1;
     pthread_t *tid = (pthread_t *)malloc(sizeof(pthread_t) * threads);
     gcm_job_t *jobs = (gcm_job_t *)calloc(threads, sizeof(gcm_job_t));
     struct timespec t0, t1;
     clock_gettime(CLOCK_MONOTONIC, &t0);
     for (int t = 0; t < threads; t++) {
-        jobs[t].e = &e;
+        jobs[t].e = &gcm_evp;
         jobs[t].nsec = nsec;
         jobs[t].secsize = secsize;
         pthread_create(&tid[t], NULL, gcm_worker, &jobs[t]);
@@ -228,4 +256,42 @@ double oracle_cpu_gcm_bench(int threads, int nsec, int secsize) {
     free(jobs);
     if (!ok) return -1.0;
     return (double)(t1.tv_sec - t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - t0.tv_nsec);
+}
+
+/* Timed form: `threads` workers released together by a barrier seal secsize-byte
+ * sections until a shared deadline `seconds` later; returns the sections sealed
+ * (throughput = sections x secsize / seconds), -1 when unavailable. Thread start-up is
+ * outside the timed window, so T threads measure T cores, not spawn latency. */
+double oracle_cpu_gcm_bench_timed(int threads, double seconds, int secsize) {
+    if (!gcm_load()) return -1.0;
+    if (threads < 1) threads = 1;
+    pthread_t *tid = (pthread_t *)malloc(sizeof(pthread_t) * threads);
+    gcm_job_t *jobs = (gcm_job_t *)calloc(threads, sizeof(gcm_job_t));
+    pthread_barrier_t bar;
+    pthread_barrier_init(&bar, NULL, (unsigned)threads + 1);
+    struct timespec dl;
+    for (int t = 0; t < threads; t++) {
+        jobs[t].e = &gcm_evp;
+        jobs[t].secsize = secsize;
+        jobs[t].start = &bar;
+        jobs[t].deadline = &dl;
+        pthread_create(&tid[t], NULL, gcm_worker, &jobs[t]);
+    }
+    clock_gettime(CLOCK_MONOTONIC, &dl);  /* set before the release: workers read it after the barrier */
+    const long long ns = (long long)(seconds * 1e9);
+    dl.tv_sec += ns / 1000000000LL;
+    dl.tv_nsec += ns % 1000000000LL;
+    if (dl.tv_nsec >= 1000000000L) { dl.tv_sec += 1; dl.tv_nsec -= 1000000000L; }
+    pthread_barrier_wait(&bar);
+    int ok = 1;
+    long long total = 0;
+    for (int t = 0; t < threads; t++) {
+        pthread_join(tid[t], NULL);
+        ok &= jobs[t].ok;
+        total += jobs[t].done;
+    }
+    pthread_barrier_destroy(&bar);
+    free(tid);
+    free(jobs);
+    return ok ? (double)total : -1.0;
 }

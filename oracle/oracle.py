@@ -75,6 +75,8 @@ def lib() -> ctypes.CDLL:
         L.oracle_decrypt_batch.argtypes = [vp, vp, u64, vp, u64, vp, vp]
         L.oracle_cpu_gcm_bench.restype = ctypes.c_double
         L.oracle_cpu_gcm_bench.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int]
+        L.oracle_cpu_gcm_bench_timed.restype = ctypes.c_double
+        L.oracle_cpu_gcm_bench_timed.argtypes = [ctypes.c_int, ctypes.c_double, ctypes.c_int]
         _lib = L
     return _lib
 
@@ -338,3 +340,10 @@ def decrypt_batch(key: bytes, record):
 def cpu_gcm_bench(threads: int, nsec: int, secsize: int) -> float:
     """seconds for threads x nsec AES-256-GCM seals of secsize bytes (OpenSSL); -1 if unavailable"""
     return lib().oracle_cpu_gcm_bench(threads, nsec, secsize)
+
+
+def cpu_gcm_gib_s(threads: int, seconds: float, secsize: int = 1024) -> float:
+    """Aggregate OpenSSL AES-256-GCM seal rate of `threads` workers started together and
+    stopped by one deadline (thread start-up outside the window); -1 if unavailable."""
+    n = lib().oracle_cpu_gcm_bench_timed(threads, seconds, secsize)
+    return -1.0 if n < 0 else n * secsize / seconds / 2**30

@@ -209,3 +209,36 @@ def convert_request(frame: bytes, partition_id: int, checksum_mode: int = 0):
     hdr = bytearray(frame[:256])
     struct.pack_into("<I", hdr, 48, 256 + ah.batch_length)
     return 0, (0, 0, 0, 0, 0), bytes(hdr) + admitted
+
+
+# ---- read_message on a byte stream (core/message_bus/src/framing.rs:107-164) followed by
+# Message::<GenericHeader>::try_from (core/server_common/src/consensus_message.rs:468-500)
+ERR_CAPACITY, ERR_CONNECTION_CLOSED = 102, 25  # include/iggy_codec.h
+COMMAND_OFFSET, COMMAND_MAX = 60, 29  # GenericHeader.command; Command 0..=ForwardLogoutResult
+
+
+def read_frames(stream: bytes, cap: int, max_message_size: int = 64 << 20):
+    """Frames read one after another off `stream` until the first error or its end ->
+    [(rc, frame bytes or b"", stream position after the call)]. A frame larger than cap
+    is completed as a caller that grows its buffer would (iggy_frame_read_rest)."""
+    out, pos = [], 0
+    while True:
+        if len(stream) - pos < 256:  # read_exact of the header: EOF
+            out.append((ERR_CONNECTION_CLOSED, b"", len(stream)))
+            return out
+        hdr = stream[pos:pos + 256]
+        size = struct.unpack_from("<I", hdr, 48)[0]
+        if not 256 <= size <= max_message_size:
+            out.append((ERR_INVALID_COMMAND, b"", pos + 256))
+            return out
+        if size > cap:
+            out.append((ERR_CAPACITY, b"", pos + 256))  # then the caller resumes the frame
+        if len(stream) - pos < size:  # read_exact of the body: EOF
+            out.append((ERR_CONNECTION_CLOSED, b"", len(stream)))
+            return out
+        frame = stream[pos:pos + size]
+        pos += size
+        if frame[COMMAND_OFFSET] > COMMAND_MAX:  # CheckedBitPattern of Command (command.rs:90-95)
+            out.append((ERR_INVALID_COMMAND, b"", pos))
+            continue  # the body was consumed: the stream stays in sync
+        out.append((0, frame, pos))

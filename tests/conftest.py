@@ -18,6 +18,20 @@ def pytest_configure(config):
                                        "run explicitly with -m gpu_diag, never part of -m gpu")
 
 
+# Hot-path parity first: under -x a failure in a §8(f) widening module (records,
+# SDK, encryption) must not hide the core decode/encode parity suite, which would
+# otherwise sort after it alphabetically.
+_MODULE_ORDER = ["test_parity_gpu", "test_configs_gpu", "test_robust_gpu", "test_convert_gpu",
+                 "test_records_gpu", "test_sdk_gpu", "test_crypt_gpu"]
+
+
+def pytest_collection_modifyitems(session, config, items):
+    def rank(item):
+        mod = item.module.__name__.rsplit(".", 1)[-1] if item.module else ""
+        return _MODULE_ORDER.index(mod) if mod in _MODULE_ORDER else len(_MODULE_ORDER)
+    items.sort(key=rank)  # stable: file order is kept inside a module
+
+
 @pytest.fixture(scope="session")
 def golden_dir():
     return os.path.join(ROOT, "tests", "golden")

@@ -216,3 +216,43 @@ def test_producer_flush_busy_keeps_buffer(cx):
     assert out.tobytes()[r.offset:r.offset + r.length] == S.send_messages_body(st, tp, pt, batch, 500)
     assert p.pending()[:2] == (0, 0)
     p.close()
+
+
+def test_producer_flush_reused_reqs_after_busy(cx):
+    """A caller reusing one request array across flushes: a flush that
+    writes two requests, then one that hits BUSY on its first submit, must report no
+    request and leave no stale `sent` flag in the array; the buffer stays intact and the
+    retried flush is exact."""
+    from iggy_amd.abi import ProducerRequest
+    from iggy_amd.codec import Producer
+    from oracle import sdk_ref as S
+    p = Producer(cx, batch_length=0, batch_size=0, direct=False)
+    st = (S.ID_NUMERIC, (1).to_bytes(4, "little"))
+    tps = [(S.ID_NUMERIC, (k).to_bytes(4, "little")) for k in (2, 3)]
+    pt = (S.PART_BALANCED, b"")
+    reqs = (ProducerRequest * 16)()
+    ms = [_soa(300, 0, 200, seed=70 + k) for k in range(2)]
+    for tp, m in zip(tps, ms):
+        p.append(abi.Identifier.raw(*st), abi.Identifier.raw(*tp), abi.Partitioning.raw(*pt), _raw(m))
+    cap = 8192 + sum(48 * 300 + int(m["pls"].sum()) for m in ms)
+    rc, e, out, got = p.flush(cap=cap, max_reqs=16, reqs=reqs)
+    assert rc == 0 and len(got) == 2 and all(r.sent == 1 for r in got)
+    ms2 = [_soa(200, 0, 100, seed=80 + k) for k in range(2)]
+    for tp, m in zip(tps, ms2):
+        p.append(abi.Identifier.raw(*st), abi.Identifier.raw(*tp), abi.Partitioning.raw(*pt), _raw(m))
+    before = p.pending()
+    rec = O.synth_batch(20_000, 1024, 1024, seed=61)
+    tickets = [cx.decode_submit(rec, abi.INTEGRITY_VERIFY) for _ in range(8)]
+    rc, e, out, got = p.flush(cap=cap, max_reqs=16, reqs=reqs)
+    assert rc == abi.ERR_BUSY and got == []
+    assert reqs[0].sent == 0 and reqs[1].sent == 0
+    assert p.pending() == before
+    for t in tickets:
+        assert cx.wait(t).error.kind == 0
+    rc, e, out, got = p.flush(cap=cap, max_reqs=16, reqs=reqs)
+    assert rc == 0 and len(got) == 2
+    for r, tp, m in zip(got, tps, ms2):
+        orc, oe, batch = O.encode_batch(_raw(m))
+        assert r.sent == 1 and r.error.kind == 0
+        assert out.tobytes()[r.offset:r.offset + r.length] == S.send_messages_body(st, tp, pt, batch, 200)
+    p.close()

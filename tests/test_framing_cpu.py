@@ -96,3 +96,73 @@ def test_closed_descriptor_is_tcp_error():
     a.close()
     rc, e, _ = frame_read(fd, 4096)
     assert rc == abi.ERR_TCP_ERROR
+
+
+def test_frame_larger_than_the_buffer_resumes(pair):
+    """IGGY_ERR_CAPACITY leaves the body on the socket: the caller grows its buffer and
+    finishes the frame (iggy_frame_read_rest); the next frame then reads normally."""
+    a, b = pair
+    frames = [_frame(b"w" * 5000), _frame(b"v" * 10)]
+    t = _send(a, b"".join(frames))
+    rc, e, buf = frame_read(b.fileno(), 4096, grow=True)
+    assert rc == 0 and buf.tobytes() == frames[0] and buf.ctypes.data % 4096 == 0
+    rc, e, buf = frame_read(b.fileno(), 4096)
+    assert rc == 0 and buf.tobytes() == frames[1]
+    t.join()
+
+
+@pytest.mark.parametrize("command", [0, 5, 29, 30, 99, 255])
+def test_header_bit_pattern_checked_after_the_body(pair, command):
+    """Message::<GenericHeader>::try_from (consensus_message.rs:468-500): the command
+    byte at offset 60 must be a Command discriminant (command.rs:90-95, <= 29); a bad one
+    is InvalidCommand once the whole frame is read, so the next frame stays readable.
+    Checked against the stream restatement oracle/sdk_ref.read_frames."""
+    from oracle import sdk_ref as S
+    a, b = pair
+    bad = bytearray(_frame(b"q" * 3000)); bad[60] = command
+    hdr_only = bytearray(_frame(b"")); hdr_only[60] = command
+    good = _frame(b"r" * 77)
+    stream = bytes(bad) + bytes(hdr_only) + good
+    want = S.read_frames(stream, 1 << 16)
+    t = _send(a, stream)
+    for rc_want, frame_want, _ in want:
+        rc, e, buf = frame_read(b.fileno(), 1 << 16)
+        assert rc == rc_want and e.kind == rc_want
+        assert buf.tobytes() == frame_want
+    t.join()
+    assert [w[0] for w in want][:3] == ([abi.ERR_INVALID_COMMAND] * 2 if command > 29 else [0, 0]) + [0]
+
+
+def test_random_streams_match_the_restatement():
+    """Fuzz: random frame sequences (sizes inside and outside the bounds, bad commands,
+    frames above the buffer, a truncated tail) through the C reader and the restatement."""
+    from oracle import sdk_ref as S
+    rng = np.random.default_rng(44)
+    for trial in range(60):
+        parts = []
+        for _ in range(int(rng.integers(1, 6))):
+            body = rng.integers(0, 256, int(rng.integers(0, 3000)), dtype=np.uint8).tobytes()
+            f = bytearray(_frame(body))
+            if rng.random() < 0.2:
+                f[60] = int(rng.integers(0, 256))
+            if rng.random() < 0.1:
+                struct.pack_into("<I", f, 48, int(rng.integers(0, 400)))
+            parts.append(bytes(f))
+        stream = b"".join(parts)
+        if rng.random() < 0.3:
+            stream = stream[: int(rng.integers(0, len(stream) + 1))]
+        cap = int(rng.choice([512, 2048, 1 << 16]))
+        want = S.read_frames(stream, cap, max_message_size=1 << 20)
+        a, b = socket.socketpair(socket.AF_UNIX, socket.SOCK_STREAM)
+        try:
+            t = _send(a, stream)
+            for k, (rc_want, frame_want, _) in enumerate(want):
+                if rc_want == abi.ERR_CAPACITY:  # grow=True finishes that frame in the next call
+                    continue
+                rc, e, buf = frame_read(b.fileno(), cap, max_message_size=1 << 20, grow=True)
+                assert rc == rc_want, (trial, k)
+                assert buf.tobytes() == frame_want
+            t.join()
+        finally:
+            a.close()
+            b.close()

@@ -92,6 +92,54 @@ def test_variable_random_batches(cx, n, lo, hi, uh):
     _check_decode(cx, rec)
 
 
+def _device_decode(cx, rec, integrity, cap=None):
+    """decode_device on a torch-resident copy of rec: (result, positions[:frame_count])."""
+    import torch
+    n = rec.size // 48 + 1 if cap is None else cap
+    d_rec = torch.from_numpy(np.ascontiguousarray(rec)).to("cuda")
+    d_pos = torch.zeros(max(n, 1), dtype=torch.int64, device="cuda")
+    d_res = torch.zeros(ctypes.sizeof(abi.DecodeResult), dtype=torch.uint8, device="cuda")
+    s = torch.cuda.current_stream().cuda_stream
+    torch.cuda.synchronize()
+    assert cx.decode_device(d_rec.data_ptr(), rec.size, integrity, d_pos.data_ptr(), n, d_res.data_ptr(), s) == 0
+    torch.cuda.synchronize()
+    r = abi.DecodeResult.from_buffer_copy(d_res.cpu().numpy().tobytes())
+    return r, d_pos[: min(r.frame_count, n)].cpu().numpy()
+
+
+@pytest.mark.parametrize("shape", ["sealed_2000", "c3_120k", "small_frames_600k"])
+@pytest.mark.parametrize("integrity", [abi.INTEGRITY_LAYOUT_ONLY, abi.INTEGRITY_VERIFY])
+def test_general_walk_large_grids_device(cx, shape, integrity):
+    """The general walk on device-resident records far above the 3-12-WG grids of
+    test_configs_gpu: the sealed record of GPUTEST_r03's decrypt fault (4.3 MB, user
+    headers, ~68 WGs), a C3-shaped 120,000-frame record (~255 MB, every WG of the chip)
+    and 600,000 small frames (tiles of 16 frames). Positions and results exact."""
+    if shape == "sealed_2000":
+        from crypt_util import key_for, nonces_for, raw_record
+        raw = raw_record(2000, 64, 4096, seed=11 * 2000 + 64, uh_max=20)
+        rc, e, sealed = O.encrypt_batch(key_for(2003), raw, nonces_for(2000, 2004))
+        assert rc == 0
+        rec = np.frombuffer(sealed, dtype=np.uint8).copy()
+        assert rec.size == 4_325_343
+    elif shape == "c3_120k":
+        rec = O.synth_batch(120_000, 64, 4096, 0, seed=0xC3)
+    else:
+        rec = O.synth_batch(600_000, 0, 90, 0, seed=0x600)
+    r, pos = _device_decode(cx, rec, integrity)
+    orc, oe, oh, of = O.decode_batch_slice_with(rec, integrity)
+    assert (r.error.kind, r.frame_count) == (orc, len(of)), r.error.astuple()
+    assert r.header.astuple() == oh.astuple()
+    assert np.array_equal(pos, np.asarray(of, dtype=np.int64))
+    # a frame length broken three quarters in: the walk stops or re-routes there
+    bad = rec.copy()
+    struct.pack_into("<I", bad, 256 + int(of[3 * len(of) // 4]) + 36, 5)
+    r, pos = _device_decode(cx, bad, integrity)
+    orc, oe, oh, of2 = O.decode_batch_slice_with(bad, integrity)
+    assert r.error.astuple() == oe.astuple()
+    if orc == 0:
+        assert np.array_equal(pos, np.asarray(of2, dtype=np.int64))
+
+
 @pytest.mark.parametrize("shift", [1, 3, 8, 13])
 def test_unaligned_host_buffer(cx, shift):
     """The host-buffer entry point reading a caller buffer at an odd host address
