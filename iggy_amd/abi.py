@@ -324,3 +324,8 @@ class ProducerConfig(ctypes.Structure):
 class ProducerRequest(ctypes.Structure):
     _fields_ = [("offset", u64), ("length", u64), ("first_message", u64), ("messages", u64),
                 ("entry", u32), ("sent", u32), ("error", WireError)]
+
+
+class PollFragment(ctypes.Structure):
+    """iggy_poll_fragment: one host span of a poll reply (PollFragments)."""
+    _fields_ = [("data", ctypes.c_void_p), ("len", u64)]

@@ -119,6 +119,7 @@ def load(path: str) -> ctypes.CDLL:
     L.iggy_codec_segment_write_device.argtypes = [vp, ci, u64, vp, u64, ci, ctypes.POINTER(u64)]
     L.iggy_codec_encrypt_batch_device.argtypes = [vp, vp, vp, u64, vp, vp, u64, vp, vp]
     L.iggy_codec_decrypt_batch_device.argtypes = [vp, vp, vp, u64, vp, u64, vp, vp]
+    L.iggy_codec_build_polled_body.argtypes = [vp, u32, u64, vp, u64, vp, vp, u64, ctypes.POINTER(u64), vp]
     L.iggy_codec_profile_enable.argtypes = [vp, ci]
     L.iggy_codec_profile_read.argtypes = [vp, ci, vp, vp]
     L.iggy_codec_host_register.argtypes = [vp, vp, u64]
@@ -420,6 +421,26 @@ class Codec:
             raise ValueError("AES-256 key must be 32 bytes")
         k = ctypes.create_string_buffer(bytes(key), 32)
         return self._L.iggy_codec_decrypt_batch_device(self._h, k, d_record, length, d_out, cap, d_result, stream)
+
+    def build_polled_body(self, partition_id: int, current_offset: int, fragments, key: bytes | None = None,
+                          cap: int | None = None):
+        """build_polled_messages_body (core/server/src/responses.rs:1666-1714) over host
+        fragments (bytes / numpy) -> (rc, WireError, body bytes)."""
+        arrs = [_np(f) for f in fragments]
+        spans = (abi.PollFragment * max(len(arrs), 1))()
+        for k, a in enumerate(arrs):
+            spans[k].data = a.ctypes.data if a.size else None
+            spans[k].len = a.size
+        total = sum(a.size for a in arrs)
+        cap = 16 + total if cap is None else cap
+        out = np.zeros(max(cap, 1), dtype=np.uint8)
+        n = u64(0)
+        e = WireError()
+        k = np.frombuffer(bytes(key), dtype=np.uint8).copy() if key is not None else None
+        rc = self._L.iggy_codec_build_polled_body(self._h, partition_id, current_offset, spans, len(arrs),
+                                                  k.ctypes.data if k is not None else None, out.ctypes.data, cap,
+                                                  ctypes.byref(n), ctypes.byref(e))
+        return rc, e, out[: n.value].tobytes()
 
     def select_slice_device(self, d_record: int, d_frame_pos: int, nframes: int, query: SliceQuery,
                             d_out: int, d_header: int | None = None, stream: int | None = None) -> int:

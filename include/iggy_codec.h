@@ -325,6 +325,31 @@ int iggy_codec_decrypt_batch_device(iggy_codec_ctx *ctx, const uint8_t *key, con
                                     uint64_t len, uint8_t *d_out, uint64_t cap, iggy_crypt_result *d_result,
                                     void *stream);
 
+/* ------------------------------------------------------ poll reply body */
+/* One poll fragment (PollFragments, core/server/src/responses.rs:1666-1680): a stored
+ * record served whole, or a rewritten 256-B batch header followed by a body slice
+ * (journal.rs:1096-1137; iggy_codec_walk_disk_chunk's iggy_chunk_fragment gives both:
+ * full body = chunk + batch_pos, else headers[k] then chunk[body_start, body_end)). */
+typedef struct iggy_poll_fragment {
+    const uint8_t *data;  /* host memory */
+    uint64_t len;
+} iggy_poll_fragment;
+
+/* build_polled_messages_body (core/server/src/responses.rs:1666-1714) -> out =
+ * [partition_id u32][current_offset u64][count u32][records...]: the fragments are
+ * concatenated and walked record by record (BatchHeader::decode and the record's end
+ * inside the stream, else IGGY_ERR_INVALID_COMMAND); with key (32 B, nullable) every
+ * record is decrypted (decrypt_batch_record, server_common/src/send_messages.rs:364-415:
+ * IGGY_ERR_CANNOT_DECRYPT_DATA for a failing section, IGGY_ERR_INVALID_COMMAND for a
+ * malformed record) on the GPU -- one H2D, every record's decrypt enqueued back to back,
+ * one D2H -- else copied as is; count = the records' message_count summed with
+ * checked_add (overflow -> IGGY_ERR_INVALID_COMMAND). Errors come in the reference's
+ * order (record by record). cap too small -> IGGY_ERR_CAPACITY (err->a = bytes needed).
+ * *out_len = the body's length. */
+int iggy_codec_build_polled_body(iggy_codec_ctx *ctx, uint32_t partition_id, uint64_t current_offset,
+                                 const iggy_poll_fragment *frags, uint64_t nfrags, const uint8_t *key,
+                                 uint8_t *out, uint64_t cap, uint64_t *out_len, iggy_wire_error *err);
+
 /* ------------------------------------------------- poll-path slicing (a17+) */
 /* MessageLookup (core/partitions/src/journal.rs:68-95). */
 #define IGGY_LOOKUP_OFFSET 0

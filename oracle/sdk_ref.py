@@ -242,3 +242,46 @@ def read_frames(stream: bytes, cap: int, max_message_size: int = 64 << 20):
             out.append((ERR_INVALID_COMMAND, b"", pos))
             continue  # the body was consumed: the stream stays in sync
         out.append((0, frame, pos))
+
+
+# ---- the poll reply body: build_polled_messages_body (core/server/src/responses.rs:1666-1714)
+ERR_CANNOT_DECRYPT_DATA = 24
+_KEEP = (0, ERR_INVALID_COMMAND, ERR_CANNOT_DECRYPT_DATA, 3, 4)  # + InvalidBatch/MessageChecksum
+
+
+def build_polled_messages_body(partition_id: int, current_offset: int, fragments, key: bytes | None = None):
+    """fragments: [bytes] in order -> (rc, err tuple, body bytes). Decryption through
+    the C restatement (oracle.decrypt_batch = decrypt_batch_record); its decode errors
+    pass batch_error (server_common/src/send_messages.rs:52-66): InvalidCommand."""
+    from oracle import oracle as O
+
+    stream = b"".join(bytes(f) for f in fragments)
+    body = bytearray(struct.pack("<IQI", partition_id, current_offset, 0))
+    count, pos = 0, 0
+    inv = (ERR_INVALID_COMMAND, (ERR_INVALID_COMMAND, 0, 0, 0, 0), b"")
+    while pos < len(stream):
+        rest = stream[pos:]
+        if len(rest) < 256:
+            return inv
+        bl = struct.unpack_from("<Q", rest, 32)[0]
+        if bl < 256 or any(rest[52:256]):
+            return inv
+        end = pos + bl
+        if end > len(stream):
+            return inv
+        record = stream[pos:end]
+        if key is not None:
+            rc, e, dec = O.decrypt_batch(key, record)
+            if rc:
+                kind = rc if rc in _KEEP else ERR_INVALID_COMMAND
+                t = tuple(e.astuple()) if kind == rc else (kind, 0, 0, 0, 0)
+                return kind, (kind,) + t[1:], b""
+            body += dec
+        else:
+            body += record
+        count += struct.unpack_from("<I", rest, 48)[0]
+        if count > 0xFFFFFFFF:
+            return inv
+        pos = end
+    struct.pack_into("<I", body, 12, count)
+    return 0, (0, 0, 0, 0, 0), bytes(body)

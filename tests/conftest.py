@@ -22,7 +22,7 @@ def pytest_configure(config):
 # SDK, encryption) must not hide the core decode/encode parity suite, which would
 # otherwise sort after it alphabetically.
 _MODULE_ORDER = ["test_parity_gpu", "test_configs_gpu", "test_robust_gpu", "test_convert_gpu",
-                 "test_records_gpu", "test_sdk_gpu", "test_crypt_gpu"]
+                 "test_records_gpu", "test_sdk_gpu", "test_pollbody_gpu", "test_crypt_gpu"]
 
 
 def pytest_collection_modifyitems(session, config, items):
