@@ -11,6 +11,7 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -614,14 +615,35 @@ bool records_all_planned(const uint8_t *h_base, const RecIn *recs, size_t K) {
 // Wait for a kernel to raise the host-mapped completion flag (a spin: the host
 // round trip of a stream sync or a result copy is what small host-buffer calls pay
 // most for). If the stream drains without the flag, the launch failed.
+// Bounded: a launch that neither raises the flag nor drains within kHostWaitLimit
+// (the kernels' own spin guards are 4 s) returns IGGY_ERR_TIMEOUT to the caller's
+// thread instead of holding it.
+constexpr double kHostWaitLimitS = 10.0;
 int wait_host_flag(iggy_codec_ctx *c, uint32_t v) {
     volatile uint32_t *flag = c->omap.hp<volatile uint32_t>();
+    auto dbg = [&](const char *what, int rc) {
+        if (getenv("IGGY_CODEC_DEBUG"))
+            fprintf(stderr, "iggy_codec: wait_host_flag(%u): %s (flag %u)\n", v, what, *flag);
+        return rc;
+    };
+    const auto t0 = std::chrono::steady_clock::now();
     for (uint64_t i = 1;; ++i) {
         if (__atomic_load_n(flag, __ATOMIC_ACQUIRE) == v) return 0;
         if ((i & 1023) == 0) {
             const hipError_t q = hipStreamQuery(c->stream);
-            if (q == hipSuccess) return __atomic_load_n(flag, __ATOMIC_ACQUIRE) == v ? 0 : IGGY_ERR_DEVICE;
-            if (q != hipErrorNotReady) return IGGY_ERR_DEVICE;
+            if (q == hipSuccess) {
+                // the stream drained: the flag store (system scope, over PCIe) may still be
+                // in flight behind the completion signal for a moment; then it is final
+                for (int k = 0; k < 100000; ++k) {
+                    if (__atomic_load_n(flag, __ATOMIC_ACQUIRE) == v) return 0;
+                    __builtin_ia32_pause();
+                }
+                return dbg("stream drained without the flag", IGGY_ERR_DEVICE);
+            }
+            if (q != hipErrorNotReady) return dbg(hipGetErrorString(q), IGGY_ERR_DEVICE);
+            if ((i & 0xfffff) == 0 &&
+                std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > kHostWaitLimitS)
+                return dbg("time limit", IGGY_ERR_TIMEOUT);
         }
         __builtin_ia32_pause();
     }

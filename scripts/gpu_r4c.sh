@@ -7,7 +7,7 @@ R=${GRAFT_REPO_ROOT:-$(pwd)}
 O=$R/gpurun_out
 mkdir -p $O
 cd $R
-timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 240 --timeout-method thread > $O/t3.log 2>&1
+IGGY_CODEC_DEBUG=1 timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 240 --timeout-method thread > $O/t3.log 2>&1
 rc=$?; echo "pytest rc=$rc" >> $O/t3.log; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 400 python -u bench.py > $O/bench_a.log 2>&1
 rc=$?; echo "bench rc=$rc" >> $O/bench_a.log; [ $rc -eq 0 ] || exit $rc

@@ -3,6 +3,13 @@ import sys
 
 import pytest
 
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+# the HIP runtime settings of the package (no on-the-fly pinning of pageable host
+# ranges, iggy_amd/__init__.py) before torch initialises the runtime
+import iggy_amd  # noqa: F401,E402
+
 # torch first: its bundled HIP runtime then serves the codec library too (same
 # sonames; see iggy_amd/codec.py load())
 import torch  # noqa: F401,E402
