@@ -48,8 +48,8 @@ def main():
         "messages": n, "payload": pl, "kernel": target[0], "dispatches": len(vals),
         "fetch_size_kb_median": kb, "hbm_bytes_per_decode": int(hbm_bytes),
         "algorithmic_bytes": batch + 8 * n, "ratio_to_algorithmic": round(hbm_bytes / (batch + 8 * n), 4),
-        "source": "rocprofv3 --pmc FETCH_SIZE on bench.py (profiles/pmc_fetch.json; x2 per "
-                  "MI355X_MICROARCH.md gfx950 FETCH_SIZE note)",
+        "source": f"rocprofv3 --pmc FETCH_SIZE on bench.py at HEAD {os.environ.get('PMC_HEAD', '?')} "
+                  f"({os.environ.get('PMC_PROFILE', 'profiles/')}; x2 per MI355X_MICROARCH.md gfx950 FETCH_SIZE note)",
         "all_kernels_kb_median": {k: statistics.median(v) for k, v in per_kernel.items()},
     }
     path = os.path.join(ROOT, "profiles", "pmc_fetch.json")
