@@ -28,9 +28,6 @@
 #include "poll.hip"
 #include "slice.hip"
 #include "crypt.hip"
-#ifdef IGGY_CODEC_DIAG
-#include "decode_stream.hip"  // next-round candidate: diagnostic build only (dbg bit 0x200000)
-#endif
 
 using namespace iggy;
 
@@ -170,7 +167,6 @@ struct iggy_codec_ctx {
     // multi-record decode (decode_records.hip): tasks | states | wg map, block sums,
     // results, and the pinned staging of the task table (uploaded in one copy)
     DevBuf rtab, rbsums, rres, clinks, rstate, rcount;
-    DevBuf sx;  // (diagnostic build) the streamed general decode's counters and flags
     HostMap rmap;  // task table + workgroup map (read by the kernel in place when small)
     HostMap cmap;  // chunk-walk candidates (read in place)
     HostMap omap;  // [0, 64): completion flag; then results / positions / chunk-walk outputs
@@ -384,32 +380,6 @@ int enqueue_decode(iggy_codec_ctx *c, const uint8_t *d_body, uint64_t len, int i
                            cap, d_res, ds, c->epoch, au, diag_bits(c));
     prof_end(c, 0, s);
     HIP_OK(hipGetLastError());
-#ifdef IGGY_CODEC_DIAG
-    if (diag_bits(c) & 0x200000) {  // the streamed general decode (decode_stream.hip)
-        const uint64_t L = std::max<uint64_t>(len, 1 << 20);
-        const uint64_t nt = L / kStT + 2, ng = nt / kGrpTiles + 2, nbk = (44 + 8 * (L / 48 + 2)) / 1024 + 4;
-        const uint64_t words = 2 * nt + 3 * ng + nbk + 2;
-        if (c->sx.ensure(words * 4)) return IGGY_ERR_DEVICE;
-        StreamScratch ss;
-        uint32_t *w = c->sx.as<uint32_t>();
-        ss.tile_bad = w; w += nt;
-        ss.tile_flags = w; w += nt;
-        ss.grp_done = w; w += ng;
-        ss.grp_ready = w; w += ng;
-        ss.grp_linked = w; w += ng;
-        ss.blk_count = w; w += nbk;
-        ss.final_flag = w; w += 1;
-        ss.timed_out = w;
-        if (verify)
-            hipLaunchKernelGGL(k_decode_stream<true>, dim3(ggrid), dim3(kStThreads), kStLds, s, d_body, len, d_pos,
-                               cap, d_res, gs, ss);
-        else
-            hipLaunchKernelGGL(k_decode_stream<false>, dim3(ggrid), dim3(kStThreads), kStLds, s, d_body, len, d_pos,
-                               cap, d_res, gs, ss);
-        HIP_OK(hipGetLastError());
-        return 0;
-    }
-#endif
     if (verify) {
         hipLaunchKernelGGL(k_decode_general<true>, dim3(ggrid), dim3(kGenThreads), 0, s, d_body, len, d_pos,
                            cap, d_res, gs);
@@ -800,13 +770,6 @@ int iggy_codec_create(int device, iggy_codec_ctx **out) {
             hipFuncSetAttribute((const void *)k_decode_uniform<false>,
                                 hipFuncAttributeMaxDynamicSharedMemorySize, kUniformLds) != hipSuccess)
             r = IGGY_ERR_DEVICE;
-#ifdef IGGY_CODEC_DIAG
-        if (hipFuncSetAttribute((const void *)k_decode_stream<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                kStLds) != hipSuccess ||
-            hipFuncSetAttribute((const void *)k_decode_stream<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                kStLds) != hipSuccess)
-            r = IGGY_ERR_DEVICE;
-#endif
     }
     if (!r) {
         // the general decode's grid barriers need every WG co-resident
@@ -863,7 +826,7 @@ void iggy_codec_destroy(iggy_codec_ctx *c) {
                       &c->gbsums, &c->dresult, &c->din, &c->dpos, &c->dout, &c->epl, &c->euh,
                       &c->etile, &c->ecs, &c->emisc, &c->eids, &c->eots, &c->epay, &c->eplen,
                       &c->euhb, &c->euhl, &c->hbsums, &c->ppos, &c->pmsgs, &c->pres, &c->cwk, &c->sl, &c->slres, &c->cr,
-                      &c->rtab, &c->rbsums, &c->rres, &c->clinks, &c->rstate, &c->rcount, &c->sx, &c->pbres};
+                      &c->rtab, &c->rbsums, &c->rres, &c->clinks, &c->rstate, &c->rcount, &c->pbres};
     for (DevBuf *b : bufs) b->release();
     if (c->h_pinned) (void)hipHostFree(c->h_pinned);
     if (c->pb_pinned) (void)hipHostFree(c->pb_pinned);

@@ -642,6 +642,7 @@ struct LgLane {  // per-lane constants
     uint32_t l, m, par, fg, poff;
     uint64_t s0[8], s1[8];
     uint64_t key0, key1, init0, init1, last0, last1, mrg0, mrg1;
+    uint64_t wsec[4];  // lane 0 of frame fg: secret word k + fg of the block's word t = 8k + fg, k = 4 q + wave
 };
 
 __device__ __forceinline__ int64_t lg_frame_index(uint64_t u, uint32_t w, uint32_t fg) {
@@ -691,7 +692,14 @@ __device__ __forceinline__ void lg_issue(const uint8_t *blob, const LgPlan &pl, 
 #pragma unroll
         for (int q = 0; q < 8; ++q) glds16((2 * q + c.par < pl.ns) ? hb + 128 * q : fb, slot + 1024u * q);
     }
-    glds16(fin && !c.par ? fb + 8 + pl.L - 64 + 16 * c.m : fb, slot + 8u * 1024u);
+    // ninth load: even lanes the last-stripe piece; lane 1 the frame's own start (its
+    // stored checksum); lane 3 the NEXT frame's start (its stored checksum, for the
+    // batch-checksum word that straddles the two frames, lg_words); lanes 5, 7 a sink
+    const int64_t inx = i + 1;
+    const bool nvalid = inx >= 0 && (uint64_t)inx < pl.N;
+    const uint8_t *x9 = !c.par ? (fin ? fb + 8 + pl.L - 64 + 16 * c.m : fb)
+                               : (c.m == 1 && fin && nvalid) ? blob + (uint64_t)inx * pl.S : fb;
+    glds16(x9, slot + 8u * 1024u);
 }
 __device__ __forceinline__ void lg_read(const uint8_t *smem, uint32_t slot, int lane, LgBuf &B) {
     const uint8_t *p = smem + slot + 16u * (uint32_t)lane;
@@ -708,7 +716,7 @@ __device__ __forceinline__ void lg_piece(uint64_t &a0, uint64_t &a1, uint4 p, ui
 }
 
 struct LgState {
-    uint64_t a0, a1, stored;
+    uint64_t a0, a1, stored, next;  // lane 0 of a frame: its stored checksum, the next frame's
     uint32_t sink;  // filler loads' values land here (keeps their loads live)
     bool sbad;
 };
@@ -724,6 +732,7 @@ __device__ __forceinline__ bool lg_process(const LgPlan &pl, const LgLane &c, co
         for (int q = 0; q < 8; ++q) st.sink += B.v[q].x ^ B.v[q].w;
         st.sink += B.x.y ^ B.x.x;
         st.stored = 0;
+        st.next = 0;
         return ONE || b + 1 == nsteps;
     }
     if (ONE || b == 0) {
@@ -771,11 +780,13 @@ __device__ __forceinline__ bool lg_process(const LgPlan &pl, const LgLane &c, co
     const uint64_t h = avalanche(pl.L * P64_1 + t);
     const int64_t i = lg_frame_index(u, w, c.fg);
     const bool valid = i >= 0 && (uint64_t)i < pl.N;
-    // the stored checksum, loaded by the odd lane of each pair, for the even lane
+    // the stored checksum, loaded by lane 1 of the frame's lanes, for lane 0; the next
+    // frame's, loaded by lane 3, lands in lane 2 and then (quad swap) in lane 0 too
     const uint64_t sraw = (uint64_t)B.x.x | ((uint64_t)B.x.y << 32);
     const uint64_t stored = dpp64<kDppXor1>(sraw);
     st.stored = stored;
-    const bool mism = valid && !c.par && h != stored;
+    st.next = dpp64<kDppXor2>(stored);
+    const bool mism = valid && c.l == 0 && h != stored;
     const uint64_t mb = __ballot(mism);
     if (mb) {  // the group's first mismatching frame (lowest lane)
         const int leader = __builtin_ctzll(mb);
@@ -795,78 +806,96 @@ __device__ __forceinline__ bool lg_process(const LgPlan &pl, const LgLane &c, co
     return true;
 }
 
-// ---- per-WG unit combine in LDS (after the lane-group rings)
-// The 4 producer waves deposit each unit's stored checksums in LDS; the WG's fifth
-// wave publishes the unit's sums. Publishing from the producer waves themselves
-// cost +81 us per C2 decode: a producer's constant-vmcnt wait three steps later
-// must also cover its write-through stores, whose acknowledgements are slow under
-// the full read stream (diag ablation, scripts/diag_decode.py dbg 1 vs 129).
+// ---- per-WG block combine in LDS (after the lane-group rings)
+// The batch-checksum words of a 128-frame block are formed by the producer lanes
+// that hold the stored checksums: lane 0 of each frame (stored checksum from lane 1,
+// the NEXT frame's from lane 3's extra load, lg_issue) forms the frame's word
+// t = 8k + fg (k = 4 unit + wave: the frame group), m = 128 b + t, accumulator
+// m & 7 = fg, and the 8 groups' x / y parts are combined with one DPP row rotation;
+// each group then adds its 8 accumulator contributions into the block's LDS slot
+// (ds_add_u64, 8 lanes) and counts itself in. The WG's fifth wave publishes a block
+// once its 16 groups are in: 8 sums read back, the slot zeroed and released, one
+// 128-B record stored. The block's last word (t = 127, straddling into the next
+// block) stays the gatherer's, from the spare bytes (first_lo of frame t = 0, last_hi
+// of frame t = 127, written by the two groups that hold them).
+// Round 3 had the publisher form all 127 words from the 128 deposited checksums
+// (two words, a 64-bit 8/16/32 shuffle reduction and the 8-way spread per block):
+// ~20 us of a C2 launch. Publishing from the producer waves
+// themselves (global stores) cost +81 us: a producer's constant-vmcnt wait three steps
+// later must also cover its write-through stores, whose acknowledgements are slow
+// under the full read stream -- the LDS adds here are not vector-memory operations.
 constexpr uint32_t kLgSlots = 4;    // per wave: 1 step being hashed + 3 in flight (36 KiB)
-constexpr uint32_t kUcSlots = 16;   // units the producers may run ahead of the publisher (4 blocks)
-constexpr uint32_t kUcOff = 4 * kLgSlots * kLgStepBytes;  // [kUcSlots][32] u64, then cnt[], gen[]
-constexpr uint32_t kLgLds = kUcOff + kUcSlots * 256 + 2 * 4 * kUcSlots;
-__device__ __forceinline__ uint32_t *uc_cnt(uint8_t *smem) { return (uint32_t *)(smem + kUcOff + 256u * kUcSlots); }
-__device__ __forceinline__ uint32_t *uc_gen(uint8_t *smem) { return uc_cnt(smem) + kUcSlots; }
+constexpr uint32_t kBsSlots = 8;    // blocks the producers may run ahead of the publisher
+constexpr uint32_t kBsOff = 4 * kLgSlots * kLgStepBytes;  // [kBsSlots] acc[8] u64, spare[2] u32, cnt[], gen[]
+constexpr uint32_t kLgLds = kBsOff + 80 * kBsSlots;
+__device__ __forceinline__ uint64_t *bs_acc(uint8_t *smem, uint32_t s) { return (uint64_t *)(smem + kBsOff + 64u * s); }
+__device__ __forceinline__ uint32_t *bs_spare(uint8_t *smem, uint32_t s) {
+    return (uint32_t *)(smem + kBsOff + 64u * kBsSlots + 8u * s);
+}
+__device__ __forceinline__ uint32_t *bs_cnt(uint8_t *smem) { return (uint32_t *)(smem + kBsOff + 72u * kBsSlots); }
+__device__ __forceinline__ uint32_t *bs_gen(uint8_t *smem) { return bs_cnt(smem) + kBsSlots; }
+constexpr int kDppRowRor8 = 0x128;  // row_ror:8: lane r of a 16-lane row <- lane r ^ 8
 
-// Producer wave w deposits its group's 8 stored checksums for the WG's j-th unit
-// (slot j % kUcSlots, once the publisher has released that slot's previous unit).
-__device__ __forceinline__ void lg_deposit(uint8_t *smem, const LgLane &c, uint64_t j, uint32_t wave, int lane,
-                                           uint64_t stored, uint64_t t_start) {
-    const uint32_t s = (uint32_t)(j % kUcSlots), gen = (uint32_t)(j / kUcSlots);
-    uint64_t *slotv = (uint64_t *)(smem + kUcOff + 256u * s);
-    while (__hip_atomic_load(&uc_gen(smem)[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != gen) {
+// Frame group (unit j of this WG, wave) adds its words to block jb = j / 4's slot.
+__device__ __forceinline__ void lg_words(uint8_t *smem, const LgPlan &pl, const LgLane &c, uint64_t b, uint64_t j,
+                                         uint32_t wave, int lane, const LgState &st, uint64_t t_start) {
+    const uint64_t jb = j >> 2;
+    const uint32_t q = (uint32_t)(j & 3);
+    const uint32_t s = (uint32_t)(jb % kBsSlots), gen = (uint32_t)(jb / kBsSlots);
+    const uint32_t k = 4 * q + wave;  // frame group of the block (frames 128 b - 6 + 8 k ..)
+    const uint32_t t = 8 * k + c.fg;
+    const uint64_t m = 128 * b + t;
+    const bool use = c.l == 0 && t != 127 && m >= 6 && m < pl.Mreg && !pl.nopub;
+    uint64_t x = 0, y = 0;
+    if (use) {
+        const uint64_t v = (st.stored >> 32) | (st.next << 32);
+        const uint64_t sec = q == 0 ? c.wsec[0] : q == 1 ? c.wsec[1] : q == 2 ? c.wsec[2] : c.wsec[3];
+        y = v;
+        x = mul32x32(v ^ sec);
+    }
+    const uint64_t a = x + dpp64<kDppRowRor8>(y);  // lane 8 fg: acc[fg] (x of word fg, y of word fg ^ 1)
+    while (__hip_atomic_load(&bs_gen(smem)[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != gen) {
         __builtin_amdgcn_s_sleep(1);
         if (rt_now() - t_start > kSpinLimitTicks) return;  // bug guard: the consumer times out
     }
-    if (c.l == 0) slotv[8 * wave + c.fg] = stored;
+    if (c.l == 0) {
+        __hip_atomic_fetch_add(&bs_acc(smem, s)[c.fg], a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (k == 0 && c.fg == 0) bs_spare(smem, s)[0] = (uint32_t)st.stored;           // frame t = 0: lo32
+        if (k == 15 && c.fg == 7) bs_spare(smem, s)[1] = (uint32_t)(st.stored >> 32);  // frame t = 127: hi32
+    }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    if (lane == 0) __hip_atomic_fetch_add(&uc_cnt(smem)[s], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    if (lane == 0) __hip_atomic_fetch_add(&bs_cnt(smem)[s], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
-// The publisher wave: blocks g, g + np, ... in order, each as soon as its 4 units
-// are deposited: words t = 0..126 of the block from its 128 stored checksums (two
-// per lane), then the slots are released and the block record stored.
+// The publisher wave: blocks g, g + np, ... in order, each once its 16 frame groups
+// are in: the 8 sums read, the slot zeroed and released, the block record stored.
 __device__ __forceinline__ void lg_publisher(uint8_t *smem, const LgPlan &pl, const DecodeScratch &sc,
                                              uint32_t epoch, uint32_t g, uint32_t np, int lane, uint32_t dbg) {
     const uint64_t t_start = rt_now();
-    // the secret word of checksum word m = 128b + lane (and + 64) depends on the lane
-    // only: (m >> 3) & 15 = lane >> 3 (+ 8), m & 7 = lane & 7. Loaded once here: a
-    // runtime-indexed table read per block is a vector-memory load that waits behind
-    // the producers' whole read stream, and a publisher that falls behind stalls the
-    // producers on the unit slots.
-    const uint64_t sec_lo = kSecretW8[(lane >> 3) + (lane & 7)];
-    const uint64_t sec_hi = kSecretW8[8 + (lane >> 3) + (lane & 7)];
     const uint64_t blocks = 2 * pl.nchunks;
     if (g >= blocks) return;
     const uint64_t mine = (blocks - g + np - 1) / np;
-    const uint64_t *vals = (const uint64_t *)(smem + kUcOff);
     for (uint64_t jb = 0; jb < mine; ++jb) {
-        const uint32_t s0 = (uint32_t)((4 * jb) % kUcSlots), gen = (uint32_t)((4 * jb) / kUcSlots);
-        bool ok = true;
-        for (uint32_t q = 0; q < 4 && ok; ++q) {
-            while (__hip_atomic_load(&uc_cnt(smem)[s0 + q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != 4u) {
-                __builtin_amdgcn_s_sleep(1);
-                if (rt_now() - t_start > kSpinLimitTicks) { ok = false; break; }  // bug guard
-            }
+        const uint32_t s = (uint32_t)(jb % kBsSlots), gen = (uint32_t)(jb / kBsSlots);
+        while (__hip_atomic_load(&bs_cnt(smem)[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != 16u) {
+            __builtin_amdgcn_s_sleep(1);
+            if (rt_now() - t_start > kSpinLimitTicks) return;  // bug guard
         }
-        if (!ok) return;
-        // block-relative checksum t lives in slot s0 + (t >> 5), entry t & 31
-        const uint64_t *bv = vals + 32u * s0;
-        const uint64_t c0 = bv[lane], n0 = bv[lane + 1], c1 = bv[64 + lane];
-        const uint64_t n1 = lane < 63 ? bv[65 + lane] : 0;
-        const uint32_t first_lo = (uint32_t)bv[0];
-        const uint32_t last_hi = (uint32_t)(bv[127] >> 32);
+        const uint32_t t = (uint32_t)lane & 15;
+        const uint64_t a = bs_acc(smem, s)[t >> 1];  // granule t = half (t & 1) of acc[t >> 1]
+        const uint32_t first_lo = bs_spare(smem, s)[0], last_hi = bs_spare(smem, s)[1];
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        if (lane < 4) {
-            __hip_atomic_store(&uc_cnt(smem)[s0 + lane], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            __hip_atomic_store(&uc_gen(smem)[s0 + lane], gen + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        }
+        if (lane < 8) bs_acc(smem, s)[lane] = 0;
+        if (lane == 0) bs_cnt(smem)[s] = 0;
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // zeroed before the slot goes back
+        if (lane == 0) __hip_atomic_store(&bs_gen(smem)[s], gen + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         if (!pl.long_cs || pl.nopub) continue;
         const uint64_t b = g + jb * np;
-        uint64_t x = 0, y = 0;
-        word_contrib_s(pl.Mreg, 128 * b + lane, c0, n0, true, sec_lo, x, y);
-        word_contrib_s(pl.Mreg, 128 * b + 64 + lane, c1, n1, lane < 63, sec_hi, x, y);
-        publish_block(sc, epoch, b, lane, reduce_acc8(x, y), first_lo, last_hi);
+        const uint32_t data = (t & 1) ? (uint32_t)(a >> 32) : (uint32_t)a;
+        const uint32_t sp = t < 4 ? (first_lo >> (8 * t)) & 0xffu : t < 8 ? (last_hi >> (8 * (t - 4))) & 0xffu : 0u;
+        if (lane < 16)
+            __hip_atomic_store(block_rec(sc, b) + t, (uint64_t)data | ((uint64_t)sp << 32) | ((uint64_t)epoch << 40),
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if ((dbg & 512) && b < 2 && lane == 0) ((uint64_t *)(sc.small + 256))[11 + b] = rt_now();
     }
 }
@@ -891,12 +920,16 @@ __device__ __forceinline__ void produce_lg(const uint8_t *blob, const LgPlan &pl
     c.init0 = c.par ? 0 : kAccInit[2 * c.m]; c.init1 = c.par ? 0 : kAccInit[2 * c.m + 1];
     c.last0 = kSecretLast[2 * c.m]; c.last1 = kSecretLast[2 * c.m + 1];
     c.mrg0 = kSecretMerge[2 * c.m]; c.mrg1 = kSecretMerge[2 * c.m + 1];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) c.wsec[q] = kSecretW8[4 * q + wave + c.fg];
     // materialise every lane constant here: the hot loop then holds no
     // compiler-tracked load, so its only vmcnt waits are the explicit ones
 #pragma unroll
     for (int q = 0; q < 8; ++q) { pin_after_wait(c.s0[q]); pin_after_wait(c.s1[q]); }
     pin_after_wait(c.key0); pin_after_wait(c.key1); pin_after_wait(c.init0); pin_after_wait(c.init1);
     pin_after_wait(c.last0); pin_after_wait(c.last1); pin_after_wait(c.mrg0); pin_after_wait(c.mrg1);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) pin_after_wait(c.wsec[q]);
     const uint64_t blocks = 2 * pl.nchunks;                // 128-frame blocks (tail blocks hold invalid frames)
     const uint32_t nblk = ONE ? 1u : lg_nsteps(pl);       // steps per frame group
     if (g >= blocks) return;
@@ -905,7 +938,7 @@ __device__ __forceinline__ void produce_lg(const uint8_t *blob, const LgPlan &pl
     auto unit_of = [&](uint64_t j) -> uint64_t { return 4 * (g + (j >> 2) * np) + (j & 3); };
 
     LgState st;
-    st.a0 = c.init0; st.a1 = c.init1; st.stored = 0; st.sbad = false; st.sink = 0;
+    st.a0 = c.init0; st.a1 = c.init1; st.stored = 0; st.next = 0; st.sbad = false; st.sink = 0;
     // processing cursor (pj, pb) and issue cursor (ij, ib), up to SLOTS steps ahead
     uint64_t pj = 0, ij = 0;
     uint32_t pb = 0, ib = 0;
@@ -945,7 +978,7 @@ __device__ __forceinline__ void produce_lg(const uint8_t *blob, const LgPlan &pl
         issue_next();  // step k + SLOTS into the slot just read
         const uint64_t u = unit_of(pj);
         if (lg_process<ONE>(pl, c, sc, frame_pos, cap, u, wave, pb, nblk, B, st, lane))
-            lg_deposit(smem, c, pj, wave, lane, st.stored, t_start);
+            lg_words(smem, pl, c, g + (pj >> 2) * np, pj, wave, lane, st, t_start);
         advance(pj, pb);
     }
     wait_vm(0);
@@ -1381,7 +1414,8 @@ __global__ __launch_bounds__(kUniformThreads, 1) void k_decode_uniform(const uin
         pl.nopub = (dbg & 128) != 0;
         LgPlan lp = lg_plan(pl);
         lp.dbg = dbg;
-        if (threadIdx.x < 2 * kUcSlots) uc_cnt(smem)[threadIdx.x] = 0;  // unit-combine counters, generations
+        if (threadIdx.x < 8 * kBsSlots) bs_acc(smem, 0)[threadIdx.x] = 0;  // block sums, counters, generations
+        if (threadIdx.x < 2 * kBsSlots) bs_cnt(smem)[threadIdx.x] = 0;
         __syncthreads();
         if (wave == 4) {  // the WG's publisher
             lg_publisher(smem, lp, sc, epoch, g, nprod, lane, dbg);

@@ -21,8 +21,6 @@ if ROOT not in sys.path:
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a real MI355X (gfx950) device")
-    config.addinivalue_line("markers", "gpu_diag: needs a GPU and the diagnostic build (next-round candidates); "
-                                       "run explicitly with -m gpu_diag, never part of -m gpu")
 
 
 # Hot-path parity first: under -x a failure in a §8(f) widening module (records,
