@@ -147,7 +147,7 @@ struct iggy_codec_ctx {
     uint64_t dec_cap_len = 0;
     DevBuf dsync;    // exited | first_bad | spec_fail | bar[4] | misc[16] | small[512] | bar2 (128-B stride)
     DevBuf dsums, derr;
-    DevBuf gtiles_s, gtiles_x, gtiles_cnt, gtiles_pre, gtiles_list, gtiles_e, gtiles_base, ggrp, gfpos, gcs, gtiles_lcs, gbsums;
+    DevBuf gtiles_s, gtiles_x, gtiles_cnt, gtiles_pre, gtiles_list, gtiles_e, gtiles_base, ggrp, gfpos, gcs, gvrec, gtiles_lcs, gbsums;
     int gen_grid = 0;  // WGs of k_decode_general (the ones that get a CU join its barriers)
     // encode: the batch-checksum chain of earlier frame segments runs on `side`
     // while later segments are encoded on the call's stream
@@ -240,7 +240,8 @@ int ensure_decode_scratch(iggy_codec_ctx *c, uint64_t len) {
     r |= c->ggrp.ensure(ngroups * kGrpWords * 8);
     r |= c->gtiles_base.ensure(ntiles * 8);
     r |= c->gfpos.ensure(max_frames * 8);
-    r |= c->gcs.ensure(max_frames * 8);
+    r |= c->gcs.ensure(max_frames * 8 + 16);       // verify_frames_dma reads aligned pairs
+    r |= c->gvrec.ensure((max_frames + 1) * 16);   // walk-order frame records + "none"
     r |= c->gtiles_lcs.ensure(tile_list_words(L) * 8);
     r |= c->gbsums.ensure(max_blocks * 64);
     if (r) return IGGY_ERR_DEVICE;
@@ -278,6 +279,7 @@ GeneralScratch gscratch(iggy_codec_ctx *c) {
     g.tile_base = c->gtiles_base.as<uint64_t>();
     g.fpos = c->gfpos.as<uint64_t>();
     g.cs = c->gcs.as<uint64_t>();
+    g.vrec = c->gvrec.as<uint64_t>();
     g.tile_lcs = c->gtiles_lcs.as<uint64_t>();
     g.bsums = c->gbsums.as<uint64_t>();
     g.misc = c->dsync.as<uint64_t>(kSyncMisc);
@@ -381,7 +383,7 @@ int enqueue_decode(iggy_codec_ctx *c, const uint8_t *d_body, uint64_t len, int i
     prof_end(c, 0, s);
     HIP_OK(hipGetLastError());
     if (verify) {
-        hipLaunchKernelGGL(k_decode_general<true>, dim3(ggrid), dim3(kGenThreads), 0, s, d_body, len, d_pos,
+        hipLaunchKernelGGL(k_decode_general<true>, dim3(ggrid), dim3(kGenThreads), kGenLds, s, d_body, len, d_pos,
                            cap, d_res, gs);
     } else {
         hipLaunchKernelGGL(k_decode_general<false>, dim3(ggrid), dim3(kGenThreads), 0, s, d_body, len,
@@ -768,13 +770,15 @@ int iggy_codec_create(int device, iggy_codec_ctx **out) {
         if (hipFuncSetAttribute((const void *)k_decode_uniform<true>,
                                 hipFuncAttributeMaxDynamicSharedMemorySize, kUniformLds) != hipSuccess ||
             hipFuncSetAttribute((const void *)k_decode_uniform<false>,
-                                hipFuncAttributeMaxDynamicSharedMemorySize, kUniformLds) != hipSuccess)
+                                hipFuncAttributeMaxDynamicSharedMemorySize, kUniformLds) != hipSuccess ||
+            hipFuncSetAttribute((const void *)k_decode_general<true>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, kGenLds) != hipSuccess)
             r = IGGY_ERR_DEVICE;
     }
     if (!r) {
         // the general decode's grid barriers need every WG co-resident
         int occ_t = 0, occ_f = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ_t, k_decode_general<true>, kGenThreads, 0) != hipSuccess ||
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ_t, k_decode_general<true>, kGenThreads, kGenLds) != hipSuccess ||
             hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ_f, k_decode_general<false>, kGenThreads, 0) != hipSuccess)
             r = IGGY_ERR_DEVICE;
         c->gen_grid = c->ncu * std::max(1, std::min(2, std::min(occ_t, occ_f)));
@@ -822,7 +826,7 @@ void iggy_codec_destroy(iggy_codec_ctx *c) {
     if (c->h2d) (void)hipStreamSynchronize(c->h2d);
     if (c->d2h) (void)hipStreamSynchronize(c->d2h);
     DevBuf *bufs[] = {&c->dsync, &c->dsums, &c->derr, &c->gtiles_s, &c->gtiles_x,
-                      &c->gtiles_cnt, &c->gtiles_pre, &c->gtiles_list, &c->gtiles_e, &c->gtiles_base, &c->ggrp, &c->gfpos, &c->gcs, &c->gtiles_lcs,
+                      &c->gtiles_cnt, &c->gtiles_pre, &c->gtiles_list, &c->gtiles_e, &c->gtiles_base, &c->ggrp, &c->gfpos, &c->gcs, &c->gvrec, &c->gtiles_lcs,
                       &c->gbsums, &c->dresult, &c->din, &c->dpos, &c->dout, &c->epl, &c->euh,
                       &c->etile, &c->ecs, &c->emisc, &c->eids, &c->eots, &c->epay, &c->eplen,
                       &c->euhb, &c->euhl, &c->hbsums, &c->ppos, &c->pmsgs, &c->pres, &c->cwk, &c->sl, &c->slres, &c->cr,

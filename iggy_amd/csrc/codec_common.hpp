@@ -111,6 +111,46 @@ __device__ __forceinline__ uint64_t sat_add(uint64_t a, uint64_t b) {
 __device__ __forceinline__ uint64_t rt_now() { return __builtin_amdgcn_s_memrealtime(); }
 constexpr uint64_t kSpinLimitTicks = 100000000ull * 4;  // 4 s: a bug guard, never a timing knob
 
+// LDS-DMA (global_load_lds_dwordx4) issue and the constant vmcnt wait that goes with it
+// M0 carries the LDS destination; it is declared clobbered (the compiler
+// re-materialises M0 itself wherever it needs it) instead of saved/restored.
+__device__ __forceinline__ void glds16(const void *gsrc, uint32_t lds_addr, bool nt = false) {
+    if (nt) {
+        asm volatile(
+            "s_mov_b32 m0, %1\n\t"
+            "s_nop 0\n\t"
+            "global_load_lds_dwordx4 %0, off nt"
+            :
+            : "v"(gsrc), "s"(__builtin_amdgcn_readfirstlane(lds_addr))
+            : "memory", "m0");
+        return;
+    }
+    asm volatile(
+        "s_mov_b32 m0, %1\n\t"
+        "s_nop 0\n\t"
+        "global_load_lds_dwordx4 %0, off"
+        :
+        : "v"(gsrc), "s"(__builtin_amdgcn_readfirstlane(lds_addr))
+        : "memory", "m0");
+}
+// gsrc + OFF -> lds_addr. The instruction offset is added to the LDS address too
+// (LDS_ADDR = M0 + inst_offset + 16 * lane), so M0 gets lds_addr - OFF.
+template <int OFF>
+__device__ __forceinline__ void glds16o(const void *gsrc, uint32_t lds_addr) {
+    asm volatile(
+        "s_mov_b32 m0, %1\n\t"
+        "s_nop 0\n\t"
+        "global_load_lds_dwordx4 %0, off offset:%2"
+        :
+        : "v"(gsrc), "s"(__builtin_amdgcn_readfirstlane(lds_addr - OFF)), "i"(OFF)
+        : "memory", "m0");
+}
+template <int N>
+__device__ __forceinline__ void wait_vm_const() {
+    static_assert(N >= 0 && N <= 63, "vmcnt range");
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
 // lane-group XXH3 helpers (decode_uniform / decode_general / encode): DPP quad_perm
 // and ds_swizzle moves of a 64-bit value, and one 16-B stripe-pair piece
 template <int CTRL>

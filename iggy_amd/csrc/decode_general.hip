@@ -63,7 +63,9 @@ struct GeneralScratch {
     uint64_t *tile_lcs;  // [ntiles * tile_list_cap(T)] stored checksum of each listed frame
     uint64_t *fpos;      // [max_frames] frame starts in walk order (hashed length of frame f:
                          // fpos[f+1] - fpos[f] - 8, the last frame's from the walk end)
-    uint64_t *cs;        // [max_frames] stored checksums in walk order
+    uint64_t *cs;        // [max_frames] stored checksums in walk order (+16 B: read in aligned pairs)
+    uint64_t *vrec;      // [max_frames + 1] x 2: (frame start, hashed length | frame index << 32) in
+                         // walk order, then a "none" record (index kVdNone): verify_frames_dma
     uint64_t *bsums;     // [max_blocks * 8]
     uint64_t *misc;      // [16]: 0 nwalk, 1 end (with stop bit), 2 first_bad enc
     uint32_t *bar2;      // [kBar2Words * 32]: two-level barrier counters, 128 B apart (grid_barrier2)
@@ -447,9 +449,23 @@ __device__ __forceinline__ void vissue(const uint8_t *blob, const VFrame &v, uin
     st.lnx = *(const uint32_t *)((lp && rl) ? lc + 16 : blob);
 }
 
+// Frames of <= 240 hashed bytes (XXH3's short forms): one lane each, slice sw of nsw.
+__device__ inline void verify_short(const uint8_t *blob, const GeneralScratch &gs, uint64_t nwalk, uint64_t wend,
+                                    uint32_t sw, uint32_t nsw, int lane) {
+    const uint64_t C = (nwalk + nsw - 1) / nsw;
+    const uint64_t f1 = min((uint64_t)(sw + 1) * C, nwalk);
+    for (uint64_t f = (uint64_t)sw * C + lane; f < f1; f += 64) {
+        const uint64_t p = gs.fpos[f];
+        const uint64_t L = (f + 1 < nwalk ? gs.fpos[f + 1] : wend) - p - 8;
+        if (L <= 240 && xxh3_64_lane(blob + p + 8, L) != gs.cs[f])
+            atomicMax((unsigned long long *)&gs.misc[2], (unsigned long long)~f);
+    }
+}
+
 __device__ inline void verify_frames(const uint8_t *blob, const GeneralScratch &gs, uint64_t nwalk,
                                      uint64_t wend, uint32_t vw, uint32_t nvw, uint32_t member, uint32_t nwg,
-                                     uint32_t *s_claim, int lane, uint64_t t0, const uint8_t *blob_end) {
+                                     uint32_t *s_claim, int lane, uint64_t t0, const uint8_t *blob_end,
+                                     bool all_claimed = false) {
     const uint32_t l = lane & 7, m = l >> 1, par = l & 1, fg = (uint32_t)lane >> 3;
     const uint32_t poff = 16 * (m + 4 * par);
     uint64_t s0[8], s1[8];
@@ -471,7 +487,8 @@ __device__ inline void verify_frames(const uint8_t *blob, const GeneralScratch &
     // LDS claim waits on lgkmcnt, never on the in-flight frame loads (vmcnt).
     // (same-box A/B on C3, loop end mean / max: static only 734-760 / 802-830 us,
     // last quarter claimed 766-771 / 804-818, last eighth 755-761 / 804-807)
-    const uint64_t fdyn = nwalk - nwalk / 8;
+    // (all_claimed, beside verify_frames_dma: every frame claimed, frames member + nwg k)
+    const uint64_t fdyn = all_claimed ? 0 : nwalk - nwalk / 8;
     auto next_f = [&](uint64_t f) -> uint64_t {  // f: the static successor
         if (f < fdyn) return f;
         uint32_t k = 0;
@@ -555,16 +572,7 @@ __device__ inline void verify_frames(const uint8_t *blob, const GeneralScratch &
     // frames of <= 240 hashed bytes: one lane each, a contiguous slice per wave, before
     // the streaming loop (chunks claimed from one counter after the loop serialised
     // ~4 K claims once the balanced tail made every wave finish together: +40 us on C3)
-    {
-        const uint64_t C = (nwalk + nvw - 1) / nvw;
-        const uint64_t f1 = min((uint64_t)(vw + 1) * C, nwalk);
-        for (uint64_t f = (uint64_t)vw * C + lane; f < f1; f += 64) {
-            const uint64_t p = gs.fpos[f];
-            const uint64_t L = (f + 1 < nwalk ? gs.fpos[f + 1] : wend) - p - 8;
-            if (L <= 240 && xxh3_64_lane(blob + p + 8, L) != gs.cs[f])
-                atomicMax((unsigned long long *)&gs.misc[2], (unsigned long long)~f);
-        }
-    }
+    if (!all_claimed) verify_short(blob, gs, nwalk, wend, vw, nvw, lane);
     VStep A, B;
     vissue(blob, cur, nwalk, 0, par, poff, m, A, gs.dbg, blob_end);
     while (__ballot(cur.f < nwalk)) {
@@ -580,6 +588,241 @@ __device__ inline void verify_frames(const uint8_t *blob, const GeneralScratch &
         atomicAdd((unsigned long long *)&vstat[1], (unsigned long long)d);
     }
     if (lane == 0) atomicMax((unsigned long long *)&vstat[2], (unsigned long long)(rt_now() - t0));  // [16]
+}
+
+// Frame verification through LDS rings (records under 4 GiB: the product form).
+// The register loop above keeps one step in flight per wave and loads every chunk
+// from its 4-B-aligned address plus the dword after it (18 loads per step). Here
+// each verify wave streams like the uniform kernel's lane-group producers
+// (decode_uniform.hip): exactly 9 global_load_lds_dwordx4 per step into a 4-slot
+// ring, an explicit constant vmcnt wait, three steps in flight. A frame starts at
+// any byte, so a lane group loads its block's 16-B-ALIGNED window (64 chunks,
+// lane l of instruction q takes chunk 8q + l: row q of the window lands as 128
+// contiguous bytes at slot + 1024q + 128fg) plus the chunk after it, and each lane
+// reads its 16-B pieces back at the byte offset (5 ds_read_b32 + 4 v_alignbyte).
+// Ninth instruction, lane l of the group: 0 the window's chunk 64; 1-5 the frame's
+// aligned last-stripe window (first step); 6 the aligned pair of stored checksums
+// holding cs[f] (first step); 7 the walk-order frame record (vrec) of the frame
+// four frames ahead in this group's sequence (first step), which the step's reader
+// copies into the group's 8-entry record ring. So the next frames' positions are in
+// LDS before their first block is issued, with no VGPR load in the loop (its only
+// vector-memory operations are the 9 counted DMAs).
+constexpr uint32_t kVdSlots = 4;                        // 3 steps in flight + the one being read
+constexpr uint32_t kVdStep = 9 * 1024;                  // 9 DMA instructions x 64 lanes x 16 B
+constexpr uint32_t kVdMeta = 8 * 9 * 16;                // 8 groups x (8 frame records + a spare)
+constexpr uint32_t kVdWave = kVdSlots * kVdStep + kVdMeta;
+constexpr uint32_t kGenLds = 4 * kVdWave;               // waves 4..7 of a workgroup
+static_assert(kGenLds + 64 <= 160 * 1024, "LDS budget (with the kernel's static LDS words)");
+static_assert(2 * kChainChunk * 8 * 8 <= 2 * kVdWave, "WG 0's chain buffer fits its waves 4, 5's rings");
+#ifndef IGGY_VD_REGWAVES
+#define IGGY_VD_REGWAVES 1  // (build knob for same-box A/B: 0 = the LDS-ring waves alone)
+#endif
+constexpr uint32_t kVdNone = 0xFFFFFFFFu;               // vrec frame index of "no frame"
+
+__device__ __forceinline__ uint32_t vd_nsteps(bool valid, uint64_t L) {
+    if (!valid || L <= 240) return 1;  // short frames: one empty step (verify_short hashes them)
+    const uint64_t nbF = (L - 1) / 1024, ns = ((L - 1) - 1024 * nbF) / 64;
+    return (uint32_t)(nbF + (ns > 0));
+}
+// the 16 bytes at byte offset rb of the 5 dwords d
+__device__ __forceinline__ uint4 vd_align(const uint32_t d[5], uint32_t rb) {
+    return make_uint4(__builtin_amdgcn_alignbyte(d[1], d[0], rb), __builtin_amdgcn_alignbyte(d[2], d[1], rb),
+                      __builtin_amdgcn_alignbyte(d[3], d[2], rb), __builtin_amdgcn_alignbyte(d[4], d[3], rb));
+}
+
+__device__ inline void verify_frames_dma(const uint8_t *blob, const uint8_t *dummy, const GeneralScratch &gs,
+                                         uint64_t nwalk, uint64_t fbase, uint64_t fstride, uint32_t *s_claim,
+                                         uint8_t *smem, uint32_t lbase, uint32_t region, int lane, uint64_t t0) {
+    // smem: the dynamic LDS (generic pointer, for ds reads and writes); lbase: its LDS
+    // address, which the DMA's M0 needs (the static LDS variables come first)
+    const uint32_t l = lane & 7, m = l >> 1, par = l & 1, fg = (uint32_t)lane >> 3;
+    uint64_t s0[8], s1[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+        s0[q] = kSecretW8[2 * q + par + 2 * m];
+        s1[q] = kSecretW8[2 * q + par + 2 * m + 1];
+    }
+    const uint64_t key0 = kSecretW8[16 + 2 * m], key1 = kSecretW8[17 + 2 * m];
+    const uint64_t init0 = par ? 0 : kAccInit[2 * m], init1 = par ? 0 : kAccInit[2 * m + 1];
+    const uint64_t last0 = kSecretLast[2 * m], last1 = kSecretLast[2 * m + 1];
+    const uint64_t mrg0 = kSecretMerge[2 * m], mrg1 = kSecretMerge[2 * m + 1];
+    // Every secret is waited for here, before the first DMA: a first use inside the
+    // loop (the rarely taken frame-end block) got a compiler vmcnt wait that also
+    // drained the ring's in-flight steps.
+    {
+        uint64_t sink = key0 ^ key1 ^ init0 ^ init1 ^ last0 ^ last1 ^ mrg0 ^ mrg1;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) sink ^= s0[q] ^ s1[q];
+        asm volatile("" : "+v"(sink));
+    }
+    // frame sequence of this group: claims from the workgroup's LDS counter, frames
+    // fbase + fstride k (the register loop of the other waves claims from the same one)
+    auto claim = [&]() -> uint64_t {
+        uint32_t k = 0;
+        if (l == 0) k = atomicAdd(s_claim, 1u);
+        k = (uint32_t)__shfl((int)k, lane & ~7);
+        const uint64_t f = fbase + fstride * k;
+        return f < nwalk ? f : nwalk;  // nwalk: none
+    };
+    auto succ = [&](uint64_t f) -> uint64_t { return f < nwalk ? claim() : nwalk; };
+    region = __builtin_amdgcn_readfirstlane(region);  // wave-uniform: M0 from scalar registers
+    lbase = __builtin_amdgcn_readfirstlane(lbase);
+    const uint32_t meta = region + kVdSlots * kVdStep + 144 * fg;  // this group's record ring
+    // records of the group's first four frames, straight from vrec (before the ring starts)
+    uint64_t fa = claim();
+    {
+        uint64_t fo = fa;
+#pragma unroll
+        for (uint32_t k = 0; k < 4; ++k) {
+            if (l == k) *(uint4 *)(smem + meta + 16 * k) = *(const uint4 *)(gs.vrec + 2 * fo);
+            fo = succ(fo);
+        }
+        fa = fo;  // the frame four ahead of the issue cursor
+    }
+    // issue cursor: frame ordinal ij, block ib. Branch-free per lane (the group
+    // branches only at a frame start): divergent paths would run in turn for the
+    // wave's eight groups, and a step's instruction count bounds the loop as much as
+    // its bytes do.
+    uint32_t ij = 0, ib = 0, i_nsteps = 1, i_f = kVdNone;
+    uint64_t i_p = 0, i_L = 0;
+    auto issue = [&](uint32_t slot_off) {
+        const uint32_t slot = lbase + slot_off;  // the DMA's LDS address (M0) of the slot
+        if (ib == 0) {
+            const uint4 rec = *(const uint4 *)(smem + meta + 16 * (ij & 7));
+            i_p = (uint64_t)rec.x | ((uint64_t)rec.y << 32);
+            i_L = rec.z;
+            i_f = rec.w;
+            i_nsteps = vd_nsteps(i_f != kVdNone, i_L);
+        }
+        const bool valid = i_f != kVdNone;
+        const bool lng = valid && i_L > 240;
+        const uint64_t nbF = (i_L - 1) >> 10, ns = ((i_L - 1) & 1023) >> 6;
+        const uint8_t *H = blob + i_p + 8;
+        const uint8_t *W = H + ((uint64_t)ib << 10);
+        const uint32_t r = (uint32_t)((uintptr_t)W & 15);
+        const uint8_t *g = W - r + 16 * l;
+        const bool first = ib == 0;
+        const bool full = lng && ib < nbF;
+        // window bytes this step needs: [r, r + 1024) of a full block, [r, r + 64 ns) of the
+        // partial one; a chunk is loaded when it holds one of them
+        const uint32_t used = full ? 1024u + r : (lng ? (uint32_t)(ns << 6) + r : 0u);
+#pragma unroll
+        for (uint32_t q = 0; q < 8; ++q) glds16(128 * q + 16 * l < used ? g + 128 * q : dummy, slot + 1024u * q);
+        const uint8_t *Ls = H + i_L - 64;
+        const uint32_t rl = (uint32_t)((uintptr_t)Ls & 15);
+        const uint8_t *c0 = (full && r) ? g + 1024 : dummy;  // (l == 0: g = the window start)
+        const uint8_t *cl = (lng && first && (l < 5 || rl)) ? Ls - rl + 16 * (l - 1) : dummy;
+        const uint8_t *c6 = (valid && first) ? (const uint8_t *)(gs.cs + (i_f & ~1u)) : dummy;
+        const uint8_t *c7 = first ? (const uint8_t *)(gs.vrec + 2 * fa) : dummy;
+        glds16(l == 0 ? c0 : l <= 5 ? cl : l == 6 ? c6 : c7, slot + 8u * 1024u);
+        if (first) fa = succ(fa);
+        if (++ib == i_nsteps) {
+            ib = 0;
+            ++ij;
+        }
+    };
+    // processing cursor: frame ordinal pj, block pb
+    uint32_t pj = 0, pb = 0, p_nsteps = 1, p_f = kVdNone, rb = 0, rl = 0;
+    uint64_t p_L = 0, stored = 0, bad = ~0ull, nbF = 0, ns = 0;
+    bool lng = false;
+    uint32_t o5[5] = {0, 0, 0, 0, 0};  // LDS offsets of a piece's 5 dwords from its row (this frame's r)
+    uint64_t a0 = init0, a1 = init1;
+    uint4 lastp = make_uint4(0, 0, 0, 0);
+    for (uint32_t k = 0; k < kVdSlots; ++k) issue(region + k * kVdStep);
+    for (uint32_t k = 0;; ++k) {
+        if (pb == 0) {
+            const uint4 rec = *(const uint4 *)(smem + meta + 16 * (pj & 7));
+            const uint64_t p = (uint64_t)rec.x | ((uint64_t)rec.y << 32);
+            p_L = rec.z;
+            p_f = rec.w;
+            p_nsteps = vd_nsteps(p_f != kVdNone, p_L);
+            lng = p_f != kVdNone && p_L > 240;
+            nbF = (p_L - 1) >> 10;
+            ns = ((p_L - 1) & 1023) >> 6;
+            const uint32_t r = (uint32_t)((uintptr_t)(blob + p + 8) & 15);
+            rb = r & 3;
+            const uint32_t e = (64 * par + 16 * m + r) >> 2;
+#pragma unroll
+            for (uint32_t j = 0; j < 5; ++j) o5[j] = 1024u * ((e + j) >> 5) + 4u * ((e + j) & 31);
+            rl = (uint32_t)((uintptr_t)(blob + p + 8 + p_L - 64) & 15);
+            a0 = init0;
+            a1 = init1;
+        }
+        if (!__ballot(p_f != kVdNone)) break;
+        wait_vm_const<9 * (kVdSlots - 1)>();  // step k landed; steps k+1..k+3 stay in flight
+        const uint32_t slot = region + (k % kVdSlots) * kVdStep;
+        const uint8_t *row = smem + slot + 128 * fg;
+        uint4 pc[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            uint32_t d[5];
+#pragma unroll
+            for (int j = 0; j < 5; ++j) d[j] = *(const uint32_t *)(row + 1024 * q + o5[j]);
+            pc[q] = vd_align(d, rb);
+        }
+        const bool first = pb == 0;
+        {  // first step of a frame: its last-stripe piece, stored checksum, and the record of
+           // the frame four ahead into the ring (elsewhere into the group's spare entry)
+            uint32_t d[5];
+            const uint8_t *ls = row + 8192 + 16 + ((rl + 16 * m) & ~3u);
+#pragma unroll
+            for (int j = 0; j < 5; ++j) d[j] = *(const uint32_t *)(ls + 4 * j);
+            const uint4 lp = vd_align(d, rl & 3);
+            const uint64_t sv = *(const uint64_t *)(row + 8192 + 96 + 8 * (p_f & 1));
+            const uint4 rec = *(const uint4 *)(row + 8192 + 112);
+            if (l == 7) *(uint4 *)(smem + meta + 16 * (first ? (pj + 4) & 7 : 8u)) = rec;
+            // (component-wise: a select of the whole uint4 went through scratch memory,
+            // whose vmcnt(0) drained the DMA ring every step)
+            lastp.x = first ? lp.x : lastp.x;
+            lastp.y = first ? lp.y : lastp.y;
+            lastp.z = first ? lp.z : lastp.z;
+            lastp.w = first ? lp.w : lastp.w;
+            stored = first ? sv : stored;
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // slot read out before it is refilled
+        issue(slot);  // step k + 4
+        {
+            const bool full = lng && pb < nbF;
+            uint64_t q0[4] = {0, 0, 0, 0}, q1[4] = {0, 0, 0, 0};
+#pragma unroll
+            for (int q = 0; q < 8; ++q) {
+                const uint64_t w0 = (uint64_t)pc[q].x | ((uint64_t)pc[q].y << 32);
+                const uint64_t w1 = (uint64_t)pc[q].z | ((uint64_t)pc[q].w << 32);
+                // partial block: stripes < ns only (a mask, not a branch per piece)
+                const uint64_t use = 0ull - (uint64_t)(full || (uint64_t)(2 * q + par) < ns);
+                q0[q & 3] += (mul32x32(w0 ^ s0[q]) + w1) & use;
+                q1[q & 3] += (mul32x32(w1 ^ s1[q]) + w0) & use;
+            }
+            a0 += (q0[0] + q0[1]) + (q0[2] + q0[3]);
+            a1 += (q1[0] + q1[1]) + (q1[2] + q1[3]);
+            // a full block ends with the pair fold and the scramble; the even lane keeps it
+            const uint64_t f0 = a0 + gdpp64<0xB1>(a0), f1 = a1 + gdpp64<0xB1>(a1);
+            a0 = full ? (par ? 0 : scramble1(f0, key0)) : a0;
+            a1 = full ? (par ? 0 : scramble1(f1, key1)) : a1;
+            const bool fin = pb + 1 == p_nsteps;
+            if (__ballot(fin && lng)) {  // some group's frame ends here: last stripe, merge, compare
+                uint64_t b0 = a0 + gdpp64<0xB1>(a0), b1 = a1 + gdpp64<0xB1>(a1);
+                piece(b0, b1, lastp, last0, last1);
+                uint64_t t = fold64(b0 ^ mrg0, b1 ^ mrg1);
+                t += gdpp64<0x4E>(t);
+                t += gswz_xor4(t);
+                const uint64_t h = avalanche(p_L * P64_1 + t);
+                bad = (fin && lng && h != stored && bad == ~0ull) ? p_f : bad;
+            }
+        }
+        if (++pb == p_nsteps) {
+            pb = 0;
+            ++pj;
+        }
+    }
+    wait_vm_const<0>();  // the dummy steps issued past the end land before the ring is reused
+    if (l == 0 && bad != ~0ull) atomicMax((unsigned long long *)&gs.misc[2], (unsigned long long)~bad);
+    uint64_t *vstat = (uint64_t *)(gs.small + 512) + 14;  // phase clock: [14] last / [15] sum of loop ends
+    if (lane == 0) {
+        const uint64_t d = rt_now() - t0;
+        atomicMax((unsigned long long *)&vstat[0], (unsigned long long)d);
+        atomicAdd((unsigned long long *)&vstat[1], (unsigned long long)d);
+    }
 }
 
 // ------------------------------------------------------------------ kernel
@@ -600,7 +843,10 @@ __global__ __launch_bounds__(kGenThreads) void k_decode_general(const uint8_t *_
         return;
     const uint64_t t0 = rt_now();
     __shared__ uint32_t s_mem[3];
-    __shared__ uint64_t s_cbuf[2 * kChainChunk * 8];  // the chain's staged block sums (64 KiB)
+    // dynamic LDS (kGenLds, Verify only): the verify waves' rings (verify_frames_dma); in
+    // WG 0 its first 64 KiB hold the chain's staged block sums instead
+    extern __shared__ __attribute__((aligned(16))) uint8_t s_gdyn[];
+    uint64_t *s_cbuf = (uint64_t *)s_gdyn;
     __shared__ uint32_t s_cflags[3];
     if (threadIdx.x < 3) s_cflags[threadIdx.x] = 0;  // (ordered by the barriers before phase D + F)
     join_members(gs, t0, s_mem);
@@ -1080,6 +1326,20 @@ __global__ __launch_bounds__(kGenThreads) void k_decode_general(const uint8_t *_
             if (lane < 8) gs.bsums[b * 8 + lane] = t8;
         }
     }
+    // walk-order frame records for verify_frames_dma (vrec), and the "none" record after them
+    const bool vdma = VERIFY && bl < (1ull << 32) && !(kDiagMask && (gs.dbg & 0x200000));
+    if (vdma) {
+        const uint64_t wend = __hip_atomic_load(&gs.misc[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & ~kStopBit;
+        for (uint64_t f = gtid; f <= nwalk; f += gthreads) {
+            uint4 v = make_uint4(0, 0, 0, kVdNone);
+            if (f < nwalk) {
+                const uint64_t p = gs.fpos[f];
+                const uint64_t L = (f + 1 < nwalk ? gs.fpos[f + 1] : wend) - p - 8;  // frames tile the walk
+                v = make_uint4((uint32_t)p, (uint32_t)(p >> 32), (uint32_t)L, (uint32_t)f);
+            }
+            *(uint4 *)(gs.vrec + 2 * f) = v;
+        }
+    }
     // (a grid barrier, not a block-sum count only the chain wave waits for: with the
     // verify waves going straight on, the C3 decode measured 15-25 us slower)
     ok &= grid_barrier2(gs.bar2, member, nwg, ++phase, t0);
@@ -1121,7 +1381,37 @@ __global__ __launch_bounds__(kGenThreads) void k_decode_general(const uint8_t *_
         }
     } else if (member == 0 && wave == 1 && long_cs) {
         chain_stager(gs.bsums, nb, s_cbuf, s_cflags, lane, t0);
+    } else if (VERIFY && vdma) {
+        // Frames of <= 240 B first, a slice per wave of every WG. Then the long frames,
+        // claimed one per lane group from the workgroup's LDS counter (WG member m of
+        // the verifying set takes frames m + nv k, a chip-wide front) by two loops side
+        // by side: waves 4..7 stream through LDS rings (verify_frames_dma), waves 0..3
+        // run the register loop (verify_frames); the counter balances the two. WG 0
+        // runs the chain and only verifies when it is alone (then with waves ws..5 and
+        // 6, 7: its waves 4, 5's ring space holds the chain buffer).
+        const uint32_t ws = long_cs ? 2 : 1;  // WG 0's waves below ws chain (and stage)
+        const uint64_t wend = __hip_atomic_load(&gs.misc[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & ~kStopBit;
+        const uint32_t nsw = nwg * 8 - ws;
+        verify_short(blob, gs, nwalk, wend, member * 8 + wave - ws, nsw, lane);
+        if (lane == 0)  // phase clock [16]: the short frames' end
+            atomicMax((unsigned long long *)((uint64_t *)(gs.small + 512) + 16), (unsigned long long)(rt_now() - t0));
+        const bool alone = nwg == 1;
+        if (alone || member > 0) {
+            const uint64_t fbase = alone ? 0 : member - 1, fstride = alone ? 1 : nwg - 1;
+            if (wave >= (member == 0 ? 6u : 4u)) {
+                typedef __attribute__((address_space(3))) uint8_t lds_u8;
+                const uint32_t lbase = (uint32_t)(uintptr_t)(lds_u8 *)s_gdyn;
+                verify_frames_dma(blob, body, gs, nwalk, fbase, fstride, &s_mem[2], s_gdyn, lbase,
+                                  (wave - 4) * kVdWave, lane, t0);
+            } else if (IGGY_VD_REGWAVES) {
+                if (member == 1 && wave == 0 && lane == 0) ((uint64_t *)(gs.small + 512))[17] = 8 * (nwg - 1);
+                verify_frames(blob, gs, nwalk, wend, 0, 1, (uint32_t)fbase, (uint32_t)fstride, &s_mem[2], lane, t0,
+                              blob + bl, true);
+            }
+        }
     } else if (VERIFY) {
+        // (records of 4 GiB and more, whose frame lengths need not fit vrec's 32 bits;
+        // diagnostic bit 0x200000 forces it): the register loop in every other wave
         const uint32_t ws = long_cs ? 2 : 1;  // WG 0's waves below ws chain (and stage)
         const uint32_t vw = member * (blockDim.x >> 6) + wave - ws;
         const uint32_t nvw = nwg * (blockDim.x >> 6) - ws;

@@ -161,39 +161,6 @@ __device__ inline void make_plan(const HeaderInfo &hi, const uint8_t *blob, uint
 }
 
 // ------------------------------------------------------------ primitives
-// M0 carries the LDS destination; it is declared clobbered (the compiler
-// re-materialises M0 itself wherever it needs it) instead of saved/restored.
-__device__ __forceinline__ void glds16(const void *gsrc, uint32_t lds_addr, bool nt = false) {
-    if (nt) {
-        asm volatile(
-            "s_mov_b32 m0, %1\n\t"
-            "s_nop 0\n\t"
-            "global_load_lds_dwordx4 %0, off nt"
-            :
-            : "v"(gsrc), "s"(__builtin_amdgcn_readfirstlane(lds_addr))
-            : "memory", "m0");
-        return;
-    }
-    asm volatile(
-        "s_mov_b32 m0, %1\n\t"
-        "s_nop 0\n\t"
-        "global_load_lds_dwordx4 %0, off"
-        :
-        : "v"(gsrc), "s"(__builtin_amdgcn_readfirstlane(lds_addr))
-        : "memory", "m0");
-}
-// gsrc + OFF -> lds_addr. The instruction offset is added to the LDS address too
-// (LDS_ADDR = M0 + inst_offset + 16 * lane), so M0 gets lds_addr - OFF.
-template <int OFF>
-__device__ __forceinline__ void glds16o(const void *gsrc, uint32_t lds_addr) {
-    asm volatile(
-        "s_mov_b32 m0, %1\n\t"
-        "s_nop 0\n\t"
-        "global_load_lds_dwordx4 %0, off offset:%2"
-        :
-        : "v"(gsrc), "s"(__builtin_amdgcn_readfirstlane(lds_addr - OFF)), "i"(OFF)
-        : "memory", "m0");
-}
 __device__ __forceinline__ void wait_vm(uint32_t n) {
     // n = glds instructions allowed to stay in flight (multiples of 8)
     switch (n) {
@@ -208,11 +175,6 @@ __device__ __forceinline__ void wait_vm(uint32_t n) {
     }
 }
 
-template <int N>
-__device__ __forceinline__ void wait_vm_const() {
-    static_assert(N >= 0 && N <= 63, "vmcnt range");
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
-}
 
 __device__ __forceinline__ uint64_t funnel64(uint64_t lo, uint64_t hi, uint32_t t) {
     return t ? ((lo >> (8 * t)) | (hi << (64 - 8 * t))) : lo;
@@ -825,7 +787,7 @@ __device__ __forceinline__ bool lg_process(const LgPlan &pl, const LgLane &c, co
 // later must also cover its write-through stores, whose acknowledgements are slow
 // under the full read stream -- the LDS adds here are not vector-memory operations.
 constexpr uint32_t kLgSlots = 4;    // per wave: 1 step being hashed + 3 in flight (36 KiB)
-constexpr uint32_t kBsSlots = 8;    // blocks the producers may run ahead of the publisher
+constexpr uint32_t kBsSlots = 16;   // blocks the producers may run ahead of the publisher
 constexpr uint32_t kBsOff = 4 * kLgSlots * kLgStepBytes;  // [kBsSlots] acc[8] u64, spare[2] u32, cnt[], gen[]
 constexpr uint32_t kLgLds = kBsOff + 80 * kBsSlots;
 __device__ __forceinline__ uint64_t *bs_acc(uint8_t *smem, uint32_t s) { return (uint64_t *)(smem + kBsOff + 64u * s); }

@@ -34,6 +34,8 @@ def main():
     ap.add_argument("--hi", type=int, default=4096)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--no-check", action="store_true",
+                    help="ablation runs (wrong bytes by design): time the encode only, no decode check")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
@@ -63,6 +65,14 @@ def main():
     torch.cuda.synchronize()
     er = abi.EncodeResult.from_buffer_copy(res.cpu().numpy().tobytes())
     assert er.error.kind == 0 and er.batch_length == total, er.error
+    if args.no_check:
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            step()
+        torch.cuda.synchronize()
+        ms = (time.perf_counter() - t0) / args.steps * 1e3
+        print(json.dumps({"encode_ms": round(ms, 4), "checked": False}), flush=True)
+        return
     # the encoded record must decode and verify (general walk: variable frame sizes)
     cap = n
     d_pos = torch.empty(cap, dtype=torch.int64, device=dev)

@@ -11,9 +11,10 @@ import os
 import sys
 import time
 
-import torch
-
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import iggy_amd  # noqa: E402,F401  (HIP runtime settings before torch)
+import torch  # noqa: E402
+
 from iggy_amd import abi  # noqa: E402
 from iggy_amd import codec as _codec  # noqa: E402
 

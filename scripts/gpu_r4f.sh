@@ -9,5 +9,5 @@ cd $R
 export GPU_PINNED_MIN_XFER_SIZE=1048576
 timeout -k 10 600 python -u -m pytest tests/test_parity_gpu.py tests/test_configs_gpu.py tests/test_robust_gpu.py -m gpu -x -q --timeout 240 --timeout-method thread > $O/t.log 2>&1
 rc=$?; echo "pytest rc=$rc" >> $O/t.log; [ $rc -eq 0 ] || exit $rc
-timeout -k 10 300 python -u scripts/ab_libs.py ab/libbase.so iggy_amd/libiggy_codec.so > $O/ab.log 2>&1
+timeout -k 10 300 python -u scripts/ab_libs.py ${BASE:-ab/libbase.so} iggy_amd/libiggy_codec.so > $O/ab.log 2>&1
 rc=$?; echo "ab rc=$rc" >> $O/ab.log; exit $rc

@@ -366,3 +366,41 @@ def test_recovery_after_timed_out_decode():
             assert _res(res).error.kind == 0
     finally:
         cx.close()
+
+
+@pytest.mark.parametrize("shift", [0, 5])
+def test_register_verify_loop_fallback(shift):
+    """Diagnostic build only: the register verify loop of the general walk (the form
+    records of 4 GiB and more take, forced by debug bit 0x200000) gives the same
+    verdicts as the LDS-ring loop on variable-size records, clean and with a body
+    byte flipped, at a misaligned record start."""
+    import os
+    from iggy_amd import codec as C
+    if not os.path.exists(C.DIAG_LIB_PATH):
+        pytest.skip("diagnostic build not present")
+    torch = _torch()
+    L = C.load(C.DIAG_LIB_PATH)
+    cx = C.Codec(0, library=L)
+    try:
+        n = 3000
+        rec = O.synth_batch(n, 64, 4096, seed=77 + shift)
+        bad = rec.copy()
+        bad[256 + rec.size // 3] ^= 0x10
+        buf = torch.zeros(rec.size + 64, dtype=torch.uint8, device="cuda:0")
+        d_pos = torch.zeros(n, dtype=torch.int64, device="cuda:0")
+        res = torch.zeros(ctypes.sizeof(abi.DecodeResult), dtype=torch.uint8, device="cuda:0")
+        s = torch.cuda.current_stream().cuda_stream
+        for bits in (0x200000, 0):
+            L.iggy_codec_debug_set(cx.handle, bits)
+            for r in (rec, bad):
+                buf[shift: shift + r.size] = torch.from_numpy(r).to("cuda:0")
+                assert cx.decode_device(buf.data_ptr() + shift, r.size, 0, d_pos.data_ptr(), n, res.data_ptr(), s) == 0
+                torch.cuda.synchronize()
+                got = _res(res)
+                orc, oe, _, of = O.decode_batch_slice_with(r, 0)
+                assert got.error.kind == orc and got.error.astuple() == oe.astuple(), (bits, got.error.astuple())
+                if orc == 0:
+                    assert np.array_equal(d_pos.cpu().numpy().astype(np.uint64), of)
+        L.iggy_codec_debug_set(cx.handle, 0)
+    finally:
+        cx.close()
