@@ -2756,6 +2756,10 @@ int iggy_codec_debug_read(iggy_codec_ctx *c, void *out, uint64_t bytes) {
 // build, where kDiagMask is zero).
 int iggy_codec_debug_set(iggy_codec_ctx *c, uint32_t bits) {
     if (!c) return IGGY_ERR_INVALID_ARGUMENT;
+    if (kDiagMask && (bits & 0x40000000u)) {  // completion-flag sequence 16 values before its wrap
+        c->hseq = 0xFFFFFFF0u;
+        bits &= ~0x40000000u;
+    }
     c->dbg = bits;
     return 0;
 }

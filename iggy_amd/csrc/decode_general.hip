@@ -464,8 +464,7 @@ __device__ inline void verify_short(const uint8_t *blob, const GeneralScratch &g
 
 __device__ inline void verify_frames(const uint8_t *blob, const GeneralScratch &gs, uint64_t nwalk,
                                      uint64_t wend, uint32_t vw, uint32_t nvw, uint32_t member, uint32_t nwg,
-                                     uint32_t *s_claim, int lane, uint64_t t0, const uint8_t *blob_end,
-                                     bool all_claimed = false) {
+                                     uint32_t *s_claim, int lane, uint64_t t0, const uint8_t *blob_end) {
     const uint32_t l = lane & 7, m = l >> 1, par = l & 1, fg = (uint32_t)lane >> 3;
     const uint32_t poff = 16 * (m + 4 * par);
     uint64_t s0[8], s1[8];
@@ -487,8 +486,7 @@ __device__ inline void verify_frames(const uint8_t *blob, const GeneralScratch &
     // LDS claim waits on lgkmcnt, never on the in-flight frame loads (vmcnt).
     // (same-box A/B on C3, loop end mean / max: static only 734-760 / 802-830 us,
     // last quarter claimed 766-771 / 804-818, last eighth 755-761 / 804-807)
-    // (all_claimed, beside verify_frames_dma: every frame claimed, frames member + nwg k)
-    const uint64_t fdyn = all_claimed ? 0 : nwalk - nwalk / 8;
+    const uint64_t fdyn = nwalk - nwalk / 8;
     auto next_f = [&](uint64_t f) -> uint64_t {  // f: the static successor
         if (f < fdyn) return f;
         uint32_t k = 0;
@@ -572,7 +570,7 @@ __device__ inline void verify_frames(const uint8_t *blob, const GeneralScratch &
     // frames of <= 240 hashed bytes: one lane each, a contiguous slice per wave, before
     // the streaming loop (chunks claimed from one counter after the loop serialised
     // ~4 K claims once the balanced tail made every wave finish together: +40 us on C3)
-    if (!all_claimed) verify_short(blob, gs, nwalk, wend, vw, nvw, lane);
+    verify_short(blob, gs, nwalk, wend, vw, nvw, lane);
     VStep A, B;
     vissue(blob, cur, nwalk, 0, par, poff, m, A, gs.dbg, blob_end);
     while (__ballot(cur.f < nwalk)) {
@@ -611,7 +609,9 @@ constexpr uint32_t kVdSlots = 4;                        // 3 steps in flight + t
 constexpr uint32_t kVdStep = 9 * 1024;                  // 9 DMA instructions x 64 lanes x 16 B
 constexpr uint32_t kVdMeta = 8 * 9 * 16;                // 8 groups x (8 frame records + a spare)
 constexpr uint32_t kVdWave = kVdSlots * kVdStep + kVdMeta;
-constexpr uint32_t kGenLds = 4 * kVdWave;               // waves 4..7 of a workgroup
+constexpr uint32_t kVdRecOff = 4 * kVdWave;             // waves 4..7 of a workgroup: rings; then
+constexpr uint32_t kVdSecOff = kVdRecOff + 8 * 1024;    // the register loop's record slots (verify_frames_claimed),
+constexpr uint32_t kGenLds = kVdSecOff + 24 * 8;         // and its stripe secrets
 static_assert(kGenLds + 64 <= 160 * 1024, "LDS budget (with the kernel's static LDS words)");
 static_assert(2 * kChainChunk * 8 * 8 <= 2 * kVdWave, "WG 0's chain buffer fits its waves 4, 5's rings");
 #ifndef IGGY_VD_REGWAVES
@@ -816,6 +816,163 @@ __device__ inline void verify_frames_dma(const uint8_t *blob, const uint8_t *dum
         }
     }
     wait_vm_const<0>();  // the dummy steps issued past the end land before the ring is reused
+    if (l == 0 && bad != ~0ull) atomicMax((unsigned long long *)&gs.misc[2], (unsigned long long)~bad);
+    uint64_t *vstat = (uint64_t *)(gs.small + 512) + 14;  // phase clock: [14] last / [15] sum of loop ends
+    if (lane == 0) {
+        const uint64_t d = rt_now() - t0;
+        atomicMax((unsigned long long *)&vstat[0], (unsigned long long)d);
+        atomicAdd((unsigned long long *)&vstat[1], (unsigned long long)d);
+    }
+}
+
+// Register loop beside verify_frames_dma (claims mode), in waves 0..3. A record
+// (position, hashed length, index: vrec) only ever reaches a register through a
+// step's load set that the wave has already waited for: each set carries the
+// records of the two frames after the one it loads (and, on a frame's first block,
+// its stored checksum); while it hashes that set the wave writes them to the group's
+// LDS slots, where the frame switch reads them. A record loaded at the (divergent)
+// frame switch itself made the wave wait for every outstanding load there (vmcnt(0)
+// once per frame), and records kept in registers were merged through scratch.
+struct VStepC {
+    VStep s;
+    uint64_t cs;     // stored checksum of this set's frame (its first block)
+    uint32_t b, o;   // (not loaded) the block this set holds and its frame's ordinal
+};
+__device__ __forceinline__ VFrame vd_frame(uint4 r, uint64_t nwalk) {
+    VFrame v;
+    v.f = r.w == kVdNone ? nwalk : r.w;
+    v.p = (uint64_t)r.x | ((uint64_t)r.y << 32);
+    v.L = r.z;
+    v.stored = 0;
+    return v;
+}
+// recs: this lane group's 8 record slots in LDS (by frame ordinal mod 8), at LDS
+// address rbase + 128 fg (the DMA's M0 base rbase is the wave's)
+__device__ inline void verify_frames_claimed(const uint8_t *blob, const GeneralScratch &gs, uint64_t nwalk,
+                                             uint64_t fbase, uint64_t fstride, uint32_t *s_claim,
+                                             const uint4 *recs, uint32_t rbase, const uint64_t *sec, int lane,
+                                             uint64_t t0) {
+    // sec: the stripe secret words in LDS (one ds_read per piece keeps two load sets
+    // and the accumulators in registers without spilling)
+    const uint32_t l = lane & 7, m = l >> 1, par = l & 1;
+    const uint32_t poff = 16 * (m + 4 * par);
+    const uint32_t sbase = par + 2 * m;  // secret word of piece q: sbase + 2q (and + 1)
+    rbase = __builtin_amdgcn_readfirstlane(rbase);
+    const uint64_t key0 = kSecretW8[16 + 2 * m], key1 = kSecretW8[17 + 2 * m];
+    const uint64_t init0 = par ? 0 : kAccInit[2 * m], init1 = par ? 0 : kAccInit[2 * m + 1];
+    const uint64_t last0 = kSecretLast[2 * m], last1 = kSecretLast[2 * m + 1];
+    const uint64_t mrg0 = kSecretMerge[2 * m], mrg1 = kSecretMerge[2 * m + 1];
+    auto claim = [&]() -> uint64_t {
+        uint32_t k = 0;
+        if (l == 0) k = atomicAdd(s_claim, 1u);
+        k = (uint32_t)__shfl((int)k, lane & ~7);
+        const uint64_t f = fbase + fstride * k;
+        return f < nwalk ? f : nwalk;
+    };
+    // issue cursor: frame icur (ordinal io, block ib), then the claimed frames n1, n2.
+    // The records of frames 0 and 1 come straight from vrec, before the loop.
+    const uint64_t f0 = claim();
+    const uint64_t f1 = f0 < nwalk ? claim() : nwalk;
+    if (l < 2) *(uint4 *)&recs[l] = *(const uint4 *)(gs.vrec + 2 * (l == 0 ? f0 : f1));
+    VFrame icur = vd_frame(recs[0], nwalk);
+    uint64_t n1 = f1, n2 = n1 < nwalk ? claim() : nwalk;
+    // every prologue load is waited for here, before the loop: a first use inside it
+    // (the merge at the loop head) drew a compiler vmcnt wait there on every iteration
+    asm volatile("" ::"v"(key0), "v"(key1), "v"(init0), "v"(init1), "v"(last0), "v"(last1), "v"(mrg0), "v"(mrg1));
+    asm volatile("" ::"v"(icur.p), "v"(icur.L), "v"(icur.f));
+    uint32_t ib = 0, io = 0;
+    bool sw = false;  // the next set starts frame n1
+    auto issue = [&](VStepC &Y) {
+        if (sw) {  // the next frame: its record was DMA'd by a set the wave has waited for
+            icur = vd_frame(recs[(io + 1) & 7], nwalk);
+            if (n1 >= nwalk) icur.f = nwalk;
+            n1 = n2;
+            n2 = n1 < nwalk ? claim() : nwalk;
+            ib = 0;
+            ++io;
+        }
+        vissue(blob, icur, nwalk, ib, par, poff, m, Y.s);
+        Y.cs = gs.cs[(icur.f < nwalk && ib == 0) ? icur.f : 0];
+        Y.b = ib;
+        Y.o = io;
+        {  // the records of the next two frames into their slots (lanes (io+1)&7, (io+2)&7)
+            const uint32_t l1 = (io + 1) & 7, l2 = (io + 2) & 7;
+            if (l == l1 || l == l2) glds16(gs.vrec + 2 * (l == l1 ? n1 : n2), rbase);
+        }
+        ++ib;
+        sw = icur.f < nwalk && ib == vd_nsteps(true, icur.L);
+    };
+    uint64_t a0 = init0, a1 = init1, stored = 0, bad = ~0ull;
+    uint4 lastp = make_uint4(0, 0, 0, 0);
+    auto step = [&](VStepC &X, VStepC &Y) {
+        issue(Y);
+        // X has landed on every path (also the ones that skip the hashing): otherwise the
+        // compiler waited for X at the next loop head, after Y was issued, i.e. for Y too
+#pragma unroll
+        for (int q = 0; q < 8; ++q)
+            asm volatile("" ::"v"(X.s.v[q].x), "v"(X.s.v[q].y), "v"(X.s.v[q].z), "v"(X.s.v[q].w), "v"(X.s.nx[q]));
+        asm volatile("" ::"v"(X.s.last.x), "v"(X.s.last.y), "v"(X.s.last.z), "v"(X.s.last.w), "v"(X.s.lnx), "v"(X.cs));
+        const VFrame xf = vd_frame(recs[X.o & 7], nwalk);  // X's frame (its slot is not reused before ordinal + 8)
+        if (xf.f >= nwalk) return;
+        const uint64_t L = xf.L;
+        const uint32_t b = X.b;
+        const bool lng = L > 240;
+        {  // a frame's first block: fresh accumulators, its stored checksum and last-stripe
+           // piece (selects per component: a conditional uint4 went through scratch memory)
+            const bool first = b == 0;
+            const uint4 lp = realign(X.s.last, X.s.lnx, (uint32_t)((uintptr_t)(blob + xf.p + 8 + L) & 3));
+            a0 = first ? init0 : a0;
+            a1 = first ? init1 : a1;
+            stored = first ? X.cs : stored;
+            lastp.x = first ? lp.x : lastp.x;
+            lastp.y = first ? lp.y : lastp.y;
+            lastp.z = first ? lp.z : lastp.z;
+            lastp.w = first ? lp.w : lastp.w;
+        }
+        if (!lng) return;
+        const uint64_t nbF = (L - 1) / 1024, ns = ((L - 1) - 1024 * nbF) / 64;
+        const uint32_t r = (uint32_t)((uintptr_t)(blob + xf.p + 8) & 3);
+        uint4 pc[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) pc[q] = realign(X.s.v[q], X.s.nx[q], r);
+        if (b < nbF) {
+            uint64_t p0[4] = {0, 0, 0, 0}, p1[4] = {0, 0, 0, 0};
+#pragma unroll
+            for (int q = 0; q < 8; ++q) piece(p0[q & 3], p1[q & 3], pc[q], sec[sbase + 2 * q], sec[sbase + 2 * q + 1]);
+            a0 += (p0[0] + p0[1]) + (p0[2] + p0[3]);
+            a1 += (p1[0] + p1[1]) + (p1[2] + p1[3]);
+            a0 += gdpp64<0xB1>(a0);
+            a1 += gdpp64<0xB1>(a1);
+            a0 = scramble1(a0, key0);
+            a1 = scramble1(a1, key1);
+            if (par) { a0 = 0; a1 = 0; }
+        } else {
+#pragma unroll
+            for (int q = 0; q < 8; ++q)
+                if (2 * q + par < ns) piece(a0, a1, pc[q], sec[sbase + 2 * q], sec[sbase + 2 * q + 1]);
+        }
+        if (b + 1 == vd_nsteps(true, L)) {
+            a0 += gdpp64<0xB1>(a0);
+            a1 += gdpp64<0xB1>(a1);
+            piece(a0, a1, lastp, last0, last1);
+            uint64_t t = fold64(a0 ^ mrg0, a1 ^ mrg1);
+            t += gdpp64<0x4E>(t);
+            t += gswz_xor4(t);
+            const uint64_t h = avalanche(L * P64_1 + t);
+            if (h != stored && bad == ~0ull) bad = xf.f;
+        }
+    };
+    VStepC A, B;
+    issue(A);
+    bool more = true;
+    while (more) {
+        step(A, B);
+        more = __ballot(vd_frame(recs[B.o & 7], nwalk).f < nwalk) != 0;
+        if (!more) break;
+        step(B, A);
+        more = __ballot(vd_frame(recs[A.o & 7], nwalk).f < nwalk) != 0;
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the last record DMAs land before the LDS is reused
     if (l == 0 && bad != ~0ull) atomicMax((unsigned long long *)&gs.misc[2], (unsigned long long)~bad);
     uint64_t *vstat = (uint64_t *)(gs.small + 512) + 14;  // phase clock: [14] last / [15] sum of loop ends
     if (lane == 0) {
@@ -1329,6 +1486,7 @@ __global__ __launch_bounds__(kGenThreads) void k_decode_general(const uint8_t *_
     // walk-order frame records for verify_frames_dma (vrec), and the "none" record after them
     const bool vdma = VERIFY && bl < (1ull << 32) && !(kDiagMask && (gs.dbg & 0x200000));
     if (vdma) {
+        if (threadIdx.x < 24) ((uint64_t *)(s_gdyn + kVdSecOff))[threadIdx.x] = kSecretW8[threadIdx.x];
         const uint64_t wend = __hip_atomic_load(&gs.misc[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & ~kStopBit;
         for (uint64_t f = gtid; f <= nwalk; f += gthreads) {
             uint4 v = make_uint4(0, 0, 0, kVdNone);
@@ -1405,8 +1563,11 @@ __global__ __launch_bounds__(kGenThreads) void k_decode_general(const uint8_t *_
                                   (wave - 4) * kVdWave, lane, t0);
             } else if (IGGY_VD_REGWAVES) {
                 if (member == 1 && wave == 0 && lane == 0) ((uint64_t *)(gs.small + 512))[17] = 8 * (nwg - 1);
-                verify_frames(blob, gs, nwalk, wend, 0, 1, (uint32_t)fbase, (uint32_t)fstride, &s_mem[2], lane, t0,
-                              blob + bl, true);
+                typedef __attribute__((address_space(3))) uint8_t lds_u8;
+                const uint32_t lbase = (uint32_t)(uintptr_t)(lds_u8 *)s_gdyn;
+                verify_frames_claimed(blob, gs, nwalk, fbase, fstride, &s_mem[2],
+                                      (const uint4 *)(s_gdyn + kVdRecOff + 1024 * wave + 128 * ((uint32_t)lane >> 3)),
+                                      lbase + kVdRecOff + 1024 * wave, (const uint64_t *)(s_gdyn + kVdSecOff), lane, t0);
             }
         }
     } else if (VERIFY) {

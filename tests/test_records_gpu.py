@@ -171,3 +171,48 @@ def test_poll_one_launch(cx, mode):
         orc, oe, om = O.poll_decode(b, mode)
         assert rc == orc and e.astuple() == oe.astuple()
         assert [m.astuple() for m in msgs] == [m.astuple() for m in om]
+
+
+def test_completion_flag_sequence_wrap():
+    """Diagnostic build only: the host-mapped completion flags' sequence wraps (2^32
+    values, 0 skipped) in the middle of a run of one-launch chunk walks and segment
+    recoveries; every result still matches the oracle."""
+    import os
+    from iggy_amd import codec as C
+    if not os.path.exists(C.DIAG_LIB_PATH):
+        pytest.skip("diagnostic build not present")
+    L = C.load(C.DIAG_LIB_PATH)
+    c = C.Codec(0, library=L)
+    try:
+        chunk, starts = _chunk(C1_CHUNK)
+        seg, _ = _segment([(1000, 256)] * 3 + [(24, 100)], 500)
+        L.iggy_codec_debug_set(c.handle, 0x40000000)
+        for k in range(40):
+            _walk_same(c, chunk, abi.LOOKUP_OFFSET, 1000 + 37 * k, 500, integrity=k & 1)
+            if k % 4 == 0:
+                rc, out = c.recover_segment(seg, 500)
+                orc, oout = O.recover_segment(seg, 500)
+                assert rc == orc == 0 and out.astuple() == oout.astuple()
+    finally:
+        c.close()
+
+
+def test_segment_above_zero_copy_table_limit(cx):
+    """A segment whose one launch needs more than 4,096 workgroups (560 C1 batches,
+    170 MB): the task table and workgroup map go up with one H2D copy instead of being
+    read from host-mapped memory. Walk, recovery and a corruption near the end exact."""
+    base = _record([256] * 1000, 9, 0, 1)
+    recs, off = [], 0
+    for k in range(560):
+        rc, e, h, st = O.stamp_batch(base, off, 10 + k)
+        recs.append(np.frombuffer(st, dtype=np.uint8).copy())
+        off += 1000
+    seg = np.concatenate(recs)
+    rc, w, idx = cx.walk_segment_payload(seg, 0)
+    orc, ow, oidx = O.walk_segment_payload(seg, 0)
+    assert rc == orc == 0 and w.astuple() == ow.astuple() and idx == oidx
+    assert w.batches == 560
+    b = seg.copy(); b[304256 * 541 + 256 + 304 * 17 + 100] ^= 1
+    rc, out = cx.recover_segment(b, 0)
+    orc, oout = O.recover_segment(b, 0)
+    assert out.astuple() == oout.astuple() and out.batches == 541
