@@ -69,12 +69,16 @@ struct DevBuf {
 
 // Mapped, coherent pinned host memory that kernels read and write directly (small
 // tables in, results / positions / flags out): no copy operation on the stream.
+constexpr size_t kHostMapKeep = 8ull << 20;  // pinned bytes a context keeps between calls
 struct HostMap {
     void *h = nullptr;
     uint8_t *d = nullptr;  // the device's address of the same bytes
     size_t cap = 0;
     int ensure(size_t n) {
-        if (n <= cap) return 0;
+        // grown past kHostMapKeep by one large call (a poll of many small frames, a
+        // 16 MiB decode with positions): given back at the next ordinary-sized call
+        // instead of staying pinned for the context's life
+        if (n <= cap && !(cap > kHostMapKeep && n <= kHostMapKeep)) return 0;
         release();
         const size_t want = std::max<size_t>(n, 64 << 10);
         if (hipHostMalloc(&h, want, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess) {
