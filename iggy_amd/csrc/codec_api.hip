@@ -214,7 +214,8 @@ namespace {
 
 constexpr size_t kSyncExited = 0, kSyncFirstBad = 8, kSyncSpecFail = 16, kSyncBar = 32,
                  kSyncMisc = 64, kSyncSmall = 256, kSyncBar2 = 1024,  // + kBar2Words u32 at 128-B stride
-                 kSyncBytes = kSyncBar2 + kBar2Words * 128;
+                 kSyncSink = kSyncBar2 + kBar2Words * 128,            // 64 x u64 (DecodeScratch::sink)
+                 kSyncBytes = kSyncSink + 512;
 
 int ensure_decode_scratch(iggy_codec_ctx *c, uint64_t len) {
     if (len <= c->dec_cap_len && c->dsync.p) return 0;
@@ -261,6 +262,7 @@ DecodeScratch dscratch(iggy_codec_ctx *c) {
     s.sums = c->dsums.as<uint64_t>();
     s.errslot = c->derr.as<uint64_t>();
     s.small = c->dsync.as<uint8_t>(kSyncSmall);
+    s.sink = c->dsync.as<uint64_t>(kSyncSink);
     s.gbar = c->dsync.as<uint32_t>(kSyncBar);
     s.gbar2 = c->dsync.as<uint32_t>(kSyncBar2);
     s.gmisc = c->dsync.as<uint64_t>(kSyncMisc);

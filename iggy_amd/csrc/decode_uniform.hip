@@ -50,6 +50,8 @@ struct DecodeScratch {
                           // 128-frame checksum block, 2 per chunk; see publish_block
     uint64_t *errslot;    // [max_chunks*32][2] (stored, computed) of the first mismatch per 8-frame group
     uint8_t *small;       // >= 512 B: short batch-checksum inputs
+    uint64_t *sink;       // 64 x u64: the lane-group producers' frame-position stores that
+                          // have no frame (past N or the caller's capacity) land here
     uint32_t *gbar2;      // the general kernel's two-level barrier counters (kBar2Words, 128-B stride)
     uint32_t *gbar;       // the general kernel's barrier / registration words and its
     uint64_t *gmisc;      // first-bad slot: re-armed here (see k_decode_general)
@@ -630,6 +632,9 @@ __device__ __forceinline__ uint32_t lg_nsteps(const LgPlan &pl) {
 // i of instruction k lands at slot + 1024k + 16i, so each lane later reads back
 // exactly its own 16 B. The loads bypass VGPRs: the wave waits for them with an
 // explicit vmcnt, and never blocks on the step it has just issued.
+#ifndef IGGY_LG_POS_EXACT
+#define IGGY_LG_POS_EXACT 0  // (build knob for a same-box A/B)
+#endif
 constexpr uint32_t kLgLoads = 9;
 constexpr uint32_t kLgStepBytes = kLgLoads * 1024;
 template <bool ONE>
@@ -764,7 +769,16 @@ __device__ __forceinline__ bool lg_process(const LgPlan &pl, const LgLane &c, co
         const int leader = __builtin_ctzll(sb);
         if (lane == leader) atomicMax((unsigned long long *)sc.spec_fail, (unsigned long long)~(uint64_t)i);
     }
-    if (c.l == 0 && !pl.nopub && valid && (uint64_t)i < cap && frame_pos) frame_pos[i] = (uint64_t)i * pl.S;
+    if (ONE && IGGY_LG_POS_EXACT) {
+        // one store instruction per step on every path (the group's 8 lanes write the same
+        // word; lanes without a frame write the sink), so the ring's vmcnt wait can count it
+        if (frame_pos && !pl.nopub) {
+            uint64_t *dst = (valid && (uint64_t)i < cap) ? frame_pos + i : sc.sink + lane;
+            asm volatile("global_store_dwordx2 %0, %1, off" ::"v"(dst), "v"((uint64_t)i * pl.S) : "memory");
+        }
+    } else if (c.l == 0 && !pl.nopub && valid && (uint64_t)i < cap && frame_pos) {
+        frame_pos[i] = (uint64_t)i * pl.S;
+    }
     return true;
 }
 
@@ -894,6 +908,7 @@ __device__ __forceinline__ void produce_lg(const uint8_t *blob, const LgPlan &pl
     for (int q = 0; q < 4; ++q) pin_after_wait(c.wsec[q]);
     const uint64_t blocks = 2 * pl.nchunks;                // 128-frame blocks (tail blocks hold invalid frames)
     const uint32_t nblk = ONE ? 1u : lg_nsteps(pl);       // steps per frame group
+    const bool pos_st = frame_pos && !pl.nopub;            // (ONE form) a position store every step
     if (g >= blocks) return;
     const uint64_t mine = 4 * ((blocks - g + np - 1) / np);  // units of blocks g, g + np, ...
     const uint64_t total = mine * nblk;                   // steps of this wave
@@ -929,7 +944,12 @@ __device__ __forceinline__ void produce_lg(const uint8_t *blob, const LgPlan &pl
     for (uint32_t d = 0; d < SLOTS; ++d) issue_next();
     for (uint64_t k = 0; k < total; ++k) {
         // step k landed; the later steps stay in flight (the last SLOTS-1 steps drain all)
-        if (k + SLOTS <= total) wait_vm_const<kLgLoads * (SLOTS - 1)>();
+        // steps k+1..k+3 stay in flight; with a position store per step (ONE form) the
+        // stores of steps k-4..k-1 were issued after step k's loads too
+        if (k + SLOTS <= total) {
+            if (ONE && IGGY_LG_POS_EXACT && pos_st) wait_vm_const<kLgLoads * (SLOTS - 1) + SLOTS>();
+            else wait_vm_const<kLgLoads * (SLOTS - 1)>();
+        }
         else wait_vm_const<0>();
         LgBuf B;
         const uint32_t slot = ring + (k % SLOTS) * kLgStepBytes;
