@@ -614,6 +614,9 @@ constexpr uint32_t kVdSecOff = kVdRecOff + 8 * 1024;    // the register loop's r
 constexpr uint32_t kGenLds = kVdSecOff + 24 * 8;         // and its stripe secrets
 static_assert(kGenLds + 64 <= 160 * 1024, "LDS budget (with the kernel's static LDS words)");
 static_assert(2 * kChainChunk * 8 * 8 <= 2 * kVdWave, "WG 0's chain buffer fits its waves 4, 5's rings");
+#ifndef IGGY_VD_SHORT_SPLIT
+#define IGGY_VD_SHORT_SPLIT 1  // (build knob for same-box A/B: 0 = short frames in every wave first)
+#endif
 #ifndef IGGY_VD_REGWAVES
 #define IGGY_VD_REGWAVES 1  // (build knob for same-box A/B: 0 = the LDS-ring waves alone)
 #endif
@@ -1549,11 +1552,21 @@ __global__ __launch_bounds__(kGenThreads) void k_decode_general(const uint8_t *_
         // 6, 7: its waves 4, 5's ring space holds the chain buffer).
         const uint32_t ws = long_cs ? 2 : 1;  // WG 0's waves below ws chain (and stage)
         const uint64_t wend = __hip_atomic_load(&gs.misc[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & ~kStopBit;
-        const uint32_t nsw = nwg * 8 - ws;
-        verify_short(blob, gs, nwalk, wend, member * 8 + wave - ws, nsw, lane);
+        const bool alone = nwg == 1;
+        if (IGGY_VD_SHORT_SPLIT) {
+            // the short frames go to the waves that do not stream through rings (WG 0's
+            // idle waves, the register-loop waves), so the rings start at once
+            const bool ring = wave >= (member == 0 ? 6u : 4u) && (alone || member > 0);
+            if (!ring) {
+                const uint32_t sw = member == 0 ? wave - ws : (8 - ws) + 4 * (member - 1) + wave;
+                const uint32_t nsw = alone ? 6 - ws : (8 - ws) + 4 * (nwg - 1);
+                verify_short(blob, gs, nwalk, wend, sw, nsw, lane);
+            }
+        } else {
+            verify_short(blob, gs, nwalk, wend, member * 8 + wave - ws, nwg * 8 - ws, lane);
+        }
         if (lane == 0)  // phase clock [16]: the short frames' end
             atomicMax((unsigned long long *)((uint64_t *)(gs.small + 512) + 16), (unsigned long long)(rt_now() - t0));
-        const bool alone = nwg == 1;
         if (alone || member > 0) {
             const uint64_t fbase = alone ? 0 : member - 1, fstride = alone ? 1 : nwg - 1;
             if (wave >= (member == 0 ? 6u : 4u)) {
