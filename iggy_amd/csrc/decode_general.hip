@@ -605,15 +605,26 @@ __device__ inline void verify_frames(const uint8_t *blob, const GeneralScratch &
 // copies into the group's 8-entry record ring. So the next frames' positions are in
 // LDS before their first block is issued, with no VGPR load in the loop (its only
 // vector-memory operations are the 9 counted DMAs).
-constexpr uint32_t kVdSlots = 4;                        // 3 steps in flight + the one being read
+#ifndef IGGY_VD_SLOTS
+#define IGGY_VD_SLOTS 2  // (build knobs for same-box A/B: ring slots, ring waves per workgroup)
+#endif
+#ifndef IGGY_VD_NDMA
+#define IGGY_VD_NDMA 6
+#endif
+constexpr uint32_t kVdSlots = IGGY_VD_SLOTS;            // steps in flight + the one being read
+constexpr uint32_t kVdNdma = IGGY_VD_NDMA;              // ring waves: the last kVdNdma of a workgroup
+constexpr uint32_t kVdFirst = 8 - kVdNdma;
 constexpr uint32_t kVdStep = 9 * 1024;                  // 9 DMA instructions x 64 lanes x 16 B
 constexpr uint32_t kVdMeta = 8 * 9 * 16;                // 8 groups x (8 frame records + a spare)
 constexpr uint32_t kVdWave = kVdSlots * kVdStep + kVdMeta;
-constexpr uint32_t kVdRecOff = 4 * kVdWave;             // waves 4..7 of a workgroup: rings; then
-constexpr uint32_t kVdSecOff = kVdRecOff + 8 * 1024;    // the register loop's record slots (verify_frames_claimed),
+// WG 0's chain buffer (64 KiB) overlays the rings of its first ring waves; the ones
+// after it (kVdWg0First..7) verify when WG 0 is alone
+constexpr uint32_t kVdWg0First = kVdFirst + (2 * kChainChunk * 8 * 8 + kVdWave - 1) / kVdWave;
+static_assert(kVdWg0First <= 6, "WG 0 keeps at least two ring waves");
+constexpr uint32_t kVdRecOff = kVdNdma * kVdWave;       // the ring waves' rings; then
+constexpr uint32_t kVdSecOff = kVdRecOff + kVdWg0First * 1024;  // the register loop's record slots (verify_frames_claimed),
 constexpr uint32_t kGenLds = kVdSecOff + 24 * 8;         // and its stripe secrets
 static_assert(kGenLds + 64 <= 160 * 1024, "LDS budget (with the kernel's static LDS words)");
-static_assert(2 * kChainChunk * 8 * 8 <= 2 * kVdWave, "WG 0's chain buffer fits its waves 4, 5's rings");
 #ifndef IGGY_VD_SHORT_SPLIT
 #define IGGY_VD_SHORT_SPLIT 1  // (build knob for same-box A/B: 0 = short frames in every wave first)
 #endif
@@ -1546,20 +1557,21 @@ __global__ __launch_bounds__(kGenThreads) void k_decode_general(const uint8_t *_
         // Frames of <= 240 B first, a slice per wave of every WG. Then the long frames,
         // claimed one per lane group from the workgroup's LDS counter (WG member m of
         // the verifying set takes frames m + nv k, a chip-wide front) by two loops side
-        // by side: waves 4..7 stream through LDS rings (verify_frames_dma), waves 0..3
-        // run the register loop (verify_frames); the counter balances the two. WG 0
-        // runs the chain and only verifies when it is alone (then with waves ws..5 and
-        // 6, 7: its waves 4, 5's ring space holds the chain buffer).
+        // by side: the last kVdNdma waves (4..7) stream through LDS rings
+        // (verify_frames_dma), the others run the register loop (verify_frames_claimed);
+        // the counter balances the two. WG 0 runs the chain and only verifies when it
+        // is alone (its first ring waves' space holds the chain buffer).
         const uint32_t ws = long_cs ? 2 : 1;  // WG 0's waves below ws chain (and stage)
         const uint64_t wend = __hip_atomic_load(&gs.misc[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & ~kStopBit;
         const bool alone = nwg == 1;
         if (IGGY_VD_SHORT_SPLIT) {
             // the short frames go to the waves that do not stream through rings (WG 0's
             // idle waves, the register-loop waves), so the rings start at once
-            const bool ring = wave >= (member == 0 ? 6u : 4u) && (alone || member > 0);
+            const bool ring = wave >= (member == 0 ? kVdWg0First : kVdFirst) && (alone || member > 0);
             if (!ring) {
-                const uint32_t sw = member == 0 ? wave - ws : (8 - ws) + 4 * (member - 1) + wave;
-                const uint32_t nsw = alone ? 6 - ws : (8 - ws) + 4 * (nwg - 1);
+                const uint32_t n0 = alone ? kVdWg0First - ws : 8 - ws;  // WG 0's share
+                const uint32_t sw = member == 0 ? wave - ws : n0 + kVdFirst * (member - 1) + wave;
+                const uint32_t nsw = n0 + kVdFirst * (nwg - 1);
                 verify_short(blob, gs, nwalk, wend, sw, nsw, lane);
             }
         } else {
@@ -1569,11 +1581,11 @@ __global__ __launch_bounds__(kGenThreads) void k_decode_general(const uint8_t *_
             atomicMax((unsigned long long *)((uint64_t *)(gs.small + 512) + 16), (unsigned long long)(rt_now() - t0));
         if (alone || member > 0) {
             const uint64_t fbase = alone ? 0 : member - 1, fstride = alone ? 1 : nwg - 1;
-            if (wave >= (member == 0 ? 6u : 4u)) {
+            if (wave >= (member == 0 ? kVdWg0First : kVdFirst)) {
                 typedef __attribute__((address_space(3))) uint8_t lds_u8;
                 const uint32_t lbase = (uint32_t)(uintptr_t)(lds_u8 *)s_gdyn;
                 verify_frames_dma(blob, body, gs, nwalk, fbase, fstride, &s_mem[2], s_gdyn, lbase,
-                                  (wave - 4) * kVdWave, lane, t0);
+                                  (wave - kVdFirst) * kVdWave, lane, t0);
             } else if (IGGY_VD_REGWAVES) {
                 if (member == 1 && wave == 0 && lane == 0) ((uint64_t *)(gs.small + 512))[17] = 8 * (nwg - 1);
                 typedef __attribute__((address_space(3))) uint8_t lds_u8;
