@@ -592,8 +592,10 @@ __device__ inline void verify_frames(const uint8_t *blob, const GeneralScratch &
 // The register loop above keeps one step in flight per wave and loads every chunk
 // from its 4-B-aligned address plus the dword after it (18 loads per step). Here
 // each verify wave streams like the uniform kernel's lane-group producers
-// (decode_uniform.hip): exactly 9 global_load_lds_dwordx4 per step into a 4-slot
-// ring, an explicit constant vmcnt wait, three steps in flight. A frame starts at
+// (decode_uniform.hip): exactly 9 global_load_lds_dwordx4 per step into a
+// kVdSlots-slot ring, an explicit constant vmcnt wait, kVdSlots - 1 steps in flight
+// (the loop is instruction-bound: six ring waves with two slots each measured
+// faster than four with four, in the same LDS). A frame starts at
 // any byte, so a lane group loads its block's 16-B-ALIGNED window (64 chunks,
 // lane l of instruction q takes chunk 8q + l: row q of the window lands as 128
 // contiguous bytes at slot + 1024q + 128fg) plus the chunk after it, and each lane
@@ -763,7 +765,7 @@ __device__ inline void verify_frames_dma(const uint8_t *blob, const uint8_t *dum
             a1 = init1;
         }
         if (!__ballot(p_f != kVdNone)) break;
-        wait_vm_const<9 * (kVdSlots - 1)>();  // step k landed; steps k+1..k+3 stay in flight
+        wait_vm_const<9 * (kVdSlots - 1)>();  // step k landed; the later steps stay in flight
         const uint32_t slot = region + (k % kVdSlots) * kVdStep;
         const uint8_t *row = smem + slot + 128 * fg;
         uint4 pc[8];
@@ -839,7 +841,8 @@ __device__ inline void verify_frames_dma(const uint8_t *blob, const uint8_t *dum
     }
 }
 
-// Register loop beside verify_frames_dma (claims mode), in waves 0..3. A record
+// Register loop beside verify_frames_dma (claims mode), in the waves before the
+// ring waves. A record
 // (position, hashed length, index: vrec) only ever reaches a register through a
 // step's load set that the wave has already waited for: each set carries the
 // records of the two frames after the one it loads (and, on a frame's first block,
