@@ -699,39 +699,47 @@ __device__ inline void verify_frames_dma(const uint8_t *blob, const uint8_t *dum
     // branches only at a frame start): divergent paths would run in turn for the
     // wave's eight groups, and a step's instruction count bounds the loop as much as
     // its bytes do.
-    uint32_t ij = 0, ib = 0, i_nsteps = 1, i_f = kVdNone;
-    uint64_t i_p = 0, i_L = 0;
+    uint32_t ij = 0, ib = 0, i_nsteps = 1;
+    // per-frame issue state, set at the frame's first block (a group-uniform branch):
+    // the window base of block 0 for this lane, its alignment, the block counts, and
+    // the ninth load's address for the first block
+    const uint8_t *i_g = dummy, *i_x9 = dummy;
+    uint32_t i_r = 0, i_nbF = 0, i_used = 0;
+    bool i_lng = false;
     auto issue = [&](uint32_t slot_off) {
         const uint32_t slot = lbase + slot_off;  // the DMA's LDS address (M0) of the slot
-        if (ib == 0) {
-            const uint4 rec = *(const uint4 *)(smem + meta + 16 * (ij & 7));
-            i_p = (uint64_t)rec.x | ((uint64_t)rec.y << 32);
-            i_L = rec.z;
-            i_f = rec.w;
-            i_nsteps = vd_nsteps(i_f != kVdNone, i_L);
-        }
-        const bool valid = i_f != kVdNone;
-        const bool lng = valid && i_L > 240;
-        const uint64_t nbF = (i_L - 1) >> 10, ns = ((i_L - 1) & 1023) >> 6;
-        const uint8_t *H = blob + i_p + 8;
-        const uint8_t *W = H + ((uint64_t)ib << 10);
-        const uint32_t r = (uint32_t)((uintptr_t)W & 15);
-        const uint8_t *g = W - r + 16 * l;
         const bool first = ib == 0;
-        const bool full = lng && ib < nbF;
+        if (first) {
+            const uint4 rec = *(const uint4 *)(smem + meta + 16 * (ij & 7));
+            const uint64_t p = (uint64_t)rec.x | ((uint64_t)rec.y << 32);
+            const uint64_t L = rec.z;
+            const uint32_t f = rec.w;
+            const bool valid = f != kVdNone;
+            i_nsteps = vd_nsteps(valid, L);
+            i_lng = valid && L > 240;
+            i_nbF = (uint32_t)((L - 1) >> 10);
+            const uint8_t *H = blob + p + 8;
+            i_r = (uint32_t)((uintptr_t)H & 15);
+            i_g = H - i_r + 16 * l;
+            // the partial block's bytes: [r, r + 64 ns) of its window
+            i_used = i_lng ? (uint32_t)((((L - 1) & 1023) >> 6) << 6) + i_r : 0u;
+            const uint8_t *Ls = H + L - 64;
+            const uint32_t rl = (uint32_t)((uintptr_t)Ls & 15);
+            const uint8_t *c0 = (i_lng && i_nbF > 0 && i_r) ? i_g + 1024 : dummy;  // (l == 0)
+            const uint8_t *cl = (i_lng && (l < 5 || rl)) ? Ls - rl + 16 * (l - 1) : dummy;
+            const uint8_t *c6 = valid ? (const uint8_t *)(gs.cs + (f & ~1u)) : dummy;
+            const uint8_t *c7 = (const uint8_t *)(gs.vrec + 2 * fa);
+            i_x9 = l == 0 ? c0 : l <= 5 ? cl : l == 6 ? c6 : c7;
+            fa = succ(fa);
+        }
+        const uint8_t *g = i_g + ((uint64_t)ib << 10);
+        const bool full = i_lng && ib < i_nbF;
         // window bytes this step needs: [r, r + 1024) of a full block, [r, r + 64 ns) of the
         // partial one; a chunk is loaded when it holds one of them
-        const uint32_t used = full ? 1024u + r : (lng ? (uint32_t)(ns << 6) + r : 0u);
+        const uint32_t used = full ? 1024u + i_r : i_used;
 #pragma unroll
         for (uint32_t q = 0; q < 8; ++q) glds16(128 * q + 16 * l < used ? g + 128 * q : dummy, slot + 1024u * q);
-        const uint8_t *Ls = H + i_L - 64;
-        const uint32_t rl = (uint32_t)((uintptr_t)Ls & 15);
-        const uint8_t *c0 = (full && r) ? g + 1024 : dummy;  // (l == 0: g = the window start)
-        const uint8_t *cl = (lng && first && (l < 5 || rl)) ? Ls - rl + 16 * (l - 1) : dummy;
-        const uint8_t *c6 = (valid && first) ? (const uint8_t *)(gs.cs + (i_f & ~1u)) : dummy;
-        const uint8_t *c7 = first ? (const uint8_t *)(gs.vrec + 2 * fa) : dummy;
-        glds16(l == 0 ? c0 : l <= 5 ? cl : l == 6 ? c6 : c7, slot + 8u * 1024u);
-        if (first) fa = succ(fa);
+        glds16(first ? i_x9 : ((l == 0 && full && i_r) ? g + 1024 : dummy), slot + 8u * 1024u);
         if (++ib == i_nsteps) {
             ib = 0;
             ++ij;
