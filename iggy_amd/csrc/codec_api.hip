@@ -20,6 +20,10 @@
 #include <vector>
 
 #include "../../include/iggy_codec.h"
+
+#ifndef IGGY_ENC_RING
+#define IGGY_ENC_RING 1  // (build knob for same-box A/B: 0 = k_enc_lanes for segmented encodes too)
+#endif
 #include "batch_checksum.hip"
 #include "decode_general.hip"
 #include "decode_uniform.hip"
@@ -163,6 +167,7 @@ struct iggy_codec_ctx {
     // encode scratch
     DevBuf epl, euh, etile, ecs, emisc;
     DevBuf eids, eots, epay, eplen, euhb, euhl;
+    DevBuf erec, esink;  // k_enc_ring's frame records and store sink
     // big one-shot hash
     DevBuf hbsums;
     // poll
@@ -778,7 +783,9 @@ int iggy_codec_create(int device, iggy_codec_ctx **out) {
             hipFuncSetAttribute((const void *)k_decode_uniform<false>,
                                 hipFuncAttributeMaxDynamicSharedMemorySize, kUniformLds) != hipSuccess ||
             hipFuncSetAttribute((const void *)k_decode_general<true>,
-                                hipFuncAttributeMaxDynamicSharedMemorySize, kGenLds) != hipSuccess)
+                                hipFuncAttributeMaxDynamicSharedMemorySize, kGenLds) != hipSuccess ||
+            hipFuncSetAttribute((const void *)k_enc_ring,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, kErLds) != hipSuccess)
             r = IGGY_ERR_DEVICE;
     }
     if (!r) {
@@ -835,7 +842,7 @@ void iggy_codec_destroy(iggy_codec_ctx *c) {
                       &c->gtiles_cnt, &c->gtiles_pre, &c->gtiles_list, &c->gtiles_e, &c->gtiles_base, &c->ggrp, &c->gfpos, &c->gcs, &c->gvrec, &c->gtiles_lcs,
                       &c->gbsums, &c->dresult, &c->din, &c->dpos, &c->dout, &c->epl, &c->euh,
                       &c->etile, &c->ecs, &c->emisc, &c->eids, &c->eots, &c->epay, &c->eplen,
-                      &c->euhb, &c->euhl, &c->hbsums, &c->ppos, &c->pmsgs, &c->pres, &c->cwk, &c->sl, &c->slres, &c->cr,
+                      &c->euhb, &c->euhl, &c->erec, &c->esink, &c->hbsums, &c->ppos, &c->pmsgs, &c->pres, &c->cwk, &c->sl, &c->slres, &c->cr,
                       &c->rtab, &c->rbsums, &c->rres, &c->clinks, &c->rstate, &c->rcount, &c->pbres};
     for (DevBuf *b : bufs) b->release();
     if (c->h_pinned) (void)hipHostFree(c->h_pinned);
@@ -1452,6 +1459,12 @@ static int enqueue_encode(iggy_codec_ctx *c, const iggy_raw_messages *dm, uint64
         // block-sum range that reads their checksums; k_enc_lanes never writes their
         // checksum words. Unsegmented, the one k_enc_lanes launch hashes them after its
         // loop and runs the < 16-B payload-area fallback itself (own_tail).
+        const bool ring = segmented && IGGY_ENC_RING;
+        if (ring) {
+            if (c->erec.ensure((n + 1) * 32) || c->esink.ensure(kErSinkBytes)) return IGGY_ERR_DEVICE;
+            hipLaunchKernelGGL(k_enc_recs, dim3((uint32_t)std::min<uint64_t>((n + 256) / 256, (uint64_t)c->ncu * 8)),
+                               dim3(256), 0, s, m, es, c->erec.as<uint4>());
+        }
         if (segmented) {
             hipLaunchKernelGGL(k_enc_frames, dim3((waves + 3) / 4), dim3(256), 0, s, m, es, d_out, 1u);
             const dim3 sgrid((uint32_t)std::min<uint64_t>((n + 255) / 256, (uint64_t)c->ncu * 4));
@@ -1481,7 +1494,11 @@ static int enqueue_encode(iggy_codec_ctx *c, const iggy_raw_messages *dm, uint64
             const uint64_t B0 = bound(k), B1 = bound(k + 1);
             const uint64_t F0 = k == 0 ? 0 : std::min<uint64_t>(n, 128 * B0 - 5);
             const uint64_t F1 = k == nseg - 1 ? n : std::min<uint64_t>(n, 128 * B1 - 5);
-            if (segmented)
+            if (ring)
+                hipLaunchKernelGGL(k_enc_ring, dim3((uint32_t)std::min<uint64_t>((n + 63) / 64, lcu)),
+                                   dim3(kErThreads), kErLds, s, m, es, d_out, F0, F1,
+                                   (const uint4 *)c->erec.as<uint4>(), c->esink.as<uint8_t>());
+            else if (segmented)
                 hipLaunchKernelGGL(k_enc_lanes<false>, dim3(lwg), dim3(256), 0, s, m, es, d_out, F0, F1);
             else
                 hipLaunchKernelGGL(k_enc_lanes<true>, dim3(lwg), dim3(256), 0, s, m, es, d_out, F0, F1);

@@ -614,6 +614,9 @@ __device__ inline void verify_frames(const uint8_t *blob, const GeneralScratch &
 #define IGGY_VD_NDMA 6
 #endif
 constexpr uint32_t kVdSlots = IGGY_VD_SLOTS;            // steps in flight + the one being read
+// the record of a group's frame four ahead is copied into its ring at that frame's
+// start, and the issue side runs kVdSlots steps ahead of the copy: at most 4 slots
+static_assert(kVdSlots >= 2 && kVdSlots <= 4, "ring deeper than the record lookahead");
 constexpr uint32_t kVdNdma = IGGY_VD_NDMA;              // ring waves: the last kVdNdma of a workgroup
 constexpr uint32_t kVdFirst = 8 - kVdNdma;
 constexpr uint32_t kVdStep = 9 * 1024;                  // 9 DMA instructions x 64 lanes x 16 B

@@ -605,6 +605,339 @@ __global__ __launch_bounds__(256, 2) void k_enc_lanes(iggy_raw_messages m, EncSc
     }
 }
 
+// ---------------------------------------------------------------- ring encode
+// k_enc_ring: the lane-group encode of segmented launches in the decode rings' shape
+// (decode_general.hip verify_frames_dma). k_enc_lanes' waves spend half their
+// cycles in s_waitcnt: their loads and their frame stores share one vmcnt, and the
+// compiler's waits for the next register set also wait for the previous step's
+// stores. Here every wave (8 per CU) streams the payload through a 2-slot LDS ring
+// with exactly 9 global_load_lds_dwordx4 per step (the block's 16-B-aligned payload
+// window, read back at the byte offset), and issues exactly kErStores stores per
+// step from inline asm (8 pieces, 4 tail widths, 2 checksum words; a lane with
+// nothing to store writes its sink slot), so one constant vmcnt wait covers both.
+// Frame records (payload offset, length, timestamp delta, ids: erec, k_enc_recs)
+// reach LDS four frames ahead through the ninth instruction, as vrec does.
+#ifndef IGGY_ER_SLOTS
+#define IGGY_ER_SLOTS 3  // (build knobs for same-box A/B: ring slots, waves per workgroup)
+#endif
+#ifndef IGGY_ER_WAVES
+#define IGGY_ER_WAVES 4
+#endif
+constexpr uint32_t kErSlots = IGGY_ER_SLOTS;
+constexpr uint32_t kErStep = 9 * 1024;
+constexpr uint32_t kErMeta = 8 * 9 * 16;     // 8 groups x (8 records + a spare)
+constexpr uint32_t kErWave = kErSlots * kErStep + kErMeta;
+constexpr uint32_t kErWaves = IGGY_ER_WAVES;
+constexpr uint32_t kErThreads = 64 * kErWaves;
+constexpr uint32_t kErLds = kErWaves * kErWave;
+#ifndef IGGY_ER_MODE
+#define IGGY_ER_MODE 2  // (build knob: 0 every store from asm with sinks; 1 the 8 piece stores only;
+                        //  2 no unconditional store -- the ring wait then counts loads only)
+#endif
+constexpr uint32_t kErStores = IGGY_ER_MODE == 0 ? 14 : IGGY_ER_MODE == 1 ? 8 : 0;  // stores per step, at least
+constexpr uint64_t kErSinkBytes = 256 << 10; // 256 wave slots x 64 lanes x 16 B
+static_assert(kErLds <= 160 * 1024, "LDS budget");
+static_assert(9 * (kErSlots - 1) + kErStores * kErSlots <= 63, "the ring wait fits vmcnt");
+static_assert(IGGY_ER_MODE >= 0 && IGGY_ER_MODE <= 2, "store mode");
+// a frame's record is copied into the ring when its group's frame four ahead starts;
+// the issue side runs kErSlots steps ahead of that copy, so at most 4 slots (a 5-slot
+// build read a stale record and faulted)
+static_assert(kErSlots <= 4, "ring deeper than the record lookahead");
+
+typedef uint32_t er_v4u __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void er_st16(void *p, uint64_t w0, uint64_t w1) {
+    const er_v4u v = {(uint32_t)w0, (uint32_t)(w0 >> 32), (uint32_t)w1, (uint32_t)(w1 >> 32)};
+    asm volatile("global_store_dwordx4 %0, %1, off" ::"v"(p), "v"(v) : "memory");
+}
+__device__ __forceinline__ void er_st8(void *p, uint64_t v) {
+    asm volatile("global_store_dwordx2 %0, %1, off" ::"v"(p), "v"(v) : "memory");
+}
+__device__ __forceinline__ void er_st4(void *p, uint32_t v) {
+    asm volatile("global_store_dword %0, %1, off" ::"v"(p), "v"(v) : "memory");
+}
+__device__ __forceinline__ void er_st2(void *p, uint32_t v) {
+    asm volatile("global_store_short %0, %1, off" ::"v"(p), "v"(v) : "memory");
+}
+__device__ __forceinline__ void er_st1(void *p, uint32_t v) {
+    asm volatile("global_store_byte %0, %1, off" ::"v"(p), "v"(v) : "memory");
+}
+
+// erec[2 i] = {po lo, po hi, payload length, timestamp delta}, erec[2 i + 1] = the ids;
+// erec[2 n], [2 n + 1] = zero (no frame). Also the timestamp-delta check of every frame.
+__global__ __launch_bounds__(256) void k_enc_recs(iggy_raw_messages m, EncScratch es, uint4 *erec) {
+    const uint64_t n = m.count;
+    const uint64_t origin = es.misc[0];
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i <= n;
+         i += (uint64_t)gridDim.x * blockDim.x) {
+        if (i == n) {
+            erec[2 * n] = make_uint4(0, 0, 0, 0);
+            erec[2 * n + 1] = make_uint4(0, 0, 0, 0);
+            continue;
+        }
+        const uint64_t po = es.tile_pl[i / kEncTile] + es.pl_local[i];
+        const uint32_t pl = m.payload_lengths[i];
+        const uint64_t delta = m.origin_timestamps[i] - origin;
+        if (delta > IGGY_MAX_TIMESTAMP_DELTA_MICROS)
+            atomicMax((unsigned long long *)&es.misc[2], (unsigned long long)~i);
+        const uint64_t id0 = m.ids[2 * i], id1 = m.ids[2 * i + 1];
+        erec[2 * i] = make_uint4((uint32_t)po, (uint32_t)(po >> 32), pl, (uint32_t)delta);
+        erec[2 * i + 1] = make_uint4((uint32_t)id0, (uint32_t)(id0 >> 32), (uint32_t)id1, (uint32_t)(id1 >> 32));
+    }
+}
+
+__global__ __launch_bounds__(kErThreads, 1) void k_enc_ring(iggy_raw_messages m, EncScratch es, uint8_t *out,
+                                                            uint64_t f_lo, uint64_t f_hi, const uint4 *erec,
+                                                            uint8_t *sink) {
+    const uint64_t ptot = es.misc[4];
+    if (ptot < 16 || es.misc[5]) return;  // tiny payload area (k_enc_frames) or over capacity
+    const uint64_t N = m.count;           // erec[2 N]: the "no frame" record
+    const uint64_t n = f_hi < N ? f_hi : N;
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    typedef __attribute__((address_space(3))) uint8_t lds_u8;
+    const uint32_t lbase = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(lds_u8 *)smem);
+    const int lane = threadIdx.x & 63;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t l = lane & 7, m8 = l >> 1, par = l & 1, fg = (uint32_t)lane >> 3;
+    const uint32_t poff = 16 * (m8 + 4 * par);
+    const uint64_t vw = (uint64_t)blockIdx.x * kErWaves + wave, nvw = (uint64_t)gridDim.x * kErWaves;
+    const uint64_t stride = 8 * nvw;
+    const uint32_t region = __builtin_amdgcn_readfirstlane(wave * kErWave);
+    const uint8_t *P = m.payloads;
+    const uint8_t *dummy = P;  // (ptot >= 16)
+    uint8_t *my_sink = sink + ((vw & 255) << 10) + 16 * lane;
+    uint64_t s0[8], s1[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+        s0[q] = kSecretW8[2 * q + par + 2 * m8];
+        s1[q] = kSecretW8[2 * q + par + 2 * m8 + 1];
+    }
+    const uint64_t key0 = kSecretW8[16 + 2 * m8], key1 = kSecretW8[17 + 2 * m8];
+    const uint64_t init0 = par ? 0 : kAccInit[2 * m8], init1 = par ? 0 : kAccInit[2 * m8 + 1];
+    const uint64_t last0 = kSecretLast[2 * m8], last1 = kSecretLast[2 * m8 + 1];
+    const uint64_t mrg0 = kSecretMerge[2 * m8], mrg1 = kSecretMerge[2 * m8 + 1];
+    {  // every constant waited for before the first DMA (see verify_frames_dma)
+        uint64_t sk = key0 ^ key1 ^ init0 ^ init1 ^ last0 ^ last1 ^ mrg0 ^ mrg1;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) sk ^= s0[q] ^ s1[q];
+        asm volatile("" : "+v"(sk));
+    }
+    // the group's frames: ordinal j is frame f_lo + 8 vw + fg + j stride (N: none)
+    const uint64_t fbase = f_lo + 8 * vw + fg;
+    auto fidx = [&](uint64_t j) -> uint64_t {
+        const uint64_t f = fbase + j * stride;
+        return f < n ? f : N;
+    };
+    const uint32_t meta = region + kErSlots * kErStep + 144 * fg;  // the group's record ring
+#pragma unroll
+    for (uint32_t k = 0; k < 4; ++k)
+        if (l == k) *(uint4 *)(smem + meta + 16 * k) = erec[2 * fidx(k)];
+    // issue cursor: ordinal ij, block ib; per-frame state set at the frame's first block
+    uint32_t ij = 0, ib = 0, i_nsteps = 1, i_r = 0;
+    uint64_t i_L = 0;
+    bool i_valid = false;
+    const uint8_t *i_g = dummy, *i_x9 = dummy;
+    auto issue = [&](uint32_t slot_off) {
+        const uint32_t slot = lbase + slot_off;
+        const bool first = ib == 0;
+        if (first) {
+            const uint4 rec = *(const uint4 *)(smem + meta + 16 * (ij & 7));
+            const uint64_t f = fidx(ij);
+            i_valid = f < N;
+            const uint64_t po = (uint64_t)rec.x | ((uint64_t)rec.y << 32), pl = rec.z;
+            i_L = 40 + pl;
+            i_nsteps = i_valid ? (uint32_t)((i_L + 1023) >> 10) : 1u;
+            const uint8_t *W0 = P + po - 40;  // stream position 0 (the header is not loaded)
+            i_r = (uint32_t)((uintptr_t)W0 & 15);
+            i_g = W0 - i_r + 16 * l;
+            const uint64_t hi0 = i_r + (i_L < 1024 ? i_L : 1024);
+            const uint8_t *Ls = P + po + pl - 64;  // the last stripe (pl > 200 when it is hashed)
+            const uint32_t rl = (uint32_t)((uintptr_t)Ls & 15);
+            const bool lng = i_valid && i_L > 240;
+            const uint8_t *c0 = (i_valid && hi0 > 1024) ? i_g + 1024 : dummy;  // (l == 0)
+            const uint8_t *cl = (lng && (l < 5 || rl)) ? Ls - rl + 16 * (l - 1) : dummy;
+            const uint8_t *c6 = i_valid ? (const uint8_t *)(erec + 2 * f + 1) : dummy;
+            const uint8_t *c7 = (const uint8_t *)(erec + 2 * fidx(ij + 4));
+            i_x9 = l == 0 ? c0 : l <= 5 ? cl : l == 6 ? c6 : c7;
+        }
+        const uint8_t *g = i_g + ((uint64_t)ib << 10);
+        // window bytes of this block: [lo, hi) (block 0 starts after the 40 header bytes)
+        const uint64_t rem = i_L - ((uint64_t)ib << 10);
+        const uint32_t hi = i_valid ? i_r + (uint32_t)(rem < 1024 ? rem : 1024) : 0u;
+        const uint32_t lo = i_r + (first ? 40u : 0u);
+#pragma unroll
+        for (uint32_t q = 0; q < 8; ++q) {
+            const uint32_t c0 = 128 * q + 16 * l;
+            glds16(c0 < hi && c0 + 16 > lo ? g + 128 * q : dummy, slot + 1024u * q);
+        }
+        glds16(first ? i_x9 : ((l == 0 && hi > 1024) ? g + 1024 : dummy), slot + 8u * 1024u);
+        if (++ib == i_nsteps) {
+            ib = 0;
+            ++ij;
+        }
+    };
+    // processing cursor
+    uint32_t pj = 0, pb = 0, p_nsteps = 1, rb = 0, rl = 0, p_delta = 0;
+    uint64_t p_f = N, p_L = 0, p_pl = 0, nbF = 0, ns = 0;
+    bool p_valid = false, lng = false;
+    uint8_t *F = my_sink;
+    uint32_t o5[5] = {0, 0, 0, 0, 0};
+    uint64_t a0 = init0, a1 = init1, id0 = 0, id1 = 0;
+    uint4 lastp = make_uint4(0, 0, 0, 0);
+    for (uint32_t k = 0; k < kErSlots; ++k) issue(region + k * kErStep);
+    for (uint32_t k = 0;; ++k) {
+        if (pb == 0) {
+            const uint4 rec = *(const uint4 *)(smem + meta + 16 * (pj & 7));
+            p_f = fidx(pj);
+            p_valid = p_f < N;
+            const uint64_t po = (uint64_t)rec.x | ((uint64_t)rec.y << 32);
+            p_pl = rec.z;
+            p_delta = rec.w;
+            p_L = 40 + p_pl;
+            p_nsteps = p_valid ? (uint32_t)((p_L + 1023) >> 10) : 1u;
+            lng = p_valid && p_L > 240;
+            nbF = (p_L - 1) >> 10;
+            ns = ((p_L - 1) & 1023) >> 6;
+            const uint32_t r = (uint32_t)((uintptr_t)(P + po - 40) & 15);
+            rb = r & 3;
+            const uint32_t e = (64 * par + 16 * m8 + r) >> 2;
+#pragma unroll
+            for (uint32_t j = 0; j < 5; ++j) o5[j] = 1024u * ((e + j) >> 5) + 4u * ((e + j) & 31);
+            rl = (uint32_t)((uintptr_t)(P + po + p_pl - 64) & 15);
+            F = p_valid ? out + 256 + 48 * p_f + po : my_sink;
+            a0 = init0;
+            a1 = init1;
+        }
+        if (!__ballot(p_valid)) break;
+        // step k landed. Issued after its loads: the stores of the kErSlots steps
+        // before it and the loads of the later steps -- except in the first kErSlots
+        // iterations, which wait for everything.
+        if (k < kErSlots) wait_vm_const<0>();
+        else wait_vm_const<9 * (kErSlots - 1) + kErStores * kErSlots>();
+        const uint32_t slot = region + (k % kErSlots) * kErStep;
+        const uint8_t *row = smem + slot + 128 * fg;
+        uint4 pc[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            uint32_t d[5];
+#pragma unroll
+            for (int j = 0; j < 5; ++j) d[j] = *(const uint32_t *)(row + 1024 * q + o5[j]);
+            pc[q] = vd_align(d, rb);
+        }
+        const bool first = pb == 0;
+        {  // first block: last-stripe piece, ids, and the record four frames ahead
+            uint32_t d[5];
+            const uint8_t *ls = row + 8192 + 16 + ((rl + 16 * m8) & ~3u);
+#pragma unroll
+            for (int j = 0; j < 5; ++j) d[j] = *(const uint32_t *)(ls + 4 * j);
+            const uint4 lp = vd_align(d, rl & 3);
+            const uint4 ids = *(const uint4 *)(row + 8192 + 96);
+            const uint4 rec = *(const uint4 *)(row + 8192 + 112);
+            if (l == 7) *(uint4 *)(smem + meta + 16 * (first ? (pj + 4) & 7 : 8u)) = rec;
+            lastp.x = first ? lp.x : lastp.x;
+            lastp.y = first ? lp.y : lastp.y;
+            lastp.z = first ? lp.z : lastp.z;
+            lastp.w = first ? lp.w : lastp.w;
+            id0 = first ? ((uint64_t)ids.x | ((uint64_t)ids.y << 32)) : id0;
+            id1 = first ? ((uint64_t)ids.z | ((uint64_t)ids.w << 32)) : id1;
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // slot read out before it is refilled
+        issue(slot);
+        // the block's pieces: header words substituted, stored, hashed
+        const bool full = lng && pb < nbF;
+        uint64_t q0[4] = {0, 0, 0, 0}, q1[4] = {0, 0, 0, 0};
+        uint64_t tw = 0, tsp = ~0ull;  // the lane's partial last piece (1..15 bytes), if any
+        uint64_t tw1 = 0;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            const uint64_t sp = ((uint64_t)pb << 10) + 128 * q + poff;
+            uint64_t w0 = (uint64_t)pc[q].x | ((uint64_t)pc[q].y << 32);
+            uint64_t w1 = (uint64_t)pc[q].z | ((uint64_t)pc[q].w << 32);
+            if (q == 0) {  // stream bytes 0..47 of block 0: the header words
+                const bool h = pb == 0;
+                const uint64_t hw2 = (p_f & 0xFFFFFFFFull) | ((uint64_t)p_delta << 32), hw3 = p_pl << 32;
+                const uint64_t n0 = poff == 0 ? id0 : poff == 16 ? hw2 : 0;
+                const uint64_t n1 = poff == 0 ? id1 : poff == 16 ? hw3 : w1;
+                w0 = (h && poff <= 32) ? n0 : w0;
+                w1 = (h && poff <= 32) ? n1 : w1;
+            }
+            const bool whole = p_valid && sp + 16 <= p_L;
+            if (IGGY_ER_MODE < 2) {
+                er_st16(whole ? (void *)(F + 8 + sp) : (void *)my_sink, w0, w1);
+            } else if (whole) {
+                st128_any(F + 8 + sp, make_uint4((uint32_t)w0, (uint32_t)(w0 >> 32), (uint32_t)w1, (uint32_t)(w1 >> 32)));
+            }
+            const bool part = p_valid && sp < p_L && sp + 16 > p_L;
+            tsp = part ? sp : tsp;
+            tw = part ? w0 : tw;
+            tw1 = part ? w1 : tw1;
+            const uint64_t use = 0ull - (uint64_t)(full || (lng && pb == nbF && (uint64_t)(2 * q + par) < ns));
+            q0[q & 3] += (mul32x32(w0 ^ s0[q]) + w1) & use;
+            q1[q & 3] += (mul32x32(w1 ^ s1[q]) + w0) & use;
+        }
+        if (IGGY_ER_MODE > 0) {  // the partial piece and the checksum words: plain stores
+            if (tsp != ~0ull) {
+                uint8_t *d = F + 8 + tsp;
+                const uint32_t remb = (uint32_t)(p_L - tsp);
+                uint64_t v = tw;
+                if (remb & 8) { st64_any(d, v); d += 8; v = tw1; }
+                if (remb & 4) { *(u32_ua *)d = (uint32_t)v; d += 4; v >>= 32; }
+                if (remb & 2) { *(u16_ua *)d = (uint16_t)v; d += 2; v >>= 16; }
+                if (remb & 1) *d = (uint8_t)v;
+            }
+        } else {  // the partial piece: 8-, 4-, 2-, 1-byte stores (a sink write for each width not used)
+            const bool has = tsp != ~0ull;
+            const uint32_t remb = has ? (uint32_t)(p_L - tsp) : 0u;
+            uint8_t *d = F + 8 + (has ? tsp : 0);
+            uint64_t v = tw;
+            er_st8((remb & 8) ? (void *)d : (void *)my_sink, v);
+            d += (remb & 8);
+            v = (remb & 8) ? tw1 : v;
+            er_st4((remb & 4) ? (void *)d : (void *)my_sink, (uint32_t)v);
+            d += (remb & 4);
+            v = (remb & 4) ? (v >> 32) : v;
+            er_st2((remb & 2) ? (void *)d : (void *)my_sink, (uint32_t)v);
+            d += (remb & 2);
+            v = (remb & 2) ? (v >> 16) : v;
+            er_st1((remb & 1) ? (void *)d : (void *)my_sink, (uint32_t)v);
+        }
+        a0 += (q0[0] + q0[1]) + (q0[2] + q0[3]);
+        a1 += (q1[0] + q1[1]) + (q1[2] + q1[3]);
+        {
+            const uint64_t f0 = a0 + gdpp64<0xB1>(a0), f1 = a1 + gdpp64<0xB1>(a1);
+            a0 = full ? (par ? 0 : scramble1(f0, key0)) : a0;
+            a1 = full ? (par ? 0 : scramble1(f1, key1)) : a1;
+        }
+        const bool fin = pb + 1 == p_nsteps;
+        uint64_t hsh = 0;
+        if (__ballot(fin && lng)) {
+            uint64_t b0 = a0 + gdpp64<0xB1>(a0), b1 = a1 + gdpp64<0xB1>(a1);
+            piece(b0, b1, lastp, last0, last1);
+            uint64_t t = fold64(b0 ^ mrg0, b1 ^ mrg1);
+            t += gdpp64<0x4E>(t);
+            t += gswz_xor4(t);
+            hsh = avalanche(p_L * P64_1 + t);
+        }
+        {  // the frame's checksum word and its batch-checksum input (long frames; short
+           // ones are k_enc_short's)
+            const bool st = fin && lng && l == 0;
+            if (IGGY_ER_MODE > 0) {
+                if (st) {
+                    st64_any(F, hsh);
+                    es.cs[p_f] = hsh;
+                }
+            } else {
+                er_st8(st ? (void *)F : (void *)my_sink, hsh);
+                er_st8(st ? (void *)(es.cs + p_f) : (void *)(my_sink + 8), hsh);
+            }
+        }
+        if (++pb == p_nsteps) {
+            pb = 0;
+            ++pj;
+        }
+    }
+    wait_vm_const<0>();
+}
+
 // Frames of <= 240 hashed bytes of a lane-group encode: one lane each hashes the
 // stream (XXH3 17-128 / 129-240 paths) from the SoA input and backpatches.
 __device__ inline void enc_short_frame(const iggy_raw_messages &m, EncScratch es, uint8_t *out, uint64_t origin,
