@@ -13,6 +13,10 @@
 //                 hashes the same bytes in registers (wave-cooperative XXH3:
 //                 lane l owns stripe words 2l, 2l+1 of each 1 KiB block), then
 //                 backpatches the frame checksum (send_messages.rs:162-163).
+//  k_enc_lanes  : batches without user headers: 8 lanes per frame, one 1 KiB
+//                 block of the hashed stream per step, stores and hashing fused.
+//  k_enc_recs + k_enc_ring : the same for segmented (>= 2^18-message) batches with
+//                 the payload reads through LDS rings (per-frame records ahead).
 //  then k_bsum_blocks / k_bsum_chain (batch_checksum.hip) over the frame
 //  checksums and k_enc_finish (header, error precedence).
 #include "codec_common.hpp"
