@@ -208,6 +208,10 @@ __device__ inline uint32_t walk(const uint8_t *blob, uint64_t bl, uint64_t p, ui
 #define IGGY_LOC_BUF 8
 #endif
 constexpr int kLocBuf = IGGY_LOC_BUF;
+#ifndef IGGY_VREC_U
+#define IGGY_VREC_U 1
+#endif
+constexpr int kVrecU = IGGY_VREC_U;  // phase E's frame records per pass
 __device__ inline uint32_t walk_located(const uint8_t *blob, uint64_t bl, uint64_t p, uint64_t hi,
                                         uint64_t *x_out, uint32_t *list, uint64_t lo, uint64_t *lcs) {
     if (kLocBuf <= 1) return walk(blob, bl, p, hi, x_out, list, lo, lcs);
@@ -1568,14 +1572,27 @@ __global__ __launch_bounds__(kGenThreads) void k_decode_general(const uint8_t *_
     if (vdma) {
         if (threadIdx.x < 24) ((uint64_t *)(s_gdyn + kVdSecOff))[threadIdx.x] = kSecretW8[threadIdx.x];
         const uint64_t wend = __hip_atomic_load(&gs.misc[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & ~kStopBit;
-        for (uint64_t f = gtid; f <= nwalk; f += gthreads) {
-            uint4 v = make_uint4(0, 0, 0, kVdNone);
-            if (f < nwalk) {
-                const uint64_t p = gs.fpos[f];
-                const uint64_t L = (f + 1 < nwalk ? gs.fpos[f + 1] : wend) - p - 8;  // frames tile the walk
-                v = make_uint4((uint32_t)p, (uint32_t)(p >> 32), (uint32_t)L, (uint32_t)f);
+        // kVrecU records per pass, their loads issued before any store (a store ahead
+        // of the next record's loads would make them wait for its acknowledgement)
+        for (uint64_t f0 = gtid; f0 <= nwalk; f0 += (uint64_t)kVrecU * gthreads) {
+            uint64_t pa[kVrecU], pb[kVrecU];
+#pragma unroll
+            for (int u = 0; u < kVrecU; ++u) {
+                const uint64_t f = f0 + (uint64_t)u * gthreads;
+                pa[u] = f < nwalk ? gs.fpos[f] : 0;
+                pb[u] = f + 1 < nwalk ? gs.fpos[f + 1] : wend;  // frames tile the walk
             }
-            *(uint4 *)(gs.vrec + 2 * f) = v;
+#pragma unroll
+            for (int u = 0; u < kVrecU; ++u) {
+                const uint64_t f = f0 + (uint64_t)u * gthreads;
+                if (f > nwalk) continue;
+                uint4 v = make_uint4(0, 0, 0, kVdNone);
+                if (f < nwalk) {
+                    const uint64_t p = pa[u], L = pb[u] - p - 8;
+                    v = make_uint4((uint32_t)p, (uint32_t)(p >> 32), (uint32_t)L, (uint32_t)f);
+                }
+                *(uint4 *)(gs.vrec + 2 * f) = v;
+            }
         }
     }
     // (a grid barrier, not a block-sum count only the chain wave waits for: with the
