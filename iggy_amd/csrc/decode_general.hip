@@ -209,7 +209,7 @@ __device__ inline uint32_t walk(const uint8_t *blob, uint64_t bl, uint64_t p, ui
 #endif
 constexpr int kLocBuf = IGGY_LOC_BUF;
 #ifndef IGGY_VREC_U
-#define IGGY_VREC_U 1
+#define IGGY_VREC_U 8
 #endif
 constexpr int kVrecU = IGGY_VREC_U;  // phase E's frame records per pass
 __device__ inline uint32_t walk_located(const uint8_t *blob, uint64_t bl, uint64_t p, uint64_t hi,
