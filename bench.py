@@ -57,7 +57,6 @@ import numpy as np
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
-import iggy_amd  # noqa: E402,F401  (HIP runtime settings before torch: iggy_amd/__init__.py)
 
 METRIC = "GiB/s device-resident message-batch decode, 1M msgs × 1KiB payload"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s peak

@@ -124,6 +124,7 @@ def load(path: str) -> ctypes.CDLL:
     L.iggy_codec_profile_read.argtypes = [vp, ci, vp, vp]
     L.iggy_codec_host_register.argtypes = [vp, vp, u64]
     L.iggy_codec_host_unregister.argtypes = [vp, vp]
+    L.iggy_codec_host_pinned.argtypes = [vp, u64]
     L.iggy_codec_decode_submit.argtypes = [vp, vp, u64, ci, vp, u64, ctypes.POINTER(u64)]
     L.iggy_codec_encode_submit.argtypes = [vp, vp, u64, vp, u64, ctypes.POINTER(u64)]
     L.iggy_codec_poll.argtypes = [vp, u64, vp]
@@ -436,6 +437,8 @@ class Codec:
         out = np.zeros(max(cap, 1), dtype=np.uint8)
         n = u64(0)
         e = WireError()
+        if key is not None and len(key) != 32:
+            raise ValueError("AES-256 key must be 32 bytes")
         k = np.frombuffer(bytes(key), dtype=np.uint8).copy() if key is not None else None
         rc = self._L.iggy_codec_build_polled_body(self._h, partition_id, current_offset, spans, len(arrs),
                                                   k.ctypes.data if k is not None else None, out.ctypes.data, cap,
@@ -477,6 +480,10 @@ class Codec:
         rc = self._L.iggy_codec_host_unregister(self._h, arr.ctypes.data)
         if rc:
             raise CodecError(rc, None, "host_unregister")
+
+    def host_pinned(self, ptr: int, length: int) -> bool:
+        """Whether the codec copies [ptr, ptr + length) by DMA directly (pinned memory)."""
+        return bool(self._L.iggy_codec_host_pinned(ptr, length))
 
     def decode_submit(self, body: np.ndarray, integrity: int, frame_pos: np.ndarray | None = None) -> int:
         """-> ticket. `body` (and `frame_pos`) must stay alive until the ticket completes."""

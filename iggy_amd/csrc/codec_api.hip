@@ -123,11 +123,33 @@ struct Slot {
     DevBuf in, pos, out, res;                    // device input / positions / encode output / result
     DevBuf ids, ots, pay, plen, uhb, uhl;        // encode SoA inputs
     hipEvent_t ev_in = nullptr, ev_k = nullptr, ev_done = nullptr;
+    // a pageable caller output is never a DMA target: the copy-out stream lands it in
+    // this pinned bounce and iggy_codec_poll copies it to the caller (hout_dst, hout_len)
+    void *hout = nullptr;
+    size_t hout_cap = 0;
+    uint8_t *hout_dst = nullptr;
+    uint64_t hout_len = 0;
+    int hout_ensure(size_t n) {
+        if (n <= hout_cap && !(hout_cap > (8ull << 20) && n <= (8ull << 20))) return 0;
+        if (hout) (void)hipHostFree(hout);
+        hout = nullptr;
+        hout_cap = 0;
+        const size_t want = std::max<size_t>(n, 64 << 10);
+        if (hipHostMalloc(&hout, want, hipHostMallocDefault) != hipSuccess) {
+            hout = nullptr;
+            return IGGY_ERR_DEVICE;
+        }
+        hout_cap = want;
+        return 0;
+    }
     void release() {
         DevBuf *b[] = {&in, &pos, &out, &res, &ids, &ots, &pay, &plen, &uhb, &uhl};
         for (DevBuf *x : b) x->release();
         for (hipEvent_t *e : {&ev_in, &ev_k, &ev_done})
             if (*e) (void)hipEventDestroy(*e), *e = nullptr;
+        if (hout) (void)hipHostFree(hout);
+        hout = nullptr;
+        hout_cap = 0;
     }
 };
 
@@ -201,6 +223,14 @@ struct iggy_codec_ctx {
     bool cr_key_set = false;
     // pinned host mirror of results
     void *h_pinned = nullptr;
+    // caller host memory (put_host / get_host): the two pinned chunks pageable bytes are
+    // staged through, their last copies' events, and the event after a call's last H2D
+    void *xst = nullptr;
+    hipEvent_t xev[2] = {nullptr, nullptr};
+    bool xlive[2] = {false, false};
+    uint32_t xnext = 0;
+    hipEvent_t xin_ev = nullptr;
+    bool xin_live = false;
     // asynchronous host-buffer operations: copy-in stream -> the context's stream -> copy-out
     // stream, so one operation's H2D, another's kernels and a third's D2H overlap
     hipStream_t h2d = nullptr, d2h = nullptr;
@@ -336,6 +366,150 @@ struct DevGuard {
     }
 };
 
+// ------------------------------------------------------- caller host memory
+// Every byte of caller host memory that crosses PCIe goes through put_host / get_host.
+// The reference codec borrows `&[u8]` for the call only (batch.rs:391); the caller may
+// free or reuse the memory the moment a call returns. Pinned memory (hipHostMalloc,
+// hipHostRegister, iggy_codec_host_register: the server's socket and segment buffers)
+// is a DMA source / target as it is. PAGEABLE memory is never handed to the runtime's
+// copy engine: for such a copy ROCclr pins (locks) the caller's range and releases
+// the lock only when it retires the copy command, at a later synchronisation of that
+// stream. The host-flag entries (round 3) returned without one, so a lock could
+// outlive the call, the caller freed the range, and a later copy to a new allocation
+// at the same addresses went through the stale lock: the hipErrorIllegalAddress /
+// "Memory Fault" faults of GPUTEST_r03 and round 4. Pageable bytes are
+// therefore staged through the context's own two pinned chunks (memcpy of chunk k+1
+// under the DMA of chunk k), so no runtime lock on caller memory ever exists.
+constexpr uint64_t kXferChunk = 4ull << 20;
+std::mutex g_reg_mu;
+std::vector<std::pair<uintptr_t, uint64_t>> g_reg;  // ranges registered through the codec
+
+bool host_pinned(const void *p, uint64_t n) {
+    if (!p || !n) return true;
+    const uintptr_t a = (uintptr_t)p;
+    {
+        std::lock_guard<std::mutex> lk(g_reg_mu);
+        for (const auto &r : g_reg)
+            if (a >= r.first && a - r.first <= r.second && n <= r.second - (a - r.first)) return true;
+    }
+    hipPointerAttribute_t at;
+    if (hipPointerGetAttributes(&at, p) != hipSuccess) {
+        (void)hipGetLastError();  // pageable: not an error for the caller's HIP code
+        return false;
+    }
+    if (at.type != hipMemoryTypeHost) return false;
+    void *start = nullptr;
+    size_t size = 0;
+    if (hipPointerGetAttribute(&start, HIP_POINTER_ATTRIBUTE_RANGE_START_ADDR, (hipDeviceptr_t)p) != hipSuccess ||
+        hipPointerGetAttribute(&size, HIP_POINTER_ATTRIBUTE_RANGE_SIZE, (hipDeviceptr_t)p) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    // only a range the query reports in host addresses that covers [p, p + n) counts;
+    // anything else is staged (always correct, only slower)
+    const uintptr_t s0 = (uintptr_t)start;
+    return a >= s0 && a - s0 <= size && n <= size - (a - s0);
+}
+
+int xfer_init(iggy_codec_ctx *c) {
+    if (c->xst) return 0;
+    if (hipHostMalloc(&c->xst, 2 * kXferChunk, hipHostMallocDefault) != hipSuccess) {
+        c->xst = nullptr;
+        return IGGY_ERR_DEVICE;
+    }
+    for (auto &ev : c->xev)
+        if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) return IGGY_ERR_DEVICE;
+    return 0;
+}
+
+// the next staging chunk, free for the host (its previous copy has run)
+int xfer_chunk(iggy_codec_ctx *c, uint8_t **chunk, int *idx) {
+    const int b = (int)(c->xnext++ & 1);
+    if (c->xlive[b]) {
+        HIP_OK(hipEventSynchronize(c->xev[b]));
+        c->xlive[b] = false;
+    }
+    *chunk = (uint8_t *)c->xst + (size_t)b * kXferChunk;
+    *idx = b;
+    return 0;
+}
+
+// H2D of n caller bytes on stream s. Returns with the caller's bytes consumed as far
+// as the caller is concerned: staged into pinned chunks (pageable), or enqueued from
+// memory the caller keeps pinned, whose copy every synchronous entry has completed
+// before it returns (xfer_settle).
+int put_host(iggy_codec_ctx *c, void *d_dst, const void *h_src, uint64_t n, hipStream_t s) {
+    if (!n) return 0;
+    if (host_pinned(h_src, n)) {
+        HIP_OK(hipMemcpyAsync(d_dst, h_src, n, hipMemcpyHostToDevice, s));
+    } else {
+        if (xfer_init(c)) return IGGY_ERR_DEVICE;
+        for (uint64_t off = 0; off < n; off += kXferChunk) {
+            const uint64_t m = std::min(kXferChunk, n - off);
+            uint8_t *st;
+            int b;
+            int r = xfer_chunk(c, &st, &b);
+            if (r) return r;
+            memcpy(st, (const uint8_t *)h_src + off, m);
+            HIP_OK(hipMemcpyAsync((uint8_t *)d_dst + off, st, m, hipMemcpyHostToDevice, s));
+            HIP_OK(hipEventRecord(c->xev[b], s));
+            c->xlive[b] = true;
+        }
+    }
+    if (!c->xin_ev && hipEventCreateWithFlags(&c->xin_ev, hipEventDisableTiming) != hipSuccess) {
+        c->xin_ev = nullptr;
+        return IGGY_ERR_DEVICE;
+    }
+    HIP_OK(hipEventRecord(c->xin_ev, s));
+    c->xin_live = true;
+    return 0;
+}
+
+// Before a synchronous entry that saw its completion through a host-mapped flag (no
+// stream sync) returns: its H2D copies are done. They ran before the kernel that
+// raised the flag, so this costs one signal read.
+int xfer_settle(iggy_codec_ctx *c) {
+    if (c->xin_live) {
+        HIP_OK(hipEventSynchronize(c->xin_ev));
+        c->xin_live = false;
+    }
+    return 0;
+}
+
+// D2H of n bytes into caller memory on stream s; synchronous (returns with the bytes
+// in h_dst and nothing of the call outstanding on s).
+int get_host(iggy_codec_ctx *c, void *h_dst, const void *d_src, uint64_t n, hipStream_t s) {
+    if (!n) return 0;
+    if (host_pinned(h_dst, n)) {
+        HIP_OK(hipMemcpyAsync(h_dst, d_src, n, hipMemcpyDeviceToHost, s));
+        HIP_OK(hipStreamSynchronize(s));
+        return 0;
+    }
+    if (xfer_init(c)) return IGGY_ERR_DEVICE;
+    const uint64_t nk = (n + kXferChunk - 1) / kXferChunk;
+    uint8_t *st[2] = {nullptr, nullptr};
+    int bi[2] = {0, 0};
+    auto issue = [&](uint64_t k) -> int {
+        const uint64_t off = k * kXferChunk, m = std::min(kXferChunk, n - off);
+        int r = xfer_chunk(c, &st[k & 1], &bi[k & 1]);
+        if (r) return r;
+        HIP_OK(hipMemcpyAsync(st[k & 1], (const uint8_t *)d_src + off, m, hipMemcpyDeviceToHost, s));
+        HIP_OK(hipEventRecord(c->xev[bi[k & 1]], s));
+        c->xlive[bi[k & 1]] = true;
+        return 0;
+    };
+    int r = issue(0);
+    for (uint64_t k = 0; k < nk && !r; ++k) {
+        HIP_OK(hipEventSynchronize(c->xev[bi[k & 1]]));
+        c->xlive[bi[k & 1]] = false;
+        const uint8_t *src = st[k & 1];
+        if (k + 1 < nk) r = issue(k + 1);  // the next chunk's copy runs under this memcpy
+        const uint64_t off = k * kXferChunk;
+        memcpy((uint8_t *)h_dst + off, src, std::min(kXferChunk, n - off));
+    }
+    return r;
+}
+
 
 void prof_begin(iggy_codec_ctx *c, int which, hipStream_t s) {
     if (!c->profile) return;
@@ -436,7 +610,8 @@ int decode_host(iggy_codec_ctx *c, const uint8_t *body, uint64_t len, int integr
     const uint64_t pcap = frame_pos ? std::min<uint64_t>(cap, len / 48 + 1) : 0;
     r |= c->dpos.ensure((pcap + 1) * 8);
     if (r) return IGGY_ERR_DEVICE;
-    if (len) HIP_OK(hipMemcpyAsync(c->din.p, body, len, hipMemcpyHostToDevice, c->stream));
+    r = put_host(c, c->din.p, body, len, c->stream);
+    if (r) return r;
     iggy_decode_result *d_res = c->dresult.as<iggy_decode_result>();
     r = enqueue_decode(c, c->din.as<uint8_t>(), len, integrity, pcap ? c->dpos.as<uint64_t>() : nullptr,
                        pcap, d_res, c->stream);
@@ -448,7 +623,7 @@ int decode_host(iggy_codec_ctx *c, const uint8_t *body, uint64_t len, int integr
     if (res_out->error.kind == IGGY_ERR_TIMEOUT) reset_after_timeout(c);
     if (frame_pos && pcap && res_out->error.kind == IGGY_OK) {
         const uint64_t n = std::min<uint64_t>(res_out->frame_count, pcap);
-        if (n) HIP_OK(hipMemcpy(frame_pos, c->dpos.p, n * 8, hipMemcpyDeviceToHost));
+        if (n) return get_host(c, frame_pos, c->dpos.p, n * 8, c->stream);
     }
     (void)keep_on_device;
     return 0;
@@ -663,9 +838,11 @@ int redo_general(iggy_codec_ctx *c, const uint8_t *d_base, const RecIn *recs, si
         r = enqueue_decode(c, d_base + recs[k].off, recs[k].len, integrity, d_pos ? d_pos + recs[k].pos_base : nullptr,
                            d_pos ? recs[k].pos_cap : 0, d_res + k, c->stream);
         if (r) return r;
-        HIP_OK(hipMemcpyAsync(res + k, d_res + k, sizeof(iggy_decode_result), hipMemcpyDeviceToHost, c->stream));
     }
-    HIP_OK(hipStreamSynchronize(c->stream));
+    for (size_t k : redo) {
+        r = get_host(c, res + k, d_res + k, sizeof(iggy_decode_result), c->stream);
+        if (r) return r;
+    }
     for (size_t k : redo)
         if (res[k].error.kind == IGGY_ERR_TIMEOUT) {
             reset_after_timeout(c);
@@ -690,15 +867,15 @@ int decode_records_to_host(iggy_codec_ctx *c, const uint8_t *d_base, const uint8
                                 c->omap.dp<iggy_decode_result>(64), &single, nullptr, c->omap.dp<uint32_t>(), v);
         if (r) return r;
         r = wait_host_flag(c, v);
+        if (!r) r = xfer_settle(c);
         if (r) return r;
         memcpy(res, c->omap.hp<uint8_t>(64), rb);
     } else {
         if (c->rres.ensure(rb)) return IGGY_ERR_DEVICE;
         iggy_decode_result *d_res = c->rres.as<iggy_decode_result>();
         int r = enqueue_records(c, d_base, h_base, recs, K, integrity, nullptr, nullptr, d_res, &single);
+        if (!r) r = get_host(c, res, d_res, rb, c->stream);
         if (r) return r;
-        HIP_OK(hipMemcpyAsync(res, d_res, rb, hipMemcpyDeviceToHost, c->stream));
-        HIP_OK(hipStreamSynchronize(c->stream));
     }
     return redo_general(c, d_base, recs, K, integrity, nullptr, res, nullptr);
 }
@@ -717,15 +894,17 @@ int decode_host_fast(iggy_codec_ctx *c, const uint8_t *body, uint64_t len, int i
     if (len > kHostFastBytes || !rec_plan(body, len, &nf)) return 0;
     const uint64_t pcap = frame_pos ? std::min<uint64_t>(cap, len / 48 + 1) : 0;
     if (c->din.ensure(len + 16) || c->omap.ensure(64 + 128 + pcap * 8)) return IGGY_ERR_DEVICE;
-    if (len) HIP_OK(hipMemcpyAsync(c->din.p, body, len, hipMemcpyHostToDevice, c->stream));
+    int r = put_host(c, c->din.p, body, len, c->stream);
+    if (r) return r;
     const RecIn rec{0, len, 0, pcap, 0};
     std::vector<size_t> single;
     const uint32_t v = next_flag(c);
-    int r = enqueue_records(c, c->din.as<uint8_t>(), body, &rec, 1, integrity,
-                            pcap ? c->omap.dp<uint64_t>(192) : nullptr, nullptr, c->omap.dp<iggy_decode_result>(64),
-                            &single, nullptr, c->omap.dp<uint32_t>(), v);
+    r = enqueue_records(c, c->din.as<uint8_t>(), body, &rec, 1, integrity,
+                        pcap ? c->omap.dp<uint64_t>(192) : nullptr, nullptr, c->omap.dp<iggy_decode_result>(64),
+                        &single, nullptr, c->omap.dp<uint32_t>(), v);
     if (r) return r;
     r = wait_host_flag(c, v);
+    if (!r) r = xfer_settle(c);
     if (r) return r;
     const iggy_decode_result res = *c->omap.hp<iggy_decode_result>(64);
     if (res.status == kStatusNeedGeneral) return 0;
@@ -804,17 +983,20 @@ int iggy_codec_create(int device, iggy_codec_ctx **out) {
         // probe: does global_load_lds_dwordx4 honour unaligned sources here?
         DevBuf pb;
         if (pb.ensure(8192) == 0) {
-            std::vector<uint8_t> pat(4096);
-            for (size_t i = 0; i < pat.size(); ++i) pat[i] = (uint8_t)(i * 131 + 7);
+            // (pattern and verdict through the pinned result mirror, unused until now)
+            uint8_t *pat = (uint8_t *)c->h_pinned;
+            for (size_t i = 0; i < 4096; ++i) pat[i] = (uint8_t)(i * 131 + 7);
             uint32_t *flag = c->dresult.as<uint32_t>(1024);
-            if (hipMemcpy(pb.p, pat.data(), pat.size(), hipMemcpyHostToDevice) == hipSuccess &&
-                hipMemset(flag, 0, 4) == hipSuccess) {
+            if (hipMemcpyAsync(pb.p, pat, 4096, hipMemcpyHostToDevice, c->stream) == hipSuccess &&
+                hipMemsetAsync(flag, 0, 4, c->stream) == hipSuccess) {
                 hipLaunchKernelGGL(k_probe_glds_unaligned, dim3(1), dim3(64), 16 * 64 * 4, c->stream,
                                    (const uint8_t *)pb.p, flag);
-                uint32_t ok = 0;
-                if (hipStreamSynchronize(c->stream) == hipSuccess &&
-                    hipMemcpy(&ok, flag, 4, hipMemcpyDeviceToHost) == hipSuccess)
+                if (hipMemcpyAsync(pat, flag, 4, hipMemcpyDeviceToHost, c->stream) == hipSuccess &&
+                    hipStreamSynchronize(c->stream) == hipSuccess) {
+                    uint32_t ok = 0;
+                    memcpy(&ok, pat, 4);
                     c->allow_unaligned = ok == 1;
+                }
             }
             pb.release();
         }
@@ -847,6 +1029,10 @@ void iggy_codec_destroy(iggy_codec_ctx *c) {
     for (DevBuf *b : bufs) b->release();
     if (c->h_pinned) (void)hipHostFree(c->h_pinned);
     if (c->pb_pinned) (void)hipHostFree(c->pb_pinned);
+    if (c->xst) (void)hipHostFree(c->xst);
+    for (auto &ev : c->xev)
+        if (ev) (void)hipEventDestroy(ev);
+    if (c->xin_ev) (void)hipEventDestroy(c->xin_ev);
     for (int w = 0; w < 2; ++w) {
         if (c->ev0[w]) (void)hipEventDestroy(c->ev0[w]);
         if (c->ev1[w]) (void)hipEventDestroy(c->ev1[w]);
@@ -925,8 +1111,7 @@ static int stage_record(iggy_codec_ctx *c, const iggy_batch_header &h, const uin
     uint8_t *hb = (uint8_t *)c->h_pinned + 2048;  // pinned: the copy is truly async
     iggy_batch_header_encode(&h, hb);
     HIP_OK(hipMemcpyAsync(c->din.p, hb, 256, hipMemcpyHostToDevice, c->stream));
-    if (blob_len) HIP_OK(hipMemcpyAsync(c->din.as<uint8_t>(256), blob, blob_len, hipMemcpyHostToDevice, c->stream));
-    return 0;
+    return put_host(c, c->din.as<uint8_t>(256), blob, blob_len, c->stream);
 }
 
 int iggy_codec_verify_and_recompute_batch_checksum(iggy_codec_ctx *c, const iggy_batch_header *hdr,
@@ -1099,7 +1284,8 @@ int iggy_codec_admit_batch(iggy_codec_ctx *c, const uint8_t *batch, uint64_t len
     r |= c->dpos.ensure((pcap + 1) * 8);
     r |= c->gbsums.ensure(((44 + 8 * pcap) / 1024 + 2) * 64);
     if (r) return IGGY_ERR_DEVICE;
-    if (len) HIP_OK(hipMemcpyAsync(c->din.p, batch, len, hipMemcpyHostToDevice, c->stream));
+    r = put_host(c, c->din.p, batch, len, c->stream);
+    if (r) return r;
     iggy_decode_result *d_res = c->dresult.as<iggy_decode_result>();
     r = enqueue_decode(c, c->din.as<uint8_t>(), len, IGGY_INTEGRITY_VERIFY, c->dpos.as<uint64_t>(), pcap, d_res,
                        c->stream);
@@ -1160,7 +1346,8 @@ int iggy_codec_decode_records(iggy_codec_ctx *c, const uint8_t *buf, uint64_t le
     DevGuard dg(c->device);
     bind(c, nullptr);
     if (c->din.ensure(len + 16)) return IGGY_ERR_DEVICE;
-    if (len) HIP_OK(hipMemcpyAsync(c->din.p, buf, len, hipMemcpyHostToDevice, c->stream));
+    int r = put_host(c, c->din.p, buf, len, c->stream);
+    if (r) return r;
     std::vector<RecIn> recs(nrec);
     for (uint64_t k = 0; k < nrec; ++k) recs[k] = RecIn{offsets[k], len - offsets[k], 0, 0, 0};
     return decode_records_to_host(c, c->din.as<uint8_t>(), buf, recs.data(), nrec, integrity, out);
@@ -1200,12 +1387,13 @@ int iggy_codec_recover_segment(iggy_codec_ctx *c, const uint8_t *messages, uint6
         const size_t K = cand.size();
         if (c->din.ensure(span + 16)) return IGGY_ERR_DEVICE;
         (void)maxlen;
-        HIP_OK(hipMemcpyAsync(c->din.p, messages, span, hipMemcpyHostToDevice, c->stream));
+        int r = put_host(c, c->din.p, messages, span, c->stream);
+        if (r) return r;
         std::vector<RecIn> recs(K);
         for (size_t k = 0; k < K; ++k) recs[k] = RecIn{cand[k].pos, cand[k].h.batch_length, 0, 0, 0};
         std::vector<iggy_decode_result> res(K);
-        int r = decode_records_to_host(c, c->din.as<uint8_t>(), messages, recs.data(), K, IGGY_INTEGRITY_VERIFY,
-                                       res.data());
+        r = decode_records_to_host(c, c->din.as<uint8_t>(), messages, recs.data(), K, IGGY_INTEGRITY_VERIFY,
+                                   res.data());
         if (r) return r;
         for (; accepted < K; ++accepted)
             if (res[accepted].error.kind != IGGY_OK) break;
@@ -1259,10 +1447,11 @@ int iggy_codec_walk_segment_payload(iggy_codec_ctx *c, const uint8_t *bytes, uin
         const size_t K = cand.size();
         if (c->din.ensure(len + 16)) return IGGY_ERR_DEVICE;
         (void)maxlen;
-        HIP_OK(hipMemcpyAsync(c->din.p, bytes, len, hipMemcpyHostToDevice, c->stream));
+        int r = put_host(c, c->din.p, bytes, len, c->stream);
+        if (r) return r;
         std::vector<RecIn> recs(K);
         for (size_t k = 0; k < K; ++k) recs[k] = RecIn{cand[k].pos, len - cand[k].pos, 0, 0, 0};
-        int r = decode_records_to_host(c, c->din.as<uint8_t>(), bytes, recs.data(), K, IGGY_INTEGRITY_VERIFY,
+        r = decode_records_to_host(c, c->din.as<uint8_t>(), bytes, recs.data(), K, IGGY_INTEGRITY_VERIFY,
                                        res.data());
         if (r) return r;
     }
@@ -1397,7 +1586,8 @@ int iggy_codec_xxh3_64(iggy_codec_ctx *c, const void *data, uint64_t len, uint64
     const uint64_t nb = len ? (len - 1) / 1024 + 1 : 1;
     r |= c->hbsums.ensure(nb * 64 + 64);
     if (r) return IGGY_ERR_DEVICE;
-    if (len) HIP_OK(hipMemcpyAsync(c->din.p, data, len, hipMemcpyHostToDevice, c->stream));
+    r = put_host(c, c->din.p, data, len, c->stream);
+    if (r) return r;
     uint64_t *dout = c->dresult.as<uint64_t>(3088);
     if (len > 240)
         hipLaunchKernelGGL(k_xxh3_big_blocks, dim3(c->ncu * 4), dim3(256), 0, c->stream,
@@ -1405,9 +1595,7 @@ int iggy_codec_xxh3_64(iggy_codec_ctx *c, const void *data, uint64_t len, uint64
     hipLaunchKernelGGL(k_xxh3_big_chain, dim3(1), dim3(64), 0, c->stream, c->din.as<uint8_t>(), len,
                        (const uint64_t *)c->hbsums.as<uint64_t>(), dout);
     HIP_OK(hipGetLastError());
-    HIP_OK(hipMemcpyAsync(out, dout, 8, hipMemcpyDeviceToHost, c->stream));
-    HIP_OK(hipStreamSynchronize(c->stream));
-    return 0;
+    return get_host(c, out, dout, 8, c->stream);
 }
 
 // ---------------------------------------------------------------- encode
@@ -1585,15 +1773,16 @@ int iggy_codec_encode_batch(iggy_codec_ctx *c, const iggy_raw_messages *m, uint6
     r |= c->dout.ensure(need + 16);
     if (r) return IGGY_ERR_DEVICE;
     hipStream_t s = c->stream;
-    HIP_OK(hipMemcpyAsync(c->eids.p, m->ids, n * 16, hipMemcpyHostToDevice, s));
-    HIP_OK(hipMemcpyAsync(c->eots.p, m->origin_timestamps, n * 8, hipMemcpyHostToDevice, s));
-    if (spl) HIP_OK(hipMemcpyAsync(c->epay.p, m->payloads, spl, hipMemcpyHostToDevice, s));
-    HIP_OK(hipMemcpyAsync(c->eplen.p, m->payload_lengths, n * 4, hipMemcpyHostToDevice, s));
+    r |= put_host(c, c->eids.p, m->ids, n * 16, s);
+    r |= put_host(c, c->eots.p, m->origin_timestamps, n * 8, s);
+    r |= put_host(c, c->epay.p, m->payloads, spl, s);
+    r |= put_host(c, c->eplen.p, m->payload_lengths, n * 4, s);
     const bool has_uh = m->user_headers_lengths != nullptr;
     if (has_uh) {
-        if (suh) HIP_OK(hipMemcpyAsync(c->euhb.p, m->user_headers, suh, hipMemcpyHostToDevice, s));
-        HIP_OK(hipMemcpyAsync(c->euhl.p, m->user_headers_lengths, n * 4, hipMemcpyHostToDevice, s));
+        r |= put_host(c, c->euhb.p, m->user_headers, suh, s);
+        r |= put_host(c, c->euhl.p, m->user_headers_lengths, n * 4, s);
     }
+    if (r) return IGGY_ERR_DEVICE;
     iggy_raw_messages dm;
     dm.count = n;
     dm.ids = c->eids.as<uint64_t>();
@@ -1612,7 +1801,8 @@ int iggy_codec_encode_batch(iggy_codec_ctx *c, const iggy_raw_messages *m, uint6
         fill_err(err, h_res->error);
         return (int)h_res->error.kind;
     }
-    HIP_OK(hipMemcpy(out, c->dout.p, need, hipMemcpyDeviceToHost));
+    r = get_host(c, out, c->dout.p, need, s);
+    if (r) return r;
     if (out_len) *out_len = need;
     return 0;
 }
@@ -1689,14 +1879,16 @@ int iggy_codec_poll_decode(iggy_codec_ctx *c, const uint8_t *buf, uint64_t len, 
         const size_t rb = K * sizeof(iggy_decode_result), mo = (64 + rb + 127) & ~(size_t)127;
         if (c->din.ensure(len + 16) || c->omap.ensure(mo + (nslots + 1) * sizeof(iggy_polled_message)))
             return IGGY_ERR_DEVICE;
-        if (len) HIP_OK(hipMemcpyAsync(c->din.p, buf, len, hipMemcpyHostToDevice, c->stream));
+        int r = put_host(c, c->din.p, buf, len, c->stream);
+        if (r) return r;
         std::vector<size_t> single;
         const uint32_t v = next_flag(c);
-        int r = enqueue_records(c, c->din.as<uint8_t>(), buf, rin.data(), K, IGGY_INTEGRITY_LAYOUT_ONLY, nullptr,
-                                c->omap.dp<iggy_polled_message>(mo), c->omap.dp<iggy_decode_result>(64), &single,
-                                nullptr, c->omap.dp<uint32_t>(), v);
+        r = enqueue_records(c, c->din.as<uint8_t>(), buf, rin.data(), K, IGGY_INTEGRITY_LAYOUT_ONLY, nullptr,
+                            c->omap.dp<iggy_polled_message>(mo), c->omap.dp<iggy_decode_result>(64), &single,
+                            nullptr, c->omap.dp<uint32_t>(), v);
         if (r) return r;
         r = wait_host_flag(c, v);
+        if (!r) r = xfer_settle(c);
         if (r) return r;
         const iggy_decode_result *res = c->omap.hp<iggy_decode_result>(64);
         bool general = false;
@@ -1746,7 +1938,8 @@ int iggy_codec_poll_decode(iggy_codec_ctx *c, const uint8_t *buf, uint64_t len, 
     r |= c->pres.ensure((K + 1) * sizeof(iggy_decode_result));
     r |= c->pmsgs.ensure((nslots + pwords + 1) * sizeof(iggy_polled_message));
     if (r) return IGGY_ERR_DEVICE;
-    if (len) HIP_OK(hipMemcpyAsync(c->din.p, buf, len, hipMemcpyHostToDevice, c->stream));
+    r = put_host(c, c->din.p, buf, len, c->stream);
+    if (r) return r;
     iggy_decode_result *d_res = c->pres.as<iggy_decode_result>();
     iggy_polled_message *d_msgs = c->pmsgs.as<iggy_polled_message>();
     std::vector<size_t> single, redone;
@@ -1754,8 +1947,8 @@ int iggy_codec_poll_decode(iggy_codec_ctx *c, const uint8_t *buf, uint64_t len, 
                         d_msgs, d_res, &single);
     if (r) return r;
     std::vector<iggy_decode_result> res(K);
-    if (K) HIP_OK(hipMemcpyAsync(res.data(), d_res, K * sizeof(iggy_decode_result), hipMemcpyDeviceToHost, c->stream));
-    HIP_OK(hipStreamSynchronize(c->stream));
+    r = get_host(c, res.data(), d_res, K * sizeof(iggy_decode_result), c->stream);
+    if (r) return r;
     r = redo_general(c, c->din.as<uint8_t>(), rin.data(), K, IGGY_INTEGRITY_LAYOUT_ONLY, c->ppos.as<uint64_t>(),
                      res.data(), &redone);
     if (r) {
@@ -1809,8 +2002,8 @@ int iggy_codec_poll_decode(iggy_codec_ctx *c, const uint8_t *buf, uint64_t len, 
     }
     uint64_t o = 0;
     for (const Span &sp : spans) {
-        HIP_OK(hipMemcpyAsync(out + o, d_msgs + sp.src, sp.n * sizeof(iggy_polled_message), hipMemcpyDeviceToHost,
-                              c->stream));
+        r = get_host(c, out + o, d_msgs + sp.src, sp.n * sizeof(iggy_polled_message), c->stream);
+        if (r) return r;
         o += sp.n;
     }
     HIP_OK(hipStreamSynchronize(c->stream));
@@ -2096,7 +2289,9 @@ uint32_t poll_error_kind(uint32_t kind) {
     }
 }
 int pb_pinned_ensure(iggy_codec_ctx *c, size_t n) {
-    if (n <= c->pb_cap) return 0;
+    // grown past kHostMapKeep by one large decrypting poll: given back at the next
+    // ordinary-sized one instead of staying pinned for the context's life
+    if (n <= c->pb_cap && !(c->pb_cap > kHostMapKeep && n <= kHostMapKeep)) return 0;
     if (c->pb_pinned) (void)hipHostFree(c->pb_pinned);
     c->pb_pinned = nullptr;
     c->pb_cap = 0;
@@ -2126,10 +2321,16 @@ int iggy_codec_build_polled_body(iggy_codec_ctx *c, uint32_t partition_id, uint6
         return (int)kind;
     };
     // 1. the concatenated stream: straight into the body when it fits and nothing is
-    //    decrypted (the reply IS the stored encoding), else into the pinned staging
+    //    decrypted (the reply IS the stored encoding); into host memory when it does
+    //    not fit (only walked, for the reference's error order, then CAPACITY); into
+    //    the pinned staging (stream, then the plaintext) when records are decrypted
     uint8_t *stream;
+    std::vector<uint8_t> walk_only;
     if (!key && cap >= 16 + total) {
         stream = out + 16;
+    } else if (!key) {
+        walk_only.resize(total + 1);
+        stream = walk_only.data();
     } else {
         if (pb_pinned_ensure(c, 2 * total + 64)) return IGGY_ERR_DEVICE;
         stream = (uint8_t *)c->pb_pinned;
@@ -2186,9 +2387,8 @@ int iggy_codec_build_polled_body(iggy_codec_ctx *c, uint32_t partition_id, uint6
         uint8_t *hout = stream + total + 32;
         res.resize(recs.size());
         HIP_OK(hipMemcpyAsync(hout, c->dout.p, span, hipMemcpyDeviceToHost, c->stream));
-        HIP_OK(hipMemcpyAsync(res.data(), d_res, recs.size() * sizeof(iggy_crypt_result), hipMemcpyDeviceToHost,
-                              c->stream));
-        HIP_OK(hipStreamSynchronize(c->stream));
+        r = get_host(c, res.data(), d_res, recs.size() * sizeof(iggy_crypt_result), c->stream);
+        if (r) return r;
         for (const iggy_crypt_result &q : res)
             if (q.error.kind == IGGY_ERR_TIMEOUT) { reset_after_timeout(c); break; }
     }
@@ -2320,7 +2520,8 @@ static int walk_chunk_per_batch(iggy_codec_ctx *c, const uint8_t *chunk, uint64_
     uint8_t *slots = c->cwk.as<uint8_t>(kState + K * 8);
     iggy_chunk_fragment *d_frags = c->cwk.as<iggy_chunk_fragment>(kState + K * (kSlot + 8));
     uint8_t *d_hdrs = (uint8_t *)(d_frags + cap);
-    if (len) HIP_OK(hipMemcpyAsync(c->din.p, chunk, len, hipMemcpyHostToDevice, s));
+    r = put_host(c, c->din.p, chunk, len, s);
+    if (r) return r;
     hipLaunchKernelGGL(k_chunk_init, dim3(1), dim3(64), 0, s, st, q->already_matched);
     iggy_decode_result *d_res = c->pres.as<iggy_decode_result>();
     for (uint64_t k = 0; k < K; ++k) {
@@ -2341,12 +2542,13 @@ static int walk_chunk_per_batch(iggy_codec_ctx *c, const uint8_t *chunk, uint64_
     }
     HIP_OK(hipGetLastError());
     ChunkState hs{};
-    HIP_OK(hipMemcpyAsync(&hs, st, sizeof(hs), hipMemcpyDeviceToHost, s));
-    HIP_OK(hipStreamSynchronize(s));
+    r = get_host(c, &hs, st, sizeof(hs), s);
+    if (r) return r;
     const uint64_t nf = std::min<uint64_t>(hs.nfrag, cap);
     if (nf) {
-        HIP_OK(hipMemcpy(frags, d_frags, nf * sizeof(iggy_chunk_fragment), hipMemcpyDeviceToHost));
-        if (headers) HIP_OK(hipMemcpy(headers, d_hdrs, nf * 256, hipMemcpyDeviceToHost));
+        r = get_host(c, frags, d_frags, nf * sizeof(iggy_chunk_fragment), s);
+        if (!r && headers) r = get_host(c, headers, d_hdrs, nf * 256, s);
+        if (r) return r;
     }
     if (hs.error.kind == IGGY_ERR_TIMEOUT) {  // a bug guard fired, not a verdict on the chunk
         reset_after_timeout(c);
@@ -2415,7 +2617,8 @@ int iggy_codec_walk_disk_chunk(iggy_codec_ctx *c, const uint8_t *chunk, uint64_t
     r |= c->clinks.ensure(link_bytes);
     if (r) return IGGY_ERR_DEVICE;
     hipStream_t s = c->stream;
-    HIP_OK(hipMemcpyAsync(c->din.p, chunk, len, hipMemcpyHostToDevice, s));
+    r = put_host(c, c->din.p, chunk, len, s);
+    if (r) return r;
     std::vector<RecIn> rin(K);
     for (uint64_t k = 0; k < K; ++k)
         rin[k] = RecIn{cand[k].pos, len - cand[k].pos, cand[k].pbase, cand[k].bl ? (cand[k].bl - 256) / 48 + 1 : 0, 0};
@@ -2441,6 +2644,7 @@ int iggy_codec_walk_disk_chunk(iggy_codec_ctx *c, const uint8_t *chunk, uint64_t
                        headers ? d_hdrs : nullptr, capk, c->sl.as<uint64_t>(), c->omap.dp<uint32_t>(), v);
     HIP_OK(hipGetLastError());
     r = wait_host_flag(c, v);
+    if (!r) r = xfer_settle(c);
     if (r) return r;
     ChunkState hs;
     memcpy(&hs, pin_res, sizeof(hs));
@@ -2477,7 +2681,8 @@ int iggy_codec_select_slice(iggy_codec_ctx *c, const uint8_t *record, uint64_t l
     r |= c->dpos.ensure((cap + 1) * 8);
     r |= c->slres.ensure(512);
     if (r) return IGGY_ERR_DEVICE;
-    if (len) HIP_OK(hipMemcpyAsync(c->din.p, record, len, hipMemcpyHostToDevice, c->stream));
+    r = put_host(c, c->din.p, record, len, c->stream);
+    if (r) return r;
     // the reference selects on a decoded batch: decode it (layout) first
     iggy_decode_result *d_res = c->dresult.as<iggy_decode_result>();
     r = enqueue_decode(c, c->din.as<uint8_t>(), len, IGGY_INTEGRITY_LAYOUT_ONLY, c->dpos.as<uint64_t>(), cap, d_res,
@@ -2570,15 +2775,27 @@ int iggy_codec_host_register(iggy_codec_ctx *c, void *ptr, uint64_t len) {
     if (!c || !ptr || !len) return IGGY_ERR_INVALID_ARGUMENT;
     DevGuard dg(c->device);
     HIP_OK(hipHostRegister(ptr, len, hipHostRegisterDefault));
+    std::lock_guard<std::mutex> lk(g_reg_mu);
+    g_reg.emplace_back((uintptr_t)ptr, len);
     return 0;
 }
 
 int iggy_codec_host_unregister(iggy_codec_ctx *c, void *ptr) {
     if (!c || !ptr) return IGGY_ERR_INVALID_ARGUMENT;
     DevGuard dg(c->device);
+    {
+        std::lock_guard<std::mutex> lk(g_reg_mu);
+        for (size_t i = 0; i < g_reg.size(); ++i)
+            if (g_reg[i].first == (uintptr_t)ptr) {
+                g_reg.erase(g_reg.begin() + (long)i);
+                break;
+            }
+    }
     HIP_OK(hipHostUnregister(ptr));
     return 0;
 }
+
+int iggy_codec_host_pinned(const void *ptr, uint64_t len) { return host_pinned(ptr, len) ? 1 : 0; }
 
 int iggy_codec_decode_submit(iggy_codec_ctx *c, const uint8_t *body, uint64_t len, int integrity,
                              uint64_t *frame_pos, uint64_t cap, iggy_ticket *ticket) {
@@ -2599,7 +2816,15 @@ int iggy_codec_decode_submit(iggy_codec_ctx *c, const uint8_t *body, uint64_t le
     }
     sl.cap = cap;
     sl.frame_pos = frame_pos;
-    if (len) HIP_OK(hipMemcpyAsync(sl.in.p, body, len, hipMemcpyHostToDevice, c->h2d));
+    sl.hout_dst = nullptr;
+    sl.hout_len = 0;
+    const bool pos_pinned = host_pinned(frame_pos, pcap * 8);
+    if (pcap && !pos_pinned && sl.hout_ensure(pcap * 8)) r = IGGY_ERR_DEVICE;
+    if (!r) r = put_host(c, sl.in.p, body, len, c->h2d);
+    if (r) {
+        sl.busy = false;
+        return r;
+    }
     HIP_OK(hipEventRecord(sl.ev_in, c->h2d));
     hipStream_t s = bind(c, nullptr);
     HIP_OK(hipStreamWaitEvent(s, sl.ev_in, 0));
@@ -2613,7 +2838,13 @@ int iggy_codec_decode_submit(iggy_codec_ctx *c, const uint8_t *body, uint64_t le
     HIP_OK(hipStreamWaitEvent(c->d2h, sl.ev_k, 0));
     HIP_OK(hipMemcpyAsync((uint8_t *)c->slot_pinned + 256 * k, d_res, sizeof(iggy_decode_result),
                           hipMemcpyDeviceToHost, c->d2h));
-    if (pcap) HIP_OK(hipMemcpyAsync(frame_pos, sl.pos.p, pcap * 8, hipMemcpyDeviceToHost, c->d2h));
+    // positions: straight into pinned caller memory; a pageable array gets them from the
+    // slot's pinned bounce in iggy_codec_poll (and only when the decode succeeded)
+    if (pcap) {
+        if (!pos_pinned) sl.hout_dst = (uint8_t *)frame_pos;
+        HIP_OK(hipMemcpyAsync(pos_pinned ? (void *)frame_pos : sl.hout, sl.pos.p, pcap * 8, hipMemcpyDeviceToHost,
+                              c->d2h));
+    }
     HIP_OK(hipEventRecord(sl.ev_done, c->d2h));
     *ticket = sl.ticket;
     return 0;
@@ -2651,14 +2882,24 @@ int iggy_codec_encode_submit(iggy_codec_ctx *c, const iggy_raw_messages *m, uint
     sl.cap = cap;
     sl.out_len = need;
     sl.frame_pos = nullptr;
+    sl.hout_dst = nullptr;
+    sl.hout_len = 0;
+    const bool out_pinned = host_pinned(out, need);
+    if (cap >= need && !out_pinned && sl.hout_ensure(need)) r = IGGY_ERR_DEVICE;
     hipStream_t h = c->h2d;
-    HIP_OK(hipMemcpyAsync(sl.ids.p, m->ids, n * 16, hipMemcpyHostToDevice, h));
-    HIP_OK(hipMemcpyAsync(sl.ots.p, m->origin_timestamps, n * 8, hipMemcpyHostToDevice, h));
-    if (spl) HIP_OK(hipMemcpyAsync(sl.pay.p, m->payloads, spl, hipMemcpyHostToDevice, h));
-    HIP_OK(hipMemcpyAsync(sl.plen.p, m->payload_lengths, n * 4, hipMemcpyHostToDevice, h));
-    if (has_uh) {
-        if (suh) HIP_OK(hipMemcpyAsync(sl.uhb.p, m->user_headers, suh, hipMemcpyHostToDevice, h));
-        HIP_OK(hipMemcpyAsync(sl.uhl.p, m->user_headers_lengths, n * 4, hipMemcpyHostToDevice, h));
+    if (!r) {
+        r |= put_host(c, sl.ids.p, m->ids, n * 16, h);
+        r |= put_host(c, sl.ots.p, m->origin_timestamps, n * 8, h);
+        r |= put_host(c, sl.pay.p, m->payloads, spl, h);
+        r |= put_host(c, sl.plen.p, m->payload_lengths, n * 4, h);
+        if (has_uh) {
+            r |= put_host(c, sl.uhb.p, m->user_headers, suh, h);
+            r |= put_host(c, sl.uhl.p, m->user_headers_lengths, n * 4, h);
+        }
+    }
+    if (r) {
+        sl.busy = false;
+        return IGGY_ERR_DEVICE;
     }
     HIP_OK(hipEventRecord(sl.ev_in, h));
     hipStream_t s = bind(c, nullptr);
@@ -2682,7 +2923,10 @@ int iggy_codec_encode_submit(iggy_codec_ctx *c, const iggy_raw_messages *m, uint
     HIP_OK(hipStreamWaitEvent(c->d2h, sl.ev_k, 0));
     HIP_OK(hipMemcpyAsync((uint8_t *)c->slot_pinned + 256 * k, d_res, sizeof(iggy_encode_result),
                           hipMemcpyDeviceToHost, c->d2h));
-    if (cap >= need) HIP_OK(hipMemcpyAsync(out, sl.out.p, need, hipMemcpyDeviceToHost, c->d2h));
+    if (cap >= need) {  // (a pageable `out` from the slot's pinned bounce, in iggy_codec_poll)
+        if (!out_pinned) sl.hout_dst = out;
+        HIP_OK(hipMemcpyAsync(out_pinned ? (void *)out : sl.hout, sl.out.p, need, hipMemcpyDeviceToHost, c->d2h));
+    }
     HIP_OK(hipEventRecord(sl.ev_done, c->d2h));
     *ticket = sl.ticket;
     return 0;
@@ -2713,6 +2957,8 @@ int iggy_codec_poll(iggy_codec_ctx *c, iggy_ticket ticket, iggy_completion *out)
         out->computed_checksum = res.computed_checksum;
         if (res.error.kind == IGGY_OK && sl.frame_pos && res.frame_count > sl.cap) {
             out->error = iggy_wire_error{IGGY_ERR_CAPACITY, 0, res.frame_count, sl.cap, 0};
+        } else if (res.error.kind == IGGY_OK && sl.hout_dst && res.frame_count) {
+            memcpy(sl.hout_dst, sl.hout, std::min<uint64_t>(res.frame_count, sl.cap) * 8);
         }
     } else {
         iggy_encode_result res;
@@ -2720,6 +2966,7 @@ int iggy_codec_poll(iggy_codec_ctx *c, iggy_ticket ticket, iggy_completion *out)
         out->header = res.header;
         out->error = res.error;
         out->bytes = res.error.kind == IGGY_OK ? res.batch_length : 0;
+        if (res.error.kind == IGGY_OK && sl.hout_dst) memcpy(sl.hout_dst, sl.hout, sl.out_len);
     }
     return 0;
 }
@@ -2771,9 +3018,8 @@ int iggy_codec_debug_read(iggy_codec_ctx *c, void *out, uint64_t bytes) {
     if (!c || !out) return IGGY_ERR_INVALID_ARGUMENT;
     HIP_OK(hipStreamSynchronize(c->stream));
     HIP_OK(hipDeviceSynchronize());
-    HIP_OK(hipMemcpy(out, c->dsync.as<uint8_t>(kSyncSmall), std::min<uint64_t>(bytes, kSyncBytes - kSyncSmall),
-                     hipMemcpyDeviceToHost));
-    return 0;
+    return get_host(c, out, c->dsync.as<uint8_t>(kSyncSmall), std::min<uint64_t>(bytes, kSyncBytes - kSyncSmall),
+                    c->stream);
 }
 // Diagnostics only: set the ablation bits of a context (no effect in the product
 // build, where kDiagMask is zero).

@@ -615,7 +615,7 @@ int iggy_producer_flush(iggy_producer *p, uint8_t *out, uint64_t cap, iggy_produ
     std::vector<uint8_t> live(sendable.size(), 0);
     // every request slot this flush may report is cleared first: a caller reusing its
     // array from an earlier flush must not see a stale `sent` past a failure
-    memset(reqs, 0, sendable.size() * sizeof(iggy_producer_request));
+    if (!sendable.empty()) memset(reqs, 0, sendable.size() * sizeof(iggy_producer_request));
     size_t oldest = 0;
     int rc = 0;
     auto retire = [&](size_t r) -> int {

@@ -557,9 +557,13 @@ int iggy_codec_segment_write_device(iggy_codec_ctx *ctx, int fd, uint64_t positi
  * ticket at once; iggy_codec_poll tells whether it has finished. Successive
  * submits overlap (one operation's H2D, another's kernels, a third's D2H).
  * Kernels never read host memory. Caller buffers must stay valid (and
- * unmodified, for inputs) until the ticket completes. Copies from pageable
- * memory are staged by the HIP runtime and block the caller for their
- * duration: register long-lived buffers (the server's 4096-aligned
+ * unmodified, for inputs) until the ticket completes. Pinned caller memory
+ * (hipHostMalloc, hipHostRegister, iggy_codec_host_register) is copied by DMA
+ * directly. Pageable memory is never a DMA source or target: an input is
+ * staged through the context's pinned chunks inside the submit (which blocks
+ * for that memcpy), an output lands in the slot's pinned bounce and is copied
+ * to the caller by the iggy_codec_poll / _wait that completes the ticket (only
+ * on success). Register long-lived buffers (the server's 4096-aligned
  * Owned<MESSAGE_ALIGN> pool, server_common/src/iobuf.rs) once with
  * iggy_codec_host_register. At most 8 operations per context are in flight
  * (IGGY_ERR_BUSY otherwise). */
@@ -580,6 +584,12 @@ typedef struct iggy_completion {
 /* Page-lock a caller buffer for the context's device (hipHostRegister) / undo it. */
 int iggy_codec_host_register(iggy_codec_ctx *ctx, void *ptr, uint64_t len);
 int iggy_codec_host_unregister(iggy_codec_ctx *ctx, void *ptr);
+/* 1 when every host entry point copies [ptr, ptr + len) by DMA directly (pinned:
+ * registered through the codec, hipHostRegister, hipHostMalloc), 0 when it stages the
+ * bytes through the context's pinned chunks (pageable memory). Every synchronous
+ * host entry point borrows its buffers for the call only (batch.rs:391): nothing of
+ * the call touches caller memory after it returns, pinned or not. */
+int iggy_codec_host_pinned(const void *ptr, uint64_t len);
 /* decode_batch_slice_with (batch.rs:391-422) of a host record; frame_pos
  * (nullable, host) receives up to `cap` blob-relative frame starts (entries
  * past frame_count are unspecified; more frames than cap -> IGGY_ERR_CAPACITY

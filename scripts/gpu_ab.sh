@@ -5,6 +5,5 @@ R=${GRAFT_REPO_ROOT:-$(pwd)}
 O=$R/gpurun_out/ab
 mkdir -p $O
 cd $R
-export GPU_PINNED_MIN_XFER_SIZE=1048576
 timeout -k 10 400 python -u scripts/ab_libs.py $LIBS --rounds ${ROUNDS:-6} > $O/abn.log 2>&1
 rc=$?; echo "ab rc=$rc" >> $O/abn.log; exit $rc

@@ -6,7 +6,6 @@ R=${GRAFT_REPO_ROOT:-$(pwd)}
 O=$R/gpurun_out/encab
 mkdir -p $O
 cd $R
-export GPU_PINNED_MIN_XFER_SIZE=1048576
 for r in 1 2; do
   for lib in $LIBS; do
     IGGY_DIAG_LIB=$lib timeout -k 10 120 python3 -u scripts/bench_encode.py --steps 10 > $O/run.log 2>&1 || { cat $O/run.log; exit 1; }

@@ -6,9 +6,10 @@ import pytest
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
-# the HIP runtime settings of the package (no on-the-fly pinning of pageable host
-# ranges, iggy_amd/__init__.py) before torch initialises the runtime
-import iggy_amd  # noqa: F401,E402
+# The suite runs with the HIP runtime's defaults: the round-4 override of on-the-fly
+# pinning (GPU_PINNED_MIN_XFER_SIZE) is gone, and a stale one from the caller's
+# environment is dropped before anything initialises the runtime.
+os.environ.pop("GPU_PINNED_MIN_XFER_SIZE", None)
 
 # torch first: its bundled HIP runtime then serves the codec library too (same
 # sonames; see iggy_amd/codec.py load())
@@ -27,7 +28,7 @@ def pytest_configure(config):
 # SDK, encryption) must not hide the core decode/encode parity suite, which would
 # otherwise sort after it alphabetically.
 _MODULE_ORDER = ["test_parity_gpu", "test_configs_gpu", "test_robust_gpu", "test_convert_gpu",
-                 "test_records_gpu", "test_sdk_gpu", "test_pollbody_gpu", "test_crypt_gpu"]
+                 "test_records_gpu", "test_sdk_gpu", "test_pollbody_gpu", "test_crypt_gpu", "test_hostmem_gpu"]
 
 
 def pytest_collection_modifyitems(session, config, items):

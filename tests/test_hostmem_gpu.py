@@ -1,0 +1,109 @@
+"""Caller host memory at the boundary.
+
+The reference borrows `&[u8]` for the call only (core/binary_protocol/src/batch.rs:391):
+the caller may free or reuse a buffer the moment a codec call returns. These tests run
+with the HIP runtime's defaults (no GPU_PINNED_MIN_XFER_SIZE override) and drive every
+host entry point with freshly allocated PAGEABLE numpy buffers that are freed right
+after the call, interleaved with torch's own pageable copies into new allocations --
+the sequence that faulted in rounds 3-4 -- and check each result against the oracle.
+They also pin the codec's pinned / pageable classification (iggy_codec_host_pinned)."""
+import ctypes
+import gc
+import os
+
+import numpy as np
+import pytest
+
+from iggy_amd import abi
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def cx():
+    from iggy_amd.codec import Codec
+    c = Codec(0)
+    yield c
+    c.close()
+
+
+def test_runtime_defaults_in_this_process():
+    assert "GPU_PINNED_MIN_XFER_SIZE" not in os.environ
+
+
+def test_host_pinned_classification(cx):
+    import torch
+    a = np.zeros(1 << 20, dtype=np.uint8)
+    assert not cx.host_pinned(a.ctypes.data, a.size)
+    b = np.zeros(3 << 20, dtype=np.uint8)
+    cx.host_register(b)
+    try:
+        assert cx.host_pinned(b.ctypes.data, b.size)
+        assert cx.host_pinned(b.ctypes.data + 4097, 1000)
+        assert not cx.host_pinned(b.ctypes.data + 4096, b.size)  # runs past the range
+    finally:
+        cx.host_unregister(b)
+    assert not cx.host_pinned(b.ctypes.data, b.size)
+    t = torch.empty(1 << 20, dtype=torch.uint8).pin_memory()  # hipHostMalloc
+    assert cx.host_pinned(t.data_ptr(), t.numel())
+    assert cx.host_pinned(t.data_ptr() + 100, 1000)
+    assert cx.host_pinned(0, 0)  # nothing to copy
+
+
+def _fresh(rec):
+    """A new pageable copy of rec (a new allocation, freed by the caller's del)."""
+    x = np.empty(rec.size, dtype=np.uint8)
+    x[:] = rec
+    return x
+
+
+def test_pageable_buffers_freed_after_every_call(cx):
+    import torch
+    big = O.synth_batch(150_000, 1024, seed=5)            # 161 MB: persistent decode path
+    small = O.synth_batch(3000, 200, 300, seed=6)         # < 16 MiB: host-flag path
+    seg = np.concatenate([O.synth_batch(1000, 256, seed=s) for s in range(8)])
+    ob = O.decode_batch_slice_with(big, 0)
+    osm = O.decode_batch_slice_with(small, 0)
+    dev = torch.randint(0, 255, (64 << 20,), dtype=torch.uint8, device="cuda")
+    ref_sum = int(dev.sum().item())
+    for it in range(4):
+        x = _fresh(big)
+        rc, e, h, f = cx.decode_batch_slice_with(x, abi.INTEGRITY_VERIFY)
+        del x
+        assert (rc, h.astuple()) == (ob[0], ob[2].astuple()) and np.array_equal(f, ob[3])
+        # torch: pageable D2H into a new allocation, then a pageable H2D
+        host = dev.cpu()
+        assert int(host.sum().item()) == ref_sum
+        back = torch.from_numpy(host.numpy().copy()).to("cuda")
+        assert torch.equal(back, dev)
+        del host, back
+        x = _fresh(small)
+        rc, e, h, f = cx.decode_batch_slice_with(x, abi.INTEGRITY_VERIFY)
+        del x
+        assert (rc, h.astuple()) == (osm[0], osm[2].astuple()) and np.array_equal(f, osm[3])
+        x = _fresh(seg)
+        rc, rec = cx.recover_segment(x, 0)
+        del x
+        orc, orec = O.recover_segment(seg, 0)
+        assert rc == orc == 0 and rec.batches == orec.batches == 8
+        gc.collect()
+
+
+def test_pageable_submit_outputs(cx):
+    """Asynchronous submits with pageable inputs and outputs: nothing lands in the
+    caller's output before the ticket completes, and only on success."""
+    rec = O.synth_batch(20000, 100, 2000, seed=19)
+    orc, oe, oh, of = O.decode_batch_slice_with(rec, 0)
+    pos = np.full(20000, 7, dtype=np.uint64)
+    body = _fresh(rec)
+    t = cx.decode_submit(body, abi.INTEGRITY_VERIFY, pos)
+    del body  # the input was staged inside the submit
+    c = cx.wait(t)
+    assert c.error.kind == 0 and c.header.astuple() == oh.astuple()
+    assert np.array_equal(pos, of)
+    # frame capacity too small: a capacity error and the caller's array untouched
+    short = np.full(10, 7, dtype=np.uint64)
+    t = cx.decode_submit(rec, abi.INTEGRITY_VERIFY, short)
+    assert cx.wait(t).error.kind == abi.ERR_CAPACITY
+    assert (short == 7).all()

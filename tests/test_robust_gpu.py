@@ -113,7 +113,8 @@ def test_submit_registered_buffers_and_busy(cx):
         cx.host_unregister(buf)
         cx.host_unregister(pos)
     # frame capacity too small for the record
-    t = cx.decode_submit(rec, abi.INTEGRITY_VERIFY, np.zeros(10, dtype=np.uint64))
+    short = np.zeros(10, dtype=np.uint64)  # kept alive until the ticket completes (the API's contract)
+    t = cx.decode_submit(rec, abi.INTEGRITY_VERIFY, short)
     assert cx.wait(t).error.kind == abi.ERR_CAPACITY
 
 
