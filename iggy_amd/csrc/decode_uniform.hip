@@ -788,9 +788,10 @@ __device__ __forceinline__ bool lg_process(const LgPlan &pl, const LgLane &c, co
 // the NEXT frame's from lane 3's extra load, lg_issue) forms the frame's word
 // t = 8k + fg (k = 4 unit + wave: the frame group), m = 128 b + t, accumulator
 // m & 7 = fg, and the 8 groups' x / y parts are combined with one DPP row rotation;
-// each group then adds its 8 accumulator contributions into the block's LDS slot
-// (ds_add_u64, 8 lanes) and counts itself in. The WG's fifth wave publishes a block
-// once its 16 groups are in: 8 sums read back, the slot zeroed and released, one
+// each wave sums its 4 groups of the block in registers, then adds the 8 accumulator
+// contributions into the block's LDS slot (ds_add_u64, 8 lanes) and counts itself in.
+// The WG's fifth wave publishes a block once its 4 waves are in: 8 sums read back,
+// the slot zeroed and released, one
 // 128-B record stored. The block's last word (t = 127, straddling into the next
 // block) stays the gatherer's, from the spare bytes (first_lo of frame t = 0, last_hi
 // of frame t = 127, written by the two groups that hold them).
@@ -813,11 +814,18 @@ __device__ __forceinline__ uint32_t *bs_gen(uint8_t *smem) { return bs_cnt(smem)
 constexpr int kDppRowRor8 = 0x128;  // row_ror:8: lane r of a 16-lane row <- lane r ^ 8
 
 // Frame group (unit j of this WG, wave) adds its words to block jb = j / 4's slot.
+// A wave takes the 4 units of a block on 4 consecutive steps (unit q = j & 3), so its
+// contributions are summed in registers (wacc) and flushed into the block's LDS slot
+// once per block, on its q = 3 step: one slot wait, one ds_add per accumulator and one
+// count add per wave and block (round 4 did all three on every step: the LDS round
+// trips stalled the wave, alone on its SIMD, between its ring waits). The count add is
+// not ordered behind the sum adds by a wait: DS instructions of one wave execute in
+// issue order, and the publisher reads the sums after it has seen the count.
 __device__ __forceinline__ void lg_words(uint8_t *smem, const LgPlan &pl, const LgLane &c, uint64_t b, uint64_t j,
-                                         uint32_t wave, int lane, const LgState &st, uint64_t t_start) {
+                                         uint32_t wave, int lane, const LgState &st, uint64_t t_start,
+                                         uint64_t &wacc, uint32_t &wfirst) {
     const uint64_t jb = j >> 2;
     const uint32_t q = (uint32_t)(j & 3);
-    const uint32_t s = (uint32_t)(jb % kBsSlots), gen = (uint32_t)(jb / kBsSlots);
     const uint32_t k = 4 * q + wave;  // frame group of the block (frames 128 b - 6 + 8 k ..)
     const uint32_t t = 8 * k + c.fg;
     const uint64_t m = 128 * b + t;
@@ -829,21 +837,25 @@ __device__ __forceinline__ void lg_words(uint8_t *smem, const LgPlan &pl, const 
         y = v;
         x = mul32x32(v ^ sec);
     }
-    const uint64_t a = x + dpp64<kDppRowRor8>(y);  // lane 8 fg: acc[fg] (x of word fg, y of word fg ^ 1)
+    wacc += x + dpp64<kDppRowRor8>(y);  // lane 8 fg: acc[fg] (x of word fg, y of word fg ^ 1)
+    if (q == 0) wfirst = (uint32_t)st.stored;  // (wave 0, lane 0: frame t = 0 of the block)
+    if (q != 3) return;
+    const uint32_t s = (uint32_t)(jb % kBsSlots), gen = (uint32_t)(jb / kBsSlots);
     while (__hip_atomic_load(&bs_gen(smem)[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != gen) {
         __builtin_amdgcn_s_sleep(1);
         if (rt_now() - t_start > kSpinLimitTicks) return;  // bug guard: the consumer times out
     }
     if (c.l == 0) {
-        __hip_atomic_fetch_add(&bs_acc(smem, s)[c.fg], a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        if (k == 0 && c.fg == 0) bs_spare(smem, s)[0] = (uint32_t)st.stored;           // frame t = 0: lo32
-        if (k == 15 && c.fg == 7) bs_spare(smem, s)[1] = (uint32_t)(st.stored >> 32);  // frame t = 127: hi32
+        __hip_atomic_fetch_add(&bs_acc(smem, s)[c.fg], wacc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (wave == 0 && c.fg == 0) bs_spare(smem, s)[0] = wfirst;                       // frame t = 0: lo32
+        if (wave == 3 && c.fg == 7) bs_spare(smem, s)[1] = (uint32_t)(st.stored >> 32);  // frame t = 127: hi32
     }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    asm volatile("" ::: "memory");  // (compiler order only: the DS adds above issue first)
     if (lane == 0) __hip_atomic_fetch_add(&bs_cnt(smem)[s], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    wacc = 0;
 }
 
-// The publisher wave: blocks g, g + np, ... in order, each once its 16 frame groups
+// The publisher wave: blocks g, g + np, ... in order, each once its 4 producer waves
 // are in: the 8 sums read, the slot zeroed and released, the block record stored.
 __device__ __forceinline__ void lg_publisher(uint8_t *smem, const LgPlan &pl, const DecodeScratch &sc,
                                              uint32_t epoch, uint32_t g, uint32_t np, int lane, uint32_t dbg) {
@@ -853,7 +865,7 @@ __device__ __forceinline__ void lg_publisher(uint8_t *smem, const LgPlan &pl, co
     const uint64_t mine = (blocks - g + np - 1) / np;
     for (uint64_t jb = 0; jb < mine; ++jb) {
         const uint32_t s = (uint32_t)(jb % kBsSlots), gen = (uint32_t)(jb / kBsSlots);
-        while (__hip_atomic_load(&bs_cnt(smem)[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != 16u) {
+        while (__hip_atomic_load(&bs_cnt(smem)[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != 4u) {
             __builtin_amdgcn_s_sleep(1);
             if (rt_now() - t_start > kSpinLimitTicks) return;  // bug guard
         }
@@ -916,6 +928,8 @@ __device__ __forceinline__ void produce_lg(const uint8_t *blob, const LgPlan &pl
 
     LgState st;
     st.a0 = c.init0; st.a1 = c.init1; st.stored = 0; st.next = 0; st.sbad = false; st.sink = 0;
+    uint64_t wacc = 0;    // this wave's words of the current block (lg_words)
+    uint32_t wfirst = 0;
     // processing cursor (pj, pb) and issue cursor (ij, ib), up to SLOTS steps ahead
     uint64_t pj = 0, ij = 0;
     uint32_t pb = 0, ib = 0;
@@ -960,7 +974,7 @@ __device__ __forceinline__ void produce_lg(const uint8_t *blob, const LgPlan &pl
         issue_next();  // step k + SLOTS into the slot just read
         const uint64_t u = unit_of(pj);
         if (lg_process<ONE>(pl, c, sc, frame_pos, cap, u, wave, pb, nblk, B, st, lane))
-            lg_words(smem, pl, c, g + (pj >> 2) * np, pj, wave, lane, st, t_start);
+            lg_words(smem, pl, c, g + (pj >> 2) * np, pj, wave, lane, st, t_start, wacc, wfirst);
         advance(pj, pb);
     }
     wait_vm(0);

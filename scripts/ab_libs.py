@@ -16,7 +16,6 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
-import iggy_amd  # noqa: E402,F401  (HIP runtime settings before torch)
 import torch  # noqa: E402
 from iggy_amd import abi  # noqa: E402
 from iggy_amd.codec import Codec, load  # noqa: E402

@@ -12,7 +12,6 @@ import sys
 import time
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-import iggy_amd  # noqa: E402,F401  (HIP runtime settings before torch)
 import torch  # noqa: E402
 
 from iggy_amd import abi  # noqa: E402

@@ -62,7 +62,9 @@ def test_pageable_buffers_freed_after_every_call(cx):
     import torch
     big = O.synth_batch(150_000, 1024, seed=5)            # 161 MB: persistent decode path
     small = O.synth_batch(3000, 200, 300, seed=6)         # < 16 MiB: host-flag path
-    seg = np.concatenate([O.synth_batch(1000, 256, seed=s) for s in range(8)])
+    # 8 batches with contiguous offsets (recover_segment walks them all)
+    seg = np.concatenate([np.frombuffer(O.stamp_batch(O.synth_batch(1000, 256, seed=s), 1000 * s, 10 + s)[3],
+                                        dtype=np.uint8) for s in range(8)])
     ob = O.decode_batch_slice_with(big, 0)
     osm = O.decode_batch_slice_with(small, 0)
     dev = torch.randint(0, 255, (64 << 20,), dtype=torch.uint8, device="cuda")
@@ -86,7 +88,7 @@ def test_pageable_buffers_freed_after_every_call(cx):
         rc, rec = cx.recover_segment(x, 0)
         del x
         orc, orec = O.recover_segment(seg, 0)
-        assert rc == orc == 0 and rec.batches == orec.batches == 8
+        assert rc == orc == 0 and rec.batches == orec.batches == 8 and rec.walked_bytes == orec.walked_bytes == seg.size
         gc.collect()
 
 
