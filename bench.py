@@ -57,6 +57,7 @@ import numpy as np
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
+from iggy_amd.torch_io import to_device, to_host  # noqa: E402  (copies through pinned staging)
 
 METRIC = "GiB/s device-resident message-batch decode, 1M msgs × 1KiB payload"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s peak
@@ -143,7 +144,7 @@ def make_batch(cx, n: int, pl_lo: int, pl_hi: int, rank: int, dev, stream: int):
     if rc:
         raise RuntimeError(f"encode_device rc={rc}")
     torch.cuda.synchronize(dev)
-    er = abi.EncodeResult.from_buffer_copy(res.cpu().numpy().tobytes())
+    er = abi.EncodeResult.from_buffer_copy(to_host(res).tobytes())
     if er.error.kind != 0 or er.batch_length != total:
         raise RuntimeError(f"encode failed: {er.error!r}")
     return out, (raw, ids, ots, payload, pls, res), total_pl
@@ -175,11 +176,11 @@ def c3_leg(cx, dev, steps: int):
         return (time.perf_counter() - t0) / steps
 
     enc_s = timed(lambda: cx.encode_device(raw, 8, out.data_ptr(), L, res.data_ptr(), s.cuda_stream))
-    er = abi.EncodeResult.from_buffer_copy(res.cpu().numpy().tobytes())
+    er = abi.EncodeResult.from_buffer_copy(to_host(res).tobytes())
     assert er.error.kind == 0 and er.batch_length == L, er.error
     dec_s = timed(lambda: cx.decode_device(out.data_ptr(), L, abi.INTEGRITY_VERIFY, pos.data_ptr(), n,
                                            dres.data_ptr(), s.cuda_stream))
-    dr = abi.DecodeResult.from_buffer_copy(dres.cpu().numpy().tobytes())
+    dr = abi.DecodeResult.from_buffer_copy(to_host(dres).tobytes())
     assert dr.error.kind == 0 and dr.frame_count == n, dr.error
     enc_alg = total_pl + 32 * n + L  # payload + ids/timestamps/lengths in, batch out
     dec_alg = L + 8 * n
@@ -226,11 +227,11 @@ def crypt_leg(cx, dev, rec, n: int, steps: int, cpu: bool):
 
     enc_s = timed(lambda: cx.encrypt_batch_device(key, rec.data_ptr(), L, nonces.data_ptr(), enc.data_ptr(), cap,
                                                   res.data_ptr(), s.cuda_stream))
-    r = abi.CryptResult.from_buffer_copy(res.cpu().numpy().tobytes())
+    r = abi.CryptResult.from_buffer_copy(to_host(res).tobytes())
     assert r.error.kind == 0 and r.out_len == cap, r.error
     dec_s = timed(lambda: cx.decrypt_batch_device(key, enc.data_ptr(), cap, dec.data_ptr(), L, res.data_ptr(),
                                                   s.cuda_stream))
-    r = abi.CryptResult.from_buffer_copy(res.cpu().numpy().tobytes())
+    r = abi.CryptResult.from_buffer_copy(to_host(res).tobytes())
     assert r.error.kind == 0 and r.out_len == L, r.error
     assert torch.equal(dec, rec), "decrypt(encrypt(x)) != x"
     out = {"workload": "encrypt_batch_request / decrypt_batch_record on the C2 record (1,048,576 x 1 KiB), "
@@ -288,7 +289,7 @@ def c1_leg(cx, dev, seconds: float):
     # GPU: device-resident decode of each batch (latency-bound at 304 KB) and the
     # host round trip through the asynchronous API (H2D, decode, D2H), per batch
     s = torch.cuda.Stream(dev)
-    drecs = [torch.from_numpy(r).to(dev) for r in recs]
+    drecs = [to_device(r, dev) for r in recs]
     dres = torch.zeros(ctypes.sizeof(abi.DecodeResult), dtype=torch.uint8, device=dev)
     for _ in range(3):
         for d, r in zip(drecs, recs):
@@ -303,7 +304,7 @@ def c1_leg(cx, dev, seconds: float):
     # device-resident encode of each batch (SendMessagesEncoder::encode from SoA input in HBM)
     denc = []
     for (ids, ots, pay, pls), r in zip(keep, recs):
-        t = [torch.from_numpy(a.view(np.int64) if a.dtype == np.uint64 else a).to(dev) for a in (ids, ots, pay, pls)]
+        t = [to_device(a.view(np.int64) if a.dtype == np.uint64 else a, dev) for a in (ids, ots, pay, pls)]
         out = torch.empty(r.size, dtype=torch.uint8, device=dev)
         eres = torch.zeros(ctypes.sizeof(abi.EncodeResult), dtype=torch.uint8, device=dev)
         raw = abi.RawMessages(n, t[0].data_ptr(), t[1].data_ptr(), t[2].data_ptr(), t[3].data_ptr(), None, None)
@@ -320,7 +321,7 @@ def c1_leg(cx, dev, seconds: float):
     torch.cuda.synchronize(dev)
     enc_us = (time.perf_counter() - t0) / (10 * nb) * 1e6
     for _raw, _t, _out, eres in denc:
-        er = abi.EncodeResult.from_buffer_copy(eres.cpu().numpy().tobytes())
+        er = abi.EncodeResult.from_buffer_copy(to_host(eres).tobytes())
         assert er.error.kind == 0, er.error
     t0 = time.perf_counter()
     for _ in range(5):
@@ -422,7 +423,7 @@ def c4_leg(dev, batches: int):
         ms = {k: ev[i].elapsed_time(ev[i + 1]) for i, k in
               enumerate(["h2d_soa", "encode", "d2h_wire", "h2d_wire", "decode", "d2h_positions"])}
     cx.close()
-    dr = abi.DecodeResult.from_buffer_copy(d_dres.cpu().numpy().tobytes())
+    dr = abi.DecodeResult.from_buffer_copy(to_host(d_dres).tobytes())
     assert dr.error.kind == 0 and dr.frame_count == n, dr.error
     soa = 16 * n + 8 * n + n * pl + 4 * n
     pcie = soa + 2 * total + 8 * n + 2 * ctypes.sizeof(abi.DecodeResult)
@@ -553,10 +554,10 @@ def run(args, world: int, rank: int, local: int, dist):
         step(i)
     torch.cuda.synchronize(dev)
     for ln in lanes:
-        res = abi.DecodeResult.from_buffer_copy(ln["res"].cpu().numpy().tobytes())
+        res = abi.DecodeResult.from_buffer_copy(to_host(ln["res"]).tobytes())
         if res.error.kind != 0 or res.frame_count != n or res.path != 1:
             raise RuntimeError(f"decode check failed: {res.error!r} frames={res.frame_count} path={res.path}")
-        pos = ln["pos"][:4].cpu().tolist()
+        pos = to_host(ln["pos"][:4]).tolist()
         assert pos == [i * (48 + PAYLOAD) for i in range(4)], pos
 
     if dist:
@@ -571,7 +572,7 @@ def run(args, world: int, rank: int, local: int, dist):
         dist.barrier()
     elapsed = max_over_ranks(elapsed, dist)
     for ln in lanes:  # every timed decode left a clean result
-        res = abi.DecodeResult.from_buffer_copy(ln["res"].cpu().numpy().tobytes())
+        res = abi.DecodeResult.from_buffer_copy(to_host(ln["res"]).tobytes())
         if res.error.kind != 0 or res.frame_count != n:
             raise RuntimeError(f"timed decode failed: {res.error!r}")
 

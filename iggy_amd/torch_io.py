@@ -1,0 +1,34 @@
+"""Copies between host numpy arrays and torch device tensors through pinned staging.
+
+Plumbing for the Python callers of the codec that move their own buffers with torch
+(the tests, smoke(), bench.py). The HIP runtime copies PAGEABLE host memory by page-
+locking the caller's range on the fly (ROCclr, transfers above GPU_PINNED_MIN_XFER_SIZE).
+On this pool that path faulted (hipErrorIllegalAddress inside a pageable copy) in rounds
+3-5, once inside torch's own `.to("cuda")` with no codec call since the last stream
+synchronisation. The codec never uses that path (codec_api.hip put_host /
+get_host stage pageable bytes through its own pinned chunks); these helpers keep the
+callers' own copies off it too: a host memcpy into torch's pinned (hipHostMalloc) cache,
+then a DMA from page-locked memory.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+
+def to_device(a, device="cuda"):
+    """A device tensor holding a copy of the numpy array `a` (same dtype and shape)."""
+    import torch
+    t = torch.from_numpy(np.ascontiguousarray(a))
+    p = torch.empty(t.shape, dtype=t.dtype, pin_memory=True)
+    p.copy_(t)
+    return p.to(device)
+
+
+def to_host(t) -> np.ndarray:
+    """A numpy copy of tensor `t` (synchronous; the copy lands in pinned memory)."""
+    import torch
+    if t.device.type == "cpu":
+        return t.numpy()
+    p = torch.empty(t.shape, dtype=t.dtype, pin_memory=True)
+    p.copy_(t)
+    return p.numpy()

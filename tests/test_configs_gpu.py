@@ -20,6 +20,7 @@ import numpy as np
 import pytest
 
 from iggy_amd import abi
+from iggy_amd.torch_io import to_device, to_host
 from iggy_amd.codec import raw_messages
 from oracle import oracle as O
 
@@ -120,7 +121,7 @@ def _torch():
 
 
 def _res(t):
-    return abi.DecodeResult.from_buffer_copy(t.cpu().numpy().tobytes())
+    return abi.DecodeResult.from_buffer_copy(to_host(t).tobytes())
 
 
 def test_uniform_beside_general_two_contexts():
@@ -140,7 +141,7 @@ def test_uniform_beside_general_two_contexts():
     def run(k):
         try:
             s = torch.cuda.Stream()
-            d = torch.from_numpy(recs[k]).to("cuda:0")
+            d = to_device(recs[k], "cuda:0")
             n = int(expect[k][2].message_count)
             pos = torch.zeros(n, dtype=torch.int64, device="cuda:0")
             res = [torch.zeros(ctypes.sizeof(abi.DecodeResult), dtype=torch.uint8, device="cuda:0")
@@ -155,7 +156,7 @@ def test_uniform_beside_general_two_contexts():
                 assert got.error.kind == 0, (k, it, got.error.kind)
                 assert got.path == paths[k]
                 assert got.computed_checksum == expect[k][2].batch_checksum
-            assert np.array_equal(pos.cpu().numpy().astype(np.uint64), expect[k][3])
+            assert np.array_equal(to_host(pos).astype(np.uint64), expect[k][3])
         except Exception as ex:  # surfaced below
             errors.append(ex)
 

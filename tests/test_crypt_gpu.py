@@ -10,6 +10,7 @@ import pytest
 
 from crypt_util import frame_sections, key_for, nonces_for, raw_record
 from iggy_amd import abi
+from iggy_amd.torch_io import to_device, to_host
 from oracle import oracle as O
 
 pytestmark = pytest.mark.gpu
@@ -25,7 +26,7 @@ def cx():
 
 def _dev(a):
     import torch
-    return torch.from_numpy(np.ascontiguousarray(a)).to("cuda")
+    return to_device(a)
 
 
 def _run(cx, enc: bool, key, rec, nonces=None, cap=None, length=None):
@@ -46,8 +47,8 @@ def _run(cx, enc: bool, key, rec, nonces=None, cap=None, length=None):
         rc = cx.decrypt_batch_device(key, d_rec.data_ptr(), ln, d_out.data_ptr(), cap, d_res.data_ptr(), s)
     assert rc == 0
     torch.cuda.synchronize()
-    r = abi.CryptResult.from_buffer_copy(d_res.cpu().numpy().tobytes())
-    out = d_out.cpu().numpy()[: r.out_len].tobytes() if r.error.kind == 0 else b""
+    r = abi.CryptResult.from_buffer_copy(to_host(d_res).tobytes())
+    out = to_host(d_out)[: r.out_len].tobytes() if r.error.kind == 0 else b""
     return r, out
 
 
@@ -159,16 +160,16 @@ def test_full_size_c2_round_trip(cx):
     assert cx.encrypt_batch_device(key, d_rec.data_ptr(), rec.size, d_non.data_ptr(), d_enc.data_ptr(), cap,
                                    d_res.data_ptr(), s) == 0
     torch.cuda.synchronize()
-    r = abi.CryptResult.from_buffer_copy(d_res.cpu().numpy().tobytes())
+    r = abi.CryptResult.from_buffer_copy(to_host(d_res).tobytes())
     assert r.error.kind == 0 and r.out_len == rec.size + 28 * n and r.frame_count == n
     d_pos = torch.zeros(n, dtype=torch.int64, device="cuda")
     d_dres = torch.zeros(ctypes.sizeof(abi.DecodeResult), dtype=torch.uint8, device="cuda")
     assert cx.decode_device(d_enc.data_ptr(), r.out_len, abi.INTEGRITY_VERIFY, d_pos.data_ptr(), n,
                             d_dres.data_ptr(), s) == 0
     torch.cuda.synchronize()
-    dr = abi.DecodeResult.from_buffer_copy(d_dres.cpu().numpy().tobytes())
+    dr = abi.DecodeResult.from_buffer_copy(to_host(d_dres).tobytes())
     assert dr.error.kind == 0 and dr.frame_count == n
-    enc = d_enc[: r.out_len].cpu().numpy()
+    enc = to_host(d_enc[: r.out_len])
     for i in (0, 1, 4095, 524287, n - 1):  # frames: 1100 B encrypted, 1072 B plain
         f_in, f_out = 256 + 1072 * i, 256 + 1100 * i
         assert enc[f_out + 48: f_out + 48 + 1052].tobytes() == O.gcm_seal(
@@ -177,6 +178,6 @@ def test_full_size_c2_round_trip(cx):
     assert cx.decrypt_batch_device(key, d_enc.data_ptr(), r.out_len, d_dec.data_ptr(), rec.size,
                                    d_res.data_ptr(), s) == 0
     torch.cuda.synchronize()
-    r2 = abi.CryptResult.from_buffer_copy(d_res.cpu().numpy().tobytes())
+    r2 = abi.CryptResult.from_buffer_copy(to_host(d_res).tobytes())
     assert r2.error.kind == 0 and r2.out_len == rec.size
     assert torch.equal(d_dec, d_rec)

@@ -15,6 +15,7 @@ import numpy as np
 import pytest
 
 from iggy_amd import abi
+from iggy_amd.torch_io import to_device, to_host
 from oracle import oracle as O
 
 pytestmark = pytest.mark.gpu
@@ -74,10 +75,10 @@ def test_pageable_buffers_freed_after_every_call(cx):
         rc, e, h, f = cx.decode_batch_slice_with(x, abi.INTEGRITY_VERIFY)
         del x
         assert (rc, h.astuple()) == (ob[0], ob[2].astuple()) and np.array_equal(f, ob[3])
-        # torch: pageable D2H into a new allocation, then a pageable H2D
-        host = dev.cpu()
-        assert int(host.sum().item()) == ref_sum
-        back = torch.from_numpy(host.numpy().copy()).to("cuda")
+        # the caller's own copies between (through pinned staging, iggy_amd/torch_io.py)
+        host = to_host(dev)
+        assert int(host.sum(dtype=np.uint64)) == ref_sum
+        back = to_device(host.copy())
         assert torch.equal(back, dev)
         del host, back
         x = _fresh(small)

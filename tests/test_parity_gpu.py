@@ -8,6 +8,7 @@ import pytest
 
 from golden_util import batch_cases, expect_matches, reference_vectors, xxh3_vectors
 from iggy_amd import abi
+from iggy_amd.torch_io import to_device, to_host
 from oracle import oracle as O
 
 pytestmark = pytest.mark.gpu
@@ -96,15 +97,15 @@ def _device_decode(cx, rec, integrity, cap=None):
     """decode_device on a torch-resident copy of rec: (result, positions[:frame_count])."""
     import torch
     n = rec.size // 48 + 1 if cap is None else cap
-    d_rec = torch.from_numpy(np.ascontiguousarray(rec)).to("cuda")
+    d_rec = to_device(rec)
     d_pos = torch.zeros(max(n, 1), dtype=torch.int64, device="cuda")
     d_res = torch.zeros(ctypes.sizeof(abi.DecodeResult), dtype=torch.uint8, device="cuda")
     s = torch.cuda.current_stream().cuda_stream
     torch.cuda.synchronize()
     assert cx.decode_device(d_rec.data_ptr(), rec.size, integrity, d_pos.data_ptr(), n, d_res.data_ptr(), s) == 0
     torch.cuda.synchronize()
-    r = abi.DecodeResult.from_buffer_copy(d_res.cpu().numpy().tobytes())
-    return r, d_pos[: min(r.frame_count, n)].cpu().numpy()
+    r = abi.DecodeResult.from_buffer_copy(to_host(d_res).tobytes())
+    return r, to_host(d_pos[: min(r.frame_count, n)])
 
 
 @pytest.mark.parametrize("shape", ["sealed_2000", "c3_120k", "small_frames_600k"])
@@ -518,7 +519,7 @@ def test_device_select_and_stamp(cx):
     import torch
     rec = _stamped_rec(20000, 64, 2000, 100, 200, seed=11)
     n = 20000
-    d_rec = torch.from_numpy(rec).to("cuda:0")
+    d_rec = to_device(rec, "cuda:0")
     d_pos = torch.zeros(n, dtype=torch.int64, device="cuda:0")
     d_res = torch.zeros(ctypes.sizeof(abi.DecodeResult), dtype=torch.uint8, device="cuda:0")
     s = torch.cuda.current_stream().cuda_stream
@@ -531,13 +532,13 @@ def test_device_select_and_stamp(cx):
     d_h = torch.zeros(64, dtype=torch.uint8, device="cuda:0")
     assert cx.stamp_device(d_rec.data_ptr(), d_pos.data_ptr(), n, 424242, 999, d_h.data_ptr(), s) == 0
     torch.cuda.synchronize()
-    sr = abi.SliceResult.from_buffer_copy(d_sr.cpu().numpy().tobytes())
+    sr = abi.SliceResult.from_buffer_copy(to_host(d_sr).tobytes())
     orc, orr, ohdr = O.select_slice(rec, abi.LOOKUP_OFFSET, 5100, 777)
-    assert sr.astuple() == orr.astuple() and d_hdr.cpu().numpy().tobytes() == ohdr
-    stamped = d_rec.cpu().numpy()
+    assert sr.astuple() == orr.astuple() and to_host(d_hdr).tobytes() == ohdr
+    stamped = to_host(d_rec)
     orc, oe, oh, oout = O.stamp_batch(rec.copy(), 424242, 999)
     assert stamped.tobytes() == oout
-    h = abi.BatchHeader.from_buffer_copy(d_h.cpu().numpy().tobytes())
+    h = abi.BatchHeader.from_buffer_copy(to_host(d_h).tobytes())
     assert h.astuple() == oh.astuple()
     rc, e, hh, _ = cx.decode_batch_slice_with(stamped, abi.INTEGRITY_VERIFY)
     assert rc == 0, e
@@ -703,7 +704,7 @@ def test_segment_write_device_then_verify(cx, tmp_path):
     import os
     import torch
     seg, starts = _segment_chunk([(20000, 1024, 1024), (3000, 10, 3000), (5000, 100, 100)], base_offset=0, seed=9)
-    d = torch.from_numpy(seg).to("cuda:0")
+    d = to_device(seg, "cuda:0")
     torch.cuda.synchronize()
     path = str(tmp_path / "00000000000000000000.log")
     fd = os.open(path, os.O_RDWR | os.O_CREAT, 0o644)

@@ -13,6 +13,7 @@ import pytest
 
 from golden_util import reference_vectors
 from iggy_amd import abi
+from iggy_amd.torch_io import to_device, to_host
 from oracle import oracle as O
 
 pytestmark = pytest.mark.gpu
@@ -41,7 +42,7 @@ def _torch():
 
 
 def _res(t):
-    return abi.DecodeResult.from_buffer_copy(t.cpu().numpy().tobytes())
+    return abi.DecodeResult.from_buffer_copy(to_host(t).tobytes())
 
 
 def _same(a_rc, a_e, b_rc, b_e):
@@ -141,7 +142,7 @@ def test_encode_device_matches_oracle_and_capacity(cx):
     for n, lo, hi, uh in [(5000, 64, 4096, False), (700, 0, 300, True), (2049, 1024, 1024, False)]:
         raw, keep = _raw(n, lo, hi, seed=7 * n, uh=uh)
         ids, ots, pay, pls, uhb, uhl = keep
-        d = lambda a: torch.from_numpy(a.view(np.uint8)).to("cuda:0") if a is not None and a.size else None
+        d = lambda a: to_device(a.view(np.uint8), "cuda:0") if a is not None and a.size else None
         dids, dots, dpay, dpls, duhb, duhl = (d(a) for a in keep)
         draw = abi.RawMessages(n, dids.data_ptr(), dots.data_ptr(), dpay.data_ptr() if dpay is not None else None,
                                dpls.data_ptr(), duhb.data_ptr() if duhb is not None else None,
@@ -153,17 +154,17 @@ def test_encode_device_matches_oracle_and_capacity(cx):
         s = torch.cuda.current_stream().cuda_stream
         assert cx.encode_device(draw, 0, out.data_ptr(), need, res.data_ptr(), s) == 0
         torch.cuda.synchronize()
-        er = abi.EncodeResult.from_buffer_copy(res.cpu().numpy().tobytes())
+        er = abi.EncodeResult.from_buffer_copy(to_host(res).tobytes())
         assert er.error.kind == 0 and er.batch_length == need
-        got = out.cpu().numpy()
+        got = to_host(out)
         assert got[:need].tobytes() == oout and (got[need:] == 0xCD).all()
         # capacity one byte short: the device reports it and writes nothing
         out.fill_(0xCD)
         assert cx.encode_device(draw, 0, out.data_ptr(), need - 1, res.data_ptr(), s) == 0
         torch.cuda.synchronize()
-        er = abi.EncodeResult.from_buffer_copy(res.cpu().numpy().tobytes())
+        er = abi.EncodeResult.from_buffer_copy(to_host(res).tobytes())
         assert er.error.kind == abi.ERR_CAPACITY and er.error.a == need and er.error.b == need - 1
-        assert (out.cpu().numpy() == 0xCD).all()
+        assert (to_host(out) == 0xCD).all()
 
 
 def test_golden_produce_vector_encoded_on_gpu(cx):
@@ -213,8 +214,8 @@ def test_batch_checksum_and_xxh3_ranges_device(cx):
     rec = O.synth_batch(50_000, 10, 900, 4, seed=12)
     rc, e, h, frames = O.decode_batch_slice_with(rec, 1)
     assert rc == 0
-    d_rec = torch.from_numpy(rec).to("cuda:0")
-    d_pos = torch.from_numpy(frames.view(np.int64)).to("cuda:0")
+    d_rec = to_device(rec, "cuda:0")
+    d_pos = to_device(frames.view(np.int64), "cuda:0")
     d_out = torch.zeros(4, dtype=torch.int64, device="cuda:0")
     s = torch.cuda.current_stream().cuda_stream
     h2 = abi.BatchHeader.from_buffer_copy(bytes(h))
@@ -229,13 +230,13 @@ def test_batch_checksum_and_xxh3_ranges_device(cx):
     lens = np.array([struct.unpack_from("<I", rec, 256 + int(p) + 36)[0] +
                      struct.unpack_from("<I", rec, 256 + int(p) + 32)[0] + 40 for p in frames], dtype=np.uint32)
     offs = (frames + 256 + 8).astype(np.uint64)
-    d_offs = torch.from_numpy(offs.view(np.int64)).to("cuda:0")
-    d_lens = torch.from_numpy(lens.view(np.int32)).to("cuda:0")
+    d_offs = to_device(offs.view(np.int64), "cuda:0")
+    d_lens = to_device(lens.view(np.int32), "cuda:0")
     d_h = torch.zeros(len(frames), dtype=torch.int64, device="cuda:0")
     assert cx.xxh3_ranges_device(d_rec.data_ptr(), d_offs.data_ptr(), d_lens.data_ptr(), len(frames),
                                  d_h.data_ptr(), s) == 0
     torch.cuda.synchronize()
-    got = d_h.cpu().numpy().view(np.uint64)
+    got = to_host(d_h).view(np.uint64)
     stored = np.array([struct.unpack_from("<Q", rec, 256 + int(p))[0] for p in frames], dtype=np.uint64)
     assert np.array_equal(got, stored)
 
@@ -249,14 +250,14 @@ def test_misaligned_device_records(cx, shift, shape):
     n, lo, hi = shape
     rec = O.synth_batch(n, lo, hi, seed=shift * 31 + n)
     buf = torch.zeros(rec.size + 64, dtype=torch.uint8, device="cuda:0")
-    buf[shift: shift + rec.size] = torch.from_numpy(rec).to("cuda:0")
+    buf[shift: shift + rec.size] = to_device(rec, "cuda:0")
     d_pos = torch.zeros(n, dtype=torch.int64, device="cuda:0")
     d_res = torch.zeros(ctypes.sizeof(abi.DecodeResult), dtype=torch.uint8, device="cuda:0")
     s = torch.cuda.current_stream().cuda_stream
     bad = rec.copy()
     bad[256 + rec.size // 2 - 128] ^= 0x20
     for r in (rec, bad):
-        buf[shift: shift + rec.size] = torch.from_numpy(r).to("cuda:0")
+        buf[shift: shift + rec.size] = to_device(r, "cuda:0")
         for integ in (0, 1):
             assert cx.decode_device(buf.data_ptr() + shift, r.size, integ, d_pos.data_ptr(), n, d_res.data_ptr(), s) == 0
             torch.cuda.synchronize()
@@ -264,7 +265,7 @@ def test_misaligned_device_records(cx, shift, shape):
             orc, oe, oh, of = O.decode_batch_slice_with(r, integ)
             assert res.error.kind == orc and res.error.astuple() == oe.astuple()
             if orc == 0:
-                assert np.array_equal(d_pos.cpu().numpy().astype(np.uint64), of)
+                assert np.array_equal(to_host(d_pos).astype(np.uint64), of)
 
 
 def test_one_context_two_streams(cx):
@@ -275,7 +276,7 @@ def test_one_context_two_streams(cx):
     bad = recs[1].copy()
     bad[256 + 5000] ^= 1
     recs.append(bad)
-    drecs = [torch.from_numpy(r).to("cuda:0") for r in recs]
+    drecs = [to_device(r, "cuda:0") for r in recs]
     streams = [torch.cuda.Stream(), torch.cuda.Stream()]
     res = [torch.zeros(ctypes.sizeof(abi.DecodeResult), dtype=torch.uint8, device="cuda:0") for _ in range(12)]
     torch.cuda.synchronize()
@@ -305,7 +306,7 @@ def test_two_contexts_concurrent_variable_decodes():
     def run(k):
         try:
             s = torch.cuda.Stream()
-            d = torch.from_numpy(recs[k]).to("cuda:0")
+            d = to_device(recs[k], "cuda:0")
             n = int(expect[k][2].message_count)
             pos = torch.zeros(n, dtype=torch.int64, device="cuda:0")
             res = torch.zeros(ctypes.sizeof(abi.DecodeResult), dtype=torch.uint8, device="cuda:0")
@@ -317,7 +318,7 @@ def test_two_contexts_concurrent_variable_decodes():
             got = _res(res)
             assert got.error.kind == 0, got.error
             assert got.path == 2
-            assert np.array_equal(pos.cpu().numpy().astype(np.uint64), expect[k][3])
+            assert np.array_equal(to_host(pos).astype(np.uint64), expect[k][3])
         except Exception as ex:  # surfaced below
             errors.append(ex)
 
@@ -346,8 +347,8 @@ def test_recovery_after_timed_out_decode():
         rec = O.synth_batch(200_000, 1024, 1024, seed=41)
         bad = rec.copy()
         bad[256 + 1072 * 150_000 + 700] ^= 8  # body byte: stored checksums intact
-        d_good = torch.from_numpy(rec).to("cuda:0")
-        d_bad = torch.from_numpy(bad).to("cuda:0")
+        d_good = to_device(rec, "cuda:0")
+        d_bad = to_device(bad, "cuda:0")
         res = torch.zeros(ctypes.sizeof(abi.DecodeResult), dtype=torch.uint8, device="cuda:0")
         s = torch.cuda.current_stream().cuda_stream
         L.iggy_codec_debug_set(cx.handle, 4096)
@@ -394,14 +395,14 @@ def test_register_verify_loop_fallback(shift):
         for bits in (0x200000, 0):
             L.iggy_codec_debug_set(cx.handle, bits)
             for r in (rec, bad):
-                buf[shift: shift + r.size] = torch.from_numpy(r).to("cuda:0")
+                buf[shift: shift + r.size] = to_device(r, "cuda:0")
                 assert cx.decode_device(buf.data_ptr() + shift, r.size, 0, d_pos.data_ptr(), n, res.data_ptr(), s) == 0
                 torch.cuda.synchronize()
                 got = _res(res)
                 orc, oe, _, of = O.decode_batch_slice_with(r, 0)
                 assert got.error.kind == orc and got.error.astuple() == oe.astuple(), (bits, got.error.astuple())
                 if orc == 0:
-                    assert np.array_equal(d_pos.cpu().numpy().astype(np.uint64), of)
+                    assert np.array_equal(to_host(d_pos).astype(np.uint64), of)
         L.iggy_codec_debug_set(cx.handle, 0)
     finally:
         cx.close()
