@@ -35,6 +35,11 @@ constexpr uint32_t kDiagMask = 0u;
 constexpr uint32_t kStatusDone = 0;
 constexpr uint32_t kStatusNeedGeneral = 1;
 constexpr uint32_t kStatusPending = 2;
+// words of the decode's misc scratch (DecodeScratch::gmisc == GeneralScratch::misc): the
+// stride and count of the frame positions a lane-group uniform decode leaves to
+// k_decode_general (decode_uniform.hip kPosEpilogue); the count is re-armed (zeroed) by
+// every uniform launch
+constexpr uint32_t kPosStrideWord = 8, kPosCountWord = 9;
 
 // Wave-uniform header parse shared by every role of every decode kernel.
 struct HeaderInfo {

@@ -1079,6 +1079,15 @@ __global__ __launch_bounds__(kGenThreads) void k_decode_general(const uint8_t *_
         __hip_atomic_store(gs.u_first_bad, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(gs.u_spec_fail, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
+    // positions of a record the uniform kernel decoded by lane groups (kPosEpilogue):
+    // frame i at i * S, one 8-B store per thread and pass, the whole grid
+    const uint64_t npos = __hip_atomic_load(&gs.misc[kPosCountWord], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (npos) {
+        const uint64_t S = __hip_atomic_load(&gs.misc[kPosStrideWord], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const uint64_t nth = (uint64_t)gridDim.x * blockDim.x;
+        for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < npos; i += nth) frame_pos[i] = i * S;
+        return;
+    }
     if (__hip_atomic_load(&result->status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) !=
         kStatusNeedGeneral)
         return;

@@ -54,7 +54,8 @@ struct DecodeScratch {
                           // have no frame (past N or the caller's capacity) land here
     uint32_t *gbar2;      // the general kernel's two-level barrier counters (kBar2Words, 128-B stride)
     uint32_t *gbar;       // the general kernel's barrier / registration words and its
-    uint64_t *gmisc;      // first-bad slot: re-armed here (see k_decode_general)
+    uint64_t *gmisc;      // first-bad slot: re-armed here (see k_decode_general); [8] stride and
+                          // [9] count of the frame positions k_decode_general writes (kPosEpilogue)
     uint64_t max_chunks;
 };
 
@@ -821,6 +822,10 @@ constexpr int kDppRowRor8 = 0x128;  // row_ror:8: lane r of a 16-lane row <- lan
 // trips stalled the wave, alone on its SIMD, between its ring waits). The count add is
 // not ordered behind the sum adds by a wait: DS instructions of one wave execute in
 // issue order, and the publisher reads the sums after it has seen the count.
+#ifndef IGGY_LG_FLUSH_PER_BLOCK
+#define IGGY_LG_FLUSH_PER_BLOCK 0  // (build knob for a same-box A/B: 1 = one LDS flush per wave and block)
+#endif
+constexpr bool kLgFlushPerBlock = IGGY_LG_FLUSH_PER_BLOCK != 0;
 __device__ __forceinline__ void lg_words(uint8_t *smem, const LgPlan &pl, const LgLane &c, uint64_t b, uint64_t j,
                                          uint32_t wave, int lane, const LgState &st, uint64_t t_start,
                                          uint64_t &wacc, uint32_t &wfirst) {
@@ -839,7 +844,7 @@ __device__ __forceinline__ void lg_words(uint8_t *smem, const LgPlan &pl, const 
     }
     wacc += x + dpp64<kDppRowRor8>(y);  // lane 8 fg: acc[fg] (x of word fg, y of word fg ^ 1)
     if (q == 0) wfirst = (uint32_t)st.stored;  // (wave 0, lane 0: frame t = 0 of the block)
-    if (q != 3) return;
+    if (kLgFlushPerBlock && q != 3) return;
     const uint32_t s = (uint32_t)(jb % kBsSlots), gen = (uint32_t)(jb / kBsSlots);
     while (__hip_atomic_load(&bs_gen(smem)[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != gen) {
         __builtin_amdgcn_s_sleep(1);
@@ -847,8 +852,8 @@ __device__ __forceinline__ void lg_words(uint8_t *smem, const LgPlan &pl, const 
     }
     if (c.l == 0) {
         __hip_atomic_fetch_add(&bs_acc(smem, s)[c.fg], wacc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        if (wave == 0 && c.fg == 0) bs_spare(smem, s)[0] = wfirst;                       // frame t = 0: lo32
-        if (wave == 3 && c.fg == 7) bs_spare(smem, s)[1] = (uint32_t)(st.stored >> 32);  // frame t = 127: hi32
+        if (wave == 0 && c.fg == 0 && (kLgFlushPerBlock || q == 0)) bs_spare(smem, s)[0] = wfirst;  // frame t = 0: lo32
+        if (wave == 3 && c.fg == 7 && q == 3) bs_spare(smem, s)[1] = (uint32_t)(st.stored >> 32);  // t = 127: hi32
     }
     asm volatile("" ::: "memory");  // (compiler order only: the DS adds above issue first)
     if (lane == 0) __hip_atomic_fetch_add(&bs_cnt(smem)[s], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -865,7 +870,8 @@ __device__ __forceinline__ void lg_publisher(uint8_t *smem, const LgPlan &pl, co
     const uint64_t mine = (blocks - g + np - 1) / np;
     for (uint64_t jb = 0; jb < mine; ++jb) {
         const uint32_t s = (uint32_t)(jb % kBsSlots), gen = (uint32_t)(jb / kBsSlots);
-        while (__hip_atomic_load(&bs_cnt(smem)[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != 4u) {
+        while (__hip_atomic_load(&bs_cnt(smem)[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) !=
+               (kLgFlushPerBlock ? 4u : 16u)) {
             __builtin_amdgcn_s_sleep(1);
             if (rt_now() - t_start > kSpinLimitTicks) return;  // bug guard
         }
@@ -1132,7 +1138,7 @@ template <bool VERIFY>
 __device__ __forceinline__ void consumer(const uint8_t *body, const HeaderInfo &hi, const UPlan &pl,
                                          iggy_decode_result *result, const DecodeScratch &sc,
                                          uint32_t epoch, uint32_t nwaves_prod, uint32_t wave,
-                                         uint8_t *smem, uint32_t dbg) {
+                                         uint8_t *smem, uint32_t dbg, uint64_t pos_epilogue_cap) {
     const int lane = threadIdx.x & 63;
     const uint8_t *blob = body + kHdr;
 
@@ -1354,6 +1360,13 @@ __device__ __forceinline__ void consumer(const uint8_t *body, const HeaderInfo &
         a = hi.h.batch_checksum; b = computed; c = hi.h.base_offset;
     }
     write_result(result, hi, kind, reason, a, b, c, nframes, computed, 1, status, nframes * pl.S);
+    // frame positions the producers left to k_decode_general (kPosEpilogue): the walked
+    // frames' (entries past frame_count are unspecified, include/iggy_codec.h)
+    const uint64_t npos = nframes < pos_epilogue_cap ? nframes : pos_epilogue_cap;
+    if (status == kStatusDone && npos) {
+        __hip_atomic_store(&sc.gmisc[kPosStrideWord], pl.S, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&sc.gmisc[kPosCountWord], npos, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
     // re-arm the scratch for the next call on this stream
     __hip_atomic_store(sc.exited, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __hip_atomic_store(sc.first_bad, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1361,6 +1374,17 @@ __device__ __forceinline__ void consumer(const uint8_t *body, const HeaderInfo &
 }
 
 // ------------------------------------------------------------- kernel
+// Frame positions of a lane-group decode: written by the next kernel of the same decode
+// (k_decode_general, which every decode launches and which otherwise returns at once
+// when the uniform kernel finished the record), i * S for the walked frames, with the
+// whole chip. Stored from the producer waves (8 B per frame, 8 lanes per step) they
+// cost ~17 us of a C2 decode's producer phase: a store behind a step's ring loads
+// lengthens the constant-vmcnt wait of the steps after it (same box, chain off:
+// 0.211 -> 0.194 ms without them, scripts/diag_decode.py DIAG_NOPOS).
+#ifndef IGGY_POS_EPILOGUE
+#define IGGY_POS_EPILOGUE 1  // (build knob for a same-box A/B: 0 = producers store positions)
+#endif
+constexpr bool kPosEpilogue = IGGY_POS_EPILOGUE != 0;
 template <bool VERIFY>
 __device__ __forceinline__ bool uniform_uses_lg(const UPlan &pl, uint32_t dbg) {
     return VERIFY && pl.state == 0 && pl.long_frames && !(dbg & 32);  // dbg bit 32: force the LDS form
@@ -1388,6 +1412,7 @@ __global__ __launch_bounds__(kUniformThreads, 1) void k_decode_uniform(const uin
         __hip_atomic_store(&sc.gbar[2], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(&sc.gbar[3], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(&sc.gmisc[2], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&sc.gmisc[kPosCountWord], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     if (blockIdx.x == 0 && threadIdx.x < kBar2Words)
         __hip_atomic_store(&sc.gbar2[32 * threadIdx.x], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1398,8 +1423,10 @@ __global__ __launch_bounds__(kUniformThreads, 1) void k_decode_uniform(const uin
     const bool lg = uniform_uses_lg<VERIFY>(pl, dbg);
     if (lg) pl.tail_unsafe = false;  // every lane-group load stays inside its frame
     const uint32_t nprod = gridDim.x - 1;
+    // lane-group decodes leave the frame positions to k_decode_general (kPosEpilogue)
+    const uint64_t pos_epi = (kPosEpilogue && lg && frame_pos) ? cap : 0;
     if (blockIdx.x == 0) {
-        consumer<VERIFY>(body, hi, pl, result, sc, epoch, 4 * nprod, wave, smem, dbg);
+        consumer<VERIFY>(body, hi, pl, result, sc, epoch, 4 * nprod, wave, smem, dbg, pos_epi);
         return;
     }
     if (pl.state != 0) return;
@@ -1417,10 +1444,11 @@ __global__ __launch_bounds__(kUniformThreads, 1) void k_decode_uniform(const uin
             lg_publisher(smem, lp, sc, epoch, g, nprod, lane, dbg);
             return;
         }
+        uint64_t *fp = kPosEpilogue ? nullptr : frame_pos;
         if (lp.nbF == 1 && lp.ns == 0)
-            produce_lg<kLgSlots, true>(blob, lp, frame_pos, cap, sc, epoch, g, nprod, wave, lane, smem);
+            produce_lg<kLgSlots, true>(blob, lp, fp, cap, sc, epoch, g, nprod, wave, lane, smem);
         else
-            produce_lg<kLgSlots, false>(blob, lp, frame_pos, cap, sc, epoch, g, nprod, wave, lane, smem);
+            produce_lg<kLgSlots, false>(blob, lp, fp, cap, sc, epoch, g, nprod, wave, lane, smem);
         // Exit count: relaxed after this wave's own vmcnt drain. Everything the
         // consumer reads after it (first_bad, spec_fail, errslot, unit sums) was
         // written by device atomics or sc1 stores and is read with sc1 loads, so no

@@ -20,6 +20,7 @@ from iggy_amd import codec as _codec  # noqa: E402
 _codec.use_library(os.environ.get("IGGY_DIAG_LIB", _codec.DIAG_LIB_PATH))  # ablation bits: diagnostic build only
 from iggy_amd.codec import Codec  # noqa: E402
 import bench  # noqa: E402
+from iggy_amd.torch_io import to_host  # noqa: E402
 
 
 def main():
@@ -60,6 +61,8 @@ def main():
         batch = _Rec(ptr.value, L)
         print(f"record at hipMalloc {ptr.value:#x}", flush=True)
     d_pos = torch.empty(n, dtype=torch.int64, device=dev)
+    nopos = bool(os.environ.get("DIAG_NOPOS"))  # no frame-position output (the producers store none)
+    pos_ptr, pos_cap = (None, 0) if nopos else (d_pos.data_ptr(), n)
     d_res = torch.zeros(ctypes.sizeof(abi.DecodeResult), dtype=torch.uint8, device=dev)
     for v, cx in ctxs.items():
         cx.reserve(L)
@@ -70,7 +73,7 @@ def main():
                 if integ == 1 and v != variants[0]:
                     continue
                 for _ in range(2):
-                    rc = cx.decode_device(batch.data_ptr(), L, integ, d_pos.data_ptr(), n, d_res.data_ptr(), stream)
+                    rc = cx.decode_device(batch.data_ptr(), L, integ, pos_ptr, pos_cap, d_res.data_ptr(), stream)
                     assert rc == 0, rc
                 torch.cuda.synchronize()
                 e0 = torch.cuda.Event(enable_timing=True)
@@ -78,12 +81,12 @@ def main():
                 e0.record()
                 d_res.zero_()
                 for _ in range(10):
-                    rc = cx.decode_device(batch.data_ptr(), L, integ, d_pos.data_ptr(), n, d_res.data_ptr(), stream)
+                    rc = cx.decode_device(batch.data_ptr(), L, integ, pos_ptr, pos_cap, d_res.data_ptr(), stream)
                     assert rc == 0, rc
                 e1.record()
                 torch.cuda.synchronize()
                 ms = e0.elapsed_time(e1) / 10
-                r = abi.DecodeResult.from_buffer_copy(d_res.cpu().numpy().tobytes())
+                r = abi.DecodeResult.from_buffer_copy(to_host(d_res).tobytes())
                 print(f"integ={integ} dbg={v} round={rnd} ms={ms:.4f} GiB/s={L/ms/1e-3/2**30:.1f} "
                       f"err={r.error.kind} frames={r.frame_count} path={r.path}", flush=True)
                 if v & 512 and rnd == 2 and integ == 0:  # progress stamps (10 ns ticks) of one more decode
@@ -91,7 +94,7 @@ def main():
                     L_.iggy_codec_debug_clear.argtypes = [ctypes.c_void_p]
                     L_.iggy_codec_debug_read.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64]
                     assert L_.iggy_codec_debug_clear(cx._h) == 0
-                    rc = cx.decode_device(batch.data_ptr(), L, integ, d_pos.data_ptr(), n, d_res.data_ptr(), stream)
+                    rc = cx.decode_device(batch.data_ptr(), L, integ, pos_ptr, pos_cap, d_res.data_ptr(), stream)
                     buf = (ctypes.c_uint64 * 96)()
                     assert L_.iggy_codec_debug_read(cx._h, buf, 768) == 0
                     for gw in range(4):
