@@ -195,6 +195,68 @@ __device__ __forceinline__ uint64_t chain_step(uint64_t y, uint64_t s, uint32_t 
     return t + s;
 }
 
+// A span of 16 * n16 chain steps over block sums staged in LDS (lane j: block k's sum at
+// LDS byte address addr + 64 k), in one asm statement: y = f(y) + S_k per step, f the
+// XXH3 scramble. The split form: the next sum is the 64-bit addend of the mad and the high
+// word's product is added after it, so the multiply of the high word runs beside the
+// mad instead of feeding it; two 8-sum register buffers are refilled by ds_read2_b64 two
+// groups ahead, with constant lgkmcnt waits. The step's own latency is ~12 ns
+// (scripts/lat_micro.hip, sums in registers: 12.3 ns; the compiler's form 15.8), against
+// ~22 ns for the C++ loop over LDS reads that the compiler waited for group by group.
+// Reads run up to 31 blocks past the span (inside the consumer's LDS; never used).
+#ifndef IGGY_CHAIN_ASM
+#define IGGY_CHAIN_ASM 1  // (build knob for a same-box A/B: 0 = the C++ chain loop only)
+#endif
+#define IGGY_CH_STEP(S)                                      \
+    "v_lshrrev_b32 v42, 15, v41\n\t"                         \
+    "v_xor_b32 v43, v41, %[khi]\n\t"                         \
+    "v_bitop3_b32 v42, v40, v42, %[klo] bitop3:0x96\n\t"     \
+    "v_mul_lo_u32 v43, v43, %[pr]\n\t"                       \
+    "v_mad_u64_u32 v[40:41], s[20:21], v42, %[pr], " S "\n\t" \
+    "v_add_u32 v41, v41, v43\n\t"
+__device__ __forceinline__ uint64_t chain_span(uint64_t y, uint32_t addr, uint32_t n16, uint32_t klo, uint32_t khi) {
+    uint32_t cnt = __builtin_amdgcn_readfirstlane(n16);
+    const uint32_t pr = P32_1;
+    asm volatile(
+        "s_waitcnt lgkmcnt(0)\n\t"
+        "ds_read2_b64 v[48:51], %[ad] offset0:0 offset1:8\n\t"
+        "ds_read2_b64 v[52:55], %[ad] offset0:16 offset1:24\n\t"
+        "ds_read2_b64 v[56:59], %[ad] offset0:32 offset1:40\n\t"
+        "ds_read2_b64 v[60:63], %[ad] offset0:48 offset1:56\n\t"
+        "ds_read2_b64 v[64:67], %[ad] offset0:64 offset1:72\n\t"
+        "ds_read2_b64 v[68:71], %[ad] offset0:80 offset1:88\n\t"
+        "ds_read2_b64 v[72:75], %[ad] offset0:96 offset1:104\n\t"
+        "ds_read2_b64 v[76:79], %[ad] offset0:112 offset1:120\n\t"
+        "v_lshl_add_u64 v[40:41], %[y], 0, 0\n\t"
+        "L_chain_%=:\n\t"
+        "s_waitcnt lgkmcnt(4)\n\t"
+        IGGY_CH_STEP("v[48:49]") IGGY_CH_STEP("v[50:51]") IGGY_CH_STEP("v[52:53]") IGGY_CH_STEP("v[54:55]")
+        IGGY_CH_STEP("v[56:57]") IGGY_CH_STEP("v[58:59]") IGGY_CH_STEP("v[60:61]") IGGY_CH_STEP("v[62:63]")
+        "ds_read2_b64 v[48:51], %[ad] offset0:128 offset1:136\n\t"
+        "ds_read2_b64 v[52:55], %[ad] offset0:144 offset1:152\n\t"
+        "ds_read2_b64 v[56:59], %[ad] offset0:160 offset1:168\n\t"
+        "ds_read2_b64 v[60:63], %[ad] offset0:176 offset1:184\n\t"
+        "s_waitcnt lgkmcnt(4)\n\t"
+        IGGY_CH_STEP("v[64:65]") IGGY_CH_STEP("v[66:67]") IGGY_CH_STEP("v[68:69]") IGGY_CH_STEP("v[70:71]")
+        IGGY_CH_STEP("v[72:73]") IGGY_CH_STEP("v[74:75]") IGGY_CH_STEP("v[76:77]") IGGY_CH_STEP("v[78:79]")
+        "ds_read2_b64 v[64:67], %[ad] offset0:192 offset1:200\n\t"
+        "ds_read2_b64 v[68:71], %[ad] offset0:208 offset1:216\n\t"
+        "ds_read2_b64 v[72:75], %[ad] offset0:224 offset1:232\n\t"
+        "ds_read2_b64 v[76:79], %[ad] offset0:240 offset1:248\n\t"
+        "v_add_u32 %[ad], 0x400, %[ad]\n\t"
+        "s_sub_u32 %[cnt], %[cnt], 1\n\t"
+        "s_cmp_lg_u32 %[cnt], 0\n\t"
+        "s_cbranch_scc1 L_chain_%=\n\t"
+        "s_waitcnt lgkmcnt(0)\n\t"
+        "v_lshl_add_u64 %[y], v[40:41], 0, 0\n\t"
+        : [y] "+v"(y), [ad] "+v"(addr), [cnt] "+s"(cnt)
+        : [klo] "v"(klo), [khi] "v"(khi), [pr] "v"(pr)
+        : "memory", "scc", "s20", "s21", "v40", "v41", "v42", "v43", "v48", "v49", "v50", "v51", "v52", "v53",
+          "v54", "v55", "v56", "v57", "v58", "v59", "v60", "v61", "v62", "v63", "v64", "v65", "v66", "v67", "v68",
+          "v69", "v70", "v71", "v72", "v73", "v74", "v75", "v76", "v77", "v78", "v79");
+    return y;
+}
+
 // issue phase p of this wave's 64 frames of chunk c: instruction k moves frames
 // (64/PH)k .. (64/PH)k + 64/PH - 1, PH lanes x 16 B = PH*16 contiguous bytes each
 template <int PH>
@@ -1248,6 +1310,12 @@ __device__ __forceinline__ void consumer(const uint8_t *body, const HeaderInfo &
                 if (k == 0 && (dbg & 512) && lane == 0 && (bi & 7) == 0)
                     dbg_stamp(sc, dbg, bi == 0 ? 1 : 2 + (int)(bi >> 3));
                 if (bi == 0 && k == 0) { y += src[0]; k = 1; }
+                if (IGGY_CHAIN_ASM && k + 16 <= avail) {  // 16-step groups in asm (chain_span)
+                    typedef __attribute__((address_space(3))) const uint64_t lds_u64;
+                    const uint32_t n16 = (avail - k) >> 4;
+                    y = chain_span(y, (uint32_t)(uintptr_t)(lds_u64 *)(src + 8 * k), n16, klo, khi);
+                    k += 16 * n16;
+                }
                 // groups of 16 blocks, the next group's LDS reads in flight during this group
                 if (k + 16 <= avail) {
                     ld16(va, k);
@@ -1374,17 +1442,20 @@ __device__ __forceinline__ void consumer(const uint8_t *body, const HeaderInfo &
 }
 
 // ------------------------------------------------------------- kernel
-// Frame positions of a lane-group decode: written by the next kernel of the same decode
-// (k_decode_general, which every decode launches and which otherwise returns at once
-// when the uniform kernel finished the record), i * S for the walked frames, with the
-// whole chip. Stored from the producer waves (8 B per frame, 8 lanes per step) they
-// cost ~17 us of a C2 decode's producer phase: a store behind a step's ring loads
-// lengthens the constant-vmcnt wait of the steps after it (same box, chain off:
-// 0.211 -> 0.194 ms without them, scripts/diag_decode.py DIAG_NOPOS).
-#ifndef IGGY_POS_EPILOGUE
-#define IGGY_POS_EPILOGUE 1  // (build knob for a same-box A/B: 0 = producers store positions)
+// Frame positions of a lane-group decode (i * S). Stored from the producer waves inside
+// their step loop (8 B per frame, 8 lanes per step) they cost ~17 us of a C2 decode's
+// producer phase: a store behind a step's ring loads lengthens the constant-vmcnt wait
+// of the steps after it (same box, chain off: 0.211 -> 0.194 ms without them,
+// scripts/diag_decode.py DIAG_NOPOS). Mode 2 (default): each producer wave stores a
+// contiguous share of them after its loop (coalesced 512-B wave stores, no ring wait
+// left to lengthen), beside the chain's tail. Mode 1: the next kernel of the decode
+// (k_decode_general, which otherwise returns at once) writes them with the whole chip.
+// Mode 0: the round-4 per-step stores.
+#ifndef IGGY_POS_MODE
+#define IGGY_POS_MODE 2  // (build knob for a same-box A/B)
 #endif
-constexpr bool kPosEpilogue = IGGY_POS_EPILOGUE != 0;
+constexpr bool kPosEpilogue = IGGY_POS_MODE == 1;
+constexpr bool kPosTail = IGGY_POS_MODE == 2;
 template <bool VERIFY>
 __device__ __forceinline__ bool uniform_uses_lg(const UPlan &pl, uint32_t dbg) {
     return VERIFY && pl.state == 0 && pl.long_frames && !(dbg & 32);  // dbg bit 32: force the LDS form
@@ -1444,11 +1515,17 @@ __global__ __launch_bounds__(kUniformThreads, 1) void k_decode_uniform(const uin
             lg_publisher(smem, lp, sc, epoch, g, nprod, lane, dbg);
             return;
         }
-        uint64_t *fp = kPosEpilogue ? nullptr : frame_pos;
+        uint64_t *fp = IGGY_POS_MODE ? nullptr : frame_pos;
         if (lp.nbF == 1 && lp.ns == 0)
             produce_lg<kLgSlots, true>(blob, lp, fp, cap, sc, epoch, g, nprod, wave, lane, smem);
         else
             produce_lg<kLgSlots, false>(blob, lp, fp, cap, sc, epoch, g, nprod, wave, lane, smem);
+        if (kPosTail && frame_pos) {  // this wave's contiguous share of the positions
+            const uint64_t n = pl.N < cap ? pl.N : cap;
+            const uint64_t nw = 4ull * nprod, per = ((n + nw - 1) / nw + 63) & ~63ull;
+            const uint64_t i0 = (4ull * g + wave) * per, i1 = i0 + per < n ? i0 + per : n;
+            for (uint64_t i = i0 + (uint64_t)lane; i < i1; i += 64) frame_pos[i] = i * pl.S;
+        }
         // Exit count: relaxed after this wave's own vmcnt drain. Everything the
         // consumer reads after it (first_bad, spec_fail, errslot, unit sums) was
         // written by device atomics or sc1 stores and is read with sc1 loads, so no

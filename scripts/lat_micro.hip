@@ -135,6 +135,75 @@ __global__ void c_v1(const uint64_t *sums, uint64_t nb, const uint64_t *keys, ui
 CHAIN_KERNEL(c_split, SPLIT, , )
 CHAIN_KERNEL(c_split24, SPLIT24, , )
 
+
+// ---- chain steps fed from registers (16 sums cycled: the step's own latency, no load)
+__device__ __forceinline__ uint64_t regsum(int k, int j) { return 0x9E3779B97F4A7C15ull * (uint64_t)(16 * j + k + 1); }
+__global__ void r_v1(uint64_t nb, const uint64_t *keys, uint64_t *out) {
+    const int j = threadIdx.x & 7;
+    const uint64_t key = keys[j];
+    const uint32_t klo = (uint32_t)key, khi = (uint32_t)(key >> 32);
+    uint64_t v[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) { v[k] = regsum(k, j); asm volatile("" : "+v"(v[k])); }
+    uint64_t y = 0x1234 + j + v[0];
+    for (uint64_t b = 0; b < nb; b += 16) {
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            const uint32_t hi = (uint32_t)(y >> 32);
+            const uint32_t lo = (uint32_t)y ^ (hi >> 15) ^ klo;
+            const uint32_t h2 = hi ^ khi;
+            uint64_t t = (uint64_t)lo * P + ((uint64_t)(h2 * P) << 32);
+            asm volatile("" : "+v"(t));
+            y = t + v[(k + 1) & 15];
+        }
+    }
+    out[threadIdx.x] = y;
+}
+#define RCHAIN_KERNEL(NAME, STEP)                                                                              \
+    __global__ void NAME(uint64_t nb, const uint64_t *keys, uint64_t *out) {                                   \
+        const int j = threadIdx.x & 7;                                                                         \
+        const uint64_t key = keys[j];                                                                          \
+        const uint32_t klo = (uint32_t)key, khi = (uint32_t)(key >> 32);                                     \
+        const uint32_t pl = P & 0xffff, ph = P >> 16;                                                          \
+        uint64_t v[16];                                                                                        \
+        _Pragma("unroll") for (int k = 0; k < 16; ++k) { v[k] = regsum(k, j); asm volatile("" : "+v"(v[k])); } \
+        uint64_t y = 0x1234 + j + v[0];                                                                        \
+        for (uint64_t b = 0; b < nb; b += 16) {                                                                \
+            asm volatile("v_lshl_add_u64 v[40:41], %0, 0, 0\n\t" STEP("%7") STEP("%8") STEP("%9") STEP("%10") \
+                         STEP("%11") STEP("%12") STEP("%13") STEP("%14") STEP("%15") STEP("%16") STEP("%17")   \
+                         STEP("%18") STEP("%19") STEP("%20") STEP("%21") STEP("%6")                            \
+                         "v_lshl_add_u64 %0, v[40:41], 0, 0\n\t"                                               \
+                         : "+v"(y)                                                                             \
+                         : "v"(klo), "v"(khi), "v"(P), "v"(pl), "v"(ph), "v"(v[0]), "v"(v[1]), "v"(v[2]),      \
+                           "v"(v[3]), "v"(v[4]), "v"(v[5]), "v"(v[6]), "v"(v[7]), "v"(v[8]), "v"(v[9]),        \
+                           "v"(v[10]), "v"(v[11]), "v"(v[12]), "v"(v[13]), "v"(v[14]), "v"(v[15])              \
+                         : "s20", "s21", "v40", "v41", "v42", "v43", "v44", "v45", "v46");                     \
+        }                                                                                                      \
+        out[threadIdx.x] = y;                                                                                  \
+    }
+// the product form as the compiler emits it: y = mad(lo', P, {0, h2 * P}) + s
+#define V1ASM(VK)                                       \
+    "v_lshrrev_b32 v42, 15, v41\n\t"                    \
+    "v_xor_b32 v43, v41, %2\n\t"                        \
+    "v_bitop3_b32 v42, v40, v42, %1 bitop3:0x96\n\t"    \
+    "v_mul_lo_u32 v45, v43, %3\n\t"                     \
+    "v_mov_b32 v44, 0\n\t"                              \
+    "v_mad_u64_u32 v[40:41], s[20:21], v42, %3, v[44:45]\n\t" \
+    "v_lshl_add_u64 v[40:41], v[40:41], 0, " VK "\n\t"
+RCHAIN_KERNEL(r_split, SPLIT)
+RCHAIN_KERNEL(r_split24, SPLIT24)
+RCHAIN_KERNEL(r_v1asm, V1ASM)
+static uint64_t host_ref_reg(uint64_t nb, const uint64_t *keys, int j) {
+    uint64_t acc = 0x1234 + j;
+    for (uint64_t b = 0; b < nb; ++b) {
+        uint64_t x = acc + 0x9E3779B97F4A7C15ull * (uint64_t)(16 * j + (b & 15) + 1);
+        x ^= x >> 47;
+        x ^= keys[j];
+        acc = x * P;
+    }
+    return acc + 0x9E3779B97F4A7C15ull * (uint64_t)(16 * j + 1);  // y after the last step adds v[0] again
+}
+
 static uint64_t host_ref(const std::vector<uint64_t> &s, uint64_t nb, const uint64_t *keys, int j) {
     uint64_t acc = 0x1234 + j;
     for (uint64_t b = 0; b < nb; ++b) {
@@ -202,6 +271,19 @@ int main() {
             bool ok = true;
             // y after the last block is acc_nb (the "next sum" after the last block is 0)
             for (int j = 0; j < 8; ++j) ok &= o[j] == host_ref(hs, nb, keys, j);
+            printf("%-40s %.1f ns/step ok=%d\n", c.n, ms * 1e6 / nb, ok);
+        }
+    struct { const char *n; void (*k)(uint64_t, const uint64_t *, uint64_t *); } rs[] = {
+        {"reg-fed v1 (product form, compiler)", r_v1}, {"reg-fed v1 asm", r_v1asm},
+        {"reg-fed split", r_split}, {"reg-fed split24", r_split24}};
+    for (int rep = 0; rep < 2; ++rep)
+        for (auto &c : rs) {
+            hipMemset(dout, 0, 512);
+            const float ms = timeit(c.k, nb, (const uint64_t *)dk, dout);
+            uint64_t o[64];
+            hipMemcpy(o, dout, 512, hipMemcpyDeviceToHost);
+            bool ok = true;
+            for (int j = 0; j < 8; ++j) ok &= o[j] == host_ref_reg(nb, keys, j);
             printf("%-40s %.1f ns/step ok=%d\n", c.n, ms * 1e6 / nb, ok);
         }
     return 0;
