@@ -140,12 +140,21 @@ __device__ __forceinline__ void glds16(const void *gsrc, uint32_t lds_addr, bool
 }
 // gsrc + OFF -> lds_addr. The instruction offset is added to the LDS address too
 // (LDS_ADDR = M0 + inst_offset + 16 * lane), so M0 gets lds_addr - OFF.
+// (IGGY_LG_NT: the non-temporal policy on these loads, a build knob for a same-box A/B)
+#ifndef IGGY_LG_NT
+#define IGGY_LG_NT 0
+#endif
+#if IGGY_LG_NT
+#define IGGY_LG_NT_SUFFIX " nt"
+#else
+#define IGGY_LG_NT_SUFFIX ""
+#endif
 template <int OFF>
 __device__ __forceinline__ void glds16o(const void *gsrc, uint32_t lds_addr) {
     asm volatile(
         "s_mov_b32 m0, %1\n\t"
         "s_nop 0\n\t"
-        "global_load_lds_dwordx4 %0, off offset:%2"
+        "global_load_lds_dwordx4 %0, off offset:%2" IGGY_LG_NT_SUFFIX
         :
         : "v"(gsrc), "s"(__builtin_amdgcn_readfirstlane(lds_addr - OFF)), "i"(OFF)
         : "memory", "m0");

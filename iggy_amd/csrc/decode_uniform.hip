@@ -885,7 +885,7 @@ constexpr int kDppRowRor8 = 0x128;  // row_ror:8: lane r of a 16-lane row <- lan
 // not ordered behind the sum adds by a wait: DS instructions of one wave execute in
 // issue order, and the publisher reads the sums after it has seen the count.
 #ifndef IGGY_LG_FLUSH_PER_BLOCK
-#define IGGY_LG_FLUSH_PER_BLOCK 0  // (build knob for a same-box A/B: 1 = one LDS flush per wave and block)
+#define IGGY_LG_FLUSH_PER_BLOCK 1  // (build knob for a same-box A/B: 0 = one LDS flush per step)
 #endif
 constexpr bool kLgFlushPerBlock = IGGY_LG_FLUSH_PER_BLOCK != 0;
 __device__ __forceinline__ void lg_words(uint8_t *smem, const LgPlan &pl, const LgLane &c, uint64_t b, uint64_t j,
