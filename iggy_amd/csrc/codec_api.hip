@@ -24,6 +24,10 @@
 #ifndef IGGY_ENC_RING
 #define IGGY_ENC_RING 1  // (build knob for same-box A/B: 0 = k_enc_lanes for segmented encodes too)
 #endif
+#ifndef IGGY_ENC_SPLIT
+#define IGGY_ENC_SPLIT 0  // (build knob for same-box A/B: 1 = copier waves in k_enc_ring; measured
+                          //  2.51-2.71 ms against 1.36 ms without, encode.hip)
+#endif
 #include "batch_checksum.hip"
 #include "decode_general.hip"
 #include "decode_uniform.hip"
@@ -965,7 +969,9 @@ int iggy_codec_create(int device, iggy_codec_ctx **out) {
                                 hipFuncAttributeMaxDynamicSharedMemorySize, kUniformLds) != hipSuccess ||
             hipFuncSetAttribute((const void *)k_decode_general<true>,
                                 hipFuncAttributeMaxDynamicSharedMemorySize, kGenLds) != hipSuccess ||
-            hipFuncSetAttribute((const void *)k_enc_ring,
+            hipFuncSetAttribute((const void *)k_enc_ring<false>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, kErLds) != hipSuccess ||
+            hipFuncSetAttribute((const void *)k_enc_ring<true>,
                                 hipFuncAttributeMaxDynamicSharedMemorySize, kErLds) != hipSuccess)
             r = IGGY_ERR_DEVICE;
     }
@@ -1650,6 +1656,9 @@ static int enqueue_encode(iggy_codec_ctx *c, const iggy_raw_messages *dm, uint64
         // checksum words. Unsegmented, the one k_enc_lanes launch hashes them after its
         // loop and runs the < 16-B payload-area fallback itself (own_tail).
         const bool ring = segmented && IGGY_ENC_RING;
+        // copier waves beside the hashers (k_enc_ring<true>) when every frame's payload
+        // keeps its source offset mod 16 in the output (P - out = 0 mod 16, encode.hip)
+        const bool split = IGGY_ENC_SPLIT && ((((uintptr_t)m.payloads) - (uintptr_t)d_out) & 15) == 0;
         if (ring) {
             if (c->erec.ensure((n + 1) * 32) || c->esink.ensure(kErSinkBytes)) return IGGY_ERR_DEVICE;
             hipLaunchKernelGGL(k_enc_recs, dim3((uint32_t)std::min<uint64_t>((n + 256) / 256, (uint64_t)c->ncu * 8)),
@@ -1684,8 +1693,12 @@ static int enqueue_encode(iggy_codec_ctx *c, const iggy_raw_messages *dm, uint64
             const uint64_t B0 = bound(k), B1 = bound(k + 1);
             const uint64_t F0 = k == 0 ? 0 : std::min<uint64_t>(n, 128 * B0 - 5);
             const uint64_t F1 = k == nseg - 1 ? n : std::min<uint64_t>(n, 128 * B1 - 5);
-            if (ring)
-                hipLaunchKernelGGL(k_enc_ring, dim3((uint32_t)std::min<uint64_t>((n + 63) / 64, lcu)),
+            if (ring && split)
+                hipLaunchKernelGGL(k_enc_ring<true>, dim3((uint32_t)std::min<uint64_t>((n + 63) / 64, lcu)),
+                                   dim3(2 * kErThreads), kErLds, s, m, es, d_out, F0, F1,
+                                   (const uint4 *)c->erec.as<uint4>(), c->esink.as<uint8_t>());
+            else if (ring)
+                hipLaunchKernelGGL(k_enc_ring<false>, dim3((uint32_t)std::min<uint64_t>((n + 63) / 64, lcu)),
                                    dim3(kErThreads), kErLds, s, m, es, d_out, F0, F1,
                                    (const uint4 *)c->erec.as<uint4>(), c->esink.as<uint8_t>());
             else if (segmented)

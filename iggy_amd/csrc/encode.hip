@@ -689,9 +689,106 @@ __global__ __launch_bounds__(256) void k_enc_recs(iggy_raw_messages m, EncScratc
     }
 }
 
-__global__ __launch_bounds__(kErThreads, 1) void k_enc_ring(iggy_raw_messages m, EncScratch es, uint8_t *out,
-                                                            uint64_t f_lo, uint64_t f_hi, const uint4 *erec,
-                                                            uint8_t *sink) {
+// ---- copier waves (SPLIT form): the hasher waves above store no payload bytes.
+// A SPLIT workgroup has kErWaves copier waves beside its kErWaves hashers; copier
+// wave kErWaves + w copies the payloads of hasher w's frames (same frame order) from
+// the input to the output, 16-B chunks, without any hand-off: a frame's record (erec,
+// k_enc_recs) gives its payload offset and length. The payload is read twice, by the
+// hasher's LDS-DMA and by the copier, in the same order and close in time, so the
+// second read mostly hits L2 or MALL (the profile's FETCH_SIZE says how much).
+// An earlier form passed the hasher's landed LDS slots to a writer wave with LDS flags.
+// Near the end of a wave's frames its writer's global stores stalled for as long as
+// the hasher spun on the writer's flag, and were released the moment the hasher
+// stopped spinning: the 4-s bug guard tripped and the encode failed. Store-free writers
+// never stalled, and no flag form (DS or FLAT, sleep or not, drained DMA, another SIMD)
+// helped; independent copiers need no flag at all. They are correct but slower: same
+// box, C3 encode 2.51 / 2.59 / 2.71 ms (16-B chunks in flight per lane 32 / 16 / 8)
+// against 1.36 ms for the hashers storing the payload themselves, so the host builds
+// without them (IGGY_ENC_SPLIT 0, codec_api.hip).
+// With payloads and output 16-B congruent (P - out = 0 mod 16: 48-B frame headers keep
+// every payload at the same offset mod 16 from its source; the host launches the SPLIT
+// form only then), each chunk is one aligned 16-B load and store, except the two that
+// straddle the payload's ends (aligned 8/4/2/1-B pieces).
+typedef __attribute__((address_space(1))) uint8_t g_u8;
+typedef __attribute__((address_space(1))) uint16_t g_u16;
+typedef __attribute__((address_space(1))) uint32_t g_u32;
+typedef __attribute__((address_space(1))) uint64_t g_u64;
+typedef unsigned int es_u32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(1))) es_u32x4 g_u128;
+
+// bytes [x0, x1) of the 16-B value v to the 16-B-aligned address d: aligned 8/4/2/1-B pieces
+__device__ inline void es_store_range(g_u8 *d, es_u32x4 v, uint32_t x0, uint32_t x1) {
+    while (x0 < x1) {
+        const uint32_t dw = x0 >> 2;
+        const uint32_t w = dw == 0 ? v.x : dw == 1 ? v.y : dw == 2 ? v.z : v.w;
+        if ((x0 & 7) == 0 && x0 + 8 <= x1) {
+            const uint32_t w2 = dw == 0 ? v.y : v.w;
+            *(g_u64 *)(d + x0) = (uint64_t)w | ((uint64_t)w2 << 32);
+            x0 += 8;
+        } else if ((x0 & 3) == 0 && x0 + 4 <= x1) {
+            *(g_u32 *)(d + x0) = w;
+            x0 += 4;
+        } else if ((x0 & 1) == 0 && x0 + 2 <= x1) {
+            *(g_u16 *)(d + x0) = (uint16_t)(w >> (8 * (x0 & 3)));
+            x0 += 2;
+        } else {
+            d[x0] = (uint8_t)(w >> (8 * (x0 & 3)));
+            x0 += 1;
+        }
+    }
+}
+
+// the payloads of frames f_lo + 8 vw + fg + j stride (j = 0, 1, ...; < n): lane l of
+// frame group fg copies chunks l, l + 8, ... of its frame, kEcUnroll per pass
+#ifndef IGGY_EC_UNROLL
+#define IGGY_EC_UNROLL 16  // (build knob: chunks in flight per lane)
+#endif
+constexpr uint32_t kEcUnroll = IGGY_EC_UNROLL;
+__device__ __forceinline__ void enc_ring_copier(const uint8_t *P, uint8_t *out, const uint4 *erec, uint64_t f_lo,
+                                                uint64_t n, uint64_t vw, uint64_t nvw, int lane) {
+    const uint32_t l = lane & 7, fg = (uint32_t)lane >> 3;
+    const uint64_t stride = 8 * nvw;
+    for (uint64_t f = f_lo + 8 * vw + fg;; f += stride) {
+        const bool v = f < n;
+        if (!__ballot(v)) break;
+        uint64_t po = 0;
+        uint32_t pl = 0;
+        if (v) {
+            const uint4 rec = erec[2 * f];
+            po = (uint64_t)rec.x | ((uint64_t)rec.y << 32);
+            pl = rec.z;
+        }
+        const uint64_t s0 = (uint64_t)(uintptr_t)(P + po), s1 = s0 + pl, a0 = s0 & ~15ull;
+        // destination of source byte s: s + delta (frame payload at out + 256 + 48 (f + 1) + po)
+        const uint64_t delta = (uint64_t)(uintptr_t)(out + 304 + 48 * f) - (uint64_t)(uintptr_t)P;
+        const uint32_t nch = v && pl ? (uint32_t)((s1 + 15 - a0) >> 4) : 0u;
+        for (uint32_t c = l; c < nch; c += 8 * kEcUnroll) {
+            es_u32x4 d[kEcUnroll];
+#pragma unroll
+            for (uint32_t u = 0; u < kEcUnroll; ++u) {
+                const uint32_t cc = c + 8 * u;
+                if (cc < nch) d[u] = *(const g_u128 *)(uintptr_t)(a0 + 16ull * cc);
+            }
+#pragma unroll
+            for (uint32_t u = 0; u < kEcUnroll; ++u) {
+                const uint32_t cc = c + 8 * u;
+                if (cc >= nch) break;
+                const uint64_t sc = a0 + 16ull * cc;
+                const uint32_t x0 = sc < s0 ? (uint32_t)(s0 - sc) : 0u;
+                const uint32_t x1 = sc + 16 > s1 ? (uint32_t)(s1 - sc) : 16u;
+                g_u8 *dd = (g_u8 *)(uintptr_t)(sc + delta);
+                if (x0 == 0 && x1 == 16) *(g_u128 *)dd = d[u];
+                else es_store_range(dd, d[u], x0, x1);
+            }
+        }
+    }
+}
+
+template <bool SPLIT>
+__global__ __launch_bounds__(SPLIT ? 2 * kErThreads : kErThreads, 1) void k_enc_ring(iggy_raw_messages m, EncScratch es,
+                                                                                uint8_t *out, uint64_t f_lo, uint64_t f_hi,
+                                                                                const uint4 *erec, uint8_t *sink) {
+    constexpr uint32_t S = kErSlots;  // ring slots per hasher wave
     const uint64_t ptot = es.misc[4];
     if (ptot < 16 || es.misc[5]) return;  // tiny payload area (k_enc_frames) or over capacity
     const uint64_t N = m.count;           // erec[2 N]: the "no frame" record
@@ -701,6 +798,11 @@ __global__ __launch_bounds__(kErThreads, 1) void k_enc_ring(iggy_raw_messages m,
     const uint32_t lbase = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(lds_u8 *)smem);
     const int lane = threadIdx.x & 63;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    if (SPLIT && wave >= kErWaves) {  // the copier of hasher wave - kErWaves
+        enc_ring_copier(m.payloads, out, erec, f_lo, n, (uint64_t)blockIdx.x * kErWaves + (wave - kErWaves),
+                        (uint64_t)gridDim.x * kErWaves, lane);
+        return;
+    }
     const uint32_t l = lane & 7, m8 = l >> 1, par = l & 1, fg = (uint32_t)lane >> 3;
     const uint32_t poff = 16 * (m8 + 4 * par);
     const uint64_t vw = (uint64_t)blockIdx.x * kErWaves + wave, nvw = (uint64_t)gridDim.x * kErWaves;
@@ -731,7 +833,7 @@ __global__ __launch_bounds__(kErThreads, 1) void k_enc_ring(iggy_raw_messages m,
         const uint64_t f = fbase + j * stride;
         return f < n ? f : N;
     };
-    const uint32_t meta = region + kErSlots * kErStep + 144 * fg;  // the group's record ring
+    const uint32_t meta = region + S * kErStep + 144 * fg;  // the group's record ring
 #pragma unroll
     for (uint32_t k = 0; k < 4; ++k)
         if (l == k) *(uint4 *)(smem + meta + 16 * k) = erec[2 * fidx(k)];
@@ -787,8 +889,9 @@ __global__ __launch_bounds__(kErThreads, 1) void k_enc_ring(iggy_raw_messages m,
     uint32_t o5[5] = {0, 0, 0, 0, 0};
     uint64_t a0 = init0, a1 = init1, id0 = 0, id1 = 0;
     uint4 lastp = make_uint4(0, 0, 0, 0);
-    for (uint32_t k = 0; k < kErSlots; ++k) issue(region + k * kErStep);
-    for (uint32_t k = 0;; ++k) {
+    for (uint32_t k = 0; k < S; ++k) issue(region + k * kErStep);
+    uint32_t k = 0;
+    for (;; ++k) {
         if (pb == 0) {
             const uint4 rec = *(const uint4 *)(smem + meta + 16 * (pj & 7));
             p_f = fidx(pj);
@@ -815,9 +918,9 @@ __global__ __launch_bounds__(kErThreads, 1) void k_enc_ring(iggy_raw_messages m,
         // step k landed. Issued after its loads: the stores of the kErSlots steps
         // before it and the loads of the later steps -- except in the first kErSlots
         // iterations, which wait for everything.
-        if (k < kErSlots) wait_vm_const<0>();
+        if (k < S) wait_vm_const<0>();
         else wait_vm_const<9 * (kErSlots - 1) + kErStores * kErSlots>();
-        const uint32_t slot = region + (k % kErSlots) * kErStep;
+        const uint32_t slot = region + (k % S) * kErStep;
         const uint8_t *row = smem + slot + 128 * fg;
         uint4 pc[8];
 #pragma unroll
@@ -865,7 +968,9 @@ __global__ __launch_bounds__(kErThreads, 1) void k_enc_ring(iggy_raw_messages m,
                 w1 = (h && poff <= 32) ? n1 : w1;
             }
             const bool whole = p_valid && sp + 16 <= p_L;
-            if (IGGY_ER_MODE < 2) {
+            if (SPLIT) {
+                // (the writer wave stores the payload; the header words are stored below)
+            } else if (IGGY_ER_MODE < 2) {
                 er_st16(whole ? (void *)(F + 8 + sp) : (void *)my_sink, w0, w1);
             } else if (whole) {
                 st128_any(F + 8 + sp, make_uint4((uint32_t)w0, (uint32_t)(w0 >> 32), (uint32_t)w1, (uint32_t)(w1 >> 32)));
@@ -878,7 +983,16 @@ __global__ __launch_bounds__(kErThreads, 1) void k_enc_ring(iggy_raw_messages m,
             q0[q & 3] += (mul32x32(w0 ^ s0[q]) + w1) & use;
             q1[q & 3] += (mul32x32(w1 ^ s1[q]) + w0) & use;
         }
-        if (IGGY_ER_MODE > 0) {  // the partial piece and the checksum words: plain stores
+        if (SPLIT) {
+            // the frame header at its first block: lanes 0-4 of the group store its five
+            // words (ids, index | timestamp delta, lengths, reserved) at F + 8
+            if (pb == 0 && p_valid && l < 5) {
+                const uint64_t hw = l == 0 ? id0 : l == 1 ? id1
+                                  : l == 2 ? ((p_f & 0xFFFFFFFFull) | ((uint64_t)p_delta << 32))
+                                  : l == 3 ? (p_pl << 32) : 0ull;
+                st64_any(F + 8 + 8 * l, hw);
+            }
+        } else if (IGGY_ER_MODE > 0) {  // the partial piece and the checksum words: plain stores
             if (tsp != ~0ull) {
                 uint8_t *d = F + 8 + tsp;
                 const uint32_t remb = (uint32_t)(p_L - tsp);
@@ -924,7 +1038,10 @@ __global__ __launch_bounds__(kErThreads, 1) void k_enc_ring(iggy_raw_messages m,
         {  // the frame's checksum word and its batch-checksum input (long frames; short
            // ones are k_enc_short's)
             const bool st = fin && lng && l == 0;
-            if (IGGY_ER_MODE > 0) {
+            if (SPLIT) {  // lane 0 the frame's checksum word, lane 2 (the same hash) its copy
+                if (fin && lng && l == 0) st64_any(F, hsh);
+                if (fin && lng && l == 2) es.cs[p_f] = hsh;
+            } else if (IGGY_ER_MODE > 0) {
                 if (st) {
                     st64_any(F, hsh);
                     es.cs[p_f] = hsh;

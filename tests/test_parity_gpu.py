@@ -349,6 +349,41 @@ def test_encode_segmented_matches_oracle(cx, n, lo, hi):
     assert out == oout
 
 
+@pytest.mark.parametrize("pay_shift,out_shift", [(0, 0), (0, 5), (7, 7), (3, 12)])
+def test_encode_segmented_device_alignments(cx, pay_shift, out_shift):
+    """Segmented device encodes with payloads and output at every congruence: the writer-
+    wave ring when P - out = 0 mod 16 (shifts (0, 0) and (7, 7)), the one-role ring
+    otherwise: byte-identical to the oracle either way (encode.hip k_enc_ring)."""
+    import torch
+    from iggy_amd.codec import raw_messages
+    n = 262_144
+    rng = np.random.default_rng(n + pay_shift * 16 + out_shift)
+    pls = rng.integers(100, 1101, size=n).astype(np.uint32)
+    ids, ots, pay, _ = _raw_from_arrays(n, pls, None, rng)
+    raw = raw_messages(ids, ots, pay, pls)
+    orc, oe, oout = O.encode_batch(raw, 6)
+    assert orc == 0
+    d_ids = to_device(ids.view(np.int64))
+    d_ots = to_device(ots.view(np.int64))
+    d_pls = to_device(pls.view(np.int32))
+    d_payb = torch.zeros(pay.size + 64, dtype=torch.uint8, device="cuda")
+    d_payb[pay_shift: pay_shift + pay.size] = to_device(pay)
+    need = len(oout)
+    d_outb = torch.full((need + 64,), 0xCD, dtype=torch.uint8, device="cuda")
+    d_res = torch.zeros(ctypes.sizeof(abi.EncodeResult), dtype=torch.uint8, device="cuda")
+    draw = abi.RawMessages(n, d_ids.data_ptr(), d_ots.data_ptr(), d_payb.data_ptr() + pay_shift, d_pls.data_ptr(),
+                           None, None)
+    s = torch.cuda.current_stream().cuda_stream
+    torch.cuda.synchronize()
+    assert cx.encode_device(draw, 6, d_outb.data_ptr() + out_shift, need, d_res.data_ptr(), s) == 0
+    torch.cuda.synchronize()
+    er = abi.EncodeResult.from_buffer_copy(to_host(d_res).tobytes())
+    assert er.error.kind == 0 and er.batch_length == need
+    got = to_host(d_outb)
+    assert got[out_shift: out_shift + need].tobytes() == oout
+    assert (got[:out_shift] == 0xCD).all() and (got[out_shift + need:] == 0xCD).all()
+
+
 def test_encode_errors(cx):
     from iggy_amd.codec import raw_messages
     rng = np.random.default_rng(1)
