@@ -329,6 +329,30 @@ def c1_leg(cx, dev, seconds: float):
             for t in [cx.decode_submit(r, 0) for r in group]:
                 cx.wait(t)
     host_us = (time.perf_counter() - t0) / (5 * nb) * 1e6
+    # the synchronous host decode (iggy_codec_decode_batch: one k_decode_records launch
+    # and a host-mapped flag), pageable records, then the same records registered
+    # (iggy_codec_host_register: the kernel reads them in place, no H2D)
+    poss = [np.zeros(r.size // 48 + 1, dtype=np.uint64) for r in recs]
+
+    def sync_us(reps=20):
+        for r, p in zip(recs, poss):
+            rc, nf = cx.decode_batch_into(r, abi.INTEGRITY_VERIFY, p)
+            assert rc == 0 and nf == n, (rc, nf)
+        t = time.perf_counter()
+        for _ in range(reps):
+            for r, p in zip(recs, poss):
+                cx.decode_batch_into(r, abi.INTEGRITY_VERIFY, p)
+        return (time.perf_counter() - t) / (reps * nb) * 1e6
+
+    sync_pageable_us = sync_us()
+    for a in recs + poss:
+        cx.host_register(a)
+    try:
+        sync_registered_us = sync_us()
+        assert all(int(p[1]) == 48 + pl for p in poss)
+    finally:
+        for a in recs + poss:
+            cx.host_unregister(a)
     return {
         "workload": "C1 shapes: 10 batches x 1000 msgs x 256 B (iggy-bench over TCP not run: no Rust toolchain)",
         "iggy_bench": None,
@@ -337,6 +361,9 @@ def c1_leg(cx, dev, seconds: float):
         "gpu_device_decode_us_per_batch": round(dev_us, 1),
         "gpu_device_encode_us_per_batch": round(enc_us, 1),
         "gpu_host_roundtrip_us_per_batch": round(host_us, 1),
+        "gpu_host_sync_us_per_batch": round(sync_pageable_us, 1),
+        "gpu_host_sync_registered_us_per_batch": round(sync_registered_us, 1),
+        "cpu_ref_decode_us_per_batch": round(recs[0].size / dec * 1e6, 1),
         "wire_bytes": wire,
     }
 

@@ -259,6 +259,18 @@ class Codec:
         frames = pos[: n.value].copy() if (rc == 0 and want_frames) else None
         return rc, e, h, frames
 
+    def decode_batch_into(self, body: np.ndarray, integrity: int, pos: np.ndarray | None,
+                          h: BatchHeader | None = None, e: WireError | None = None) -> tuple[int, int]:
+        """decode_batch_slice_with into caller arrays (no allocation: latency
+        measurements, registered buffers) -> (rc, frame count)."""
+        h = h if h is not None else BatchHeader()
+        e = e if e is not None else WireError()
+        n = u64(0)
+        rc = self._L.iggy_codec_decode_batch(self._h, body.ctypes.data, body.nbytes, integrity, ctypes.byref(h),
+                                             pos.ctypes.data if pos is not None else None,
+                                             pos.size if pos is not None else 0, ctypes.byref(n), ctypes.byref(e))
+        return rc, n.value
+
     def verify_and_recompute_batch_checksum(self, h: BatchHeader, blob):
         a = _np(blob)
         out = u64(0)

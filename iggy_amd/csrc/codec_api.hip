@@ -605,6 +605,7 @@ int reset_after_timeout(iggy_codec_ctx *c) {
 
 // synchronous decode of a host buffer; also used by stamp / checksum helpers
 constexpr uint64_t kHostFastBytes = 16ull << 20;
+constexpr uint64_t kZeroCopyBytes = 1ull << 20;  // registered inputs up to this size are read in place
 int decode_host_fast(iggy_codec_ctx *c, const uint8_t *body, uint64_t len, int integrity,
                      iggy_decode_result *res_out, uint64_t *frame_pos, uint64_t cap, bool *done);
 int decode_host(iggy_codec_ctx *c, const uint8_t *body, uint64_t len, int integrity,
@@ -898,26 +899,58 @@ int decode_host_fast(iggy_codec_ctx *c, const uint8_t *body, uint64_t len, int i
     *done = false;
     uint64_t nf = 0;
     if (len > kHostFastBytes || !rec_plan(body, len, &nf)) return 0;
+    // (diagnostic build, IGGY_CODEC_TIMING=N: mean stage times of the next N calls)
+    static int timing = kDiagMask && getenv("IGGY_CODEC_TIMING") ? atoi(getenv("IGGY_CODEC_TIMING")) : 0;
+    static double tsum[4] = {0, 0, 0, 0};
+    static int tn = 0;
+    using tclk = std::chrono::steady_clock;
+    const auto tt0 = tclk::now();
+    auto tmark = [&](int k) {
+        if (timing) tsum[k] += std::chrono::duration<double, std::micro>(tclk::now() - tt0).count();
+    };
     const uint64_t pcap = frame_pos ? std::min<uint64_t>(cap, len / 48 + 1) : 0;
-    if (c->din.ensure(len + 16) || c->omap.ensure(64 + 128 + pcap * 8)) return IGGY_ERR_DEVICE;
-    int r = put_host(c, c->din.p, body, len, c->stream);
-    if (r) return r;
+    if (c->omap.ensure(64 + 128 + pcap * 8)) return IGGY_ERR_DEVICE;
+    // a registered (page-locked, device-mapped) record of at most kZeroCopyBytes is read
+    // by the kernel in place over the host link: no H2D, one launch and the flag
+    const uint8_t *d_base = nullptr;
+    if (len <= kZeroCopyBytes && host_pinned(body, len)) {
+        void *dp = nullptr;
+        if (hipHostGetDevicePointer(&dp, (void *)body, 0) == hipSuccess && dp) d_base = (const uint8_t *)dp;
+        else (void)hipGetLastError();
+    }
+    int r = 0;
+    if (!d_base) {
+        if (c->din.ensure(len + 16)) return IGGY_ERR_DEVICE;
+        r = put_host(c, c->din.p, body, len, c->stream);
+        if (r) return r;
+        d_base = c->din.as<uint8_t>();
+    }
+    tmark(0);
     const RecIn rec{0, len, 0, pcap, 0};
     std::vector<size_t> single;
     const uint32_t v = next_flag(c);
-    r = enqueue_records(c, c->din.as<uint8_t>(), body, &rec, 1, integrity,
+    r = enqueue_records(c, d_base, body, &rec, 1, integrity,
                         pcap ? c->omap.dp<uint64_t>(192) : nullptr, nullptr, c->omap.dp<iggy_decode_result>(64),
                         &single, nullptr, c->omap.dp<uint32_t>(), v);
     if (r) return r;
+    tmark(1);
     r = wait_host_flag(c, v);
     if (!r) r = xfer_settle(c);
     if (r) return r;
+    tmark(2);
     const iggy_decode_result res = *c->omap.hp<iggy_decode_result>(64);
     if (res.status == kStatusNeedGeneral) return 0;
     *res_out = res;
     if (frame_pos && pcap && res.error.kind == IGGY_OK)
         memcpy(frame_pos, c->omap.hp<uint64_t>(192), std::min<uint64_t>(res.frame_count, pcap) * 8);
     *done = true;
+    tmark(3);
+    if (timing && ++tn == timing) {
+        fprintf(stderr, "iggy_codec timing (%d calls, us from entry): staged %.2f launched %.2f flag %.2f done %.2f\n",
+                tn, tsum[0] / tn, tsum[1] / tn, tsum[2] / tn, tsum[3] / tn);
+        tn = 0;
+        tsum[0] = tsum[1] = tsum[2] = tsum[3] = 0;
+    }
     return 0;
 }
 

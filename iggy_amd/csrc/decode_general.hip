@@ -1081,16 +1081,17 @@ __global__ __launch_bounds__(kGenThreads) void k_decode_general(const uint8_t *_
     }
     // positions of a record the uniform kernel decoded by lane groups (kPosEpilogue):
     // frame i at i * S, one 8-B store per thread and pass, the whole grid
+    // (both words loaded before either is tested: one memory latency for the common
+    // early exit of a decode the uniform kernel finished, not two)
     const uint64_t npos = __hip_atomic_load(&gs.misc[kPosCountWord], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t ustatus = __hip_atomic_load(&result->status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (npos) {
         const uint64_t S = __hip_atomic_load(&gs.misc[kPosStrideWord], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         const uint64_t nth = (uint64_t)gridDim.x * blockDim.x;
         for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < npos; i += nth) frame_pos[i] = i * S;
         return;
     }
-    if (__hip_atomic_load(&result->status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) !=
-        kStatusNeedGeneral)
-        return;
+    if (ustatus != kStatusNeedGeneral) return;
     const uint64_t t0 = rt_now();
     __shared__ uint32_t s_mem[3];
     // dynamic LDS (kGenLds, Verify only): the verify waves' rings (verify_frames_dma); in

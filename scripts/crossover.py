@@ -24,21 +24,30 @@ from oracle import oracle as O  # noqa: E402  (the CPU leg)
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--integrity", type=int, default=0)
+    ap.add_argument("--registered", action="store_true",
+                    help="register the record and the positions array first (records <= 1 MiB read in place)")
     args = ap.parse_args()
     cx = Codec(0)
     rows = []
     for kib in (64, 256, 1024, 4096, 16384, 65536):
         n = max(1, kib * 1024 // 1072)
         rec = O.synth_batch(n, 1024, 1024, seed=kib)
+        pos = np.zeros(rec.size // 48 + 1, dtype=np.uint64)
+        if args.registered:
+            cx.host_register(rec)
+            cx.host_register(pos)
         for _ in range(3):
-            rc, e, h, fr = cx.decode_batch_slice_with(rec, args.integrity)
-            assert rc == 0, e.astuple()
+            rc, nf = cx.decode_batch_into(rec, args.integrity, pos)
+            assert rc == 0 and nf == n, rc
         ts = []
         for _ in range(15):
             t0 = time.perf_counter()
-            cx.decode_batch_slice_with(rec, args.integrity)
+            cx.decode_batch_into(rec, args.integrity, pos)
             ts.append(time.perf_counter() - t0)
         gpu = float(np.median(ts))
+        if args.registered:
+            cx.host_unregister(pos)
+            cx.host_unregister(rec)
         reps = max(1, int(0.2 / max(rec.size / 3e9, 1e-6)))
         secs, _ = O.cpu_decode_bench(rec, 1, reps)  # one thread walks `reps` copies (Verify)
         cpu = secs / reps
@@ -47,7 +56,8 @@ def main():
         rows.append(row)
         print(json.dumps(row), flush=True)
     cross = next((r["record_bytes"] for r in rows if r["gpu_faster"]), None)
-    print(json.dumps({"crossover_record_bytes": cross, "integrity": args.integrity}), flush=True)
+    print(json.dumps({"crossover_record_bytes": cross, "integrity": args.integrity,
+                      "registered": args.registered}), flush=True)
 
 
 if __name__ == "__main__":

@@ -1,4 +1,3 @@
 set -u
 cd $GRAFT_REPO_ROOT
-rm -f gpurun_out/encab/summary.log
-LIBS="ab/lib_ns.so ab/lib_u8.so ab/lib_u16.so ab/lib_u32.so" bash scripts/gpu_encab.sh && cat gpurun_out/encab/summary.log
+timeout -k 10 200 python -u scripts/c1_timing.py 2>&1 | grep -v amdgpu.ids

@@ -110,3 +110,34 @@ def test_pageable_submit_outputs(cx):
     t = cx.decode_submit(rec, abi.INTEGRITY_VERIFY, short)
     assert cx.wait(t).error.kind == abi.ERR_CAPACITY
     assert (short == 7).all()
+
+
+def test_registered_record_read_in_place(cx):
+    """A registered record of <= 1 MiB is decoded in place (the kernel reads the
+    host-mapped bytes, no H2D): same verdicts as the oracle, at the start of the
+    registered range and at an interior, unaligned offset, clean and corrupted, and a
+    larger registered record (copied as before)."""
+    recs = [O.synth_batch(1000, 256, seed=31), O.synth_batch(700, 100, 900, seed=32),
+            O.synth_batch(1500, 1024, seed=33)]  # the last one is 1.6 MB: not in place
+    bad = recs[0].copy()
+    bad[256 + 48 * 500 + 60] ^= 0x40  # one payload bit of frame 500
+    recs.append(bad)
+    for rec in recs:
+        want = O.decode_batch_slice_with(rec, 0)
+        for off in (0, 4099):
+            buf = np.zeros(off + rec.size + 64, dtype=np.uint8)
+            buf[off:off + rec.size] = rec
+            pos = np.zeros(rec.size // 48 + 1, dtype=np.uint64)
+            cx.host_register(buf)
+            cx.host_register(pos)
+            try:
+                view = buf[off:off + rec.size]
+                assert cx.host_pinned(view.ctypes.data, view.size)
+                h, e = abi.BatchHeader(), abi.WireError()
+                rc, nf = cx.decode_batch_into(view, abi.INTEGRITY_VERIFY, pos, h, e)
+            finally:
+                cx.host_unregister(pos)
+                cx.host_unregister(buf)
+            assert rc == want[0] and e.astuple() == want[1].astuple() and h.astuple() == want[2].astuple()
+            if rc == 0:
+                assert np.array_equal(pos[:nf], np.asarray(want[3], dtype=np.uint64))
