@@ -89,13 +89,19 @@ __device__ __forceinline__ uint64_t wg_min(uint64_t v, uint64_t *s4) {
 // a D2H copy of the results, ~5 us more; scripts/latency_micro.cpp).
 __device__ __forceinline__ void launch_done(uint32_t *counter, uint32_t *host_flag, uint32_t value) {
     if (!host_flag) return;
+#ifndef IGGY_REC_K1
     __threadfence_system();  // every wave: its own host-visible writes (a fence orders only its wave's)
+#endif
     __syncthreads();
     if (threadIdx.x == 0) {
         if (atomicAdd(counter, 1u) == gridDim.x - 1) {
             __hip_atomic_store(counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#ifndef IGGY_REC_K2
             __threadfence_system();
             __hip_atomic_store(host_flag, value, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+#else
+            __hip_atomic_store(host_flag, value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+#endif
         }
     }
 }
@@ -116,10 +122,20 @@ __device__ __forceinline__ void decode_record_block(const uint8_t *__restrict__ 
     const uint8_t *blob = body + kHdr;
     const int lane = threadIdx.x & 63;
     const uint32_t wave = threadIdx.x >> 6;
+    // the batch header and the first frame header (304 B) staged in LDS with one load
+    // round, so the header parse and the plan cost no further memory round trips (each
+    // one is microseconds for a registered record read in place over the host link)
+    __shared__ __attribute__((aligned(16))) uint8_t s_head[kHdr + kFrameHdr];
+    const bool staged = tk.len >= kHdr + kFrameHdr;
+    if (staged) {
+        if (threadIdx.x < (kHdr + kFrameHdr) / 16)
+            *(uint4 *)(s_head + 16 * threadIdx.x) = ld128_any(body + 16 * threadIdx.x);
+        __syncthreads();
+    }
     HeaderInfo hi;
-    parse_header(body, tk.len, hi);
+    parse_header(staged ? s_head : body, tk.len, hi);
     UPlan pl;
-    make_plan(hi, blob, tk.len, VERIFY, ~0ull, true, pl);
+    make_plan(hi, staged ? s_head + kHdr : blob, tk.len, VERIFY, ~0ull, true, pl);
     iggy_decode_result *res = results + t;
 
     if (pl.state != 0 || tk.nwg < rec_blocks(pl.N)) {
@@ -151,6 +167,21 @@ __device__ __forceinline__ void decode_record_block(const uint8_t *__restrict__ 
     const int64_t i0 = (int64_t)kRecFrames * blk - 6;
     const uint64_t base_offset = hi.h.base_offset, base_ts = hi.h.base_timestamp, origin = hi.h.origin_timestamp;
     uint64_t mybad = ~0ull, mysf = ~0ull;
+    // frame 128b + 122's stored checksum (its low half closes word 128b + 127), loaded
+    // beside the frames
+    uint64_t cs_next = 0;
+    if (threadIdx.x == 0) {
+        const int64_t i = i0 + kRecFrames;
+        if (i >= 0 && (uint64_t)i < N) cs_next = ld64_any(blob + (uint64_t)i * S);
+    }
+    // the resolver's inputs from the record (frame 0's stored checksum, the last eight
+    // frames' ones: lane j of wave 0), loaded now by every workgroup so the one that
+    // resolves does not wait for them afterwards
+    uint64_t r_cs0 = 0, r_lv = 0;
+    if (VERIFY && pl.long_cs && threadIdx.x < 8) {
+        r_cs0 = ld64_any(blob);
+        r_lv = ld64_any(blob + (N - 8 + threadIdx.x) * S);
+    }
 
     if (VERIFY && pl.long_frames) {
         // lane groups: group g = 8 wave + (lane >> 3) takes frames i0 + g + 32 k, k = 0..3
@@ -167,6 +198,55 @@ __device__ __forceinline__ void decode_record_block(const uint8_t *__restrict__ 
         const uint64_t last0 = kSecretLast[2 * m], last1 = kSecretLast[2 * m + 1];
         const uint64_t mrg0 = kSecretMerge[2 * m], mrg1 = kSecretMerge[2 * m + 1];
         const uint64_t nbF = pl.nbF, ns = pl.ns;
+        // one frame's hash from its loaded pieces (the last, partial block and the last
+        // stripe), the header checks and the outputs
+        auto finish = [&](uint32_t k, int64_t i, bool valid, uint4 hdr, uint64_t stored, uint64_t a0, uint64_t a1,
+                          const uint4 *pc, uint4 lastp) {
+#pragma unroll
+            for (int q = 0; q < 8; ++q)
+                if (2 * (uint64_t)q + par < ns) piece(a0, a1, pc[q], s0[q], s1[q]);
+            a0 += gdpp64<0xB1>(a0);
+            a1 += gdpp64<0xB1>(a1);
+            piece(a0, a1, lastp, last0, last1);  // odd lanes: never used
+            uint64_t tt = fold64(a0 ^ mrg0, a1 ^ mrg1);
+            tt += gdpp64<0x4E>(tt);
+            tt += gswz_xor4(tt);
+            const uint64_t h = avalanche(L * P64_1 + tt);
+            if (l == 0) {
+                if (valid) {
+                    if (hdr.z | hdr.w || (uint64_t)kFrameHdr + hdr.x + hdr.y != S) mysf = min(mysf, (uint64_t)i);
+                    if (h != stored) mybad = min(mybad, (uint64_t)i);
+                    if (frame_pos && (uint64_t)i < tk.pos_cap) frame_pos[tk.pos_base + i] = (uint64_t)i * S;
+                }
+                s_cs[g + 32 * k] = valid ? stored : 0;
+            }
+        };
+        if (nbF == 0) {
+            // frames of at most one block (C1: 296 B): the four frames' loads first, then
+            // the hashes -- one memory round trip instead of four (a registered record
+            // is read in place over the host link, where each round trip is microseconds)
+            constexpr uint32_t K = kRecFrames / 32;
+            uint4 hdr[K], pc[K][8], lastp[K];
+            uint64_t stored[K];
+#pragma unroll
+            for (uint32_t k = 0; k < K; ++k) {
+                const int64_t i = i0 + g + 32 * k;
+                const bool valid = i >= 0 && (uint64_t)i < N;
+                const uint8_t *fb = blob + (valid ? (uint64_t)i : 0) * S;
+                const uint8_t *hb = fb + 8 + poff;
+                hdr[k] = l == 0 ? ld128_any(fb + 32) : make_uint4(0, 0, 0, 0);
+                stored[k] = l == 0 ? ld64_any(fb) : 0;
+#pragma unroll
+                for (int q = 0; q < 8; ++q)
+                    pc[k][q] = (2 * (uint64_t)q + par < ns) ? ld128_any(hb + 128 * q) : make_uint4(0, 0, 0, 0);
+                lastp[k] = par ? make_uint4(0, 0, 0, 0) : ld128_any(fb + 8 + L - 64 + 16 * m);
+            }
+#pragma unroll
+            for (uint32_t k = 0; k < K; ++k) {
+                const int64_t i = i0 + g + 32 * k;
+                finish(k, i, i >= 0 && (uint64_t)i < N, hdr[k], stored[k], init0, init1, pc[k], lastp[k]);
+            }
+        } else
 #pragma unroll 1
         for (uint32_t k = 0; k < kRecFrames / 32; ++k) {
             const int64_t i = i0 + g + 32 * k;
@@ -195,31 +275,12 @@ __device__ __forceinline__ void decode_record_block(const uint8_t *__restrict__ 
                 a1 = scramble1(a1, key1);
                 if (par) { a0 = 0; a1 = 0; }
             }
-            {
-                uint4 pc[8];
+            uint4 pc[8];
 #pragma unroll
-                for (int q = 0; q < 8; ++q)
-                    pc[q] = (2 * (uint64_t)q + par < ns) ? ld128_any(hb + 1024 * nbF + 128 * q) : make_uint4(0, 0, 0, 0);
-                const uint4 lastp = par ? make_uint4(0, 0, 0, 0) : ld128_any(fb + 8 + L - 64 + 16 * m);
-#pragma unroll
-                for (int q = 0; q < 8; ++q)
-                    if (2 * (uint64_t)q + par < ns) piece(a0, a1, pc[q], s0[q], s1[q]);
-                a0 += gdpp64<0xB1>(a0);
-                a1 += gdpp64<0xB1>(a1);
-                piece(a0, a1, lastp, last0, last1);  // odd lanes: never used
-            }
-            uint64_t tt = fold64(a0 ^ mrg0, a1 ^ mrg1);
-            tt += gdpp64<0x4E>(tt);
-            tt += gswz_xor4(tt);
-            const uint64_t h = avalanche(L * P64_1 + tt);
-            if (l == 0) {
-                if (valid) {
-                    if (hdr.z | hdr.w || (uint64_t)kFrameHdr + hdr.x + hdr.y != S) mysf = min(mysf, (uint64_t)i);
-                    if (h != stored) mybad = min(mybad, (uint64_t)i);
-                    if (frame_pos && (uint64_t)i < tk.pos_cap) frame_pos[tk.pos_base + i] = (uint64_t)i * S;
-                }
-                s_cs[g + 32 * k] = valid ? stored : 0;
-            }
+            for (int q = 0; q < 8; ++q)
+                pc[q] = (2 * (uint64_t)q + par < ns) ? ld128_any(hb + 1024 * nbF + 128 * q) : make_uint4(0, 0, 0, 0);
+            const uint4 lastp = par ? make_uint4(0, 0, 0, 0) : ld128_any(fb + 8 + L - 64 + 16 * m);
+            finish(k, i, valid, hdr, stored, a0, a1, pc, lastp);
         }
     } else if (threadIdx.x < kRecFrames) {
         // one lane per frame: header checks, short-frame hashes (<= 240 B), positions
@@ -244,10 +305,7 @@ __device__ __forceinline__ void decode_record_block(const uint8_t *__restrict__ 
                 rec_fill_msg(body, tk.off, (uint64_t)i * S, base_offset, base_ts, origin, msgs + tk.msg_base + i);
         }
     }
-    if (threadIdx.x == 0) {  // frame 128b + 122: its low half closes word 128b + 127
-        const int64_t i = i0 + kRecFrames;
-        s_cs[kRecFrames] = (i >= 0 && (uint64_t)i < N) ? ld64_any(blob + (uint64_t)i * S) : 0;
-    }
+    if (threadIdx.x == 0) s_cs[kRecFrames] = cs_next;
     const uint64_t wbad = wg_min(mybad, s_min);  // (its barriers also publish s_cs)
     const uint64_t wsf = wg_min(mysf, s_min);
     if (threadIdx.x == 0) {
@@ -264,16 +322,21 @@ __device__ __forceinline__ void decode_record_block(const uint8_t *__restrict__ 
         const uint64_t t8 = reduce_acc8(x, y);
         if (lane < 8) bsums[8 * (tk.bsum_base + blk) + lane] = t8;
     }
-    // the last block workgroup of the record resolves it
+    // the last block workgroup of the record resolves it (a one-block record: its only
+    // workgroup, with no device-scope fence or counter)
     __syncthreads();
-    if (threadIdx.x == 0) {
-        __threadfence();  // release: this WG's block sums, positions and atomics
-        const uint32_t old = atomicAdd(&st[t].done, 1u);
-        s_last = old + 1 == (uint32_t)nblk;
+    if (nblk > 1) {
+        if (threadIdx.x == 0) {
+            __threadfence();  // release: this WG's block sums, positions and atomics
+            const uint32_t old = atomicAdd(&st[t].done, 1u);
+            s_last = old + 1 == (uint32_t)nblk;
+        }
+        __syncthreads();
+        if (!s_last || wave != 0) return;
+        __threadfence();  // acquire: every block workgroup's stores of this record
+    } else if (wave != 0) {
+        return;
     }
-    __syncthreads();
-    if (!s_last || wave != 0) return;
-    __threadfence();  // acquire: every block workgroup's stores of this record
 
     uint64_t computed = 0;
     if (VERIFY && pl.long_cs) {
@@ -282,7 +345,7 @@ __device__ __forceinline__ void decode_record_block(const uint8_t *__restrict__ 
         const uint64_t key = kSecretW8[16 + j];
         const uint32_t klo = (uint32_t)key, khi = (uint32_t)(key >> 32);
         {  // words 0..5: header fields, then count | lo32(cs_0)
-            const uint64_t cs0 = ld64_any(blob);
+            const uint64_t cs0 = __shfl(r_cs0, 0);
             const uint64_t w6[6] = {hi.h.partition_id, hi.h.base_offset, hi.h.base_timestamp,
                                     hi.h.origin_timestamp, hi.h.batch_length,
                                     (uint64_t)hi.h.message_count | (cs0 << 32)};
@@ -307,7 +370,7 @@ __device__ __forceinline__ void decode_record_block(const uint8_t *__restrict__ 
         for (; b <= nb; ++b) y = chain_step(y, src[8 * b], klo, khi);
         acc = y;
         // last stripe = stored checksums of frames N-8 .. N-1 (secret offset 121)
-        const uint64_t lv = ld64_any(blob + (N - 8 + j) * S);
+        const uint64_t lv = __shfl(r_lv, j);
         acc += __shfl_xor(lv, 1);
         acc += mul32x32(lv ^ kSecretLast[j]);
         uint64_t a[8];

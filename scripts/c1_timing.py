@@ -11,7 +11,7 @@ os.environ["IGGY_CODEC_TIMING"] = "200"
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from iggy_amd import abi  # noqa: E402
 from iggy_amd import codec as _codec  # noqa: E402
-_codec.use_library(_codec.DIAG_LIB_PATH)
+_codec.use_library(os.environ.get("IGGY_DIAG_LIB", _codec.DIAG_LIB_PATH))
 from iggy_amd.codec import Codec  # noqa: E402
 from oracle import oracle as O  # noqa: E402
 
