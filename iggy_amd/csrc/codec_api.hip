@@ -386,7 +386,12 @@ struct DevGuard {
 // under the DMA of chunk k), so no runtime lock on caller memory ever exists.
 constexpr uint64_t kXferChunk = 4ull << 20;
 std::mutex g_reg_mu;
-std::vector<std::pair<uintptr_t, uint64_t>> g_reg;  // ranges registered through the codec
+struct RegRange {
+    uintptr_t h;   // host address
+    uint64_t len;
+    uintptr_t d;   // its device-mapped address (0: not mapped)
+};
+std::vector<RegRange> g_reg;  // ranges registered through the codec
 
 bool host_pinned(const void *p, uint64_t n) {
     if (!p || !n) return true;
@@ -394,7 +399,7 @@ bool host_pinned(const void *p, uint64_t n) {
     {
         std::lock_guard<std::mutex> lk(g_reg_mu);
         for (const auto &r : g_reg)
-            if (a >= r.first && a - r.first <= r.second && n <= r.second - (a - r.first)) return true;
+            if (a >= r.h && a - r.h <= r.len && n <= r.len - (a - r.h)) return true;
     }
     hipPointerAttribute_t at;
     if (hipPointerGetAttributes(&at, p) != hipSuccess) {
@@ -413,6 +418,25 @@ bool host_pinned(const void *p, uint64_t n) {
     // anything else is staged (always correct, only slower)
     const uintptr_t s0 = (uintptr_t)start;
     return a >= s0 && a - s0 <= size && n <= size - (a - s0);
+}
+
+// the device-mapped address of pinned host memory [p, p + n) (nullptr: not pinned or
+// not mapped); ranges registered through the codec answer from the registry
+const uint8_t *host_device_ptr(const void *p, uint64_t n) {
+    const uintptr_t a = (uintptr_t)p;
+    {
+        std::lock_guard<std::mutex> lk(g_reg_mu);
+        for (const auto &r : g_reg)
+            if (a >= r.h && a - r.h <= r.len && n <= r.len - (a - r.h))
+                return r.d ? (const uint8_t *)(r.d + (a - r.h)) : nullptr;
+    }
+    if (!host_pinned(p, n)) return nullptr;
+    void *dp = nullptr;
+    if (hipHostGetDevicePointer(&dp, (void *)p, 0) != hipSuccess || !dp) {
+        (void)hipGetLastError();
+        return nullptr;
+    }
+    return (const uint8_t *)dp;
 }
 
 int xfer_init(iggy_codec_ctx *c) {
@@ -913,11 +937,7 @@ int decode_host_fast(iggy_codec_ctx *c, const uint8_t *body, uint64_t len, int i
     // a registered (page-locked, device-mapped) record of at most kZeroCopyBytes is read
     // by the kernel in place over the host link: no H2D, one launch and the flag
     const uint8_t *d_base = nullptr;
-    if (len <= kZeroCopyBytes && host_pinned(body, len)) {
-        void *dp = nullptr;
-        if (hipHostGetDevicePointer(&dp, (void *)body, 0) == hipSuccess && dp) d_base = (const uint8_t *)dp;
-        else (void)hipGetLastError();
-    }
+    if (len <= kZeroCopyBytes) d_base = host_device_ptr(body, len);
     int r = 0;
     if (!d_base) {
         if (c->din.ensure(len + 16)) return IGGY_ERR_DEVICE;
@@ -2823,8 +2843,13 @@ int iggy_codec_host_register(iggy_codec_ctx *c, void *ptr, uint64_t len) {
     if (!c || !ptr || !len) return IGGY_ERR_INVALID_ARGUMENT;
     DevGuard dg(c->device);
     HIP_OK(hipHostRegister(ptr, len, hipHostRegisterDefault));
+    void *dp = nullptr;
+    if (hipHostGetDevicePointer(&dp, ptr, 0) != hipSuccess) {
+        (void)hipGetLastError();
+        dp = nullptr;
+    }
     std::lock_guard<std::mutex> lk(g_reg_mu);
-    g_reg.emplace_back((uintptr_t)ptr, len);
+    g_reg.push_back(RegRange{(uintptr_t)ptr, len, (uintptr_t)dp});
     return 0;
 }
 
@@ -2834,7 +2859,7 @@ int iggy_codec_host_unregister(iggy_codec_ctx *c, void *ptr) {
     {
         std::lock_guard<std::mutex> lk(g_reg_mu);
         for (size_t i = 0; i < g_reg.size(); ++i)
-            if (g_reg[i].first == (uintptr_t)ptr) {
+            if (g_reg[i].h == (uintptr_t)ptr) {
                 g_reg.erase(g_reg.begin() + (long)i);
                 break;
             }

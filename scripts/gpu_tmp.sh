@@ -1,3 +1,6 @@
 set -u
 cd $GRAFT_REPO_ROOT
-timeout -k 10 200 python -u scripts/c1_timing.py 2>&1 | grep -v amdgpu.ids
+STEPS="tests smoke bench phase" bash scripts/gpu_round.sh r5o || exit $?
+bash scripts/profile_round.sh r05c || exit $?
+bash scripts/c3_profile.sh || exit $?
+bash scripts/enc_pmc.sh || exit $?
