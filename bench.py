@@ -344,11 +344,27 @@ def c1_leg(cx, dev, seconds: float):
                 cx.decode_batch_into(r, abi.INTEGRITY_VERIFY, p)
         return (time.perf_counter() - t) / (reps * nb) * 1e6
 
+    def async_us(reps=5, with_pos=True):
+        t = time.perf_counter()
+        for _ in range(reps):
+            for lo in (0, 8):  # at most 8 in flight per context
+                tks = [cx.decode_submit(recs[b], abi.INTEGRITY_VERIFY, poss[b] if with_pos else None)
+                       for b in range(lo, min(lo + 8, nb))]
+                for tk in tks:
+                    c = cx.wait(tk)
+                    assert c.error.kind == 0 and c.frame_count == n, c.error
+        return (time.perf_counter() - t) / (reps * nb) * 1e6
+
     sync_pageable_us = sync_us()
     for a in recs + poss:
         cx.host_register(a)
     try:
         sync_registered_us = sync_us()
+        assert all(int(p[1]) == 48 + pl for p in poss)
+        for p in poss:
+            p[:] = 0
+        async_us(1)
+        async_registered_us = async_us()
         assert all(int(p[1]) == 48 + pl for p in poss)
     finally:
         for a in recs + poss:
@@ -363,6 +379,7 @@ def c1_leg(cx, dev, seconds: float):
         "gpu_host_roundtrip_us_per_batch": round(host_us, 1),
         "gpu_host_sync_us_per_batch": round(sync_pageable_us, 1),
         "gpu_host_sync_registered_us_per_batch": round(sync_registered_us, 1),
+        "gpu_host_async_registered_us_per_batch": round(async_registered_us, 1),
         "cpu_ref_decode_us_per_batch": round(recs[0].size / dec * 1e6, 1),
         "wire_bytes": wire,
     }

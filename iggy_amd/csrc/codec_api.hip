@@ -126,6 +126,7 @@ struct Slot {
     uint64_t *frame_pos = nullptr;               // host destination of the decode's positions
     DevBuf in, pos, out, res;                    // device input / positions / encode output / result
     DevBuf ids, ots, pay, plen, uhb, uhl;        // encode SoA inputs
+    HostMap tab;                                 // k_decode_records task table of an in-flight decode
     hipEvent_t ev_in = nullptr, ev_k = nullptr, ev_done = nullptr;
     // a pageable caller output is never a DMA target: the copy-out stream lands it in
     // this pinned bounce and iggy_codec_poll copies it to the caller (hout_dst, hout_len)
@@ -149,6 +150,7 @@ struct Slot {
     void release() {
         DevBuf *b[] = {&in, &pos, &out, &res, &ids, &ots, &pay, &plen, &uhb, &uhl};
         for (DevBuf *x : b) x->release();
+        tab.release();
         for (hipEvent_t *e : {&ev_in, &ev_k, &ev_done})
             if (*e) (void)hipEventDestroy(*e), *e = nullptr;
         if (hout) (void)hipHostFree(hout);
@@ -240,6 +242,7 @@ struct iggy_codec_ctx {
     hipStream_t h2d = nullptr, d2h = nullptr;
     Slot slots[kSlots];
     void *slot_pinned = nullptr;  // kSlots x 256 B: completion records
+    uint8_t *slot_pinned_d = nullptr;  // its device-mapped address (kernels write decode verdicts there)
     uint64_t seq = 0;
     // profiling
     int profile = 0;
@@ -566,6 +569,20 @@ static uint32_t bsum_grid(const iggy_codec_ctx *c, uint64_t max_frames) {
     return (uint32_t)std::min<uint64_t>((uint64_t)c->ncu * 4, (blocks + 3) / 4);
 }
 
+// k_decode_general after a first-pass kernel on stream s: it returns at once unless that
+// kernel left d_res->status == kStatusNeedGeneral (ensure_decode_scratch done by the caller)
+void launch_general(iggy_codec_ctx *c, const uint8_t *d_body, uint64_t len, int integrity, uint64_t *d_pos,
+                    uint64_t cap, iggy_decode_result *d_res, hipStream_t s) {
+    GeneralScratch gs = gscratch(c);
+    const uint32_t ggrid = (uint32_t)std::min<uint64_t>((uint64_t)c->gen_grid, len / (64 << 10) + 2);
+    if (integrity == IGGY_INTEGRITY_VERIFY)
+        hipLaunchKernelGGL(k_decode_general<true>, dim3(ggrid), dim3(kGenThreads), kGenLds, s, d_body, len, d_pos,
+                           cap, d_res, gs);
+    else
+        hipLaunchKernelGGL(k_decode_general<false>, dim3(ggrid), dim3(kGenThreads), 0, s, d_body, len, d_pos, cap,
+                           d_res, gs);
+}
+
 int enqueue_decode(iggy_codec_ctx *c, const uint8_t *d_body, uint64_t len, int integrity,
                    uint64_t *d_pos, uint64_t cap, iggy_decode_result *d_res, hipStream_t s) {
     int r = ensure_decode_scratch(c, len);
@@ -576,7 +593,6 @@ int enqueue_decode(iggy_codec_ctx *c, const uint8_t *d_body, uint64_t len, int i
     }
     const bool verify = integrity == IGGY_INTEGRITY_VERIFY;
     DecodeScratch ds = dscratch(c);
-    GeneralScratch gs = gscratch(c);
     // one persistent grid: one WG per CU, block 0 the consumer (chain) WG. Small
     // records get grids sized to their work (at most one producer WG per 128-frame
     // block of 48-B frames; one general WG per 64 KiB): dispatching two full
@@ -584,7 +600,6 @@ int enqueue_decode(iggy_codec_ctx *c, const uint8_t *d_body, uint64_t len, int i
     // over whatever grid they get.
     const uint64_t ub_blocks = len / (48 * 128) + 2;
     const uint32_t grid = (uint32_t)std::min<uint64_t>((uint64_t)c->ugrid, ub_blocks + 1);
-    const uint32_t ggrid = (uint32_t)std::min<uint64_t>((uint64_t)c->gen_grid, len / (64 << 10) + 2);
     const uint32_t au = (uint32_t)c->allow_unaligned;
     prof_begin(c, 0, s);
     if (verify)
@@ -594,13 +609,7 @@ int enqueue_decode(iggy_codec_ctx *c, const uint8_t *d_body, uint64_t len, int i
         hipLaunchKernelGGL(k_decode_uniform<false>, dim3(grid), dim3(kUniformThreads), kUniformLds, s, d_body, len, d_pos,
                            cap, d_res, ds, c->epoch, au, diag_bits(c));
     HIP_OK(hipGetLastError());
-    if (verify) {
-        hipLaunchKernelGGL(k_decode_general<true>, dim3(ggrid), dim3(kGenThreads), kGenLds, s, d_body, len, d_pos,
-                           cap, d_res, gs);
-    } else {
-        hipLaunchKernelGGL(k_decode_general<false>, dim3(ggrid), dim3(kGenThreads), 0, s, d_body, len,
-                           d_pos, cap, d_res, gs);
-    }
+    launch_general(c, d_body, len, integrity, d_pos, cap, d_res, s);
     // the profiled interval is the whole decode: both kernels (the general one writes a
     // lane-group decode's frame positions, decode_uniform.hip kPosEpilogue)
     prof_end(c, 0, s);
@@ -715,8 +724,11 @@ constexpr uint64_t kRecZeroCopyWgs = 4096;  // larger launches upload their tabl
 int enqueue_records(iggy_codec_ctx *c, const uint8_t *d_base, const uint8_t *h_base, const RecIn *recs, size_t K,
                     int integrity, uint64_t *d_pos, iggy_polled_message *d_msgs, iggy_decode_result *d_res,
                     std::vector<size_t> *single, std::vector<uint64_t> *n_frames = nullptr,
-                    uint32_t *host_flag = nullptr, uint32_t flag_value = 0) {
+                    uint32_t *host_flag = nullptr, uint32_t flag_value = 0, HostMap *tab = nullptr) {
+    // tab (nullable): host-mapped memory for the launch's task table that stays the
+    // caller's until the launch completes (asynchronous submits); else the context's
     hipStream_t s = c->stream;
+    HostMap &rm = tab ? *tab : c->rmap;
     std::vector<RecTask> tasks(K);
     std::vector<uint32_t> wgmap;
     uint64_t nbs = 0, maxlen = 0;
@@ -745,7 +757,7 @@ int enqueue_records(iggy_codec_ctx *c, const uint8_t *d_base, const uint8_t *h_b
     const uint64_t W = wgmap.size();
     if (W) {
         const size_t tb = K * sizeof(RecTask), wb = W * 4;
-        int r = c->rmap.ensure(tb + wb);
+        int r = rm.ensure(tb + wb);
         r |= c->rbsums.ensure(nbs * 64 + 64);
         const size_t st_before = c->rstate.cap;
         r |= c->rstate.ensure(K * sizeof(RecState));
@@ -756,14 +768,14 @@ int enqueue_records(iggy_codec_ctx *c, const uint8_t *d_base, const uint8_t *h_b
         if (r) return IGGY_ERR_DEVICE;
         if (c->rstate.cap != st_before)  // fresh state: zero (the resolvers keep it zero after)
             HIP_OK(hipMemsetAsync(c->rstate.p, 0, c->rstate.cap, s));
-        memcpy(c->rmap.hp<uint8_t>(), tasks.data(), tb);
-        memcpy(c->rmap.hp<uint8_t>(tb), wgmap.data(), wb);
-        const RecTask *dt = c->rmap.dp<RecTask>();
-        const uint32_t *dw = c->rmap.dp<uint32_t>(tb);
-        if (W > kRecZeroCopyWgs) {  // a big launch: every workgroup would read its task over PCIe
+        memcpy(rm.hp<uint8_t>(), tasks.data(), tb);
+        memcpy(rm.hp<uint8_t>(tb), wgmap.data(), wb);
+        const RecTask *dt = rm.dp<RecTask>();
+        const uint32_t *dw = rm.dp<uint32_t>(tb);
+        if (W > kRecZeroCopyWgs && !tab) {  // a big launch: every workgroup would read its task over PCIe
             r = c->rtab.ensure(tb + wb);
             if (r) return IGGY_ERR_DEVICE;
-            HIP_OK(hipMemcpyAsync(c->rtab.p, c->rmap.h, tb + wb, hipMemcpyHostToDevice, s));
+            HIP_OK(hipMemcpyAsync(c->rtab.p, rm.h, tb + wb, hipMemcpyHostToDevice, s));
             dt = c->rtab.as<RecTask>();
             dw = c->rtab.as<uint32_t>(tb);
         }
@@ -2816,6 +2828,14 @@ int async_init(iggy_codec_ctx *c) {
         hipStreamCreateWithFlags(&c->d2h, hipStreamNonBlocking) != hipSuccess ||
         hipHostMalloc(&c->slot_pinned, kSlots * 256, hipHostMallocDefault) != hipSuccess)
         return IGGY_ERR_DEVICE;
+    {
+        void *dp = nullptr;
+        if (hipHostGetDevicePointer(&dp, c->slot_pinned, 0) != hipSuccess) {
+            (void)hipGetLastError();
+            dp = nullptr;
+        }
+        c->slot_pinned_d = (uint8_t *)dp;
+    }
     for (Slot &sl : c->slots)
         if (hipEventCreateWithFlags(&sl.ev_in, hipEventDisableTiming) != hipSuccess ||
             hipEventCreateWithFlags(&sl.ev_k, hipEventDisableTiming) != hipSuccess ||
@@ -2893,6 +2913,42 @@ int iggy_codec_decode_submit(iggy_codec_ctx *c, const uint8_t *body, uint64_t le
     sl.hout_len = 0;
     const bool pos_pinned = host_pinned(frame_pos, pcap * 8);
     if (pcap && !pos_pinned && sl.hout_ensure(pcap * 8)) r = IGGY_ERR_DEVICE;
+    uint64_t nf = 0;
+    if (!r && c->slot_pinned_d && len <= kHostFastBytes && rec_plan(body, len, &nf)) {
+        // a single-stride record of <= 16 MiB, all on the context's stream: the input
+        // (read in place when registered and <= 1 MiB, else copied), one
+        // k_decode_records launch whose verdict lands in the slot's host-mapped
+        // completion record, k_decode_general behind it for a stride that breaks
+        // mid-record, the positions back, the completion event
+        hipStream_t s = bind(c, nullptr);
+        const uint8_t *d_in = len <= kZeroCopyBytes ? host_device_ptr(body, len) : nullptr;
+        if (!d_in) {
+            r = put_host(c, sl.in.p, body, len, s);
+            d_in = sl.in.as<uint8_t>();
+        }
+        iggy_decode_result *d_res = (iggy_decode_result *)(c->slot_pinned_d + 256 * k);
+        std::vector<size_t> single;
+        const RecIn rec{0, len, 0, pcap, 0};
+        if (!r)
+            r = enqueue_records(c, d_in, body, &rec, 1, integrity, pcap ? sl.pos.as<uint64_t>() : nullptr, nullptr,
+                                d_res, &single, nullptr, nullptr, 0, &sl.tab);
+        if (!r) launch_general(c, d_in, len, integrity, pcap ? sl.pos.as<uint64_t>() : nullptr, pcap, d_res, s);
+        if (!r && hipGetLastError() != hipSuccess) r = IGGY_ERR_DEVICE;
+        if (!r && pcap) {
+            if (!pos_pinned) sl.hout_dst = (uint8_t *)frame_pos;
+            if (hipMemcpyAsync(pos_pinned ? (void *)frame_pos : sl.hout, sl.pos.p, pcap * 8, hipMemcpyDeviceToHost,
+                               s) != hipSuccess)
+                r = IGGY_ERR_DEVICE;
+        }
+        if (!r && hipEventRecord(sl.ev_done, s) != hipSuccess) r = IGGY_ERR_DEVICE;
+        if (!r && xfer_settle(c)) r = IGGY_ERR_DEVICE;  // (a staged pageable input: its last chunk copied)
+        if (r) {
+            sl.busy = false;
+            return r;
+        }
+        *ticket = sl.ticket;
+        return 0;
+    }
     if (!r) r = put_host(c, sl.in.p, body, len, c->h2d);
     if (r) {
         sl.busy = false;

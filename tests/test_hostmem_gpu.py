@@ -141,3 +141,51 @@ def test_registered_record_read_in_place(cx):
             assert rc == want[0] and e.astuple() == want[1].astuple() and h.astuple() == want[2].astuple()
             if rc == 0:
                 assert np.array_equal(pos[:nf], np.asarray(want[3], dtype=np.uint64))
+
+
+def _stride_break_record():
+    """1000 frames: 256-B payloads, except frames 500 / 501 (272 / 240 B), so the blob
+    is still a multiple of frame 0's size and only the walk finds the break."""
+    from iggy_amd.codec import raw_messages
+    n = 1000
+    rng = np.random.default_rng(41)
+    pls = np.full(n, 256, dtype=np.uint32)
+    pls[500], pls[501] = 272, 240
+    ids = rng.integers(1, 2**63, size=2 * n, dtype=np.uint64)
+    ots = (1_700_000_000_000_000 + np.arange(n)).astype(np.uint64)
+    pay = rng.integers(0, 256, size=int(pls.sum()), dtype=np.uint8)
+    rc, e, out = O.encode_batch(raw_messages(ids, ots, pay, pls), 0)
+    assert rc == 0
+    return np.frombuffer(out, dtype=np.uint8).copy()
+
+
+@pytest.mark.parametrize("registered", [False, True])
+def test_submit_single_stride_fast_path(cx, registered):
+    """decode_submit of records <= 16 MiB (one k_decode_records launch on the context's
+    stream, the verdict straight into the slot's host-mapped record, k_decode_general
+    behind it): clean, corrupted and stride-breaking records, with and without
+    positions, several in flight, each against the oracle."""
+    clean = O.synth_batch(1000, 256, seed=43)
+    bad = clean.copy()
+    bad[256 + 304 * 700 + 100] ^= 1
+    recs = [clean, bad, _stride_break_record(), O.synth_batch(3000, 1000, seed=44)]
+    poss = [np.zeros(r.size // 48 + 1, dtype=np.uint64) for r in recs]
+    if registered:
+        for a in recs + poss:
+            cx.host_register(a)
+    try:
+        for with_pos in (True, False):
+            tks = [cx.decode_submit(r, abi.INTEGRITY_VERIFY, p if with_pos else None) for r, p in zip(recs, poss)]
+            for tk, r, p in zip(tks, recs, poss):
+                c = cx.wait(tk)
+                orc, oe, oh, of = O.decode_batch_slice_with(r, 0)
+                assert c.error.astuple() == oe.astuple()
+                assert c.header.astuple() == oh.astuple()
+                if orc == 0:
+                    assert c.frame_count == len(of)
+                    if with_pos:
+                        assert np.array_equal(p[:c.frame_count], np.asarray(of, dtype=np.uint64))
+    finally:
+        if registered:
+            for a in recs + poss:
+                cx.host_unregister(a)
