@@ -1268,6 +1268,9 @@ __device__ __forceinline__ void consumer(const uint8_t *body, const HeaderInfo &
                 if (j == m) acc += mul32x32(w6[m] ^ Secret::w(8 * m));
             }
         }
+        // the last stripe's stored checksums (frames N-8 .. N-1), loaded now: after the
+        // chain they would cost one more memory round trip on the decode's critical path
+        const uint64_t last_v = ld64_any(blob + (pl.N - 8 + j) * pl.S);
         // y = acc + (sum of the current block); block b >= 1: y = scramble(y) + S_b.
         // Only blocks 0 .. nb-1 are scrambled: the partial block nb just adds.
         const uint64_t nbatch = chain_batches(pl);
@@ -1342,7 +1345,7 @@ __device__ __forceinline__ void consumer(const uint8_t *body, const HeaderInfo &
         } else {
             acc = y;
             // last stripe = stored checksums of frames N-8 .. N-1 (secret offset 121)
-            const uint64_t v = ld64_any(blob + (pl.N - 8 + j) * pl.S);
+            const uint64_t v = last_v;
             acc += __shfl_xor(v, 1);
             acc += mul32x32(v ^ kSecretLast[j]);
             uint64_t a[8];
