@@ -724,7 +724,8 @@ constexpr uint64_t kRecZeroCopyWgs = 4096;  // larger launches upload their tabl
 int enqueue_records(iggy_codec_ctx *c, const uint8_t *d_base, const uint8_t *h_base, const RecIn *recs, size_t K,
                     int integrity, uint64_t *d_pos, iggy_polled_message *d_msgs, iggy_decode_result *d_res,
                     std::vector<size_t> *single, std::vector<uint64_t> *n_frames = nullptr,
-                    uint32_t *host_flag = nullptr, uint32_t flag_value = 0, HostMap *tab = nullptr) {
+                    uint32_t *host_flag = nullptr, uint32_t flag_value = 0, HostMap *tab = nullptr,
+                    GenRearm rearm = GenRearm{nullptr, nullptr, nullptr}) {
     // tab (nullable): host-mapped memory for the launch's task table that stays the
     // caller's until the launch completes (asynchronous submits); else the context's
     hipStream_t s = c->stream;
@@ -784,11 +785,11 @@ int enqueue_records(iggy_codec_ctx *c, const uint8_t *d_base, const uint8_t *h_b
         if (integrity == IGGY_INTEGRITY_VERIFY)
             hipLaunchKernelGGL(k_decode_records<true>, dim3((uint32_t)W), dim3(kRecThreads), 0, s, d_base, dt, dw, ds,
                                c->rbsums.as<uint64_t>(), d_pos, d_msgs, d_res, c->rcount.as<uint32_t>(), flag,
-                               flag_value);
+                               flag_value, rearm);
         else
             hipLaunchKernelGGL(k_decode_records<false>, dim3((uint32_t)W), dim3(kRecThreads), 0, s, d_base, dt, dw,
                                ds, c->rbsums.as<uint64_t>(), d_pos, d_msgs, d_res, c->rcount.as<uint32_t>(), flag,
-                               flag_value);
+                               flag_value, rearm);
         HIP_OK(hipGetLastError());
     }
     if (!single->empty()) {
@@ -2929,9 +2930,13 @@ int iggy_codec_decode_submit(iggy_codec_ctx *c, const uint8_t *body, uint64_t le
         iggy_decode_result *d_res = (iggy_decode_result *)(c->slot_pinned_d + 256 * k);
         std::vector<size_t> single;
         const RecIn rec{0, len, 0, pcap, 0};
-        if (!r)
+        if (!r) {
+            // k_decode_general after it relies on its barrier words being re-armed, which
+            // the uniform kernel does in the two-kernel decode: the records launch does it here
+            const DecodeScratch dsc = dscratch(c);
             r = enqueue_records(c, d_in, body, &rec, 1, integrity, pcap ? sl.pos.as<uint64_t>() : nullptr, nullptr,
-                                d_res, &single, nullptr, nullptr, 0, &sl.tab);
+                                d_res, &single, nullptr, nullptr, 0, &sl.tab, GenRearm{dsc.gbar, dsc.gbar2, dsc.gmisc});
+        }
         if (!r) launch_general(c, d_in, len, integrity, pcap ? sl.pos.as<uint64_t>() : nullptr, pcap, d_res, s);
         if (!r && hipGetLastError() != hipSuccess) r = IGGY_ERR_DEVICE;
         if (!r && pcap) {

@@ -37,6 +37,14 @@ struct RecTask {
     uint64_t bsum_base;           // block sums of this record: bsums[8 * (bsum_base + b) + j]
     uint32_t wg0, nwg;            // its workgroups in the grid
 };
+// The general kernel's barrier / registration words (DecodeScratch gbar, gbar2, gmisc),
+// re-armed by a launch that runs in the uniform kernel's place before a k_decode_general
+// (the asynchronous single-stride decode); all null otherwise.
+struct GenRearm {
+    uint32_t *gbar, *gbar2;
+    uint64_t *gmisc;
+};
+
 struct RecState {  // zero between launches: zeroed when allocated, reset by the record's resolver
     uint64_t first_bad;  // ~min index of a frame whose checksum mismatches (max-encoded), 0 = none
     uint64_t spec_fail;  // ~min index of a frame that breaks the stride
@@ -441,7 +449,19 @@ __global__ __launch_bounds__(kRecThreads) void k_decode_records(const uint8_t *_
                                                                 RecState *st, uint64_t *bsums, uint64_t *frame_pos,
                                                                 iggy_polled_message *msgs,
                                                                 iggy_decode_result *results, uint32_t *counter,
-                                                                uint32_t *host_flag, uint32_t flag_value) {
+                                                                uint32_t *host_flag, uint32_t flag_value,
+                                                                GenRearm rearm) {
+    if (rearm.gbar && blockIdx.x == 0) {  // as k_decode_uniform's prologue
+        if (threadIdx.x == 0) {
+            __hip_atomic_store(&rearm.gbar[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(&rearm.gbar[2], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(&rearm.gbar[3], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(&rearm.gmisc[2], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(&rearm.gmisc[kPosCountWord], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        if (threadIdx.x < kBar2Words)
+            __hip_atomic_store(&rearm.gbar2[32 * threadIdx.x], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
     decode_record_block<VERIFY>(base, tasks, wg_task, st, bsums, frame_pos, msgs, results);
     launch_done(counter, host_flag, flag_value);
 }
@@ -449,10 +469,10 @@ __global__ __launch_bounds__(kRecThreads) void k_decode_records(const uint8_t *_
 template __global__ void k_decode_records<true>(const uint8_t *__restrict__, const RecTask *__restrict__,
                                                 const uint32_t *__restrict__, RecState *, uint64_t *, uint64_t *,
                                                 iggy_polled_message *, iggy_decode_result *, uint32_t *, uint32_t *,
-                                                uint32_t);
+                                                uint32_t, GenRearm);
 template __global__ void k_decode_records<false>(const uint8_t *__restrict__, const RecTask *__restrict__,
                                                  const uint32_t *__restrict__, RecState *, uint64_t *, uint64_t *,
                                                  iggy_polled_message *, iggy_decode_result *, uint32_t *, uint32_t *,
-                                                 uint32_t);
+                                                 uint32_t, GenRearm);
 
 }  // namespace iggy

@@ -1049,6 +1049,20 @@ __device__ __forceinline__ void produce_lg(const uint8_t *blob, const LgPlan &pl
     if (st.sink == 0x5eed5eedu && pl.N == 0) sc.small[lane] = 1;  // never true (N >= 1); keeps `sink` live
 }
 
+#ifndef IGGY_LG_NPFIT
+#define IGGY_LG_NPFIT 1  // (build knob for a same-box A/B: 0 = every producer WG sweeps)
+#endif
+__device__ __forceinline__ uint32_t lg_sweep_wgs(uint64_t blocks, uint32_t np) {
+    if (!IGGY_LG_NPFIT || np < 16) return np;
+    uint32_t best = np;
+    uint64_t best_cost = (blocks + np - 1) / np * np;  // block slots of ceil(blocks / n) windows
+    for (uint32_t n = np - 1; n >= np - np / 16; --n) {
+        const uint64_t cost = (blocks + n - 1) / n * n;
+        if (cost < best_cost) { best = n; best_cost = cost; }
+    }
+    return best;
+}
+
 constexpr uint32_t kUniformLds = kLgLds > kXchOff + kXchBytes ? kLgLds : kXchOff + kXchBytes;  // dynamic LDS
 static_assert(kConsumerLds <= kLgLds && kConsumerLds <= kLdsBytes, "consumer WG fits either grid's LDS");
 static_assert(kUniformLds <= 160 * 1024, "LDS budget");
@@ -1514,15 +1528,24 @@ __global__ __launch_bounds__(kUniformThreads, 1) void k_decode_uniform(const uin
         if (threadIdx.x < 8 * kBsSlots) bs_acc(smem, 0)[threadIdx.x] = 0;  // block sums, counters, generations
         if (threadIdx.x < 2 * kBsSlots) bs_cnt(smem)[threadIdx.x] = 0;
         __syncthreads();
-        if (wave == 4) {  // the WG's publisher
-            lg_publisher(smem, lp, sc, epoch, g, nprod, lane, dbg);
+        // producer WGs that sweep the blocks: the count in [nprod - nprod/16, nprod] whose
+        // block windows waste the least (a last, partly filled window of blocks takes a
+        // whole block time while most WGs idle: C2's 8 194 blocks on 254 WGs leave 66 in
+        // it, on 249 WGs 226); the others only store their share of the positions
+        const uint32_t npe = lg_sweep_wgs(2 * lp.nchunks, nprod);
+        if (g < npe) {
+            if (wave == 4) {  // the WG's publisher
+                lg_publisher(smem, lp, sc, epoch, g, npe, lane, dbg);
+                return;
+            }
+            uint64_t *fp = IGGY_POS_MODE ? nullptr : frame_pos;
+            if (lp.nbF == 1 && lp.ns == 0)
+                produce_lg<kLgSlots, true>(blob, lp, fp, cap, sc, epoch, g, npe, wave, lane, smem);
+            else
+                produce_lg<kLgSlots, false>(blob, lp, fp, cap, sc, epoch, g, npe, wave, lane, smem);
+        } else if (wave == 4) {
             return;
         }
-        uint64_t *fp = IGGY_POS_MODE ? nullptr : frame_pos;
-        if (lp.nbF == 1 && lp.ns == 0)
-            produce_lg<kLgSlots, true>(blob, lp, fp, cap, sc, epoch, g, nprod, wave, lane, smem);
-        else
-            produce_lg<kLgSlots, false>(blob, lp, fp, cap, sc, epoch, g, nprod, wave, lane, smem);
         if (kPosTail && frame_pos) {  // this wave's contiguous share of the positions
             const uint64_t n = pl.N < cap ? pl.N : cap;
             const uint64_t nw = 4ull * nprod, per = ((n + nw - 1) / nw + 63) & ~63ull;
