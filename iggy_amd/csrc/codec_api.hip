@@ -123,6 +123,14 @@ struct Slot {
     uint64_t ticket = 0;
     uint32_t op = 0;
     uint64_t cap = 0, out_len = 0;
+    // a single-stride decode submitted on the fast path (one records launch): what
+    // iggy_codec_poll needs to run the general walk when its stride breaks mid-record
+    bool fast = false, g_pending = false;
+    const uint8_t *g_in = nullptr;
+    uint64_t g_len = 0, g_pcap = 0;
+    uint64_t *g_pos = nullptr;  // device-visible positions destination of the launch
+    int g_integ = 0;
+    bool g_pos_copy = false;    // positions go through `pos` and a D2H copy
     uint64_t *frame_pos = nullptr;               // host destination of the decode's positions
     DevBuf in, pos, out, res;                    // device input / positions / encode output / result
     DevBuf ids, ots, pay, plen, uhb, uhl;        // encode SoA inputs
@@ -773,7 +781,11 @@ int enqueue_records(iggy_codec_ctx *c, const uint8_t *d_base, const uint8_t *h_b
         memcpy(rm.hp<uint8_t>(tb), wgmap.data(), wb);
         const RecTask *dt = rm.dp<RecTask>();
         const uint32_t *dw = rm.dp<uint32_t>(tb);
-        if (W > kRecZeroCopyWgs && !tab) {  // a big launch: every workgroup would read its task over PCIe
+        const RecTask inl = tasks[0];
+        if (K == 1) {  // one record: the task rides in the kernel arguments
+            dt = nullptr;
+            dw = nullptr;
+        } else if (W > kRecZeroCopyWgs && !tab) {  // a big launch: every workgroup would read its task over PCIe
             r = c->rtab.ensure(tb + wb);
             if (r) return IGGY_ERR_DEVICE;
             HIP_OK(hipMemcpyAsync(c->rtab.p, rm.h, tb + wb, hipMemcpyHostToDevice, s));
@@ -785,11 +797,11 @@ int enqueue_records(iggy_codec_ctx *c, const uint8_t *d_base, const uint8_t *h_b
         if (integrity == IGGY_INTEGRITY_VERIFY)
             hipLaunchKernelGGL(k_decode_records<true>, dim3((uint32_t)W), dim3(kRecThreads), 0, s, d_base, dt, dw, ds,
                                c->rbsums.as<uint64_t>(), d_pos, d_msgs, d_res, c->rcount.as<uint32_t>(), flag,
-                               flag_value, rearm);
+                               flag_value, rearm, inl);
         else
             hipLaunchKernelGGL(k_decode_records<false>, dim3((uint32_t)W), dim3(kRecThreads), 0, s, d_base, dt, dw,
                                ds, c->rbsums.as<uint64_t>(), d_pos, d_msgs, d_res, c->rcount.as<uint32_t>(), flag,
-                               flag_value, rearm);
+                               flag_value, rearm, inl);
         HIP_OK(hipGetLastError());
     }
     if (!single->empty()) {
@@ -2928,23 +2940,46 @@ int iggy_codec_decode_submit(iggy_codec_ctx *c, const uint8_t *body, uint64_t le
             d_in = sl.in.as<uint8_t>();
         }
         iggy_decode_result *d_res = (iggy_decode_result *)(c->slot_pinned_d + 256 * k);
+        // positions straight into host memory the device can write: the caller's pinned
+        // array, else the slot's pinned bounce (copied out in iggy_codec_poll); a device
+        // buffer and a D2H copy only when neither is mapped
+        uint64_t *d_pos = nullptr;
+        bool pos_copy = false;
+        if (pcap) {
+            if (pos_pinned) d_pos = (uint64_t *)host_device_ptr(frame_pos, pcap * 8);
+            if (!d_pos && !pos_pinned) {
+                void *dp = nullptr;
+                if (hipHostGetDevicePointer(&dp, sl.hout, 0) == hipSuccess && dp) d_pos = (uint64_t *)dp;
+                else (void)hipGetLastError();
+                if (d_pos) sl.hout_dst = (uint8_t *)frame_pos;
+            }
+            if (!d_pos) {
+                d_pos = sl.pos.as<uint64_t>();
+                pos_copy = true;
+            }
+        }
         std::vector<size_t> single;
         const RecIn rec{0, len, 0, pcap, 0};
         if (!r) {
-            // k_decode_general after it relies on its barrier words being re-armed, which
-            // the uniform kernel does in the two-kernel decode: the records launch does it here
-            const DecodeScratch dsc = dscratch(c);
-            r = enqueue_records(c, d_in, body, &rec, 1, integrity, pcap ? sl.pos.as<uint64_t>() : nullptr, nullptr,
-                                d_res, &single, nullptr, nullptr, 0, &sl.tab, GenRearm{dsc.gbar, dsc.gbar2, dsc.gmisc});
+            // a stride break mid-record is left to iggy_codec_poll (k_decode_general)
+            r = enqueue_records(c, d_in, body, &rec, 1, integrity, d_pos, nullptr, d_res, &single, nullptr, nullptr,
+                                0, &sl.tab);
         }
-        if (!r) launch_general(c, d_in, len, integrity, pcap ? sl.pos.as<uint64_t>() : nullptr, pcap, d_res, s);
         if (!r && hipGetLastError() != hipSuccess) r = IGGY_ERR_DEVICE;
-        if (!r && pcap) {
+        if (!r && pos_copy) {
             if (!pos_pinned) sl.hout_dst = (uint8_t *)frame_pos;
             if (hipMemcpyAsync(pos_pinned ? (void *)frame_pos : sl.hout, sl.pos.p, pcap * 8, hipMemcpyDeviceToHost,
                                s) != hipSuccess)
                 r = IGGY_ERR_DEVICE;
         }
+        sl.fast = true;
+        sl.g_pending = false;
+        sl.g_in = d_in;
+        sl.g_len = len;
+        sl.g_pcap = pcap;
+        sl.g_pos = d_pos;
+        sl.g_integ = integrity;
+        sl.g_pos_copy = pos_copy;
         if (!r && hipEventRecord(sl.ev_done, s) != hipSuccess) r = IGGY_ERR_DEVICE;
         if (!r && xfer_settle(c)) r = IGGY_ERR_DEVICE;  // (a staged pageable input: its last chunk copied)
         if (r) {
@@ -2954,6 +2989,7 @@ int iggy_codec_decode_submit(iggy_codec_ctx *c, const uint8_t *body, uint64_t le
         *ticket = sl.ticket;
         return 0;
     }
+    sl.fast = false;
     if (!r) r = put_host(c, sl.in.p, body, len, c->h2d);
     if (r) {
         sl.busy = false;
@@ -3015,6 +3051,7 @@ int iggy_codec_encode_submit(iggy_codec_ctx *c, const iggy_raw_messages *m, uint
     }
     sl.cap = cap;
     sl.out_len = need;
+    sl.fast = false;
     sl.frame_pos = nullptr;
     sl.hout_dst = nullptr;
     sl.hout_len = 0;
@@ -3076,6 +3113,28 @@ int iggy_codec_poll(iggy_codec_ctx *c, iggy_ticket ticket, iggy_completion *out)
         (void)hipGetLastError();  // not an error: leave no sticky status for the caller's HIP code
         return IGGY_ERR_PENDING;
     }
+    if (q == hipSuccess && sl.op == IGGY_OP_DECODE && sl.fast && !sl.g_pending) {
+        // the records launch found a stride break the walk goes past: the general walk
+        // (its barrier words re-armed first), the positions, the completion event again
+        const size_t k = ticket & (kSlots - 1);
+        const iggy_decode_result *rr = (const iggy_decode_result *)((const uint8_t *)c->slot_pinned + 256 * k);
+        if (rr->status == kStatusNeedGeneral) {
+            hipStream_t s = bind(c, nullptr);
+            const DecodeScratch dsc = dscratch(c);
+            iggy_decode_result *d_res = (iggy_decode_result *)(c->slot_pinned_d + 256 * k);
+            hipLaunchKernelGGL(k_general_rearm, dim3(1), dim3(64), 0, s, GenRearm{dsc.gbar, dsc.gbar2, dsc.gmisc});
+            launch_general(c, sl.g_in, sl.g_len, sl.g_integ, sl.g_pos, sl.g_pcap, d_res, s);
+            if (sl.g_pos_copy)
+                (void)hipMemcpyAsync(host_pinned(sl.frame_pos, sl.g_pcap * 8) ? (void *)sl.frame_pos : sl.hout,
+                                     sl.pos.p, sl.g_pcap * 8, hipMemcpyDeviceToHost, s);
+            sl.g_pending = true;
+            if (hipGetLastError() != hipSuccess || hipEventRecord(sl.ev_done, s) != hipSuccess) {
+                sl.busy = false;
+                return IGGY_ERR_DEVICE;
+            }
+            return IGGY_ERR_PENDING;
+        }
+    }
     sl.busy = false;
     if (q != hipSuccess) return IGGY_ERR_DEVICE;
     memset(out, 0, sizeof(*out));
@@ -3109,11 +3168,14 @@ int iggy_codec_wait(iggy_codec_ctx *c, iggy_ticket ticket, iggy_completion *out)
     if (!c || !out) return IGGY_ERR_INVALID_ARGUMENT;
     Slot &sl = c->slots[ticket & (kSlots - 1)];
     if (!sl.busy || sl.ticket != ticket) return IGGY_ERR_INVALID_ARGUMENT;
-    {
-        DevGuard dg(c->device);
-        HIP_OK(hipEventSynchronize(sl.ev_done));
+    while (true) {  // (a fast-path decode's general walk, started by poll, means one more round)
+        {
+            DevGuard dg(c->device);
+            HIP_OK(hipEventSynchronize(sl.ev_done));
+        }
+        const int r = iggy_codec_poll(c, ticket, out);
+        if (r != IGGY_ERR_PENDING) return r;
     }
-    return iggy_codec_poll(c, ticket, out);
 }
 
 // -------------------------------------------------------------- profiling

@@ -45,6 +45,20 @@ struct GenRearm {
     uint64_t *gmisc;
 };
 
+// k_decode_general's barrier words re-armed on their own (before a general walk that no
+// uniform or records launch directly precedes)
+__global__ void k_general_rearm(GenRearm rearm) {
+    if (threadIdx.x == 0) {
+        __hip_atomic_store(&rearm.gbar[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&rearm.gbar[2], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&rearm.gbar[3], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&rearm.gmisc[2], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&rearm.gmisc[kPosCountWord], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (threadIdx.x < kBar2Words)
+        __hip_atomic_store(&rearm.gbar2[32 * threadIdx.x], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 struct RecState {  // zero between launches: zeroed when allocated, reset by the record's resolver
     uint64_t first_bad;  // ~min index of a frame whose checksum mismatches (max-encoded), 0 = none
     uint64_t spec_fail;  // ~min index of a frame that breaks the stride
@@ -115,7 +129,8 @@ __device__ __forceinline__ void launch_done(uint32_t *counter, uint32_t *host_fl
 }
 
 template <bool VERIFY>
-__device__ __forceinline__ void decode_record_block(const uint8_t *__restrict__ base, const RecTask *__restrict__ tasks,
+__device__ __forceinline__ void decode_record_block(const RecTask &inl, const uint8_t *__restrict__ base,
+                                                    const RecTask *__restrict__ tasks,
                                                     const uint32_t *__restrict__ wg_task, RecState *st,
                                                     uint64_t *bsums, uint64_t *frame_pos, iggy_polled_message *msgs,
                                                     iggy_decode_result *results) {
@@ -123,8 +138,10 @@ __device__ __forceinline__ void decode_record_block(const uint8_t *__restrict__ 
     __shared__ uint64_t s_min[4];
     __shared__ uint32_t s_last;
     __shared__ uint8_t s_small[256];  // short checksum inputs (N <= 24): 44 + 8 N bytes
-    const uint32_t t = wg_task[blockIdx.x];
-    const RecTask tk = tasks[t];
+    // one record: its task comes in the kernel arguments (tasks == nullptr), not from a
+    // table in host-mapped memory (two dependent PCIe reads before anything else)
+    const uint32_t t = tasks ? wg_task[blockIdx.x] : 0u;
+    const RecTask tk = tasks ? tasks[t] : inl;
     const uint32_t blk = blockIdx.x - tk.wg0;
     const uint8_t *body = base + tk.off;
     const uint8_t *blob = body + kHdr;
@@ -346,6 +363,10 @@ __device__ __forceinline__ void decode_record_block(const uint8_t *__restrict__ 
         return;
     }
 
+    // the record's first-bad / stride-fail words: final now, loaded beside the chain's
+    // block sums (one memory round trip, not two)
+    const uint64_t fb_enc = __hip_atomic_load(&st[t].first_bad, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint64_t sf_enc = __hip_atomic_load(&st[t].spec_fail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     uint64_t computed = 0;
     if (VERIFY && pl.long_cs) {
         const int j = lane & 7;
@@ -400,8 +421,6 @@ __device__ __forceinline__ void decode_record_block(const uint8_t *__restrict__ 
     }
     if (lane != 0) return;
     // precedence, as the uniform kernel's consumer (batch.rs:395-421, 461-506)
-    const uint64_t fb_enc = __hip_atomic_load(&st[t].first_bad, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const uint64_t sf_enc = __hip_atomic_load(&st[t].spec_fail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     // every block workgroup of the record has arrived: re-arm its state for the next launch
     __hip_atomic_store(&st[t].first_bad, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __hip_atomic_store(&st[t].spec_fail, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -450,7 +469,7 @@ __global__ __launch_bounds__(kRecThreads) void k_decode_records(const uint8_t *_
                                                                 iggy_polled_message *msgs,
                                                                 iggy_decode_result *results, uint32_t *counter,
                                                                 uint32_t *host_flag, uint32_t flag_value,
-                                                                GenRearm rearm) {
+                                                                GenRearm rearm, RecTask inl) {
     if (rearm.gbar && blockIdx.x == 0) {  // as k_decode_uniform's prologue
         if (threadIdx.x == 0) {
             __hip_atomic_store(&rearm.gbar[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -462,17 +481,17 @@ __global__ __launch_bounds__(kRecThreads) void k_decode_records(const uint8_t *_
         if (threadIdx.x < kBar2Words)
             __hip_atomic_store(&rearm.gbar2[32 * threadIdx.x], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-    decode_record_block<VERIFY>(base, tasks, wg_task, st, bsums, frame_pos, msgs, results);
+    decode_record_block<VERIFY>(inl, base, tasks, wg_task, st, bsums, frame_pos, msgs, results);
     launch_done(counter, host_flag, flag_value);
 }
 
 template __global__ void k_decode_records<true>(const uint8_t *__restrict__, const RecTask *__restrict__,
                                                 const uint32_t *__restrict__, RecState *, uint64_t *, uint64_t *,
                                                 iggy_polled_message *, iggy_decode_result *, uint32_t *, uint32_t *,
-                                                uint32_t, GenRearm);
+                                                uint32_t, GenRearm, RecTask);
 template __global__ void k_decode_records<false>(const uint8_t *__restrict__, const RecTask *__restrict__,
                                                  const uint32_t *__restrict__, RecState *, uint64_t *, uint64_t *,
                                                  iggy_polled_message *, iggy_decode_result *, uint32_t *, uint32_t *,
-                                                 uint32_t, GenRearm);
+                                                 uint32_t, GenRearm, RecTask);
 
 }  // namespace iggy
