@@ -634,6 +634,9 @@ constexpr uint32_t kErWave = kErSlots * kErStep + kErMeta;
 constexpr uint32_t kErWaves = IGGY_ER_WAVES;
 constexpr uint32_t kErThreads = 64 * kErWaves;
 constexpr uint32_t kErLds = kErWaves * kErWave;
+#ifndef IGGY_ER_NT
+#define IGGY_ER_NT 0
+#endif
 #ifndef IGGY_ER_MODE
 #define IGGY_ER_MODE 2  // (build knob: 0 every store from asm with sinks; 1 the 8 piece stores only;
                         //  2 no unconditional store -- the ring wait then counts loads only)
@@ -973,7 +976,12 @@ __global__ __launch_bounds__(SPLIT ? 2 * kErThreads : kErThreads, 1) void k_enc_
             } else if (IGGY_ER_MODE < 2) {
                 er_st16(whole ? (void *)(F + 8 + sp) : (void *)my_sink, w0, w1);
             } else if (whole) {
+#if IGGY_ER_NT  // (build knob for a same-box A/B: non-temporal piece stores)
+                const er_v4u v = {(uint32_t)w0, (uint32_t)(w0 >> 32), (uint32_t)w1, (uint32_t)(w1 >> 32)};
+                asm volatile("global_store_dwordx4 %0, %1, off nt" ::"v"(F + 8 + sp), "v"(v) : "memory");
+#else
                 st128_any(F + 8 + sp, make_uint4((uint32_t)w0, (uint32_t)(w0 >> 32), (uint32_t)w1, (uint32_t)(w1 >> 32)));
+#endif
             }
             const bool part = p_valid && sp < p_L && sp + 16 > p_L;
             tsp = part ? sp : tsp;

@@ -1,5 +1,4 @@
 set -u
 cd $GRAFT_REPO_ROOT
-timeout -k 10 120 python -u scripts/dbg_async.py 2>&1 | grep -v amdgpu.ids
-timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread > gpurun_out/t2.log 2>&1 || { echo "tests failed"; tail -30 gpurun_out/t2.log; exit 1; }
-tail -2 gpurun_out/t2.log
+rm -f gpurun_out/encab/summary.log
+LIBS="ab/lib_ernt0.so ab/lib_ernt1.so" bash scripts/gpu_encab.sh && cat gpurun_out/encab/summary.log | sed 's/"config".*"encode_ms"/encode_ms/; s/, "encode_gib_s.*hbm_frac/ hbm_frac/'
