@@ -25,8 +25,7 @@
 #define IGGY_ENC_RING 1  // (build knob for same-box A/B: 0 = k_enc_lanes for segmented encodes too)
 #endif
 #ifndef IGGY_ENC_SPLIT
-#define IGGY_ENC_SPLIT 0  // (build knob for same-box A/B: 1 = copier waves in k_enc_ring; measured
-                          //  2.51-2.71 ms against 1.36 ms without, encode.hip)
+#define IGGY_ENC_SPLIT 0  // (build knob for same-box A/B: 1 = writer waves in k_enc_ring, encode.hip)
 #endif
 #include "batch_checksum.hip"
 #include "decode_general.hip"
@@ -1050,7 +1049,7 @@ int iggy_codec_create(int device, iggy_codec_ctx **out) {
             hipFuncSetAttribute((const void *)k_enc_ring<false>,
                                 hipFuncAttributeMaxDynamicSharedMemorySize, kErLds) != hipSuccess ||
             hipFuncSetAttribute((const void *)k_enc_ring<true>,
-                                hipFuncAttributeMaxDynamicSharedMemorySize, kErLds) != hipSuccess)
+                                hipFuncAttributeMaxDynamicSharedMemorySize, kEsLds) != hipSuccess)
             r = IGGY_ERR_DEVICE;
     }
     if (!r) {
@@ -1734,7 +1733,7 @@ static int enqueue_encode(iggy_codec_ctx *c, const iggy_raw_messages *dm, uint64
         // checksum words. Unsegmented, the one k_enc_lanes launch hashes them after its
         // loop and runs the < 16-B payload-area fallback itself (own_tail).
         const bool ring = segmented && IGGY_ENC_RING;
-        // copier waves beside the hashers (k_enc_ring<true>) when every frame's payload
+        // writer waves beside the hashers (k_enc_ring<true>) when every frame's payload
         // keeps its source offset mod 16 in the output (P - out = 0 mod 16, encode.hip)
         const bool split = IGGY_ENC_SPLIT && ((((uintptr_t)m.payloads) - (uintptr_t)d_out) & 15) == 0;
         if (ring) {
@@ -1773,7 +1772,7 @@ static int enqueue_encode(iggy_codec_ctx *c, const iggy_raw_messages *dm, uint64
             const uint64_t F1 = k == nseg - 1 ? n : std::min<uint64_t>(n, 128 * B1 - 5);
             if (ring && split)
                 hipLaunchKernelGGL(k_enc_ring<true>, dim3((uint32_t)std::min<uint64_t>((n + 63) / 64, lcu)),
-                                   dim3(2 * kErThreads), kErLds, s, m, es, d_out, F0, F1,
+                                   dim3(2 * kErThreads), kEsLds, s, m, es, d_out, F0, F1,
                                    (const uint4 *)c->erec.as<uint4>(), c->esink.as<uint8_t>());
             else if (ring)
                 hipLaunchKernelGGL(k_enc_ring<false>, dim3((uint32_t)std::min<uint64_t>((n + 63) / 64, lcu)),

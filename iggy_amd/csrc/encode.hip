@@ -692,26 +692,37 @@ __global__ __launch_bounds__(256) void k_enc_recs(iggy_raw_messages m, EncScratc
     }
 }
 
-// ---- copier waves (SPLIT form): the hasher waves above store no payload bytes.
-// A SPLIT workgroup has kErWaves copier waves beside its kErWaves hashers; copier
-// wave kErWaves + w copies the payloads of hasher w's frames (same frame order) from
-// the input to the output, 16-B chunks, without any hand-off: a frame's record (erec,
-// k_enc_recs) gives its payload offset and length. The payload is read twice, by the
-// hasher's LDS-DMA and by the copier, in the same order and close in time, so the
-// second read mostly hits L2 or MALL (the profile's FETCH_SIZE says how much).
-// An earlier form passed the hasher's landed LDS slots to a writer wave with LDS flags.
-// Near the end of a wave's frames its writer's global stores stalled for as long as
-// the hasher spun on the writer's flag, and were released the moment the hasher
-// stopped spinning: the 4-s bug guard tripped and the encode failed. Store-free writers
-// never stalled, and no flag form (DS or FLAT, sleep or not, drained DMA, another SIMD)
-// helped; independent copiers need no flag at all. They are correct but slower: same
-// box, C3 encode 2.51 / 2.59 / 2.71 ms (16-B chunks in flight per lane 32 / 16 / 8)
-// against 1.36 ms for the hashers storing the payload themselves, so the host builds
-// without them (IGGY_ENC_SPLIT 0, codec_api.hip).
+// ---- writer waves (SPLIT form): the hasher waves above store no payload bytes.
+// A SPLIT workgroup has kErWaves writer waves beside its kErWaves hashers; writer
+// wave kErWaves + w reads hasher w's landed LDS slots back and stores the frames'
+// payload bytes, so the hashers' constant-vmcnt ring waits cover their loads (and two
+// small stores per frame) only. Hand-off in lockstep: every wave of the workgroup
+// runs the same number of steps K (the workgroup's longest hasher sequence) and
+// meets the others at one workgroup barrier per step. Step k: a hasher waits for its
+// step-k loads, reads the slot, writes the step's descriptors (per frame group: the
+// destination of stream byte 0, hashed length, block, window misalignment), reaches
+// barrier k, then refills the slot of step k - 1 with step k + S - 1 and hashes step
+// k; a writer reaches barrier k, reads slot k and its descriptors, then stores, and
+// its reads have returned before it reaches barrier k + 1. Nobody spins: the first
+// form of this split (LDS flags, the hasher polling the writer's progress) saw the
+// writer's global stores stall for as long as the hasher polled and resume the
+// moment it stopped, at the 4-s bug guard; a second form (writer waves copying the
+// payloads from the input on their own) was exact but took 2.51-2.71 ms against
+// 1.36 ms. This lockstep form is exact and never stalls, but same box: 1.60 ms against
+// 1.36 (1.02 ms with the writers storing nothing), so the host builds without it
+// (IGGY_ENC_SPLIT 0, codec_api.hip).
 // With payloads and output 16-B congruent (P - out = 0 mod 16: 48-B frame headers keep
 // every payload at the same offset mod 16 from its source; the host launches the SPLIT
-// form only then), each chunk is one aligned 16-B load and store, except the two that
-// straddle the payload's ends (aligned 8/4/2/1-B pieces).
+// form only then), each window chunk is one aligned 16-B store, except the chunks that
+// straddle the payload's ends (aligned 8/4/2/1-B pieces). The frame header (40 B) and
+// the checksum word are the hasher's.
+constexpr uint32_t kEsSlots = 4;  // 3 steps in flight while one is hashed
+constexpr uint32_t kEsDesc = kEsSlots * 128;  // [slot][group] {dst lo, dst hi, L, block | r << 16 | valid << 24}
+constexpr uint32_t kEsWave = kEsSlots * kErStep + kErMeta + kEsDesc;
+constexpr uint32_t kEsLds = kErWaves * kEsWave + 16;  // + the hashers' step counts
+static_assert(kEsLds <= 160 * 1024, "LDS budget (split ring)");
+static_assert(kEsSlots <= 4, "the issue side runs kEsSlots - 1 steps ahead of the record copy (<= 4)");
+
 typedef __attribute__((address_space(1))) uint8_t g_u8;
 typedef __attribute__((address_space(1))) uint16_t g_u16;
 typedef __attribute__((address_space(1))) uint32_t g_u32;
@@ -741,48 +752,46 @@ __device__ inline void es_store_range(g_u8 *d, es_u32x4 v, uint32_t x0, uint32_t
     }
 }
 
-// the payloads of frames f_lo + 8 vw + fg + j stride (j = 0, 1, ...; < n): lane l of
-// frame group fg copies chunks l, l + 8, ... of its frame, kEcUnroll per pass
-#ifndef IGGY_EC_UNROLL
-#define IGGY_EC_UNROLL 16  // (build knob: chunks in flight per lane)
-#endif
-constexpr uint32_t kEcUnroll = IGGY_EC_UNROLL;
-__device__ __forceinline__ void enc_ring_copier(const uint8_t *P, uint8_t *out, const uint4 *erec, uint64_t f_lo,
-                                                uint64_t n, uint64_t vw, uint64_t nvw, int lane) {
+// the workgroup barrier without a memory fence (__syncthreads would drain every
+// wave's vmcnt: the hashers' loads in flight and the writers' stores)
+__device__ __forceinline__ void es_barrier() {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+}
+
+// writer wave of the hasher whose LDS region is `region`: K lockstep steps
+__device__ __forceinline__ void enc_ring_writer(const uint8_t *smem, uint32_t region, int lane, uint32_t K) {
     const uint32_t l = lane & 7, fg = (uint32_t)lane >> 3;
-    const uint64_t stride = 8 * nvw;
-    for (uint64_t f = f_lo + 8 * vw + fg;; f += stride) {
-        const bool v = f < n;
-        if (!__ballot(v)) break;
-        uint64_t po = 0;
-        uint32_t pl = 0;
-        if (v) {
-            const uint4 rec = erec[2 * f];
-            po = (uint64_t)rec.x | ((uint64_t)rec.y << 32);
-            pl = rec.z;
-        }
-        const uint64_t s0 = (uint64_t)(uintptr_t)(P + po), s1 = s0 + pl, a0 = s0 & ~15ull;
-        // destination of source byte s: s + delta (frame payload at out + 256 + 48 (f + 1) + po)
-        const uint64_t delta = (uint64_t)(uintptr_t)(out + 304 + 48 * f) - (uint64_t)(uintptr_t)P;
-        const uint32_t nch = v && pl ? (uint32_t)((s1 + 15 - a0) >> 4) : 0u;
-        for (uint32_t c = l; c < nch; c += 8 * kEcUnroll) {
-            es_u32x4 d[kEcUnroll];
+    for (uint32_t k = 0; k < K; ++k) {
+        es_barrier();  // step k's slot and descriptors are in
+        const uint32_t slot = region + (k % kEsSlots) * kErStep;
+        const uint4 dsc = *(const uint4 *)(smem + region + kEsSlots * kErStep + kErMeta + 128 * (k % kEsSlots) + 16 * fg);
+        es_u32x4 c[8];
 #pragma unroll
-            for (uint32_t u = 0; u < kEcUnroll; ++u) {
-                const uint32_t cc = c + 8 * u;
-                if (cc < nch) d[u] = *(const g_u128 *)(uintptr_t)(a0 + 16ull * cc);
-            }
+        for (int q = 0; q < 8; ++q) c[q] = *(const es_u32x4 *)(smem + slot + 1024u * q + 16u * (uint32_t)lane);
+        const es_u32x4 c64 = *(const es_u32x4 *)(smem + slot + 8192u + 128u * fg);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // read out before barrier k + 1 (the refill)
+        if ((dsc.w >> 24) == 0) continue;
+        g_u8 *F8 = (g_u8 *)((uint64_t)dsc.x | ((uint64_t)dsc.y << 32));  // destination of stream byte 0
+        const int64_t L = dsc.z;
+        const int64_t pb = dsc.w & 0xffff;
+        const int64_t r = (dsc.w >> 16) & 0xff;
+        // window chunk cc covers stream [pb * 1024 + 16 cc - r, + 16): r == 0 -> chunks
+        // 0..63, r > 0 -> 1..64 (chunk 0 straddles the block start: the previous block's 64)
 #pragma unroll
-            for (uint32_t u = 0; u < kEcUnroll; ++u) {
-                const uint32_t cc = c + 8 * u;
-                if (cc >= nch) break;
-                const uint64_t sc = a0 + 16ull * cc;
-                const uint32_t x0 = sc < s0 ? (uint32_t)(s0 - sc) : 0u;
-                const uint32_t x1 = sc + 16 > s1 ? (uint32_t)(s1 - sc) : 16u;
-                g_u8 *dd = (g_u8 *)(uintptr_t)(sc + delta);
-                if (x0 == 0 && x1 == 16) *(g_u128 *)dd = d[u];
-                else es_store_range(dd, d[u], x0, x1);
-            }
+        for (int q = 0; q < 9; ++q) {
+            if (q == 8 && l != 0) break;
+            const int64_t cc = q < 8 ? 8 * q + l : 64;
+            if (cc == 0 && r != 0) continue;
+            if (cc == 64 && r == 0) continue;
+            const int64_t sp = pb * 1024 + 16 * cc - r;
+            const int64_t a = sp > 40 ? sp : 40, b = sp + 16 < L ? sp + 16 : L;
+            if (a >= b) continue;
+            const es_u32x4 v = q < 8 ? c[q] : c64;
+            g_u8 *d = F8 + sp;
+            if (a == sp && b == sp + 16) *(g_u128 *)d = v;
+            else es_store_range(d, v, (uint32_t)(a - sp), (uint32_t)(b - sp));
         }
     }
 }
@@ -791,7 +800,9 @@ template <bool SPLIT>
 __global__ __launch_bounds__(SPLIT ? 2 * kErThreads : kErThreads, 1) void k_enc_ring(iggy_raw_messages m, EncScratch es,
                                                                                 uint8_t *out, uint64_t f_lo, uint64_t f_hi,
                                                                                 const uint4 *erec, uint8_t *sink) {
-    constexpr uint32_t S = kErSlots;  // ring slots per hasher wave
+    constexpr uint32_t S = SPLIT ? kEsSlots : kErSlots;   // ring slots per hasher wave
+    constexpr uint32_t WAVE = SPLIT ? kEsWave : kErWave;   // LDS per hasher wave
+    constexpr uint32_t AHEAD = SPLIT ? S - 1 : S;           // steps issued ahead of the processed one
     const uint64_t ptot = es.misc[4];
     if (ptot < 16 || es.misc[5]) return;  // tiny payload area (k_enc_frames) or over capacity
     const uint64_t N = m.count;           // erec[2 N]: the "no frame" record
@@ -801,16 +812,18 @@ __global__ __launch_bounds__(SPLIT ? 2 * kErThreads : kErThreads, 1) void k_enc_
     const uint32_t lbase = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(lds_u8 *)smem);
     const int lane = threadIdx.x & 63;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    if (SPLIT && wave >= kErWaves) {  // the copier of hasher wave - kErWaves
-        enc_ring_copier(m.payloads, out, erec, f_lo, n, (uint64_t)blockIdx.x * kErWaves + (wave - kErWaves),
-                        (uint64_t)gridDim.x * kErWaves, lane);
+    uint32_t *s_steps = (uint32_t *)(smem + kErWaves * kEsWave);  // (SPLIT) each hasher wave's step count
+    if (SPLIT && wave >= kErWaves) {  // the writer of hasher wave - kErWaves
+        es_barrier();                 // the step counts are in
+        const uint32_t K = max(max(s_steps[0], s_steps[1]), max(s_steps[2], s_steps[3]));
+        enc_ring_writer(smem, (wave - kErWaves) * WAVE, lane, K);
         return;
     }
     const uint32_t l = lane & 7, m8 = l >> 1, par = l & 1, fg = (uint32_t)lane >> 3;
     const uint32_t poff = 16 * (m8 + 4 * par);
     const uint64_t vw = (uint64_t)blockIdx.x * kErWaves + wave, nvw = (uint64_t)gridDim.x * kErWaves;
     const uint64_t stride = 8 * nvw;
-    const uint32_t region = __builtin_amdgcn_readfirstlane(wave * kErWave);
+    const uint32_t region = __builtin_amdgcn_readfirstlane(wave * WAVE);
     const uint8_t *P = m.payloads;
     const uint8_t *dummy = P;  // (ptot >= 16)
     uint8_t *my_sink = sink + ((vw & 255) << 10) + 16 * lane;
@@ -836,6 +849,26 @@ __global__ __launch_bounds__(SPLIT ? 2 * kErThreads : kErThreads, 1) void k_enc_
         const uint64_t f = fbase + j * stride;
         return f < n ? f : N;
     };
+    uint32_t K = 0;  // (SPLIT) the workgroup's lockstep step count
+    if (SPLIT) {
+        // this wave's steps: per frame group the sum of its frames' blocks, the max over
+        // the groups; the workgroup runs the largest of its hashers' counts
+        uint32_t st = 0;
+        for (uint64_t j = l;; j += 8) {
+            const uint64_t f = fidx(j);
+            if (!__ballot(f < N)) break;
+            if (f < N) st += (uint32_t)((40 + (uint64_t)erec[2 * f].z + 1023) >> 10);
+        }
+        st += __shfl_xor(st, 1);
+        st += __shfl_xor(st, 2);
+        st += __shfl_xor(st, 4);
+        st = max(st, (uint32_t)__shfl_xor(st, 8));
+        st = max(st, (uint32_t)__shfl_xor(st, 16));
+        st = max(st, (uint32_t)__shfl_xor(st, 32));
+        if (lane == 0) s_steps[wave] = st;
+        es_barrier();
+        K = max(max(s_steps[0], s_steps[1]), max(s_steps[2], s_steps[3]));
+    }
     const uint32_t meta = region + S * kErStep + 144 * fg;  // the group's record ring
 #pragma unroll
     for (uint32_t k = 0; k < 4; ++k)
@@ -892,9 +925,9 @@ __global__ __launch_bounds__(SPLIT ? 2 * kErThreads : kErThreads, 1) void k_enc_
     uint32_t o5[5] = {0, 0, 0, 0, 0};
     uint64_t a0 = init0, a1 = init1, id0 = 0, id1 = 0;
     uint4 lastp = make_uint4(0, 0, 0, 0);
-    for (uint32_t k = 0; k < S; ++k) issue(region + k * kErStep);
+    for (uint32_t k = 0; k < AHEAD; ++k) issue(region + k * kErStep);
     uint32_t k = 0;
-    for (;; ++k) {
+    for (; !SPLIT || k < K; ++k) {
         if (pb == 0) {
             const uint4 rec = *(const uint4 *)(smem + meta + 16 * (pj & 7));
             p_f = fidx(pj);
@@ -917,12 +950,19 @@ __global__ __launch_bounds__(SPLIT ? 2 * kErThreads : kErThreads, 1) void k_enc_
             a0 = init0;
             a1 = init1;
         }
-        if (!__ballot(p_valid)) break;
+        if (!SPLIT && !__ballot(p_valid)) break;
         // step k landed. Issued after its loads: the stores of the kErSlots steps
         // before it and the loads of the later steps -- except in the first kErSlots
         // iterations, which wait for everything.
-        if (k < S) wait_vm_const<0>();
+        if (k < AHEAD) wait_vm_const<0>();
+        else if (SPLIT) wait_vm_const<9 * (S - 2)>();
         else wait_vm_const<9 * (kErSlots - 1) + kErStores * kErSlots>();
+        if (SPLIT && l == 0) {  // the step's descriptors for the writer (read after barrier k)
+            const uint64_t d8 = (uint64_t)(uintptr_t)(F + 8);
+            const uint32_t r = (uint32_t)((uintptr_t)(P + (F - out - 256 - 48 * p_f) - 40) & 15);
+            *(uint4 *)(smem + region + S * kErStep + kErMeta + 128 * (k % S) + 16 * fg) =
+                make_uint4((uint32_t)d8, (uint32_t)(d8 >> 32), (uint32_t)p_L, pb | (r << 16) | ((p_valid ? 1u : 0u) << 24));
+        }
         const uint32_t slot = region + (k % S) * kErStep;
         const uint8_t *row = smem + slot + 128 * fg;
         uint4 pc[8];
@@ -951,7 +991,12 @@ __global__ __launch_bounds__(SPLIT ? 2 * kErThreads : kErThreads, 1) void k_enc_
             id1 = first ? ((uint64_t)ids.z | ((uint64_t)ids.w << 32)) : id1;
         }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // slot read out before it is refilled
-        issue(slot);
+        if (SPLIT) {
+            es_barrier();  // barrier k: the writer reads slot k; slot k - 1 is free
+            issue(region + ((k + S - 1) % S) * kErStep);
+        } else {
+            issue(slot);
+        }
         // the block's pieces: header words substituted, stored, hashed
         const bool full = lng && pb < nbF;
         uint64_t q0[4] = {0, 0, 0, 0}, q1[4] = {0, 0, 0, 0};

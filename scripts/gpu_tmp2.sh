@@ -1,4 +1,5 @@
 set -u
 cd $GRAFT_REPO_ROOT
-rm -f gpurun_out/encab/summary.log
-LIBS="ab/lib_ernt0.so ab/lib_ernt1.so" bash scripts/gpu_encab.sh && cat gpurun_out/encab/summary.log | sed 's/"config".*"encode_ms"/encode_ms/; s/, "encode_gib_s.*hbm_frac/ hbm_frac/'
+for r in 1 2; do for lib in ab/lib_ns.so ab/lib_bs.so ab/lib_bsn.so; do
+IGGY_DIAG_LIB=$lib timeout -k 10 120 python3 -u scripts/bench_encode.py --steps 10 --no-check 2>&1 | grep '^{' | sed "s#^#$lib #"
+done; done
