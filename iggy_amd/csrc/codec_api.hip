@@ -35,6 +35,7 @@
 #include "poll.hip"
 #include "slice.hip"
 #include "crypt.hip"
+static_assert(!IGGY_ENC_SPLIT || iggy::kErWaves == 4, "the writer-wave split is built for 4 hasher waves");
 
 using namespace iggy;
 
@@ -1048,8 +1049,8 @@ int iggy_codec_create(int device, iggy_codec_ctx **out) {
                                 hipFuncAttributeMaxDynamicSharedMemorySize, kGenLds) != hipSuccess ||
             hipFuncSetAttribute((const void *)k_enc_ring<false>,
                                 hipFuncAttributeMaxDynamicSharedMemorySize, kErLds) != hipSuccess ||
-            hipFuncSetAttribute((const void *)k_enc_ring<true>,
-                                hipFuncAttributeMaxDynamicSharedMemorySize, kEsLds) != hipSuccess)
+            (IGGY_ENC_SPLIT && hipFuncSetAttribute((const void *)k_enc_ring<true>,
+                                                   hipFuncAttributeMaxDynamicSharedMemorySize, kEsLds) != hipSuccess))
             r = IGGY_ERR_DEVICE;
     }
     if (!r) {

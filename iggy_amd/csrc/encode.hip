@@ -637,15 +637,20 @@ constexpr uint32_t kErLds = kErWaves * kErWave;
 #ifndef IGGY_ER_NT
 #define IGGY_ER_NT 0
 #endif
+#ifndef IGGY_ER_NOSTORE
+#define IGGY_ER_NOSTORE 0  // (timing-only build knob, wrong output: mode 2 without the frame byte stores)
+#endif
 #ifndef IGGY_ER_MODE
 #define IGGY_ER_MODE 2  // (build knob: 0 every store from asm with sinks; 1 the 8 piece stores only;
-                        //  2 no unconditional store -- the ring wait then counts loads only)
+                        //  2 no unconditional store -- the ring wait then counts loads only;
+                        //  3 every store from asm, lanes without bytes masked off, one lane
+                        //    writing its sink only when no lane of the wave has bytes)
 #endif
-constexpr uint32_t kErStores = IGGY_ER_MODE == 0 ? 14 : IGGY_ER_MODE == 1 ? 8 : 0;  // stores per step, at least
+constexpr uint32_t kErStores = (IGGY_ER_MODE == 0 || IGGY_ER_MODE == 3) ? 14 : IGGY_ER_MODE == 1 ? 8 : 0;  // stores per step, at least
 constexpr uint64_t kErSinkBytes = 256 << 10; // 256 wave slots x 64 lanes x 16 B
 static_assert(kErLds <= 160 * 1024, "LDS budget");
 static_assert(9 * (kErSlots - 1) + kErStores * kErSlots <= 63, "the ring wait fits vmcnt");
-static_assert(IGGY_ER_MODE >= 0 && IGGY_ER_MODE <= 2, "store mode");
+static_assert(IGGY_ER_MODE >= 0 && IGGY_ER_MODE <= 3, "store mode");
 // a frame's record is copied into the ring when its group's frame four ahead starts;
 // the issue side runs kErSlots steps ahead of that copy, so at most 4 slots (a 5-slot
 // build read a stale record and faulted)
@@ -667,6 +672,12 @@ __device__ __forceinline__ void er_st2(void *p, uint32_t v) {
 }
 __device__ __forceinline__ void er_st1(void *p, uint32_t v) {
     asm volatile("global_store_byte %0, %1, off" ::"v"(p), "v"(v) : "memory");
+}
+// (mode 3) exactly one store instruction per call and wave: the lanes with bytes store
+// them; when no lane has any, lane 0 alone writes its sink slot (so the instruction
+// still issues and counts once in vmcnt)
+__device__ __forceinline__ bool er_act(bool has) {
+    return has || (__ballot(has) == 0 && (threadIdx.x & 63) == 0);
 }
 
 // erec[2 i] = {po lo, po hi, payload length, timestamp delta}, erec[2 i + 1] = the ids;
@@ -720,7 +731,7 @@ constexpr uint32_t kEsSlots = 4;  // 3 steps in flight while one is hashed
 constexpr uint32_t kEsDesc = kEsSlots * 128;  // [slot][group] {dst lo, dst hi, L, block | r << 16 | valid << 24}
 constexpr uint32_t kEsWave = kEsSlots * kErStep + kErMeta + kEsDesc;
 constexpr uint32_t kEsLds = kErWaves * kEsWave + 16;  // + the hashers' step counts
-static_assert(kEsLds <= 160 * 1024, "LDS budget (split ring)");
+static_assert(kEsLds <= 160 * 1024 || kErWaves != 4, "LDS budget (split ring; only built with 4 hashers)");
 static_assert(kEsSlots <= 4, "the issue side runs kEsSlots - 1 steps ahead of the record copy (<= 4)");
 
 typedef __attribute__((address_space(1))) uint8_t g_u8;
@@ -1018,9 +1029,11 @@ __global__ __launch_bounds__(SPLIT ? 2 * kErThreads : kErThreads, 1) void k_enc_
             const bool whole = p_valid && sp + 16 <= p_L;
             if (SPLIT) {
                 // (the writer wave stores the payload; the header words are stored below)
+            } else if (IGGY_ER_MODE == 3) {
+                if (er_act(whole)) er_st16(whole ? (void *)(F + 8 + sp) : (void *)my_sink, w0, w1);
             } else if (IGGY_ER_MODE < 2) {
                 er_st16(whole ? (void *)(F + 8 + sp) : (void *)my_sink, w0, w1);
-            } else if (whole) {
+            } else if (whole && !IGGY_ER_NOSTORE) {
 #if IGGY_ER_NT  // (build knob for a same-box A/B: non-temporal piece stores)
                 const er_v4u v = {(uint32_t)w0, (uint32_t)(w0 >> 32), (uint32_t)w1, (uint32_t)(w1 >> 32)};
                 asm volatile("global_store_dwordx4 %0, %1, off nt" ::"v"(F + 8 + sp), "v"(v) : "memory");
@@ -1045,8 +1058,23 @@ __global__ __launch_bounds__(SPLIT ? 2 * kErThreads : kErThreads, 1) void k_enc_
                                   : l == 3 ? (p_pl << 32) : 0ull;
                 st64_any(F + 8 + 8 * l, hw);
             }
+        } else if (IGGY_ER_MODE == 3) {  // the partial piece: 8-, 4-, 2-, 1-byte stores, masked
+            const bool has = tsp != ~0ull;
+            const uint32_t remb = has ? (uint32_t)(p_L - tsp) : 0u;
+            uint8_t *d = F + 8 + (has ? tsp : 0);
+            uint64_t v = tw;
+            if (er_act(remb & 8)) er_st8((remb & 8) ? (void *)d : (void *)my_sink, v);
+            d += (remb & 8);
+            v = (remb & 8) ? tw1 : v;
+            if (er_act(remb & 4)) er_st4((remb & 4) ? (void *)d : (void *)my_sink, (uint32_t)v);
+            d += (remb & 4);
+            v = (remb & 4) ? (v >> 32) : v;
+            if (er_act(remb & 2)) er_st2((remb & 2) ? (void *)d : (void *)my_sink, (uint32_t)v);
+            d += (remb & 2);
+            v = (remb & 2) ? (v >> 16) : v;
+            if (er_act(remb & 1)) er_st1((remb & 1) ? (void *)d : (void *)my_sink, (uint32_t)v);
         } else if (IGGY_ER_MODE > 0) {  // the partial piece and the checksum words: plain stores
-            if (tsp != ~0ull) {
+            if (!IGGY_ER_NOSTORE && tsp != ~0ull) {
                 uint8_t *d = F + 8 + tsp;
                 const uint32_t remb = (uint32_t)(p_L - tsp);
                 uint64_t v = tw;
@@ -1094,6 +1122,9 @@ __global__ __launch_bounds__(SPLIT ? 2 * kErThreads : kErThreads, 1) void k_enc_
             if (SPLIT) {  // lane 0 the frame's checksum word, lane 2 (the same hash) its copy
                 if (fin && lng && l == 0) st64_any(F, hsh);
                 if (fin && lng && l == 2) es.cs[p_f] = hsh;
+            } else if (IGGY_ER_MODE == 3) {
+                if (er_act(st)) er_st8(st ? (void *)F : (void *)my_sink, hsh);
+                if (er_act(st)) er_st8(st ? (void *)(es.cs + p_f) : (void *)(my_sink + 8), hsh);
             } else if (IGGY_ER_MODE > 0) {
                 if (st) {
                     st64_any(F, hsh);
