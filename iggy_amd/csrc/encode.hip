@@ -640,6 +640,9 @@ constexpr uint32_t kErLds = kErWaves * kErWave;
 #ifndef IGGY_ER_NOSTORE
 #define IGGY_ER_NOSTORE 0  // (timing-only build knob, wrong output: mode 2 without the frame byte stores)
 #endif
+#ifndef IGGY_ER_A128
+#define IGGY_ER_A128 0  // (timing-only build knob, wrong output: piece stores to 128-B-aligned runs)
+#endif
 #ifndef IGGY_ER_MODE
 #define IGGY_ER_MODE 2  // (build knob: 0 every store from asm with sinks; 1 the 8 piece stores only;
                         //  2 no unconditional store -- the ring wait then counts loads only;
@@ -1033,6 +1036,11 @@ __global__ __launch_bounds__(SPLIT ? 2 * kErThreads : kErThreads, 1) void k_enc_
                 if (er_act(whole)) er_st16(whole ? (void *)(F + 8 + sp) : (void *)my_sink, w0, w1);
             } else if (IGGY_ER_MODE < 2) {
                 er_st16(whole ? (void *)(F + 8 + sp) : (void *)my_sink, w0, w1);
+            } else if (IGGY_ER_A128) {  // (timing only, wrong output: each group's run 128-B aligned)
+                if (whole) {
+                    uint8_t *Fa = (uint8_t *)((uintptr_t)(F + 8) & ~(uintptr_t)127);
+                    st128_any(Fa + sp, make_uint4((uint32_t)w0, (uint32_t)(w0 >> 32), (uint32_t)w1, (uint32_t)(w1 >> 32)));
+                }
             } else if (whole && !IGGY_ER_NOSTORE) {
 #if IGGY_ER_NT  // (build knob for a same-box A/B: non-temporal piece stores)
                 const er_v4u v = {(uint32_t)w0, (uint32_t)(w0 >> 32), (uint32_t)w1, (uint32_t)(w1 >> 32)};
