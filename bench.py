@@ -323,11 +323,15 @@ def c1_leg(cx, dev, seconds: float):
     for _raw, _t, _out, eres in denc:
         er = abi.EncodeResult.from_buffer_copy(to_host(eres).tobytes())
         assert er.error.kind == 0, er.error
-    t0 = time.perf_counter()
-    for _ in range(5):
+    def host_pass():
         for group in (recs[:8], recs[8:]):  # at most 8 in flight per context
             for t in [cx.decode_submit(r, 0) for r in group]:
                 cx.wait(t)
+
+    host_pass()  # untimed: the slots' pinned staging is allocated on first use
+    t0 = time.perf_counter()
+    for _ in range(5):
+        host_pass()
     host_us = (time.perf_counter() - t0) / (5 * nb) * 1e6
     # the synchronous host decode (iggy_codec_decode_batch: one k_decode_records launch
     # and a host-mapped flag), pageable records, then the same records registered

@@ -135,6 +135,10 @@ struct Slot {
     DevBuf in, pos, out, res;                    // device input / positions / encode output / result
     DevBuf ids, ots, pay, plen, uhb, uhl;        // encode SoA inputs
     HostMap tab;                                 // k_decode_records task table of an in-flight decode
+    // a pageable input of the fast path, copied here at submit: the kernel reads it in
+    // place (<= kZeroCopyBytes) or one DMA copies it, and the slot keeps it until it is
+    // done, so submit never waits on the stream for the caller's bytes
+    HostMap zin;
     hipEvent_t ev_in = nullptr, ev_k = nullptr, ev_done = nullptr;
     // a pageable caller output is never a DMA target: the copy-out stream lands it in
     // this pinned bounce and iggy_codec_poll copies it to the caller (hout_dst, hout_len)
@@ -159,6 +163,7 @@ struct Slot {
         DevBuf *b[] = {&in, &pos, &out, &res, &ids, &ots, &pay, &plen, &uhb, &uhl};
         for (DevBuf *x : b) x->release();
         tab.release();
+        zin.release();
         for (hipEvent_t *e : {&ev_in, &ev_k, &ev_done})
             if (*e) (void)hipEventDestroy(*e), *e = nullptr;
         if (hout) (void)hipHostFree(hout);
@@ -215,6 +220,9 @@ struct iggy_codec_ctx {
     HostMap rmap;  // task table + workgroup map (read by the kernel in place when small)
     HostMap cmap;  // chunk-walk candidates (read in place)
     HostMap omap;  // [0, 64): completion flag; then results / positions / chunk-walk outputs
+    // a pageable record of <= kZeroCopyBytes for the synchronous fast path, copied here
+    // and read by the kernel in place (no H2D)
+    HostMap zin;
     uint32_t hseq = 0;  // completion flag values
     uint32_t chunk_epoch = 0;  // k_chunk_walk link tags
     // segment writer: pinned staging halves and their copy events
@@ -646,7 +654,10 @@ int reset_after_timeout(iggy_codec_ctx *c) {
 
 // synchronous decode of a host buffer; also used by stamp / checksum helpers
 constexpr uint64_t kHostFastBytes = 16ull << 20;
-constexpr uint64_t kZeroCopyBytes = 1ull << 20;  // registered inputs up to this size are read in place
+#ifndef IGGY_ZERO_COPY_BYTES
+#define IGGY_ZERO_COPY_BYTES (4ull << 20)  // (build knob for same-box A/B: 1 MiB measured slower)
+#endif
+constexpr uint64_t kZeroCopyBytes = IGGY_ZERO_COPY_BYTES;  // host inputs up to this size are read in place
 int decode_host_fast(iggy_codec_ctx *c, const uint8_t *body, uint64_t len, int integrity,
                      iggy_decode_result *res_out, uint64_t *frame_pos, uint64_t cap, bool *done);
 int decode_host(iggy_codec_ctx *c, const uint8_t *body, uint64_t len, int integrity,
@@ -964,6 +975,13 @@ int decode_host_fast(iggy_codec_ctx *c, const uint8_t *body, uint64_t len, int i
     const uint8_t *d_base = nullptr;
     if (len <= kZeroCopyBytes) d_base = host_device_ptr(body, len);
     int r = 0;
+    if (!d_base && len <= kZeroCopyBytes && !host_pinned(body, len)) {
+        // pageable: into the context's own mapped staging, read in place (the previous
+        // fast call's kernel is done: every synchronous entry waits for its flag)
+        if (c->zin.ensure(len + 16)) return IGGY_ERR_DEVICE;
+        memcpy(c->zin.h, body, len);
+        d_base = c->zin.d;
+    }
     if (!d_base) {
         if (c->din.ensure(len + 16)) return IGGY_ERR_DEVICE;
         r = put_host(c, c->din.p, body, len, c->stream);
@@ -1130,6 +1148,7 @@ void iggy_codec_destroy(iggy_codec_ctx *c) {
     c->rmap.release();
     c->cmap.release();
     c->omap.release();
+    c->zin.release();
     if (c->cr_pinned) {  // GHASH tables of the key: cleared before the pages go back
         volatile uint8_t *z = (volatile uint8_t *)c->cr_pinned;
         for (size_t i = 0; i < kCrTabBytesHost; ++i) z[i] = 0;
@@ -2929,13 +2948,30 @@ int iggy_codec_decode_submit(iggy_codec_ctx *c, const uint8_t *body, uint64_t le
     uint64_t nf = 0;
     if (!r && c->slot_pinned_d && len <= kHostFastBytes && rec_plan(body, len, &nf)) {
         // a single-stride record of <= 16 MiB, all on the context's stream: the input
-        // (read in place when registered and <= 1 MiB, else copied), one
+        // (read in place when <= kZeroCopyBytes, else copied), one
         // k_decode_records launch whose verdict lands in the slot's host-mapped
         // completion record, k_decode_general behind it for a stride that breaks
         // mid-record, the positions back, the completion event
         hipStream_t s = bind(c, nullptr);
         const uint8_t *d_in = len <= kZeroCopyBytes ? host_device_ptr(body, len) : nullptr;
-        if (!d_in) {
+        if (!d_in && !host_pinned(body, len)) {
+            // pageable: copied into the slot's own pinned staging now (the caller's bytes
+            // are free when submit returns), then read in place or DMA'd from there; the
+            // slot holds the staging until the ticket completes, so nothing here waits
+            if (sl.zin.ensure(len + 16)) {
+                r = IGGY_ERR_DEVICE;
+            } else {
+                memcpy(sl.zin.h, body, len);
+                if (len <= kZeroCopyBytes) {
+                    d_in = sl.zin.d;
+                } else {
+                    if (hipMemcpyAsync(sl.in.p, sl.zin.h, len, hipMemcpyHostToDevice, s) != hipSuccess)
+                        r = IGGY_ERR_DEVICE;
+                    d_in = sl.in.as<uint8_t>();
+                }
+            }
+        }
+        if (!d_in && !r) {  // pinned caller memory above kZeroCopyBytes: one DMA (settled below)
             r = put_host(c, sl.in.p, body, len, s);
             d_in = sl.in.as<uint8_t>();
         }

@@ -219,9 +219,10 @@ int iggy_codec_xxh3_64(iggy_codec_ctx *ctx, const void *data, uint64_t len, uint
 
 /* decode_batch_slice_with (batch.rs:391-422). On Ok, fills *hdr and, if
  * frame_pos != NULL, the blob-relative start of every frame (up to cap;
- * IGGY_ERR_CAPACITY if more). `body` may extend past batch_length. A registered
- * (iggy_codec_host_register) record of <= 1 MiB is read by the kernel in place
- * through its device-mapped address (no copy). */
+ * IGGY_ERR_CAPACITY if more). `body` may extend past batch_length. A single-stride
+ * record of <= 4 MiB is read by the kernel in place over the host link: a registered
+ * (iggy_codec_host_register) one through its device-mapped address (no copy), a
+ * pageable one after a memcpy into the context's own mapped staging (no DMA). */
 int iggy_codec_decode_batch(iggy_codec_ctx *ctx, const uint8_t *body, uint64_t len,
                             int integrity, iggy_batch_header *hdr,
                             uint64_t *frame_pos, uint64_t cap, uint64_t *nframes,
@@ -596,9 +597,11 @@ int iggy_codec_host_pinned(const void *ptr, uint64_t len);
  * (nullable, host) receives up to `cap` blob-relative frame starts (entries
  * past frame_count are unspecified; more frames than cap -> IGGY_ERR_CAPACITY
  * in the completion). A record of <= 16 MiB whose frame 0 sets a stride that
- * tiles it is one k_decode_records launch on the context's stream: a registered
- * input of <= 1 MiB is read in place (the one exception to "kernels never read
- * host memory": pinned memory, through its device-mapped address), the verdict
+ * tiles it is one k_decode_records launch on the context's stream: an input of
+ * <= 4 MiB is read in place (the one exception to "kernels never read host memory":
+ * pinned memory through its device-mapped address; a pageable input is first copied
+ * into the slot's own mapped staging, which the slot keeps until the ticket
+ * completes, so submit never waits on the stream), the verdict
  * lands in the slot's completion record and the positions in mapped host memory;
  * if the stride breaks mid-record, the iggy_codec_poll that sees it starts the
  * general walk and the ticket stays pending one more round. */

@@ -17,6 +17,9 @@ import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
+from iggy_amd import codec as _codec  # noqa: E402
+if os.environ.get("IGGY_LIB"):  # a library build to compare (same-box A/B)
+    _codec.use_library(os.environ["IGGY_LIB"])
 from iggy_amd.codec import Codec  # noqa: E402
 from oracle import oracle as O  # noqa: E402  (the CPU leg)
 
@@ -29,7 +32,7 @@ def main():
     args = ap.parse_args()
     cx = Codec(0)
     rows = []
-    for kib in (64, 256, 1024, 4096, 16384, 65536):
+    for kib in (64, 256, 1024, 2048, 4096, 16384, 65536):
         n = max(1, kib * 1024 // 1072)
         rec = O.synth_batch(n, 1024, 1024, seed=kib)
         pos = np.zeros(rec.size // 48 + 1, dtype=np.uint64)

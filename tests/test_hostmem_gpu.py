@@ -113,12 +113,13 @@ def test_pageable_submit_outputs(cx):
 
 
 def test_registered_record_read_in_place(cx):
-    """A registered record of <= 1 MiB is decoded in place (the kernel reads the
+    """A registered record of <= 4 MiB is decoded in place (the kernel reads the
     host-mapped bytes, no H2D): same verdicts as the oracle, at the start of the
     registered range and at an interior, unaligned offset, clean and corrupted, and a
     larger registered record (copied as before)."""
     recs = [O.synth_batch(1000, 256, seed=31), O.synth_batch(700, 100, 900, seed=32),
-            O.synth_batch(1500, 1024, seed=33)]  # the last one is 1.6 MB: not in place
+            O.synth_batch(1500, 1024, seed=33),  # 1.6 MB: in place
+            O.synth_batch(5000, 1024, seed=34)]  # 5.4 MB: above the in-place limit, copied
     bad = recs[0].copy()
     bad[256 + 48 * 500 + 60] ^= 0x40  # one payload bit of frame 500
     recs.append(bad)
@@ -168,7 +169,8 @@ def test_submit_single_stride_fast_path(cx, registered):
     clean = O.synth_batch(1000, 256, seed=43)
     bad = clean.copy()
     bad[256 + 304 * 700 + 100] ^= 1
-    recs = [clean, bad, _stride_break_record(), O.synth_batch(3000, 1000, seed=44)]
+    recs = [clean, bad, _stride_break_record(), O.synth_batch(3000, 1000, seed=44),  # 3.1 MB: in place
+            O.synth_batch(5000, 1000, seed=45)]  # 5.2 MB: copied (pageable: from the slot's staging)
     poss = [np.zeros(r.size // 48 + 1, dtype=np.uint64) for r in recs]
     if registered:
         for a in recs + poss:
@@ -189,3 +191,38 @@ def test_submit_single_stride_fast_path(cx, registered):
         if registered:
             for a in recs + poss:
                 cx.host_unregister(a)
+
+
+def test_pageable_submit_buffers_reused_at_once(cx):
+    """Pageable records submitted back to back (8 in flight, the slots' own mapped
+    staging) while the caller overwrites each input right after its submit returns
+    (batch.rs:391 borrows for the call only): every verdict and position list is the
+    oracle's for the bytes the caller passed. Sizes on both sides of the in-place limit
+    (4 MiB), a corrupted record among them, and the slots reused with other records."""
+    recs = [O.synth_batch(1000, 256, seed=50 + k) for k in range(4)]          # C1 shapes, in place
+    recs += [O.synth_batch(2000, 1000, seed=60),                                # 2 MB, in place
+             O.synth_batch(4500, 1000, seed=61)]                                # 4.7 MB, staging + DMA
+    bad = O.synth_batch(1000, 256, seed=62)
+    bad[256 + 304 * 10 + 70] ^= 0x10
+    recs += [bad, O.synth_batch(30, 4000, seed=63)]
+    wants = [O.decode_batch_slice_with(r, 0) for r in recs]
+    for rnd in range(3):
+        order = list(range(len(recs)))[rnd:] + list(range(len(recs)))[:rnd]  # other slot per record
+        bufs, poss, tks = [], [], []
+        for i in order:
+            b = _fresh(recs[i])
+            p = np.zeros(recs[i].size // 48 + 1, dtype=np.uint64)
+            tks.append(cx.decode_submit(b, abi.INTEGRITY_VERIFY, p))
+            b[:] = 0xA5  # the caller reuses its buffer at once
+            bufs.append(b)
+            poss.append(p)
+        for tk, i, p in zip(tks, order, poss):
+            c = cx.wait(tk)
+            orc, oe, oh, of = wants[i]
+            assert c.error.astuple() == oe.astuple(), (rnd, i)
+            assert c.header.astuple() == oh.astuple(), (rnd, i)
+            if orc == 0:
+                assert c.frame_count == len(of)
+                assert np.array_equal(p[:c.frame_count], np.asarray(of, dtype=np.uint64)), (rnd, i)
+        del bufs
+        gc.collect()
