@@ -640,6 +640,9 @@ constexpr uint32_t kErLds = kErWaves * kErWave;
 #ifndef IGGY_ER_NOSTORE
 #define IGGY_ER_NOSTORE 0  // (timing-only build knob, wrong output: mode 2 without the frame byte stores)
 #endif
+#ifndef IGGY_ER_TSTORE
+#define IGGY_ER_TSTORE 0  // (timing-only build knob, wrong output: transposed 1-KiB store runs)
+#endif
 #ifndef IGGY_ER_A128
 #define IGGY_ER_A128 0  // (timing-only build knob, wrong output: piece stores to 128-B-aligned runs)
 #endif
@@ -1036,6 +1039,19 @@ __global__ __launch_bounds__(SPLIT ? 2 * kErThreads : kErThreads, 1) void k_enc_
                 if (er_act(whole)) er_st16(whole ? (void *)(F + 8 + sp) : (void *)my_sink, w0, w1);
             } else if (IGGY_ER_MODE < 2) {
                 er_st16(whole ? (void *)(F + 8 + sp) : (void *)my_sink, w0, w1);
+            } else if (IGGY_ER_TSTORE) {
+                // (timing only, wrong output: the store pattern of a transposed writer --
+                // instruction q writes 1 KiB of group q's frame block, 16-B aligned,
+                // every lane one chunk -- with this lane's own piece as the data)
+                const uint32_t flo = __builtin_amdgcn_readlane((uint32_t)(uintptr_t)F, 8 * q);
+                const uint32_t fhi = __builtin_amdgcn_readlane((uint32_t)((uintptr_t)F >> 32), 8 * q);
+                const uint32_t pbq = __builtin_amdgcn_readlane(pb, 8 * q);
+                const uint32_t lq = __builtin_amdgcn_readlane((uint32_t)p_L, 8 * q);
+                const uint32_t vq = __builtin_amdgcn_readlane(p_valid ? 1u : 0u, 8 * q);
+                uint8_t *Fq = (uint8_t *)((((uint64_t)fhi << 32) | flo) & ~(uint64_t)15);
+                const uint64_t spt = ((uint64_t)pbq << 10) + 16 * (uint32_t)lane;
+                if (vq && spt + 16 <= lq)
+                    st128_any(Fq + spt, make_uint4((uint32_t)w0, (uint32_t)(w0 >> 32), (uint32_t)w1, (uint32_t)(w1 >> 32)));
             } else if (IGGY_ER_A128) {  // (timing only, wrong output: each group's run 128-B aligned)
                 if (whole) {
                     uint8_t *Fa = (uint8_t *)((uintptr_t)(F + 8) & ~(uintptr_t)127);
