@@ -1,3 +1,6 @@
+#!/bin/bash
+# The round-5 record run at 89526f5: the round check, the bench with 3 / 4
+# pipelined lanes, profiles (trace, C3 phase clock, PMC), and a same-box A/B of two builds.
 set -u
 cd $GRAFT_REPO_ROOT
 STEPS="tests smoke bench phase" bash scripts/gpu_round.sh r5o || exit $?
