@@ -226,3 +226,24 @@ def test_pageable_submit_buffers_reused_at_once(cx):
                 assert np.array_equal(p[:c.frame_count], np.asarray(of, dtype=np.uint64)), (rnd, i)
         del bufs
         gc.collect()
+
+
+def test_pageable_sync_decode_around_in_place_limit(cx):
+    """The synchronous decode of pageable records on both sides of the in-place limit
+    (4 MiB: one memcpy into the context's mapped staging, read in place; above it, the
+    two staging chunks and a DMA), clean and with one corrupted payload byte, against
+    the oracle; the staging is reused call after call with other bytes."""
+    for n, pl in ((1500, 1000), (3800, 1024), (4400, 1000)):  # 1.5 / 3.9 / 4.4 MB
+        rec = O.synth_batch(n, pl, seed=n)
+        bad = rec.copy()
+        bad[256 + (48 + pl) * (n - 3) + 100] ^= 0x08
+        for r in (rec, bad, rec):
+            want = O.decode_batch_slice_with(r, 0)
+            x = _fresh(r)
+            pos = np.zeros(r.size // 48 + 1, dtype=np.uint64)
+            h, e = abi.BatchHeader(), abi.WireError()
+            rc, nf = cx.decode_batch_into(x, abi.INTEGRITY_VERIFY, pos, h, e)
+            del x
+            assert rc == want[0] and e.astuple() == want[1].astuple() and h.astuple() == want[2].astuple()
+            if rc == 0:
+                assert np.array_equal(pos[:nf], np.asarray(want[3], dtype=np.uint64))
