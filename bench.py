@@ -348,15 +348,21 @@ def c1_leg(cx, dev, seconds: float):
                 cx.decode_batch_into(r, abi.INTEGRITY_VERIFY, p)
         return (time.perf_counter() - t) / (reps * nb) * 1e6
 
+    submit_cpu = [0.0]
+
     def async_us(reps=5, with_pos=True):
         t = time.perf_counter()
+        sub = 0.0
         for _ in range(reps):
             for lo in (0, 8):  # at most 8 in flight per context
+                c0 = time.thread_time()
                 tks = [cx.decode_submit(recs[b], abi.INTEGRITY_VERIFY, poss[b] if with_pos else None)
                        for b in range(lo, min(lo + 8, nb))]
+                sub += time.thread_time() - c0
                 for tk in tks:
                     c = cx.wait(tk)
                     assert c.error.kind == 0 and c.frame_count == n, c.error
+        submit_cpu[0] = sub / (reps * nb) * 1e6
         return (time.perf_counter() - t) / (reps * nb) * 1e6
 
     sync_pageable_us = sync_us()
@@ -384,6 +390,7 @@ def c1_leg(cx, dev, seconds: float):
         "gpu_host_sync_us_per_batch": round(sync_pageable_us, 1),
         "gpu_host_sync_registered_us_per_batch": round(sync_registered_us, 1),
         "gpu_host_async_registered_us_per_batch": round(async_registered_us, 1),
+        "gpu_host_async_registered_submit_cpu_us_per_batch": round(submit_cpu[0], 1),
         "cpu_ref_decode_us_per_batch": round(recs[0].size / dec * 1e6, 1),
         "wire_bytes": wire,
     }

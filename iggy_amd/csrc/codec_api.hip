@@ -139,6 +139,11 @@ struct Slot {
     // place (<= kZeroCopyBytes) or one DMA copies it, and the slot keeps it until it is
     // done, so submit never waits on the stream for the caller's bytes
     HostMap zin;
+    // the fast path's own stream and k_decode_records scratch: fast-path decodes of
+    // different slots run side by side (a small record's launch is bound by its reads'
+    // round trips over the host link, not by the chip)
+    hipStream_t st = nullptr;
+    DevBuf rstate, rbsums, rcount;
     hipEvent_t ev_in = nullptr, ev_k = nullptr, ev_done = nullptr;
     // a pageable caller output is never a DMA target: the copy-out stream lands it in
     // this pinned bounce and iggy_codec_poll copies it to the caller (hout_dst, hout_len)
@@ -160,10 +165,11 @@ struct Slot {
         return 0;
     }
     void release() {
-        DevBuf *b[] = {&in, &pos, &out, &res, &ids, &ots, &pay, &plen, &uhb, &uhl};
+        DevBuf *b[] = {&in, &pos, &out, &res, &ids, &ots, &pay, &plen, &uhb, &uhl, &rstate, &rbsums, &rcount};
         for (DevBuf *x : b) x->release();
         tab.release();
         zin.release();
+        if (st) (void)hipStreamDestroy(st), st = nullptr;
         for (hipEvent_t *e : {&ev_in, &ev_k, &ev_done})
             if (*e) (void)hipEventDestroy(*e), *e = nullptr;
         if (hout) (void)hipHostFree(hout);
@@ -744,11 +750,16 @@ int enqueue_records(iggy_codec_ctx *c, const uint8_t *d_base, const uint8_t *h_b
                     int integrity, uint64_t *d_pos, iggy_polled_message *d_msgs, iggy_decode_result *d_res,
                     std::vector<size_t> *single, std::vector<uint64_t> *n_frames = nullptr,
                     uint32_t *host_flag = nullptr, uint32_t flag_value = 0, HostMap *tab = nullptr,
-                    GenRearm rearm = GenRearm{nullptr, nullptr, nullptr}) {
+                    GenRearm rearm = GenRearm{nullptr, nullptr, nullptr}, Slot *own = nullptr) {
     // tab (nullable): host-mapped memory for the launch's task table that stays the
-    // caller's until the launch completes (asynchronous submits); else the context's
-    hipStream_t s = c->stream;
+    // caller's until the launch completes (asynchronous submits); else the context's.
+    // own (nullable): a fast-path slot whose stream and scratch the launch uses (no
+    // context scratch: every record must plan, so nothing takes the single path)
+    hipStream_t s = own ? own->st : c->stream;
     HostMap &rm = tab ? *tab : c->rmap;
+    DevBuf &rbsums = own ? own->rbsums : c->rbsums;
+    DevBuf &rstate = own ? own->rstate : c->rstate;
+    DevBuf &rcount = own ? own->rcount : c->rcount;
     std::vector<RecTask> tasks(K);
     std::vector<uint32_t> wgmap;
     uint64_t nbs = 0, maxlen = 0;
@@ -778,16 +789,16 @@ int enqueue_records(iggy_codec_ctx *c, const uint8_t *d_base, const uint8_t *h_b
     if (W) {
         const size_t tb = K * sizeof(RecTask), wb = W * 4;
         int r = rm.ensure(tb + wb);
-        r |= c->rbsums.ensure(nbs * 64 + 64);
-        const size_t st_before = c->rstate.cap;
-        r |= c->rstate.ensure(K * sizeof(RecState));
-        if (!c->rcount.p) {
-            r |= c->rcount.ensure(64);
-            if (!r) HIP_OK(hipMemsetAsync(c->rcount.p, 0, c->rcount.cap, s));
+        r |= rbsums.ensure(nbs * 64 + 64);
+        const size_t st_before = rstate.cap;
+        r |= rstate.ensure(K * sizeof(RecState));
+        if (!rcount.p) {
+            r |= rcount.ensure(64);
+            if (!r) HIP_OK(hipMemsetAsync(rcount.p, 0, rcount.cap, s));
         }
         if (r) return IGGY_ERR_DEVICE;
-        if (c->rstate.cap != st_before)  // fresh state: zero (the resolvers keep it zero after)
-            HIP_OK(hipMemsetAsync(c->rstate.p, 0, c->rstate.cap, s));
+        if (rstate.cap != st_before)  // fresh state: zero (the resolvers keep it zero after)
+            HIP_OK(hipMemsetAsync(rstate.p, 0, rstate.cap, s));
         memcpy(rm.hp<uint8_t>(), tasks.data(), tb);
         memcpy(rm.hp<uint8_t>(tb), wgmap.data(), wb);
         const RecTask *dt = rm.dp<RecTask>();
@@ -803,19 +814,20 @@ int enqueue_records(iggy_codec_ctx *c, const uint8_t *d_base, const uint8_t *h_b
             dt = c->rtab.as<RecTask>();
             dw = c->rtab.as<uint32_t>(tb);
         }
-        RecState *ds = c->rstate.as<RecState>();
+        RecState *ds = rstate.as<RecState>();
         uint32_t *flag = single->empty() ? host_flag : nullptr;
         if (integrity == IGGY_INTEGRITY_VERIFY)
             hipLaunchKernelGGL(k_decode_records<true>, dim3((uint32_t)W), dim3(kRecThreads), 0, s, d_base, dt, dw, ds,
-                               c->rbsums.as<uint64_t>(), d_pos, d_msgs, d_res, c->rcount.as<uint32_t>(), flag,
+                               rbsums.as<uint64_t>(), d_pos, d_msgs, d_res, rcount.as<uint32_t>(), flag,
                                flag_value, rearm, inl);
         else
             hipLaunchKernelGGL(k_decode_records<false>, dim3((uint32_t)W), dim3(kRecThreads), 0, s, d_base, dt, dw,
-                               ds, c->rbsums.as<uint64_t>(), d_pos, d_msgs, d_res, c->rcount.as<uint32_t>(), flag,
+                               ds, rbsums.as<uint64_t>(), d_pos, d_msgs, d_res, rcount.as<uint32_t>(), flag,
                                flag_value, rearm, inl);
         HIP_OK(hipGetLastError());
     }
     if (!single->empty()) {
+        if (own) return IGGY_ERR_DEVICE;  // (the caller planned every record)
         int r = ensure_decode_scratch(c, maxlen);
         if (r) return r;
         for (size_t k : *single) {
@@ -2947,12 +2959,18 @@ int iggy_codec_decode_submit(iggy_codec_ctx *c, const uint8_t *body, uint64_t le
     if (pcap && !pos_pinned && sl.hout_ensure(pcap * 8)) r = IGGY_ERR_DEVICE;
     uint64_t nf = 0;
     if (!r && c->slot_pinned_d && len <= kHostFastBytes && rec_plan(body, len, &nf)) {
-        // a single-stride record of <= 16 MiB, all on the context's stream: the input
-        // (read in place when <= kZeroCopyBytes, else copied), one
-        // k_decode_records launch whose verdict lands in the slot's host-mapped
-        // completion record, k_decode_general behind it for a stride that breaks
-        // mid-record, the positions back, the completion event
-        hipStream_t s = bind(c, nullptr);
+        // a single-stride record of <= 16 MiB, on the slot's own stream with the slot's
+        // own k_decode_records scratch (so the slots' launches overlap): the input
+        // (read in place when <= kZeroCopyBytes, else copied), one launch whose verdict
+        // lands in the slot's host-mapped completion record, the positions back, the
+        // completion event; k_decode_general, for a stride that breaks mid-record, is
+        // started by iggy_codec_poll on the context's stream
+        if (!sl.st && hipStreamCreateWithFlags(&sl.st, hipStreamNonBlocking) != hipSuccess) {
+            sl.st = nullptr;
+            sl.busy = false;
+            return IGGY_ERR_DEVICE;
+        }
+        hipStream_t s = sl.st;
         const uint8_t *d_in = len <= kZeroCopyBytes ? host_device_ptr(body, len) : nullptr;
         if (!d_in && !host_pinned(body, len)) {
             // pageable: copied into the slot's own pinned staging now (the caller's bytes
@@ -2999,7 +3017,7 @@ int iggy_codec_decode_submit(iggy_codec_ctx *c, const uint8_t *body, uint64_t le
         if (!r) {
             // a stride break mid-record is left to iggy_codec_poll (k_decode_general)
             r = enqueue_records(c, d_in, body, &rec, 1, integrity, d_pos, nullptr, d_res, &single, nullptr, nullptr,
-                                0, &sl.tab);
+                                0, &sl.tab, GenRearm{nullptr, nullptr, nullptr}, &sl);
         }
         if (!r && hipGetLastError() != hipSuccess) r = IGGY_ERR_DEVICE;
         if (!r && pos_copy) {

@@ -597,7 +597,8 @@ int iggy_codec_host_pinned(const void *ptr, uint64_t len);
  * (nullable, host) receives up to `cap` blob-relative frame starts (entries
  * past frame_count are unspecified; more frames than cap -> IGGY_ERR_CAPACITY
  * in the completion). A record of <= 16 MiB whose frame 0 sets a stride that
- * tiles it is one k_decode_records launch on the context's stream: an input of
+ * tiles it is one k_decode_records launch on the slot's own stream with the slot's
+ * own scratch, so such submits run side by side on the device: an input of
  * <= 4 MiB is read in place (the one exception to "kernels never read host memory":
  * pinned memory through its device-mapped address; a pageable input is first copied
  * into the slot's own mapped staging, which the slot keeps until the ticket
