@@ -25,6 +25,9 @@ sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "tests"))
 import torch  # noqa: E402,F401  (the HIP runtime the tests and bench use)
 from iggy_amd import abi  # noqa: E402
+from iggy_amd import codec as _codec  # noqa: E402
+if os.environ.get("IGGY_LIB"):  # a library build to compare (same-box A/B)
+    _codec.use_library(os.environ["IGGY_LIB"])
 from iggy_amd.codec import Codec  # noqa: E402
 from oracle import oracle as O  # noqa: E402  (the CPU leg)
 
