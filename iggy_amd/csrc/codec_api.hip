@@ -1136,6 +1136,8 @@ void iggy_codec_destroy(iggy_codec_ctx *c) {
     if (c->side) (void)hipStreamSynchronize(c->side);
     if (c->h2d) (void)hipStreamSynchronize(c->h2d);
     if (c->d2h) (void)hipStreamSynchronize(c->d2h);
+    for (Slot &sl : c->slots)  // the fast-path decodes' own streams
+        if (sl.st) (void)hipStreamSynchronize(sl.st);
     DevBuf *bufs[] = {&c->dsync, &c->dsums, &c->derr, &c->gtiles_s, &c->gtiles_x,
                       &c->gtiles_cnt, &c->gtiles_pre, &c->gtiles_list, &c->gtiles_e, &c->gtiles_base, &c->ggrp, &c->gfpos, &c->gcs, &c->gvrec, &c->gtiles_lcs,
                       &c->gbsums, &c->dresult, &c->din, &c->dpos, &c->dout, &c->epl, &c->euh,

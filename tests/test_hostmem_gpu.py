@@ -247,3 +247,23 @@ def test_pageable_sync_decode_around_in_place_limit(cx):
             assert rc == want[0] and e.astuple() == want[1].astuple() and h.astuple() == want[2].astuple()
             if rc == 0:
                 assert np.array_equal(pos[:nf], np.asarray(want[3], dtype=np.uint64))
+
+
+def test_destroy_with_fast_submits_in_flight():
+    """A context destroyed while fast-path submits (each on its slot's own stream) are
+    still in flight drains those streams before it frees their staging and results; a
+    new context then decodes as usual."""
+    from iggy_amd.codec import Codec
+    recs = [O.synth_batch(1000, 256, seed=70 + k) for k in range(6)]
+    poss = [np.zeros(r.size // 48 + 1, dtype=np.uint64) for r in recs]
+    c = Codec(0)
+    for r, p in zip(recs, poss):
+        c.decode_submit(r, abi.INTEGRITY_VERIFY, p)
+    c.close()  # no wait: the destroy drains the slot streams
+    c2 = Codec(0)
+    try:
+        want = O.decode_batch_slice_with(recs[0], 0)
+        rc, e, h, f = c2.decode_batch_slice_with(recs[0], abi.INTEGRITY_VERIFY)
+        assert rc == want[0] == 0 and np.array_equal(f, want[3])
+    finally:
+        c2.close()
