@@ -1195,7 +1195,10 @@ void *iggy_codec_stream(iggy_codec_ctx *c) { return c ? (void *)c->stream : null
 
 int iggy_codec_synchronize(iggy_codec_ctx *c) {
     if (!c) return IGGY_ERR_INVALID_ARGUMENT;
+    DevGuard dg(c->device);
     HIP_OK(hipStreamSynchronize(c->stream));
+    for (Slot &sl : c->slots)  // the fast-path submits' own streams
+        if (sl.st) HIP_OK(hipStreamSynchronize(sl.st));
     return 0;
 }
 

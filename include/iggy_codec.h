@@ -201,7 +201,8 @@ void iggy_codec_destroy(iggy_codec_ctx *ctx);
 int iggy_codec_reserve(iggy_codec_ctx *ctx, uint64_t max_batch_bytes, uint64_t max_frames);
 /* The context's own stream (hipStream_t as void*). */
 void *iggy_codec_stream(iggy_codec_ctx *ctx);
-/* Blocks until every operation enqueued on the context's stream is done. */
+/* Blocks until every operation enqueued on the context's stream is done, and every
+ * fast-path decode_submit on a slot's own stream (their tickets still need a poll). */
 int iggy_codec_synchronize(iggy_codec_ctx *ctx);
 
 /* ------------------------------------------------------------ pure host */
