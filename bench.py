@@ -365,8 +365,27 @@ def c1_leg(cx, dev, seconds: float):
         submit_cpu[0] = sub / (reps * nb) * 1e6
         return (time.perf_counter() - t) / (reps * nb) * 1e6
 
+    # the producer side: iggy_codec_encode_submit of the same SoA batches from host
+    # memory into host wire buffers, 8 in flight (the SDK's direct-send path)
+    wires = [np.zeros(r.size, dtype=np.uint8) for r in recs]
+    enc_cpu = [0.0]
+
+    def encode_async_us(reps=5):
+        t = time.perf_counter()
+        sub = 0.0
+        for _ in range(reps):
+            for lo in (0, 8):
+                c0 = time.thread_time()
+                tks = [cx.encode_submit(raws[b], 0, wires[b]) for b in range(lo, min(lo + 8, nb))]
+                sub += time.thread_time() - c0
+                for tk in tks:
+                    c = cx.wait(tk)
+                    assert c.error.kind == 0 and c.bytes == wires[0].size, c.error
+        enc_cpu[0] = sub / (reps * nb) * 1e6
+        return (time.perf_counter() - t) / (reps * nb) * 1e6
+
     sync_pageable_us = sync_us()
-    for a in recs + poss:
+    for a in recs + poss + wires + [x for kp in keep for x in kp]:
         cx.host_register(a)
     try:
         sync_registered_us = sync_us()
@@ -376,8 +395,11 @@ def c1_leg(cx, dev, seconds: float):
         async_us(1)
         async_registered_us = async_us()
         assert all(int(p[1]) == 48 + pl for p in poss)
+        encode_async_us(1)
+        enc_async_registered_us = encode_async_us()
+        assert all(np.array_equal(w, r) for w, r in zip(wires, recs))
     finally:
-        for a in recs + poss:
+        for a in recs + poss + wires + [x for kp in keep for x in kp]:
             cx.host_unregister(a)
     return {
         "workload": "C1 shapes: 10 batches x 1000 msgs x 256 B (iggy-bench over TCP not run: no Rust toolchain)",
@@ -391,6 +413,9 @@ def c1_leg(cx, dev, seconds: float):
         "gpu_host_sync_registered_us_per_batch": round(sync_registered_us, 1),
         "gpu_host_async_registered_us_per_batch": round(async_registered_us, 1),
         "gpu_host_async_registered_submit_cpu_us_per_batch": round(submit_cpu[0], 1),
+        "gpu_host_encode_async_registered_us_per_batch": round(enc_async_registered_us, 1),
+        "gpu_host_encode_async_registered_submit_cpu_us_per_batch": round(enc_cpu[0], 1),
+        "cpu_ref_encode_us_per_batch": round(recs[0].size / enc * 1e6, 1),
         "cpu_ref_decode_us_per_batch": round(recs[0].size / dec * 1e6, 1),
         "wire_bytes": wire,
     }

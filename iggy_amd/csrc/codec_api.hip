@@ -116,6 +116,14 @@ struct HostMap {
 
 }  // namespace
 
+// an asynchronous encode's own scratch (enqueue_encode's per-batch arrays)
+struct EncOwn {
+    DevBuf epl, euh, etile, ecs, emisc, bsums;
+    void release() {
+        for (DevBuf *b : {&epl, &euh, &etile, &ecs, &emisc, &bsums}) b->release();
+    }
+};
+
 // one asynchronous host-buffer operation in flight (iggy_codec_*_submit / iggy_codec_poll)
 constexpr int kSlots = 8;
 struct Slot {
@@ -144,6 +152,7 @@ struct Slot {
     // round trips over the host link, not by the chip)
     hipStream_t st = nullptr;
     DevBuf rstate, rbsums, rcount;
+    EncOwn eown;  // (small encodes in place: the same, for enqueue_encode)
     hipEvent_t ev_in = nullptr, ev_k = nullptr, ev_done = nullptr;
     // a pageable caller output is never a DMA target: the copy-out stream lands it in
     // this pinned bounce and iggy_codec_poll copies it to the caller (hout_dst, hout_len)
@@ -169,6 +178,7 @@ struct Slot {
         for (DevBuf *x : b) x->release();
         tab.release();
         zin.release();
+        eown.release();
         if (st) (void)hipStreamDestroy(st), st = nullptr;
         for (hipEvent_t *e : {&ev_in, &ev_k, &ev_done})
             if (*e) (void)hipEventDestroy(*e), *e = nullptr;
@@ -1722,30 +1732,35 @@ int iggy_codec_xxh3_64(iggy_codec_ctx *c, const void *data, uint64_t len, uint64
 
 // ---------------------------------------------------------------- encode
 static int enqueue_encode(iggy_codec_ctx *c, const iggy_raw_messages *dm, uint64_t partition_id,
-                          uint8_t *d_out, uint64_t cap, iggy_encode_result *d_res, hipStream_t s) {
+                          uint8_t *d_out, uint64_t cap, iggy_encode_result *d_res, hipStream_t s,
+                          EncOwn *own = nullptr) {
+    // own (nullable): scratch of an asynchronous slot, so unsegmented encodes of
+    // different slots run side by side on their own streams (else the context's)
     const uint64_t n = dm->count;
+    DevBuf &epl = own ? own->epl : c->epl, &euh = own ? own->euh : c->euh, &etile = own ? own->etile : c->etile;
+    DevBuf &ecs = own ? own->ecs : c->ecs, &emisc = own ? own->emisc : c->emisc, &bsums = own ? own->bsums : c->gbsums;
     const uint64_t ntiles = (n + kEncTile - 1) / kEncTile;
     int r = 0;
-    r |= c->epl.ensure(n * 8);
-    r |= c->euh.ensure(n * 8);
-    r |= c->etile.ensure(ntiles * 24 + 64);
-    r |= c->ecs.ensure(n * 8);
-    r |= c->emisc.ensure(1024);  // misc | header | checksum | small | chain state (512)
+    r |= epl.ensure(n * 8);
+    r |= euh.ensure(n * 8);
+    r |= etile.ensure(ntiles * 24 + 64);
+    r |= ecs.ensure(n * 8);
+    r |= emisc.ensure(1024);  // misc | header | checksum | small | chain state (512)
     const uint64_t nbk = (44 + 8 * n) / 1024 + 2;
-    r |= c->gbsums.ensure(nbk * 64);
+    r |= bsums.ensure(nbk * 64);
     if (r) return IGGY_ERR_DEVICE;
     EncScratch es;
-    es.pl_local = c->epl.as<uint64_t>();
-    es.uh_local = c->euh.as<uint64_t>();
-    es.tile_pl = c->etile.as<uint64_t>();
-    es.tile_uh = c->etile.as<uint64_t>(ntiles * 8);
-    es.tile_min = c->etile.as<uint64_t>(ntiles * 16);
-    es.cs = c->ecs.as<uint64_t>();
-    es.misc = c->emisc.as<uint64_t>();
-    es.hdr = c->emisc.as<iggy_batch_header>(128);
+    es.pl_local = epl.as<uint64_t>();
+    es.uh_local = euh.as<uint64_t>();
+    es.tile_pl = etile.as<uint64_t>();
+    es.tile_uh = etile.as<uint64_t>(ntiles * 8);
+    es.tile_min = etile.as<uint64_t>(ntiles * 16);
+    es.cs = ecs.as<uint64_t>();
+    es.misc = emisc.as<uint64_t>();
+    es.hdr = emisc.as<iggy_batch_header>(128);
     es.dbg = diag_bits(c);
     iggy_raw_messages m = *dm;
-    prof_begin(c, 1, s);
+    if (!own) prof_begin(c, 1, s);
     hipLaunchKernelGGL(k_enc_prep, dim3(ntiles), dim3(256), 0, s, m, es, partition_id, cap, (uint32_t)(ntiles == 1));
     if (ntiles != 1) hipLaunchKernelGGL(k_enc_scan, dim3(1), dim3(256), 0, s, ntiles, n, partition_id, cap, es);
     const uint64_t waves = std::min<uint64_t>(n, (uint64_t)c->ncu * 32);
@@ -1758,7 +1773,7 @@ static int enqueue_encode(iggy_codec_ctx *c, const iggy_raw_messages *dm, uint64
         // no user headers: lane-group kernel (k_enc_frames only covers a < 16-B payload
         // area, and runs first so the segments' checksum chain sees its output)
         int nseg = 1;
-        if (n >= kEncSegMinFrames && nb >= 4 * kEncSegs && c->side) {
+        if (!own && n >= kEncSegMinFrames && nb >= 4 * kEncSegs && c->side) {
             nseg = kEncSegs;
             for (auto ev : c->seg_ev)
                 if (!ev) nseg = 1;
@@ -1791,7 +1806,7 @@ static int enqueue_encode(iggy_codec_ctx *c, const iggy_raw_messages *dm, uint64
         // with lane-group waves it ran 132 ns/step instead of ~31)
         const uint64_t lcu = (segmented && !(diag_bits(c) & 16384)) ? (uint64_t)c->ncu - 1 : (uint64_t)c->ncu;
         const uint64_t lwg = std::min<uint64_t>((n + 31) / 32, lcu * ((diag_bits(c) & 2048) ? 8 : 2));
-        uint64_t *state = c->emisc.as<uint64_t>(512);
+        uint64_t *state = emisc.as<uint64_t>(512);
         for (int k = 0; k < nseg; ++k) {
             // blocks [B_k, B_k+1) need frames up to 128 B_k+1 - 6: segment k encodes
             // frames [F_k, F_k+1), F_k = 128 B_k - 5
@@ -1824,9 +1839,9 @@ static int enqueue_encode(iggy_codec_ctx *c, const iggy_raw_messages *dm, uint64
                 HIP_OK(hipStreamWaitEvent(c->side, c->seg_ev[k], 0));
                 hipLaunchKernelGGL(k_bsum_blocks_range, dim3(c->ncu / 2), dim3(256), 0, c->side,
                                    (const iggy_batch_header *)es.hdr, (const uint64_t *)&es.misc[3], src,
-                                   c->gbsums.as<uint64_t>(), B0, B1);
+                                   bsums.as<uint64_t>(), B0, B1);
                 hipLaunchKernelGGL(k_chain_partial, dim3(1), dim3(256), 0, c->side, (const uint64_t *)&es.misc[3],
-                                   (const uint64_t *)c->gbsums.as<uint64_t>(), state, B0, B1);
+                                   (const uint64_t *)bsums.as<uint64_t>(), state, B0, B1);
             }
         }
         if (segmented) {
@@ -1835,31 +1850,31 @@ static int enqueue_encode(iggy_codec_ctx *c, const iggy_raw_messages *dm, uint64
             HIP_OK(hipEventRecord(c->seg_ev[kEncSegs], c->side));
             HIP_OK(hipStreamWaitEvent(s, c->seg_ev[kEncSegs], 0));
             hipLaunchKernelGGL(k_bsum_blocks_range, dim3(c->ncu), dim3(256), 0, s, (const iggy_batch_header *)es.hdr,
-                               (const uint64_t *)&es.misc[3], src, c->gbsums.as<uint64_t>(), Bl, nb + 1);
+                               (const uint64_t *)&es.misc[3], src, bsums.as<uint64_t>(), Bl, nb + 1);
             hipLaunchKernelGGL(k_chain_partial, dim3(1), dim3(256), 0, s, (const uint64_t *)&es.misc[3],
-                               (const uint64_t *)c->gbsums.as<uint64_t>(), state, Bl, nb);
+                               (const uint64_t *)bsums.as<uint64_t>(), state, Bl, nb);
         }
     } else {
         hipLaunchKernelGGL(k_enc_frames, dim3((waves + 3) / 4), dim3(256), 0, s, m, es, d_out, 0u);
     }
-    prof_end(c, 1, s);
-    uint64_t *dcs = c->emisc.as<uint64_t>(256);
+    if (!own) prof_end(c, 1, s);
+    uint64_t *dcs = emisc.as<uint64_t>(256);
     if (!segmented && nb + 1 <= kEncTailBlocks) {  // small batch: sums, chain and finish in one launch
         hipLaunchKernelGGL(k_enc_tail_small, dim3(1), dim3(256), 0, s, m, es, partition_id, cap,
-                           c->emisc.as<uint8_t>(320), d_out, d_res);
+                           emisc.as<uint8_t>(320), d_out, d_res);
         HIP_OK(hipGetLastError());
         return 0;
     }
     if (segmented) {
         hipLaunchKernelGGL(k_chain_finish, dim3(1), dim3(64), 0, s, (const iggy_batch_header *)es.hdr,
-                           (const uint64_t *)&es.misc[3], src, (const uint64_t *)c->gbsums.as<uint64_t>(),
-                           (const uint64_t *)c->emisc.as<uint64_t>(512), c->emisc.as<uint8_t>(320), dcs);
+                           (const uint64_t *)&es.misc[3], src, (const uint64_t *)bsums.as<uint64_t>(),
+                           (const uint64_t *)emisc.as<uint64_t>(512), emisc.as<uint8_t>(320), dcs);
     } else {
         hipLaunchKernelGGL(k_bsum_blocks, dim3(bsum_grid(c, n)), dim3(256), 0, s, (const iggy_batch_header *)es.hdr,
-                           (const uint64_t *)&es.misc[3], src, c->gbsums.as<uint64_t>(), nullptr);
+                           (const uint64_t *)&es.misc[3], src, bsums.as<uint64_t>(), nullptr);
         hipLaunchKernelGGL(k_bsum_chain, dim3(1), dim3(128), 0, s, (const iggy_batch_header *)es.hdr,
-                           (const uint64_t *)&es.misc[3], src, (const uint64_t *)c->gbsums.as<uint64_t>(),
-                           c->emisc.as<uint8_t>(320) /* 192 B of small */, dcs, nullptr);
+                           (const uint64_t *)&es.misc[3], src, (const uint64_t *)bsums.as<uint64_t>(),
+                           emisc.as<uint8_t>(320) /* 192 B of small */, dcs, nullptr);
     }
     hipLaunchKernelGGL(k_enc_finish, dim3(1), dim3(64), 0, s, m, es, partition_id, cap,
                        (const uint64_t *)dcs, d_out, d_res);
@@ -3120,6 +3135,74 @@ int iggy_codec_encode_submit(iggy_codec_ctx *c, const iggy_raw_messages *m, uint
     sl.hout_len = 0;
     const bool out_pinned = host_pinned(out, need);
     if (cap >= need && !out_pinned && sl.hout_ensure(need)) r = IGGY_ERR_DEVICE;
+    // Small batches (SoA input of <= kZeroCopyBytes, one segment) in place: the kernels
+    // read the SoA arrays over the host link (registered ones where they are, anything
+    // else copied with one memcpy per array into the slot's mapped staging, so the
+    // caller's bytes are free when submit returns) and write the wire bytes and the
+    // verdict straight into mapped host memory (the caller's pinned `out`, else the
+    // slot's bounce). No copy operation on any stream; the kernels on the slot's own
+    // stream with the slot's own scratch, so the slots' encodes run side by side.
+    const uint64_t in_bytes = n * 28 + spl + (has_uh ? suh + n * 4 : 0);
+    if (!r && c->slot_pinned_d && cap >= need && in_bytes <= kZeroCopyBytes && n < kEncSegMinFrames) {
+        struct Arr { const void *h; uint64_t len; const uint8_t *d; };
+        Arr a[6] = {{m->ids, n * 16, nullptr}, {m->origin_timestamps, n * 8, nullptr},
+                    {m->payloads, spl, nullptr}, {m->payload_lengths, n * 4, nullptr},
+                    {has_uh ? m->user_headers : nullptr, has_uh ? suh : 0, nullptr},
+                    {has_uh ? m->user_headers_lengths : nullptr, has_uh ? n * 4 : 0, nullptr}};
+        bool mapped = true;  // (an empty array takes the staging too: a valid address behind it)
+        for (int i = 0; i < (has_uh ? 6 : 4); ++i)
+            mapped &= a[i].len && (a[i].d = host_device_ptr(a[i].h, a[i].len)) != nullptr;
+        if (!mapped) {  // one staging area, every array 256-B aligned, 16 B of slack each
+            uint64_t off[6], tot = 0;
+            for (int i = 0; i < 6; ++i) {
+                off[i] = tot;
+                tot += (a[i].len + 16 + 255) & ~(uint64_t)255;
+            }
+            if (sl.zin.ensure(tot)) {
+                sl.busy = false;
+                return IGGY_ERR_DEVICE;
+            }
+            for (int i = 0; i < 6; ++i) {
+                if (a[i].len) memcpy(sl.zin.hp<uint8_t>(off[i]), a[i].h, a[i].len);
+                a[i].d = sl.zin.d + off[i];
+            }
+        }
+        uint8_t *d_out = out_pinned ? (uint8_t *)host_device_ptr(out, need) : nullptr;
+        if (!d_out) {
+            void *dp = nullptr;
+            if (out_pinned || !sl.hout || hipHostGetDevicePointer(&dp, sl.hout, 0) != hipSuccess || !dp) {
+                (void)hipGetLastError();
+                dp = nullptr;
+            }
+            d_out = (uint8_t *)dp;
+            if (d_out) sl.hout_dst = out;
+        }
+        if (d_out) {
+            iggy_raw_messages dm;
+            dm.count = n;
+            dm.ids = (const uint64_t *)a[0].d;
+            dm.origin_timestamps = (const uint64_t *)a[1].d;
+            dm.payloads = a[2].d;
+            dm.payload_lengths = (const uint32_t *)a[3].d;
+            dm.user_headers = has_uh ? a[4].d : nullptr;
+            dm.user_headers_lengths = has_uh ? (const uint32_t *)a[5].d : nullptr;
+            if (!sl.st && hipStreamCreateWithFlags(&sl.st, hipStreamNonBlocking) != hipSuccess) {
+                sl.st = nullptr;
+                sl.busy = false;
+                return IGGY_ERR_DEVICE;
+            }
+            iggy_encode_result *d_res = (iggy_encode_result *)(c->slot_pinned_d + 256 * k);
+            r = enqueue_encode(c, &dm, partition_id, d_out, cap, d_res, sl.st, &sl.eown);
+            if (!r && hipEventRecord(sl.ev_done, sl.st) != hipSuccess) r = IGGY_ERR_DEVICE;
+            if (r) {
+                sl.busy = false;
+                return r;
+            }
+            *ticket = sl.ticket;
+            return 0;
+        }
+        sl.hout_dst = nullptr;  // (no mapped destination: the copy path below)
+    }
     hipStream_t h = c->h2d;
     if (!r) {
         r |= put_host(c, sl.ids.p, m->ids, n * 16, h);

@@ -611,7 +611,12 @@ int iggy_codec_decode_submit(iggy_codec_ctx *ctx, const uint8_t *body, uint64_t 
                              uint64_t *frame_pos, uint64_t cap, iggy_ticket *ticket);
 /* SendMessagesEncoder::encode batch section (send_messages.rs:89-181) from host
  * SoA input into `out` (host, cap bytes; a batch larger than cap writes nothing
- * and completes with IGGY_ERR_CAPACITY). */
+ * and completes with IGGY_ERR_CAPACITY). A batch whose SoA input is <= 4 MiB is
+ * encoded in place on the slot's own stream with the slot's own scratch: the kernels
+ * read registered arrays where they are (pageable ones are first copied into the
+ * slot's mapped staging) and write the wire bytes and the verdict into mapped host
+ * memory (the caller's pinned `out`, else the slot's bounce). Registered inputs
+ * stay borrowed until the ticket completes. */
 int iggy_codec_encode_submit(iggy_codec_ctx *ctx, const iggy_raw_messages *msgs, uint64_t partition_id,
                              uint8_t *out, uint64_t cap, iggy_ticket *ticket);
 /* 0: finished, *out filled (out->error is the operation's own verdict) and the

@@ -267,3 +267,64 @@ def test_destroy_with_fast_submits_in_flight():
         assert rc == want[0] == 0 and np.array_equal(f, want[3])
     finally:
         c2.close()
+
+
+def _soa(n, lo, hi, seed, uh=False):
+    from iggy_amd.codec import raw_messages
+    rng = np.random.default_rng(seed)
+    ids = rng.integers(1, 2**63, size=2 * n, dtype=np.uint64)
+    ots = (1_700_000_000_000_000 + rng.integers(0, 10**6, size=n)).astype(np.uint64)
+    pls = rng.integers(lo, hi + 1, size=n).astype(np.uint32)
+    pay = rng.integers(0, 256, size=int(pls.sum()), dtype=np.uint8)
+    arrs = [ids, ots, pay, pls]
+    if uh:
+        uhl = rng.integers(0, 40, size=n).astype(np.uint32)
+        uhb = rng.integers(0, 256, size=int(uhl.sum()), dtype=np.uint8)
+        arrs += [uhb, uhl]
+        return arrs, raw_messages(ids, ots, pay, pls, uhb, uhl)
+    return arrs, raw_messages(ids, ots, pay, pls)
+
+
+@pytest.mark.parametrize("registered", [False, True])
+def test_encode_submit_small_batches_in_place(cx, registered):
+    """encode_submit of small batches (SoA input of <= 4 MiB: the kernels read it over
+    the host link -- registered arrays where they are, pageable ones from the slot's
+    staging -- and write the wire bytes into mapped host memory): 8 in flight, with and
+    without user headers, empty payloads, the caller's SoA arrays overwritten right
+    after each submit, each output byte-exact against the oracle; plus one batch whose
+    output capacity is too small (nothing written, capacity error)."""
+    cases = [(1000, 256, 256, False), (700, 0, 300, True), (3000, 1, 900, False), (64, 0, 0, False),
+             (1000, 256, 256, True), (5, 2000, 5000, False), (2000, 100, 1000, True), (1, 17, 17, False)]
+    wants, outs, tks, keep = [], [], [], []
+    for k, (n, lo, hi, uh) in enumerate(cases):
+        arrs, raw = _soa(n, lo, hi, 80 + k, uh)
+        rc, e, w = O.encode_batch(raw, 3)
+        assert rc == 0
+        wants.append(np.frombuffer(w, dtype=np.uint8))
+        out = np.full(len(w) + 32, 0xEE, dtype=np.uint8)
+        outs.append(out)
+        if registered:
+            for a in arrs + [out]:
+                if a.size:
+                    cx.host_register(a)
+        tks.append(cx.encode_submit(raw, 3, out))
+        if not registered:
+            for a in arrs:
+                a[...] = 0x5A  # the caller reuses its arrays at once (they were staged)
+        keep.append(arrs)
+    try:
+        for tk, w, out in zip(tks, wants, outs):
+            c = cx.wait(tk)
+            assert c.error.kind == 0 and c.bytes == w.size, c.error
+            assert np.array_equal(out[:w.size], w)
+            assert (out[w.size:] == 0xEE).all()
+    finally:
+        if registered:
+            for arrs, out in zip(keep, outs):
+                for a in arrs + [out]:
+                    if a.size:
+                        cx.host_unregister(a)
+    arrs, raw = _soa(500, 10, 50, 99)
+    small = np.full(100, 0xEE, dtype=np.uint8)
+    c = cx.wait(cx.encode_submit(raw, 0, small))
+    assert c.error.kind == abi.ERR_CAPACITY and (small == 0xEE).all()
