@@ -236,9 +236,10 @@ struct iggy_codec_ctx {
     HostMap rmap;  // task table + workgroup map (read by the kernel in place when small)
     HostMap cmap;  // chunk-walk candidates (read in place)
     HostMap omap;  // [0, 64): completion flag; then results / positions / chunk-walk outputs
-    // a pageable record of <= kZeroCopyBytes for the synchronous fast path, copied here
-    // and read by the kernel in place (no H2D)
+    // a pageable record of <= kZeroCopyBytes for the synchronous fast path (or a small
+    // synchronous encode's SoA input), copied here and read by the kernels in place
     HostMap zin;
+    HostMap zout;  // a small synchronous encode's wire bytes when the caller's `out` is not mapped
     uint32_t hseq = 0;  // completion flag values
     uint32_t chunk_epoch = 0;  // k_chunk_walk link tags
     // segment writer: pinned staging halves and their copy events
@@ -1173,6 +1174,7 @@ void iggy_codec_destroy(iggy_codec_ctx *c) {
     c->cmap.release();
     c->omap.release();
     c->zin.release();
+    c->zout.release();
     if (c->cr_pinned) {  // GHASH tables of the key: cleared before the pages go back
         volatile uint8_t *z = (volatile uint8_t *)c->cr_pinned;
         for (size_t i = 0; i < kCrTabBytesHost; ++i) z[i] = 0;
@@ -1731,6 +1733,42 @@ int iggy_codec_xxh3_64(iggy_codec_ctx *c, const void *data, uint64_t len, uint64
 }
 
 // ---------------------------------------------------------------- encode
+// A small encode's SoA input as device-visible host memory: every array read in place
+// when all are registered (and non-empty), else all copied with one memcpy each into
+// `stage` (mapped, every array 256-B aligned with 16 B of slack). dm: the result.
+static int stage_soa(const iggy_raw_messages *m, uint64_t n, uint64_t spl, uint64_t suh, HostMap &stage,
+                     iggy_raw_messages *dm) {
+    const bool has_uh = m->user_headers_lengths != nullptr;
+    struct Arr { const void *h; uint64_t len; const uint8_t *d; };
+    Arr a[6] = {{m->ids, n * 16, nullptr}, {m->origin_timestamps, n * 8, nullptr},
+                {m->payloads, spl, nullptr}, {m->payload_lengths, n * 4, nullptr},
+                {has_uh ? m->user_headers : nullptr, has_uh ? suh : 0, nullptr},
+                {has_uh ? m->user_headers_lengths : nullptr, has_uh ? n * 4 : 0, nullptr}};
+    bool mapped = true;  // (an empty array takes the staging too: a valid address behind it)
+    for (int i = 0; i < (has_uh ? 6 : 4); ++i)
+        mapped &= a[i].len && (a[i].d = host_device_ptr(a[i].h, a[i].len)) != nullptr;
+    if (!mapped) {
+        uint64_t off[6], tot = 0;
+        for (int i = 0; i < 6; ++i) {
+            off[i] = tot;
+            tot += (a[i].len + 16 + 255) & ~(uint64_t)255;
+        }
+        if (stage.ensure(tot)) return IGGY_ERR_DEVICE;
+        for (int i = 0; i < 6; ++i) {
+            if (a[i].len) memcpy(stage.hp<uint8_t>(off[i]), a[i].h, a[i].len);
+            a[i].d = stage.d + off[i];
+        }
+    }
+    dm->count = n;
+    dm->ids = (const uint64_t *)a[0].d;
+    dm->origin_timestamps = (const uint64_t *)a[1].d;
+    dm->payloads = a[2].d;
+    dm->payload_lengths = (const uint32_t *)a[3].d;
+    dm->user_headers = has_uh ? a[4].d : nullptr;
+    dm->user_headers_lengths = has_uh ? (const uint32_t *)a[5].d : nullptr;
+    return 0;
+}
+
 static int enqueue_encode(iggy_codec_ctx *c, const iggy_raw_messages *dm, uint64_t partition_id,
                           uint8_t *d_out, uint64_t cap, iggy_encode_result *d_res, hipStream_t s,
                           EncOwn *own = nullptr) {
@@ -1908,6 +1946,34 @@ int iggy_codec_encode_batch(iggy_codec_ctx *c, const iggy_raw_messages *m, uint6
         return IGGY_ERR_CAPACITY;
     }
     int r = 0;
+    const uint64_t in_bytes = n * 28 + spl + (m->user_headers_lengths ? suh + n * 4 : 0);
+    if (in_bytes <= kZeroCopyBytes && n < kEncSegMinFrames) {
+        // a small batch in place (as encode_submit's): the SoA arrays read over the host
+        // link, the wire bytes into the caller's registered `out` or the context's
+        // mapped bounce, the verdict into mapped memory; one stream sync, no copy
+        iggy_raw_messages dm;
+        if (stage_soa(m, n, spl, suh, c->zin, &dm)) return IGGY_ERR_DEVICE;
+        uint8_t *d_out = (uint8_t *)host_device_ptr(out, need);
+        const bool bounce = !d_out;
+        if (bounce) {
+            if (c->zout.ensure(need + 16)) return IGGY_ERR_DEVICE;
+            d_out = c->zout.d;
+        }
+        if (c->omap.ensure(64 + 256)) return IGGY_ERR_DEVICE;
+        iggy_encode_result *d_res = c->omap.dp<iggy_encode_result>(64);
+        hipStream_t s = c->stream;
+        r = enqueue_encode(c, &dm, partition_id, d_out, need, d_res, s);
+        if (r) return r;
+        HIP_OK(hipStreamSynchronize(s));
+        const iggy_encode_result res = *c->omap.hp<iggy_encode_result>(64);
+        if (res.error.kind != IGGY_OK) {
+            fill_err(err, res.error);
+            return (int)res.error.kind;
+        }
+        if (bounce) memcpy(out, c->zout.h, need);
+        if (out_len) *out_len = need;
+        return 0;
+    }
     r |= c->eids.ensure(n * 16);
     r |= c->eots.ensure(n * 8);
     r |= c->epay.ensure(spl + 16);
@@ -3144,28 +3210,10 @@ int iggy_codec_encode_submit(iggy_codec_ctx *c, const iggy_raw_messages *m, uint
     // stream with the slot's own scratch, so the slots' encodes run side by side.
     const uint64_t in_bytes = n * 28 + spl + (has_uh ? suh + n * 4 : 0);
     if (!r && c->slot_pinned_d && cap >= need && in_bytes <= kZeroCopyBytes && n < kEncSegMinFrames) {
-        struct Arr { const void *h; uint64_t len; const uint8_t *d; };
-        Arr a[6] = {{m->ids, n * 16, nullptr}, {m->origin_timestamps, n * 8, nullptr},
-                    {m->payloads, spl, nullptr}, {m->payload_lengths, n * 4, nullptr},
-                    {has_uh ? m->user_headers : nullptr, has_uh ? suh : 0, nullptr},
-                    {has_uh ? m->user_headers_lengths : nullptr, has_uh ? n * 4 : 0, nullptr}};
-        bool mapped = true;  // (an empty array takes the staging too: a valid address behind it)
-        for (int i = 0; i < (has_uh ? 6 : 4); ++i)
-            mapped &= a[i].len && (a[i].d = host_device_ptr(a[i].h, a[i].len)) != nullptr;
-        if (!mapped) {  // one staging area, every array 256-B aligned, 16 B of slack each
-            uint64_t off[6], tot = 0;
-            for (int i = 0; i < 6; ++i) {
-                off[i] = tot;
-                tot += (a[i].len + 16 + 255) & ~(uint64_t)255;
-            }
-            if (sl.zin.ensure(tot)) {
-                sl.busy = false;
-                return IGGY_ERR_DEVICE;
-            }
-            for (int i = 0; i < 6; ++i) {
-                if (a[i].len) memcpy(sl.zin.hp<uint8_t>(off[i]), a[i].h, a[i].len);
-                a[i].d = sl.zin.d + off[i];
-            }
+        iggy_raw_messages dm;
+        if (stage_soa(m, n, spl, suh, sl.zin, &dm)) {
+            sl.busy = false;
+            return IGGY_ERR_DEVICE;
         }
         uint8_t *d_out = out_pinned ? (uint8_t *)host_device_ptr(out, need) : nullptr;
         if (!d_out) {
@@ -3178,14 +3226,6 @@ int iggy_codec_encode_submit(iggy_codec_ctx *c, const iggy_raw_messages *m, uint
             if (d_out) sl.hout_dst = out;
         }
         if (d_out) {
-            iggy_raw_messages dm;
-            dm.count = n;
-            dm.ids = (const uint64_t *)a[0].d;
-            dm.origin_timestamps = (const uint64_t *)a[1].d;
-            dm.payloads = a[2].d;
-            dm.payload_lengths = (const uint32_t *)a[3].d;
-            dm.user_headers = has_uh ? a[4].d : nullptr;
-            dm.user_headers_lengths = has_uh ? (const uint32_t *)a[5].d : nullptr;
             if (!sl.st && hipStreamCreateWithFlags(&sl.st, hipStreamNonBlocking) != hipSuccess) {
                 sl.st = nullptr;
                 sl.busy = false;

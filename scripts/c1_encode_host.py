@@ -16,6 +16,9 @@ import numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 import torch  # noqa: E402,F401  (the HIP runtime the codec shares)
+from iggy_amd import codec as _codec  # noqa: E402
+if os.environ.get("IGGY_LIB"):  # a library build to compare (same-box A/B)
+    _codec.use_library(os.environ["IGGY_LIB"])
 from iggy_amd.codec import Codec, raw_messages  # noqa: E402
 from oracle import oracle as O  # noqa: E402  (the CPU leg and the check)
 
@@ -51,7 +54,19 @@ def main():
                     assert c.error.kind == 0, c.error
         return (time.perf_counter() - t) / (reps * nb) * 1e6, sub / (reps * nb) * 1e6
 
+    def sync(reps):
+        t = time.perf_counter()
+        for _ in range(reps):
+            for b in range(nb):
+                rc, e, o = cx.encode_batch(raws[b], 0)
+                assert rc == 0, e
+        return (time.perf_counter() - t) / (reps * nb) * 1e6
+
     line = {"batch_bytes": int(size)}
+    rc, e, o = cx.encode_batch(raws[0], 0)
+    assert rc == 0 and np.array_equal(np.frombuffer(o, dtype=np.uint8), wants[0])
+    sync(1)
+    line["sync_pageable_us_per_batch_incl_python"] = round(sync(10), 1)
     run(1)
     line["pageable_us_per_batch"], line["pageable_submit_cpu_us"] = [round(x, 1) for x in run(10)]
     assert all(np.array_equal(o, w) for o, w in zip(outs, wants))
