@@ -675,6 +675,9 @@ constexpr uint64_t kHostFastBytes = 16ull << 20;
 #define IGGY_ZERO_COPY_BYTES (4ull << 20)  // (build knob for same-box A/B: 1 MiB measured slower)
 #endif
 constexpr uint64_t kZeroCopyBytes = IGGY_ZERO_COPY_BYTES;  // host inputs up to this size are read in place
+#ifndef IGGY_POLL_IN_PLACE
+#define IGGY_POLL_IN_PLACE 1  // (build knob for same-box A/B: poll bodies read in place)
+#endif
 int decode_host_fast(iggy_codec_ctx *c, const uint8_t *body, uint64_t len, int integrity,
                      iggy_decode_result *res_out, uint64_t *frame_pos, uint64_t cap, bool *done);
 int decode_host(iggy_codec_ctx *c, const uint8_t *body, uint64_t len, int integrity,
@@ -2089,11 +2092,26 @@ int iggy_codec_poll_decode(iggy_codec_ctx *c, const uint8_t *buf, uint64_t len, 
         const size_t rb = K * sizeof(iggy_decode_result), mo = (64 + rb + 127) & ~(size_t)127;
         if (c->din.ensure(len + 16) || c->omap.ensure(mo + (nslots + 1) * sizeof(iggy_polled_message)))
             return IGGY_ERR_DEVICE;
-        int r = put_host(c, c->din.p, buf, len, c->stream);
-        if (r) return r;
+        // a body of <= kZeroCopyBytes is read in place (registered: where it is;
+        // pageable: one memcpy into the context's mapped staging), larger ones copied
+        const uint8_t *d_body = nullptr;
+        if (IGGY_POLL_IN_PLACE && len <= kZeroCopyBytes) {
+            d_body = host_device_ptr(buf, len);
+            if (!d_body && !host_pinned(buf, len)) {
+                if (c->zin.ensure(len + 16)) return IGGY_ERR_DEVICE;
+                memcpy(c->zin.h, buf, len);
+                d_body = c->zin.d;
+            }
+        }
+        int r = 0;
+        if (!d_body) {
+            r = put_host(c, c->din.p, buf, len, c->stream);
+            if (r) return r;
+            d_body = c->din.as<uint8_t>();
+        }
         std::vector<size_t> single;
         const uint32_t v = next_flag(c);
-        r = enqueue_records(c, c->din.as<uint8_t>(), buf, rin.data(), K, IGGY_INTEGRITY_LAYOUT_ONLY, nullptr,
+        r = enqueue_records(c, d_body, buf, rin.data(), K, IGGY_INTEGRITY_LAYOUT_ONLY, nullptr,
                             c->omap.dp<iggy_polled_message>(mo), c->omap.dp<iggy_decode_result>(64), &single,
                             nullptr, c->omap.dp<uint32_t>(), v);
         if (r) return r;
