@@ -88,6 +88,22 @@ def main():
         print(json.dumps({"path": "poll_decode(SDK)", "body_bytes": int(body.size), "messages": len(msgs),
                           "gpu_us": round(g * 1e6, 1), "cpu_1thread_us": round(c * 1e6, 1), "gpu_faster": g < c}),
               flush=True)
+        # the same two calls without the binding's per-call output allocation and list
+        # building: preallocated descriptor arrays, the C entry points called directly
+        import ctypes
+        cap = body.size // 48 + 1
+        gout, oout = (abi.PolledMessage * cap)(), (abi.PolledMessage * cap)()
+        n1, n2, e1, e2 = abi.u64(0), abi.u64(0), abi.WireError(), abi.WireError()
+        gcall = lambda: cx._L.iggy_codec_poll_decode(cx.handle, body.ctypes.data, body.size, 0, gout, cap,  # noqa: E731
+                                                    ctypes.byref(n1), ctypes.byref(e1))
+        ocall = lambda: O.lib().oracle_poll_decode(body.ctypes.data, body.size, 0, oout, cap,  # noqa: E731
+                                                  ctypes.byref(n2), ctypes.byref(e2))
+        assert gcall() == 0 and ocall() == 0 and n1.value == n2.value == len(msgs)
+        g = med(gcall, 200)
+        c = med(ocall, 200)
+        print(json.dumps({"path": "poll_decode(SDK), C calls", "body_bytes": int(body.size), "messages": len(msgs),
+                          "gpu_us": round(g * 1e6, 1), "cpu_1thread_us": round(c * 1e6, 1), "gpu_faster": g < c}),
+              flush=True)
         cx.host_unregister(chunk)
     if "seg" in what:
         for nb in (4, 64, 1024):
