@@ -246,7 +246,9 @@ int iggy_codec_calculate_batch_checksum(iggy_codec_ctx *ctx, const iggy_batch_he
  * (server_common/src/send_messages.rs:104-168) with a namespace partition id
  * otherwise (ids of 0 are NOT minted here: the caller mints, as the SDK does
  * at common/src/traits/binary_impls/messages.rs:343-347). `out` must hold
- * iggy_encoded_batch_size(msgs) bytes. */
+ * iggy_encoded_batch_size(msgs) bytes. On an error other than capacity its contents
+ * are unspecified (a small batch is encoded straight into a registered `out`), as
+ * the reference's encoder leaves its partly written buffer to the caller. */
 int iggy_codec_encode_batch(iggy_codec_ctx *ctx, const iggy_raw_messages *msgs,
                             uint64_t partition_id, uint8_t *out, uint64_t cap,
                             uint64_t *out_len, iggy_wire_error *err);
@@ -616,7 +618,8 @@ int iggy_codec_decode_submit(iggy_codec_ctx *ctx, const uint8_t *body, uint64_t 
  * read registered arrays where they are (pageable ones are first copied into the
  * slot's mapped staging) and write the wire bytes and the verdict into mapped host
  * memory (the caller's pinned `out`, else the slot's bounce). Registered inputs
- * stay borrowed until the ticket completes. */
+ * stay borrowed until the ticket completes; on an error other than capacity the
+ * contents of a pinned `out` are unspecified. */
 int iggy_codec_encode_submit(iggy_codec_ctx *ctx, const iggy_raw_messages *msgs, uint64_t partition_id,
                              uint8_t *out, uint64_t cap, iggy_ticket *ticket);
 /* 0: finished, *out filled (out->error is the operation's own verdict) and the
