@@ -663,14 +663,15 @@ def run(args, world: int, rank: int, local: int, dist):
 
     # Two forms of the same K steps, each timed on its own: lanes alternating (one
     # batch's chain tail under the next batch's stream) and one launch at a time on one
-    # stream. `value` is the better of the two (the pipelined form is not
-    # always the faster one); both are in the line.
+    # stream. `value` is the pipelined form, fixed up front (a partition's consecutive
+    # batches in flight together; choosing the better of two single noisy timings after
+    # the fact would bias the line upward); both numbers are in the line.
     elapsed_pipe = timed(step)
     check_lanes()
     elapsed_single = timed(lambda i: step(0)) if len(lanes) > 1 else elapsed_pipe
     check_lanes()
-    elapsed = min(elapsed_pipe, elapsed_single)
-    form = "pipelined" if elapsed_pipe <= elapsed_single else "single"
+    elapsed = elapsed_pipe
+    form = "pipelined" if len(lanes) > 1 else "single"
 
     # roofline: the decode grid's own duration, one launch at a time on one
     # stream (HIP events on the launch stream, bracketing k_decode_uniform)

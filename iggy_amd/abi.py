@@ -176,7 +176,24 @@ class Completion(ctypes.Structure):
     ]
 
 
+class HostStats(ctypes.Structure):
+    """iggy_host_stats: cumulative host-side counters of a context (diff two reads)."""
+    _fields_ = [
+        ("pinned_h2d_bytes", u64),
+        ("staged_bytes", u64),
+        ("settle_events", u64),
+        ("host_waits", u64),
+        ("device_allocs", u64),
+        ("pinned_allocs", u64),
+        ("_reserved", u64 * 2),
+    ]
+
+    def as_dict(self) -> dict:
+        return {k: getattr(self, k) for k, _ in self._fields_ if not k.startswith("_")}
+
+
 assert ctypes.sizeof(Completion) == 152
+assert ctypes.sizeof(HostStats) == 64
 assert ctypes.sizeof(SliceQuery) == 32
 assert ctypes.sizeof(SliceResult) == 128
 assert ctypes.sizeof(BatchHeader) == 64

@@ -122,6 +122,7 @@ def load(path: str) -> ctypes.CDLL:
     L.iggy_codec_build_polled_body.argtypes = [vp, u32, u64, vp, u64, vp, vp, u64, ctypes.POINTER(u64), vp]
     L.iggy_codec_profile_enable.argtypes = [vp, ci]
     L.iggy_codec_profile_read.argtypes = [vp, ci, vp, vp]
+    L.iggy_codec_host_stats.argtypes = [vp, vp]
     L.iggy_codec_host_register.argtypes = [vp, vp, u64]
     L.iggy_codec_host_unregister.argtypes = [vp, vp]
     L.iggy_codec_host_pinned.argtypes = [vp, u64]
@@ -541,6 +542,14 @@ class Codec:
         ms = ctypes.c_double(0)
         self._L.iggy_codec_profile_read(self._h, which, ctypes.byref(n), ctypes.byref(ms))
         return n.value, ms.value
+
+    def host_stats(self) -> dict:
+        """iggy_codec_host_stats: cumulative copy / wait / allocation counters."""
+        st = abi.HostStats()
+        rc = self._L.iggy_codec_host_stats(self._h, ctypes.byref(st))
+        if rc:
+            raise CodecError(rc, None, "host_stats")
+        return st.as_dict()
 
 
 def raw_messages(ids: np.ndarray, origin_timestamps: np.ndarray, payloads: np.ndarray,

@@ -11,6 +11,7 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -52,6 +53,22 @@ using namespace iggy;
 
 namespace {
 
+// IGGY_CODEC_DEBUG: host-memory history (registrations, mapped / pinned allocations and
+// their release) on stderr, so a later fault can be checked against ranges the codec
+// pinned or mapped
+bool hostmem_log_on() {
+    static const bool on = getenv("IGGY_CODEC_DEBUG") != nullptr;
+    return on;
+}
+void hostmem_log(const char *what, const void *p, uint64_t n) {
+    if (hostmem_log_on())
+        fprintf(stderr, "iggy_codec hostmem: %s [%p, %p) %llu B\n", what, p, (const void *)((const uint8_t *)p + n),
+                (unsigned long long)n);
+}
+
+// process-wide allocation counters (iggy_codec_host_stats)
+std::atomic<uint64_t> g_dev_allocs{0}, g_pin_allocs{0};
+
 // one device allocation that grows on demand (never inside an enqueue path
 // whose caller asked for graph-safety: grow happens in reserve / sync APIs)
 struct DevBuf {
@@ -64,6 +81,7 @@ struct DevBuf {
         cap = 0;
         size_t want = std::max<size_t>(n, 256);
         if (hipMalloc(&p, want) != hipSuccess) return IGGY_ERR_DEVICE;
+        g_dev_allocs.fetch_add(1, std::memory_order_relaxed);
         cap = want;
         return 0;
     }
@@ -98,6 +116,8 @@ struct HostMap {
             return IGGY_ERR_DEVICE;
         }
         cap = want;
+        g_pin_allocs.fetch_add(1, std::memory_order_relaxed);
+        hostmem_log("mapped alloc", h, want);
         // the completion flag lives in the first word: pinned memory handed back by the
         // allocator may still hold another context's flag values, one of which this
         // context's sequence could reach before its kernel writes it
@@ -107,7 +127,10 @@ struct HostMap {
     template <class T> T *hp(size_t off = 0) { return (T *)((uint8_t *)h + off); }
     template <class T> T *dp(size_t off = 0) { return (T *)(d + off); }
     void release() {
-        if (h) (void)hipHostFree(h);
+        if (h) {
+            hostmem_log("mapped free", h, cap);
+            (void)hipHostFree(h);
+        }
         h = nullptr;
         d = nullptr;
         cap = 0;
@@ -162,7 +185,10 @@ struct Slot {
     uint64_t hout_len = 0;
     int hout_ensure(size_t n) {
         if (n <= hout_cap && !(hout_cap > (8ull << 20) && n <= (8ull << 20))) return 0;
-        if (hout) (void)hipHostFree(hout);
+        if (hout) {
+            hostmem_log("bounce free", hout, hout_cap);
+            (void)hipHostFree(hout);
+        }
         hout = nullptr;
         hout_cap = 0;
         const size_t want = std::max<size_t>(n, 64 << 10);
@@ -171,6 +197,8 @@ struct Slot {
             return IGGY_ERR_DEVICE;
         }
         hout_cap = want;
+        g_pin_allocs.fetch_add(1, std::memory_order_relaxed);
+        hostmem_log("bounce alloc", hout, want);
         return 0;
     }
     void release() {
@@ -182,7 +210,10 @@ struct Slot {
         if (st) (void)hipStreamDestroy(st), st = nullptr;
         for (hipEvent_t *e : {&ev_in, &ev_k, &ev_done})
             if (*e) (void)hipEventDestroy(*e), *e = nullptr;
-        if (hout) (void)hipHostFree(hout);
+        if (hout) {
+            hostmem_log("bounce free", hout, hout_cap);
+            (void)hipHostFree(hout);
+        }
         hout = nullptr;
         hout_cap = 0;
     }
@@ -270,6 +301,7 @@ struct iggy_codec_ctx {
     uint32_t xnext = 0;
     hipEvent_t xin_ev = nullptr;
     bool xin_live = false;
+    iggy_host_stats hs = {};  // iggy_codec_host_stats (the allocation counts are process-wide)
     // asynchronous host-buffer operations: copy-in stream -> the context's stream -> copy-out
     // stream, so one operation's H2D, another's kernels and a third's D2H overlap
     hipStream_t h2d = nullptr, d2h = nullptr;
@@ -421,13 +453,21 @@ struct DevGuard {
 // therefore staged through the context's own two pinned chunks (memcpy of chunk k+1
 // under the DMA of chunk k), so no runtime lock on caller memory ever exists.
 constexpr uint64_t kXferChunk = 4ull << 20;
+// Ranges registered through iggy_codec_host_register. The registry is process-wide
+// (iggy_codec_host_pinned takes no context), but each entry belongs to the context that
+// registered it: iggy_codec_destroy unregisters that context's leftovers, so no entry
+// outlives its registration. Entries are trusted without a HIP query on every hit: a
+// range must be unregistered through the codec (iggy_codec_host_unregister), never with
+// a bare hipHostUnregister, or a later lookup would DMA from / map an unpinned range.
 std::mutex g_reg_mu;
 struct RegRange {
     uintptr_t h;   // host address
     uint64_t len;
-    uintptr_t d;   // its device-mapped address (0: not mapped)
+    uintptr_t d;   // its device-mapped address on `device` (0: not mapped)
+    int device;
+    const iggy_codec_ctx *owner;
 };
-std::vector<RegRange> g_reg;  // ranges registered through the codec
+std::vector<RegRange> g_reg;
 
 bool host_pinned(const void *p, uint64_t n) {
     if (!p || !n) return true;
@@ -460,10 +500,12 @@ bool host_pinned(const void *p, uint64_t n) {
 // not mapped); ranges registered through the codec answer from the registry
 const uint8_t *host_device_ptr(const void *p, uint64_t n) {
     const uintptr_t a = (uintptr_t)p;
+    int dev = -1;
+    (void)hipGetDevice(&dev);  // (the calling entry's DevGuard: the context's device)
     {
         std::lock_guard<std::mutex> lk(g_reg_mu);
         for (const auto &r : g_reg)
-            if (a >= r.h && a - r.h <= r.len && n <= r.len - (a - r.h))
+            if (a >= r.h && a - r.h <= r.len && n <= r.len - (a - r.h) && r.device == dev)
                 return r.d ? (const uint8_t *)(r.d + (a - r.h)) : nullptr;
     }
     if (!host_pinned(p, n)) return nullptr;
@@ -490,6 +532,7 @@ int xfer_init(iggy_codec_ctx *c) {
 int xfer_chunk(iggy_codec_ctx *c, uint8_t **chunk, int *idx) {
     const int b = (int)(c->xnext++ & 1);
     if (c->xlive[b]) {
+        c->hs.host_waits++;
         HIP_OK(hipEventSynchronize(c->xev[b]));
         c->xlive[b] = false;
     }
@@ -500,40 +543,49 @@ int xfer_chunk(iggy_codec_ctx *c, uint8_t **chunk, int *idx) {
 
 // H2D of n caller bytes on stream s. Returns with the caller's bytes consumed as far
 // as the caller is concerned: staged into pinned chunks (pageable), or enqueued from
-// memory the caller keeps pinned, whose copy every synchronous entry has completed
-// before it returns (xfer_settle).
+// memory the caller keeps pinned (a plain DMA source: the caller keeps it alive until
+// the call, or the ticket, completes; nothing of the runtime's outlives that copy).
+// Only a staged copy records xin_ev, the event a synchronous entry settles before it
+// returns (xfer_settle): an asynchronous submit of pinned memory issues no event and
+// no wait here, so its copy overlaps everything else in flight (round 5 recorded the
+// event for every copy, and its H2D / D2H no longer overlapped: C4 24.7 -> 17.6 GiB/s,
+// scripts/c4_diag.py).
 int put_host(iggy_codec_ctx *c, void *d_dst, const void *h_src, uint64_t n, hipStream_t s) {
     if (!n) return 0;
     if (host_pinned(h_src, n)) {
         HIP_OK(hipMemcpyAsync(d_dst, h_src, n, hipMemcpyHostToDevice, s));
-    } else {
-        if (xfer_init(c)) return IGGY_ERR_DEVICE;
-        for (uint64_t off = 0; off < n; off += kXferChunk) {
-            const uint64_t m = std::min(kXferChunk, n - off);
-            uint8_t *st;
-            int b;
-            int r = xfer_chunk(c, &st, &b);
-            if (r) return r;
-            memcpy(st, (const uint8_t *)h_src + off, m);
-            HIP_OK(hipMemcpyAsync((uint8_t *)d_dst + off, st, m, hipMemcpyHostToDevice, s));
-            HIP_OK(hipEventRecord(c->xev[b], s));
-            c->xlive[b] = true;
-        }
+        c->hs.pinned_h2d_bytes += n;
+        return 0;
+    }
+    c->hs.staged_bytes += n;
+    if (xfer_init(c)) return IGGY_ERR_DEVICE;
+    for (uint64_t off = 0; off < n; off += kXferChunk) {
+        const uint64_t m = std::min(kXferChunk, n - off);
+        uint8_t *st;
+        int b;
+        int r = xfer_chunk(c, &st, &b);
+        if (r) return r;
+        memcpy(st, (const uint8_t *)h_src + off, m);
+        HIP_OK(hipMemcpyAsync((uint8_t *)d_dst + off, st, m, hipMemcpyHostToDevice, s));
+        HIP_OK(hipEventRecord(c->xev[b], s));
+        c->xlive[b] = true;
     }
     if (!c->xin_ev && hipEventCreateWithFlags(&c->xin_ev, hipEventDisableTiming) != hipSuccess) {
         c->xin_ev = nullptr;
         return IGGY_ERR_DEVICE;
     }
     HIP_OK(hipEventRecord(c->xin_ev, s));
+    c->hs.settle_events++;
     c->xin_live = true;
     return 0;
 }
 
 // Before a synchronous entry that saw its completion through a host-mapped flag (no
-// stream sync) returns: its H2D copies are done. They ran before the kernel that
-// raised the flag, so this costs one signal read.
+// stream sync) returns: its staged H2D copies are done. They ran before the kernel that
+// raised the flag, so this costs one signal read (nothing at all after pinned copies).
 int xfer_settle(iggy_codec_ctx *c) {
     if (c->xin_live) {
+        c->hs.host_waits++;
         HIP_OK(hipEventSynchronize(c->xin_ev));
         c->xin_live = false;
     }
@@ -544,6 +596,7 @@ int xfer_settle(iggy_codec_ctx *c) {
 // in h_dst and nothing of the call outstanding on s).
 int get_host(iggy_codec_ctx *c, void *h_dst, const void *d_src, uint64_t n, hipStream_t s) {
     if (!n) return 0;
+    c->hs.host_waits++;  // (returns with the bytes in h_dst)
     if (host_pinned(h_dst, n)) {
         HIP_OK(hipMemcpyAsync(h_dst, d_src, n, hipMemcpyDeviceToHost, s));
         HIP_OK(hipStreamSynchronize(s));
@@ -1152,6 +1205,24 @@ void iggy_codec_destroy(iggy_codec_ctx *c) {
     if (c->d2h) (void)hipStreamSynchronize(c->d2h);
     for (Slot &sl : c->slots)  // the fast-path decodes' own streams
         if (sl.st) (void)hipStreamSynchronize(sl.st);
+    {
+        // ranges this context registered and the caller never unregistered: unpinned now,
+        // so no registry entry outlives the context that vouches for it
+        std::vector<uintptr_t> mine;
+        {
+            std::lock_guard<std::mutex> lk(g_reg_mu);
+            for (size_t i = 0; i < g_reg.size();)
+                if (g_reg[i].owner == c) {
+                    mine.push_back(g_reg[i].h);
+                    hostmem_log("unregister (context destroyed)", (const void *)g_reg[i].h, g_reg[i].len);
+                    g_reg.erase(g_reg.begin() + (long)i);
+                } else {
+                    ++i;
+                }
+        }
+        for (uintptr_t h : mine)
+            if (hipHostUnregister((void *)h) != hipSuccess) (void)hipGetLastError();
+    }
     DevBuf *bufs[] = {&c->dsync, &c->dsums, &c->derr, &c->gtiles_s, &c->gtiles_x,
                       &c->gtiles_cnt, &c->gtiles_pre, &c->gtiles_list, &c->gtiles_e, &c->gtiles_base, &c->ggrp, &c->gfpos, &c->gcs, &c->gvrec, &c->gtiles_lcs,
                       &c->gbsums, &c->dresult, &c->din, &c->dpos, &c->dout, &c->epl, &c->euh,
@@ -3020,22 +3091,26 @@ int iggy_codec_host_register(iggy_codec_ctx *c, void *ptr, uint64_t len) {
         (void)hipGetLastError();
         dp = nullptr;
     }
+    hostmem_log("register", ptr, len);
     std::lock_guard<std::mutex> lk(g_reg_mu);
-    g_reg.push_back(RegRange{(uintptr_t)ptr, len, (uintptr_t)dp});
+    g_reg.push_back(RegRange{(uintptr_t)ptr, len, (uintptr_t)dp, c->device, c});
     return 0;
 }
 
 int iggy_codec_host_unregister(iggy_codec_ctx *c, void *ptr) {
     if (!c || !ptr) return IGGY_ERR_INVALID_ARGUMENT;
     DevGuard dg(c->device);
+    uint64_t len = 0;
     {
         std::lock_guard<std::mutex> lk(g_reg_mu);
         for (size_t i = 0; i < g_reg.size(); ++i)
             if (g_reg[i].h == (uintptr_t)ptr) {
+                len = g_reg[i].len;
                 g_reg.erase(g_reg.begin() + (long)i);
                 break;
             }
     }
+    hostmem_log("unregister", ptr, len);
     HIP_OK(hipHostUnregister(ptr));
     return 0;
 }
@@ -3097,7 +3172,7 @@ int iggy_codec_decode_submit(iggy_codec_ctx *c, const uint8_t *body, uint64_t le
                 }
             }
         }
-        if (!d_in && !r) {  // pinned caller memory above kZeroCopyBytes: one DMA (settled below)
+        if (!d_in && !r) {  // pinned caller memory above kZeroCopyBytes: one DMA, no wait
             r = put_host(c, sl.in.p, body, len, s);
             d_in = sl.in.as<uint8_t>();
         }
@@ -3143,7 +3218,6 @@ int iggy_codec_decode_submit(iggy_codec_ctx *c, const uint8_t *body, uint64_t le
         sl.g_integ = integrity;
         sl.g_pos_copy = pos_copy;
         if (!r && hipEventRecord(sl.ev_done, s) != hipSuccess) r = IGGY_ERR_DEVICE;
-        if (!r && xfer_settle(c)) r = IGGY_ERR_DEVICE;  // (a staged pageable input: its last chunk copied)
         if (r) {
             sl.busy = false;
             return r;
@@ -3326,13 +3400,27 @@ int iggy_codec_poll(iggy_codec_ctx *c, iggy_ticket ticket, iggy_completion *out)
             hipStream_t s = bind(c, nullptr);
             const DecodeScratch dsc = dscratch(c);
             iggy_decode_result *d_res = (iggy_decode_result *)(c->slot_pinned_d + 256 * k);
+            // each operation checked where it is issued: the thread's last-error status is
+            // cleared first, so a launch failure is this launch's and not an unrelated
+            // earlier error of the caller's own HIP code
+            (void)hipGetLastError();
+            hipError_t e = hipSuccess;
             hipLaunchKernelGGL(k_general_rearm, dim3(1), dim3(64), 0, s, GenRearm{dsc.gbar, dsc.gbar2, dsc.gmisc});
-            launch_general(c, sl.g_in, sl.g_len, sl.g_integ, sl.g_pos, sl.g_pcap, d_res, s);
-            if (sl.g_pos_copy)
-                (void)hipMemcpyAsync(host_pinned(sl.frame_pos, sl.g_pcap * 8) ? (void *)sl.frame_pos : sl.hout,
-                                     sl.pos.p, sl.g_pcap * 8, hipMemcpyDeviceToHost, s);
+            e = hipGetLastError();
+            if (e == hipSuccess) {
+                launch_general(c, sl.g_in, sl.g_len, sl.g_integ, sl.g_pos, sl.g_pcap, d_res, s);
+                e = hipGetLastError();
+            }
+            if (e == hipSuccess && sl.g_pos_copy)
+                e = hipMemcpyAsync(host_pinned(sl.frame_pos, sl.g_pcap * 8) ? (void *)sl.frame_pos : sl.hout,
+                                   sl.pos.p, sl.g_pcap * 8, hipMemcpyDeviceToHost, s);
+            if (e == hipSuccess) e = hipEventRecord(sl.ev_done, s);
             sl.g_pending = true;
-            if (hipGetLastError() != hipSuccess || hipEventRecord(sl.ev_done, s) != hipSuccess) {
+            if (e != hipSuccess) {
+                // whatever was issued may still use the slot's buffers and the caller's
+                // memory: drain the stream before the slot is free again
+                (void)hipGetLastError();
+                (void)hipStreamSynchronize(s);
                 sl.busy = false;
                 return IGGY_ERR_DEVICE;
             }
@@ -3383,6 +3471,14 @@ int iggy_codec_wait(iggy_codec_ctx *c, iggy_ticket ticket, iggy_completion *out)
 }
 
 // -------------------------------------------------------------- profiling
+int iggy_codec_host_stats(iggy_codec_ctx *c, iggy_host_stats *out) {
+    if (!c || !out) return IGGY_ERR_INVALID_ARGUMENT;
+    *out = c->hs;
+    out->device_allocs = g_dev_allocs.load(std::memory_order_relaxed);
+    out->pinned_allocs = g_pin_allocs.load(std::memory_order_relaxed);
+    return 0;
+}
+
 int iggy_codec_profile_enable(iggy_codec_ctx *c, int enable) {
     if (!c) return IGGY_ERR_INVALID_ARGUMENT;
     c->profile = enable ? 1 : 0;

@@ -815,6 +815,21 @@ int iggy_codec_profile_enable(iggy_codec_ctx *ctx, int enable);
  * for `which` (0 = decode main kernel, 1 = encode main kernel), then resets. */
 int iggy_codec_profile_read(iggy_codec_ctx *ctx, int which, uint64_t *launches, double *total_ms);
 
+/* Host-side counters of a context since its creation (cumulative; diff two reads).
+ * The evidence that the asynchronous host API does not serialise its copies: a
+ * submit of pinned buffers of a size seen before stages nothing, records no settle
+ * event, waits for nothing and allocates nothing. */
+typedef struct iggy_host_stats {
+    uint64_t pinned_h2d_bytes;   /* caller bytes DMA'd straight from pinned memory */
+    uint64_t staged_bytes;       /* pageable caller bytes staged through the context's chunks */
+    uint64_t settle_events;      /* events recorded for xfer_settle (staged copies only) */
+    uint64_t host_waits;         /* blocking waits inside the codec's copy helpers */
+    uint64_t device_allocs;      /* device scratch (re)allocations (process-wide) */
+    uint64_t pinned_allocs;      /* pinned / mapped host (re)allocations (process-wide) */
+    uint64_t _reserved[2];
+} iggy_host_stats;
+int iggy_codec_host_stats(iggy_codec_ctx *ctx, iggy_host_stats *out);
+
 /* Human-readable text for an error kind / validation reason. */
 const char *iggy_codec_error_string(uint32_t kind, uint32_t reason);
 
