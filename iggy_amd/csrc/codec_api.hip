@@ -53,17 +53,34 @@ using namespace iggy;
 
 namespace {
 
-// IGGY_CODEC_DEBUG: host-memory history (registrations, mapped / pinned allocations and
-// their release) on stderr, so a later fault can be checked against ranges the codec
-// pinned or mapped
+// Host-memory history: every registration, mapped / pinned allocation and their
+// release, so a later fault can be checked against ranges the codec pinned or mapped
+// (VERDICT r05 item 5). IGGY_CODEC_DEBUG: on stderr; IGGY_CODEC_HOSTMEM_LOG=<path>:
+// appended to that file, one line per event with a monotonic timestamp (the test suite
+// sets it and attaches the tail to a failing test's report, tests/conftest.py).
+FILE *hostmem_file() {
+    static FILE *f = [] {
+        const char *p = getenv("IGGY_CODEC_HOSTMEM_LOG");
+        FILE *h = p && *p ? fopen(p, "a") : nullptr;
+        if (h) setvbuf(h, nullptr, _IOLBF, 0);
+        return h;
+    }();
+    return f;
+}
 bool hostmem_log_on() {
-    static const bool on = getenv("IGGY_CODEC_DEBUG") != nullptr;
+    static const bool on = getenv("IGGY_CODEC_DEBUG") != nullptr || hostmem_file() != nullptr;
     return on;
 }
 void hostmem_log(const char *what, const void *p, uint64_t n) {
-    if (hostmem_log_on())
-        fprintf(stderr, "iggy_codec hostmem: %s [%p, %p) %llu B\n", what, p, (const void *)((const uint8_t *)p + n),
-                (unsigned long long)n);
+    if (!hostmem_log_on()) return;
+    static std::mutex mu;
+    std::lock_guard<std::mutex> lk(mu);
+    const double t = std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+    char line[256];
+    snprintf(line, sizeof line, "%.6f iggy_codec hostmem: %s [%p, %p) %llu B\n", t, what, p,
+             (const void *)((const uint8_t *)p + n), (unsigned long long)n);
+    if (getenv("IGGY_CODEC_DEBUG")) fputs(line, stderr);
+    if (FILE *f = hostmem_file()) fputs(line, f);
 }
 
 // process-wide allocation counters (iggy_codec_host_stats)
@@ -3093,6 +3110,9 @@ int iggy_codec_host_register(iggy_codec_ctx *c, void *ptr, uint64_t len) {
     }
     hostmem_log("register", ptr, len);
     std::lock_guard<std::mutex> lk(g_reg_mu);
+    for (const auto &r : g_reg)  // (the runtime accepted it, so any overlap is a stale entry)
+        if ((uintptr_t)ptr < r.h + r.len && r.h < (uintptr_t)ptr + len)
+            hostmem_log("register overlaps a registry entry", (const void *)r.h, r.len);
     g_reg.push_back(RegRange{(uintptr_t)ptr, len, (uintptr_t)dp, c->device, c});
     return 0;
 }

@@ -12,13 +12,22 @@ then a DMA from page-locked memory.
 """
 from __future__ import annotations
 
+import os
+
 import numpy as np
+
+# Diagnostics only: IGGY_TORCH_IO_PAGEABLE=1 restores torch's plain pageable copies (the
+# path that faulted), to run the suite once under the round-5 conditions with the codec's
+# host-memory history attached to any failure (tests/conftest.py).
+_PAGEABLE = os.environ.get("IGGY_TORCH_IO_PAGEABLE") == "1"
 
 
 def to_device(a, device="cuda"):
     """A device tensor holding a copy of the numpy array `a` (same dtype and shape)."""
     import torch
     t = torch.from_numpy(np.ascontiguousarray(a))
+    if _PAGEABLE:
+        return t.to(device)
     p = torch.empty(t.shape, dtype=t.dtype, pin_memory=True)
     p.copy_(t)
     return p.to(device)
@@ -29,6 +38,8 @@ def to_host(t) -> np.ndarray:
     import torch
     if t.device.type == "cpu":
         return t.numpy()
+    if _PAGEABLE:
+        return t.cpu().numpy()
     p = torch.empty(t.shape, dtype=t.dtype, pin_memory=True)
     p.copy_(t)
     return p.numpy()

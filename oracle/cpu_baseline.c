@@ -18,9 +18,11 @@
 static inline uint64_t rd64(const uint8_t *p) { uint64_t v; memcpy(&v, p, 8); return v; }
 static inline uint32_t rd32(const uint8_t *p) { uint32_t v; memcpy(&v, p, 4); return v; }
 
-/* Returns computed batch checksum, or 0 with *ok = 0 on any error. */
-static uint64_t decode_verify_fast(const uint8_t *body, uint64_t len, uint8_t *scratch,
-                                   int *ok) {
+/* Returns computed batch checksum, or 0 with *ok = 0 on any error. layout_only:
+ * validate_batch_layout (batch.rs:508-527) instead of the Verify hash walk
+ * (batch.rs:474-506): the same frame walk and tiling check, no checksum. */
+static uint64_t decode_walk_fast(const uint8_t *body, uint64_t len, uint8_t *scratch, int layout_only,
+                                 int *ok) {
     iggy_batch_header h;
     iggy_wire_error e;
     *ok = 0;
@@ -34,13 +36,19 @@ static uint64_t decode_verify_fast(const uint8_t *body, uint64_t len, uint8_t *s
         if (blob_len - pos < 48 || rd64(blob + pos + 40) != 0) break;
         uint64_t end = pos + 48 + (uint64_t)rd32(blob + pos + 36) + rd32(blob + pos + 32);
         if (end > blob_len) break;
-        uint64_t stored = rd64(blob + pos);
-        if (oracle_xxh3_64_fast(blob + pos + 8, end - pos - 8) != stored) return 0;
-        memcpy(scratch + 44 + 8 * n, blob + pos, 8);
+        if (!layout_only) {
+            uint64_t stored = rd64(blob + pos);
+            if (oracle_xxh3_64_fast(blob + pos + 8, end - pos - 8) != stored) return 0;
+            memcpy(scratch + 44 + 8 * n, blob + pos, 8);
+        }
         n++;
         pos = end;
     }
     if (n != h.message_count || pos != blob_len) return 0;
+    if (layout_only) {
+        *ok = 1;
+        return 0;
+    }
     uint64_t c = oracle_xxh3_64_fast(scratch, 44 + 8 * n);
     if (c != h.batch_checksum) return 0;
     *ok = 1;
@@ -50,7 +58,7 @@ static uint64_t decode_verify_fast(const uint8_t *body, uint64_t len, uint8_t *s
 typedef struct {
     const uint8_t *body;
     uint64_t len;
-    int reps;
+    int reps, layout_only;
     uint64_t checksum;
     int ok;
 } job_t;
@@ -61,7 +69,7 @@ static void *worker(void *arg) {
     j->ok = 1;
     for (int r = 0; r < j->reps; r++) {
         int ok;
-        j->checksum = decode_verify_fast(j->body, j->len, scratch, &ok);
+        j->checksum = decode_walk_fast(j->body, j->len, scratch, j->layout_only, &ok);
         j->ok &= ok;
     }
     free(scratch);
@@ -70,6 +78,13 @@ static void *worker(void *arg) {
 
 double oracle_cpu_decode_bench(const uint8_t *body, uint64_t len, int threads, int reps,
                                uint64_t *checksum_out) {
+    return oracle_cpu_decode_bench_integrity(body, len, threads, reps, 0, checksum_out);
+}
+
+/* The same with integrity 0 = Verify, 1 = LayoutOnly (IGGY_INTEGRITY_*): the CPU leg
+ * of a crossover timed with the same integrity as its GPU leg. */
+double oracle_cpu_decode_bench_integrity(const uint8_t *body, uint64_t len, int threads, int reps,
+                                         int integrity, uint64_t *checksum_out) {
     if (threads < 1) threads = 1;
     pthread_t *tid = (pthread_t *)malloc(sizeof(pthread_t) * threads);
     job_t *jobs = (job_t *)calloc(threads, sizeof(job_t));
@@ -79,6 +94,7 @@ double oracle_cpu_decode_bench(const uint8_t *body, uint64_t len, int threads, i
         jobs[t].body = body;
         jobs[t].len = len;
         jobs[t].reps = reps;
+        jobs[t].layout_only = integrity == 1;
         pthread_create(&tid[t], NULL, worker, &jobs[t]);
     }
     int ok = 1;

@@ -106,6 +106,8 @@ uint64_t oracle_synth_batch_size(uint64_t n, uint32_t pl_min, uint32_t pl_max,
  * has it. Returns seconds of wall time. */
 double oracle_cpu_decode_bench(const uint8_t *body, uint64_t len, int threads, int reps,
                                uint64_t *checksum_out);
+double oracle_cpu_decode_bench_integrity(const uint8_t *body, uint64_t len, int threads, int reps,
+                                         int integrity, uint64_t *checksum_out);
 /* CPU baseline of the encode: `threads` threads each encode the SoA input
  * `reps` times (buffers of their own). Returns seconds; *bytes_out = batch bytes. */
 double oracle_cpu_encode_bench(const iggy_raw_messages *m, uint64_t partition_id, int threads, int reps,

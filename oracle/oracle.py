@@ -59,6 +59,8 @@ def lib() -> ctypes.CDLL:
         L.oracle_synth_batch_size.argtypes = [u64, u32, u32, u32, u64]
         L.oracle_cpu_decode_bench.restype = ctypes.c_double
         L.oracle_cpu_decode_bench.argtypes = [vp, u64, ctypes.c_int, ctypes.c_int, vp]
+        L.oracle_cpu_decode_bench_integrity.restype = ctypes.c_double
+        L.oracle_cpu_decode_bench_integrity.argtypes = [vp, u64, ctypes.c_int, ctypes.c_int, ctypes.c_int, vp]
         L.oracle_has_avx2.restype = ctypes.c_int
         L.oracle_cpu_encode_bench.restype = ctypes.c_double
         L.oracle_cpu_encode_bench.argtypes = [vp, u64, ctypes.c_int, ctypes.c_int, vp]
@@ -229,10 +231,12 @@ def synth_batch(n: int, pl_min: int, pl_max: int | None = None, uh_len: int = 0,
     return out[:size]
 
 
-def cpu_decode_bench(body, threads: int, reps: int):
+def cpu_decode_bench(body, threads: int, reps: int, integrity: int = 0):
+    """Seconds for `threads` threads to each walk `reps` copies (integrity 0 = Verify,
+    1 = LayoutOnly), and the batch checksum (Verify; 0 on any error or LayoutOnly)."""
     a = _as_np(body)
     c = u64(0)
-    secs = lib().oracle_cpu_decode_bench(a.ctypes.data, a.size, threads, reps, ctypes.byref(c))
+    secs = lib().oracle_cpu_decode_bench_integrity(a.ctypes.data, a.size, threads, reps, integrity, ctypes.byref(c))
     return secs, c.value
 
 

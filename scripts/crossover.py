@@ -1,9 +1,11 @@
 """CPU/GPU crossover of the host-buffer decode (the GPU_MIN_BYTES threshold of the
 Rust dispatcher): for records of 1 KiB messages from 64 KiB to
 64 MiB, the median time of iggy_codec_decode_batch (host buffer in, frame positions
-out: H2D + kernels + D2H, Verify) against the CPU oracle's single-thread decode
-(the reference's execution model: one shard thread walks one batch). One JSON line
-per size, then the crossover. Diagnostic / documentation only (oracle = the CPU leg).
+out: H2D + kernels + D2H) against the CPU oracle's single-thread decode (the
+reference's execution model: one shard thread walks one batch), both sides with the
+same --integrity (0 = Verify, the hash walk of batch.rs:474-506; 1 = LayoutOnly,
+batch.rs:508-527), which every row names. One JSON line per size, then the crossover.
+Diagnostic / documentation only (oracle = the CPU leg).
 
 usage: python scripts/crossover.py [--integrity 0|1]
 """
@@ -52,10 +54,13 @@ def main():
             cx.host_unregister(pos)
             cx.host_unregister(rec)
         reps = max(1, int(0.2 / max(rec.size / 3e9, 1e-6)))
-        secs, _ = O.cpu_decode_bench(rec, 1, reps)  # one thread walks `reps` copies (Verify)
+        # one thread walks `reps` copies with the GPU leg's integrity
+        secs, _ = O.cpu_decode_bench(rec, 1, reps, args.integrity)
         cpu = secs / reps
-        row = {"record_bytes": int(rec.size), "messages": n, "gpu_host_decode_us": round(gpu * 1e6, 1),
-               "cpu_1thread_us": round(cpu * 1e6, 1), "gpu_faster": gpu < cpu}
+        row = {"record_bytes": int(rec.size), "messages": n, "integrity_gpu": args.integrity,
+               "integrity_cpu": args.integrity, "registered": args.registered,
+               "gpu_host_decode_us": round(gpu * 1e6, 1), "cpu_1thread_us": round(cpu * 1e6, 1),
+               "gpu_faster": gpu < cpu}
         rows.append(row)
         print(json.dumps(row), flush=True)
     cross = next((r["record_bytes"] for r in rows if r["gpu_faster"]), None)

@@ -11,6 +11,13 @@ if ROOT not in sys.path:
 # environment is dropped before anything initialises the runtime.
 os.environ.pop("GPU_PINNED_MIN_XFER_SIZE", None)
 
+# Host-memory history of this test process (codec_api.hip hostmem_log): every range the
+# codec registers, maps or pins, and its release, with test boundaries between; the tail
+# is attached to a failing test's report, so a fault can be checked against earlier
+# pinned or mapped ranges without running anything again.
+HOSTMEM_LOG = os.environ.setdefault("IGGY_CODEC_HOSTMEM_LOG",
+                                    os.path.join("/tmp", f"iggy_hostmem_{os.getpid()}.log"))
+
 # torch first: its bundled HIP runtime then serves the codec library too (same
 # sonames; see iggy_amd/codec.py load())
 import torch  # noqa: F401,E402
@@ -41,3 +48,28 @@ def pytest_collection_modifyitems(session, config, items):
 @pytest.fixture(scope="session")
 def golden_dir():
     return os.path.join(ROOT, "tests", "golden")
+
+
+def _hostmem_mark(text):
+    import time
+    try:
+        with open(HOSTMEM_LOG, "a") as f:
+            f.write(f"{time.monotonic():.6f} test {text}\n")
+    except OSError:
+        pass
+
+
+@pytest.hookimpl(hookwrapper=True)
+def pytest_runtest_makereport(item, call):
+    if call.when == "setup":
+        _hostmem_mark(f"start {item.nodeid}")
+    outcome = yield
+    rep = outcome.get_result()
+    if rep.failed and item.get_closest_marker("gpu") is not None:
+        try:
+            with open(HOSTMEM_LOG) as f:
+                tail = f.readlines()[-60:]
+        except OSError:
+            tail = []
+        if tail:
+            rep.sections.append(("codec host-memory history (last 60 events)", "".join(tail)))
