@@ -259,22 +259,23 @@ def c1_leg(cx, dev, seconds: float):
     restatement, 1 thread) and the GPU's per-batch latency on the same shapes."""
     import torch
     from iggy_amd import abi
-    from iggy_amd.codec import raw_messages
+    from iggy_amd.codec import host_buffer, page_aligned, raw_messages
     from oracle import oracle as O  # cpu_ref leg of the bench only
 
     nb, n, pl = 10, 1000, 256
     rng = np.random.default_rng(0x16619E3779B97F4A)
     raws, keep, recs = [], [], []
     for b in range(nb):
-        ids = rng.integers(1, 2**63, size=2 * n, dtype=np.uint64)
-        ots = (1_700_000_000_000_000 + b * n + np.arange(n)).astype(np.uint64)
-        pay = rng.integers(0, 256, size=n * pl, dtype=np.uint8)
-        pls = np.full(n, pl, dtype=np.uint32)
+        # page-aligned host buffers: registered below, and registrations may not share a page
+        ids = page_aligned(rng.integers(1, 2**63, size=2 * n, dtype=np.uint64))
+        ots = page_aligned((1_700_000_000_000_000 + b * n + np.arange(n)).astype(np.uint64))
+        pay = page_aligned(rng.integers(0, 256, size=n * pl, dtype=np.uint8))
+        pls = page_aligned(np.full(n, pl, dtype=np.uint32))
         raws.append(raw_messages(ids, ots, pay, pls))
         keep.append((ids, ots, pay, pls))
         rc, e, out = O.encode_batch(raws[-1], 0)
         assert rc == 0
-        recs.append(np.frombuffer(out, dtype=np.uint8).copy())
+        recs.append(page_aligned(np.frombuffer(out, dtype=np.uint8)))
     wire = sum(r.size for r in recs)
 
     def cpu_rate(one):  # one(batch index, reps) -> seconds for reps passes over that batch
@@ -336,7 +337,7 @@ def c1_leg(cx, dev, seconds: float):
     # the synchronous host decode (iggy_codec_decode_batch: one k_decode_records launch
     # and a host-mapped flag), pageable records, then the same records registered
     # (iggy_codec_host_register: the kernel reads them in place, no H2D)
-    poss = [np.zeros(r.size // 48 + 1, dtype=np.uint64) for r in recs]
+    poss = [host_buffer(r.size // 48 + 1, np.uint64) for r in recs]
 
     def sync_us(reps=20):
         for r, p in zip(recs, poss):
@@ -367,7 +368,7 @@ def c1_leg(cx, dev, seconds: float):
 
     # the producer side: iggy_codec_encode_submit of the same SoA batches from host
     # memory into host wire buffers, 8 in flight (the SDK's direct-send path)
-    wires = [np.zeros(r.size, dtype=np.uint8) for r in recs]
+    wires = [host_buffer(r.size) for r in recs]
     enc_cpu = [0.0]
 
     def encode_async_us(reps=5):

@@ -552,6 +552,29 @@ class Codec:
         return st.as_dict()
 
 
+PAGE = 4096
+
+
+def host_buffer(shape, dtype=np.uint8) -> np.ndarray:
+    """A zeroed numpy array that starts on a page boundary and owns every page it
+    touches (its byte size rounded up to whole pages inside one allocation): a buffer
+    iggy_codec_host_register accepts beside any other such buffer (registrations may
+    not share a page, include/iggy_codec.h)."""
+    dt = np.dtype(dtype)
+    n = int(np.prod(shape)) * dt.itemsize
+    span = max(PAGE, (n + PAGE - 1) // PAGE * PAGE)
+    raw = np.zeros(span + PAGE, dtype=np.uint8)
+    off = (-raw.ctypes.data) % PAGE
+    return raw[off:off + n].view(dt).reshape(shape)
+
+
+def page_aligned(a: np.ndarray) -> np.ndarray:
+    """A host_buffer copy of `a` (same dtype, shape and bytes)."""
+    out = host_buffer(a.shape, a.dtype)
+    out[...] = a
+    return out
+
+
 def raw_messages(ids: np.ndarray, origin_timestamps: np.ndarray, payloads: np.ndarray,
                  payload_lengths: np.ndarray, user_headers: np.ndarray | None = None,
                  user_headers_lengths: np.ndarray | None = None) -> RawMessages:

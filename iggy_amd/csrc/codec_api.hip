@@ -51,1069 +51,29 @@ using namespace iggy;
         }                                                                      \
     } while (0)
 
-namespace {
+// Host runtime, by concern (each unit includes nothing itself; this order is the
+// dependency order):
+//   host_ctx      context, scratch buffers, slots, stream order
+//   host_mem      caller host memory: registry, pinned / pageable copies, history log
+//   host_decode   decode enqueue, synchronous decode / checksum / admission entries
+//   host_segment  segment recovery, state-transfer walk, segment writes
+//   host_encode   encode enqueue and entries
+//   host_poll     SDK poll decode, server conversion
+//   host_crypt    at-rest encryption host setup
+//   host_pollbody poll reply body
+//   host_slice    poll-path slicing, disk-chunk walk, device stamp
+//   host_async    asynchronous submit / poll / wait
+#include "host_ctx.hpp"
+#include "host_mem.hpp"
+#include "host_decode.hpp"
+#include "host_segment.hpp"
+#include "host_encode.hpp"
+#include "host_poll.hpp"
+#include "host_crypt.hpp"
+#include "host_pollbody.hpp"
+#include "host_slice.hpp"
+#include "host_async.hpp"
 
-// Host-memory history: every registration, mapped / pinned allocation and their
-// release, so a later fault can be checked against ranges the codec pinned or mapped
-// (VERDICT r05 item 5). IGGY_CODEC_DEBUG: on stderr; IGGY_CODEC_HOSTMEM_LOG=<path>:
-// appended to that file, one line per event with a monotonic timestamp (the test suite
-// sets it and attaches the tail to a failing test's report, tests/conftest.py).
-FILE *hostmem_file() {
-    static FILE *f = [] {
-        const char *p = getenv("IGGY_CODEC_HOSTMEM_LOG");
-        FILE *h = p && *p ? fopen(p, "a") : nullptr;
-        if (h) setvbuf(h, nullptr, _IOLBF, 0);
-        return h;
-    }();
-    return f;
-}
-bool hostmem_log_on() {
-    static const bool on = getenv("IGGY_CODEC_DEBUG") != nullptr || hostmem_file() != nullptr;
-    return on;
-}
-void hostmem_log(const char *what, const void *p, uint64_t n) {
-    if (!hostmem_log_on()) return;
-    static std::mutex mu;
-    std::lock_guard<std::mutex> lk(mu);
-    const double t = std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
-    char line[256];
-    snprintf(line, sizeof line, "%.6f iggy_codec hostmem: %s [%p, %p) %llu B\n", t, what, p,
-             (const void *)((const uint8_t *)p + n), (unsigned long long)n);
-    if (getenv("IGGY_CODEC_DEBUG")) fputs(line, stderr);
-    if (FILE *f = hostmem_file()) fputs(line, f);
-}
-
-// process-wide allocation counters (iggy_codec_host_stats)
-std::atomic<uint64_t> g_dev_allocs{0}, g_pin_allocs{0};
-
-// one device allocation that grows on demand (never inside an enqueue path
-// whose caller asked for graph-safety: grow happens in reserve / sync APIs)
-struct DevBuf {
-    void *p = nullptr;
-    size_t cap = 0;
-    int ensure(size_t n) {
-        if (n <= cap) return 0;
-        if (p) (void)hipFree(p);
-        p = nullptr;
-        cap = 0;
-        size_t want = std::max<size_t>(n, 256);
-        if (hipMalloc(&p, want) != hipSuccess) return IGGY_ERR_DEVICE;
-        g_dev_allocs.fetch_add(1, std::memory_order_relaxed);
-        cap = want;
-        return 0;
-    }
-    template <class T> T *as(size_t off = 0) { return (T *)((uint8_t *)p + off); }
-    void release() {
-        if (p) (void)hipFree(p);
-        p = nullptr;
-        cap = 0;
-    }
-};
-
-// Mapped, coherent pinned host memory that kernels read and write directly (small
-// tables in, results / positions / flags out): no copy operation on the stream.
-constexpr size_t kHostMapKeep = 8ull << 20;  // pinned bytes a context keeps between calls
-struct HostMap {
-    void *h = nullptr;
-    uint8_t *d = nullptr;  // the device's address of the same bytes
-    size_t cap = 0;
-    int ensure(size_t n) {
-        // grown past kHostMapKeep by one large call (a poll of many small frames, a
-        // 16 MiB decode with positions): given back at the next ordinary-sized call
-        // instead of staying pinned for the context's life
-        if (n <= cap && !(cap > kHostMapKeep && n <= kHostMapKeep)) return 0;
-        release();
-        const size_t want = std::max<size_t>(n, 64 << 10);
-        if (hipHostMalloc(&h, want, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess) {
-            h = nullptr;
-            return IGGY_ERR_DEVICE;
-        }
-        if (hipHostGetDevicePointer((void **)&d, h, 0) != hipSuccess) {
-            release();
-            return IGGY_ERR_DEVICE;
-        }
-        cap = want;
-        g_pin_allocs.fetch_add(1, std::memory_order_relaxed);
-        hostmem_log("mapped alloc", h, want);
-        // the completion flag lives in the first word: pinned memory handed back by the
-        // allocator may still hold another context's flag values, one of which this
-        // context's sequence could reach before its kernel writes it
-        memset(h, 0, 256);
-        return 0;
-    }
-    template <class T> T *hp(size_t off = 0) { return (T *)((uint8_t *)h + off); }
-    template <class T> T *dp(size_t off = 0) { return (T *)(d + off); }
-    void release() {
-        if (h) {
-            hostmem_log("mapped free", h, cap);
-            (void)hipHostFree(h);
-        }
-        h = nullptr;
-        d = nullptr;
-        cap = 0;
-    }
-};
-
-}  // namespace
-
-// an asynchronous encode's own scratch (enqueue_encode's per-batch arrays)
-struct EncOwn {
-    DevBuf epl, euh, etile, ecs, emisc, bsums;
-    void release() {
-        for (DevBuf *b : {&epl, &euh, &etile, &ecs, &emisc, &bsums}) b->release();
-    }
-};
-
-// one asynchronous host-buffer operation in flight (iggy_codec_*_submit / iggy_codec_poll)
-constexpr int kSlots = 8;
-struct Slot {
-    bool busy = false;
-    uint64_t ticket = 0;
-    uint32_t op = 0;
-    uint64_t cap = 0, out_len = 0;
-    // a single-stride decode submitted on the fast path (one records launch): what
-    // iggy_codec_poll needs to run the general walk when its stride breaks mid-record
-    bool fast = false, g_pending = false;
-    const uint8_t *g_in = nullptr;
-    uint64_t g_len = 0, g_pcap = 0;
-    uint64_t *g_pos = nullptr;  // device-visible positions destination of the launch
-    int g_integ = 0;
-    bool g_pos_copy = false;    // positions go through `pos` and a D2H copy
-    uint64_t *frame_pos = nullptr;               // host destination of the decode's positions
-    DevBuf in, pos, out, res;                    // device input / positions / encode output / result
-    DevBuf ids, ots, pay, plen, uhb, uhl;        // encode SoA inputs
-    HostMap tab;                                 // k_decode_records task table of an in-flight decode
-    // a pageable input of the fast path, copied here at submit: the kernel reads it in
-    // place (<= kZeroCopyBytes) or one DMA copies it, and the slot keeps it until it is
-    // done, so submit never waits on the stream for the caller's bytes
-    HostMap zin;
-    // the fast path's own stream and k_decode_records scratch: fast-path decodes of
-    // different slots run side by side (a small record's launch is bound by its reads'
-    // round trips over the host link, not by the chip)
-    hipStream_t st = nullptr;
-    DevBuf rstate, rbsums, rcount;
-    EncOwn eown;  // (small encodes in place: the same, for enqueue_encode)
-    hipEvent_t ev_in = nullptr, ev_k = nullptr, ev_done = nullptr;
-    // a pageable caller output is never a DMA target: the copy-out stream lands it in
-    // this pinned bounce and iggy_codec_poll copies it to the caller (hout_dst, hout_len)
-    void *hout = nullptr;
-    size_t hout_cap = 0;
-    uint8_t *hout_dst = nullptr;
-    uint64_t hout_len = 0;
-    int hout_ensure(size_t n) {
-        if (n <= hout_cap && !(hout_cap > (8ull << 20) && n <= (8ull << 20))) return 0;
-        if (hout) {
-            hostmem_log("bounce free", hout, hout_cap);
-            (void)hipHostFree(hout);
-        }
-        hout = nullptr;
-        hout_cap = 0;
-        const size_t want = std::max<size_t>(n, 64 << 10);
-        if (hipHostMalloc(&hout, want, hipHostMallocDefault) != hipSuccess) {
-            hout = nullptr;
-            return IGGY_ERR_DEVICE;
-        }
-        hout_cap = want;
-        g_pin_allocs.fetch_add(1, std::memory_order_relaxed);
-        hostmem_log("bounce alloc", hout, want);
-        return 0;
-    }
-    void release() {
-        DevBuf *b[] = {&in, &pos, &out, &res, &ids, &ots, &pay, &plen, &uhb, &uhl, &rstate, &rbsums, &rcount};
-        for (DevBuf *x : b) x->release();
-        tab.release();
-        zin.release();
-        eown.release();
-        if (st) (void)hipStreamDestroy(st), st = nullptr;
-        for (hipEvent_t *e : {&ev_in, &ev_k, &ev_done})
-            if (*e) (void)hipEventDestroy(*e), *e = nullptr;
-        if (hout) {
-            hostmem_log("bounce free", hout, hout_cap);
-            (void)hipHostFree(hout);
-        }
-        hout = nullptr;
-        hout_cap = 0;
-    }
-};
-
-constexpr size_t kCrTabBytesHost = (size_t)kGhPowers * 32 * 8;  // GHASH tables (= kCrTabBytes below)
-constexpr int kEncSegs = 4;                   // encode segments (checksum chain overlap); bounds below
-constexpr uint64_t kEncSegMinFrames = 1 << 18;  // below this one segment
-
-struct iggy_codec_ctx {
-    int device = 0;
-    hipStream_t stream = nullptr;
-    int ncu = 256;
-    // uniform decode grid: one WG per CU but one. A pipelined decode's consumer WG
-    // (the previous batch's chain tail) then never holds back one of the next
-    // decode's producer WGs. IGGY_CODEC_UNIFORM_GRID overrides it in the diagnostic
-    // build only.
-    int ugrid = 255;
-    uint32_t epoch = 0;
-    int allow_unaligned = 0;
-    uint32_t dbg = 0;  // IGGY_CODEC_DBG ablation bits: read only by the diagnostic build (kDiagMask)
-    // one stream order per context (its scratch is shared by every enqueue): the
-    // stream of the latest enqueue, and the event a switch to another stream waits on
-    hipStream_t last = nullptr;
-    hipEvent_t order_ev = nullptr;
-    // decode scratch
-    uint64_t dec_cap_len = 0;
-    DevBuf dsync;    // exited | first_bad | spec_fail | bar[4] | misc[16] | small[512] | bar2 (128-B stride)
-    DevBuf dsums, derr;
-    DevBuf gtiles_s, gtiles_x, gtiles_cnt, gtiles_pre, gtiles_list, gtiles_e, gtiles_base, ggrp, gfpos, gcs, gvrec, gtiles_lcs, gbsums;
-    int gen_grid = 0;  // WGs of k_decode_general (the ones that get a CU join its barriers)
-    // encode: the batch-checksum chain of earlier frame segments runs on `side`
-    // while later segments are encoded on the call's stream
-    hipStream_t side = nullptr;
-    hipEvent_t seg_ev[kEncSegs + 2] = {};  // segment ends, side-stream end, fork ([kEncSegs + 1])
-    DevBuf dresult;  // iggy_decode_result + iggy_encode_result + u64 scratch
-    // sync-API staging
-    DevBuf din, dpos, dout;
-    // encode scratch
-    DevBuf epl, euh, etile, ecs, emisc;
-    DevBuf eids, eots, epay, eplen, euhb, euhl;
-    DevBuf erec, esink;  // k_enc_ring's frame records and store sink
-    // big one-shot hash
-    DevBuf hbsums;
-    // poll
-    DevBuf ppos, pmsgs, pres;
-    DevBuf cwk;  // disk-chunk walk: state, gates, per-batch slice results, fragments
-    // multi-record decode (decode_records.hip): tasks | states | wg map, block sums,
-    // results, and the pinned staging of the task table (uploaded in one copy)
-    DevBuf rtab, rbsums, rres, clinks, rstate, rcount;
-    HostMap rmap;  // task table + workgroup map (read by the kernel in place when small)
-    HostMap cmap;  // chunk-walk candidates (read in place)
-    HostMap omap;  // [0, 64): completion flag; then results / positions / chunk-walk outputs
-    // a pageable record of <= kZeroCopyBytes for the synchronous fast path (or a small
-    // synchronous encode's SoA input), copied here and read by the kernels in place
-    HostMap zin;
-    HostMap zout;  // a small synchronous encode's wire bytes when the caller's `out` is not mapped
-    uint32_t hseq = 0;  // completion flag values
-    uint32_t chunk_epoch = 0;  // k_chunk_walk link tags
-    // segment writer: pinned staging halves and their copy events
-    void *wstage = nullptr;
-    hipEvent_t wev[2] = {nullptr, nullptr};
-    // slice / device stamp: [0,512) control words + header + small, then tile counts
-    DevBuf sl, slres;
-    // at-rest encryption: [0,64) misc, [64,192) output header, [192] n, [200] checksum,
-    // [256,384) decode result, [1024, +16 KiB) GHASH tables, then sizes / positions / tile sums
-    DevBuf cr;
-    void *cr_pinned = nullptr;   // host staging of the GHASH tables
-    // poll reply body: per-record decrypt verdicts, and the pinned host staging of the
-    // concatenated records / decrypted output (one H2D, one D2H per body)
-    DevBuf pbres;
-    void *pb_pinned = nullptr;
-    size_t pb_cap = 0;
-    // fingerprint of the key whose tables are on the device: E_K(0) || E_K(1), never the
-    // key itself (the reference keeps the key only inside its Aes256Gcm cipher object)
-    uint8_t cr_fp[32] = {};
-    bool cr_key_set = false;
-    // pinned host mirror of results
-    void *h_pinned = nullptr;
-    // caller host memory (put_host / get_host): the two pinned chunks pageable bytes are
-    // staged through, their last copies' events, and the event after a call's last H2D
-    void *xst = nullptr;
-    hipEvent_t xev[2] = {nullptr, nullptr};
-    bool xlive[2] = {false, false};
-    uint32_t xnext = 0;
-    hipEvent_t xin_ev = nullptr;
-    bool xin_live = false;
-    iggy_host_stats hs = {};  // iggy_codec_host_stats (the allocation counts are process-wide)
-    // asynchronous host-buffer operations: copy-in stream -> the context's stream -> copy-out
-    // stream, so one operation's H2D, another's kernels and a third's D2H overlap
-    hipStream_t h2d = nullptr, d2h = nullptr;
-    Slot slots[kSlots];
-    void *slot_pinned = nullptr;  // kSlots x 256 B: completion records
-    uint8_t *slot_pinned_d = nullptr;  // its device-mapped address (kernels write decode verdicts there)
-    uint64_t seq = 0;
-    // profiling
-    int profile = 0;
-    hipEvent_t ev0[2] = {nullptr, nullptr}, ev1[2] = {nullptr, nullptr};
-    uint64_t prof_n[2] = {0, 0};
-    double prof_ms[2] = {0, 0};
-    bool ev_pending[2] = {false, false};
-};
-
-namespace {
-
-constexpr size_t kSyncExited = 0, kSyncFirstBad = 8, kSyncSpecFail = 16, kSyncBar = 32,
-                 kSyncMisc = 64, kSyncSmall = 256, kSyncBar2 = 1024,  // + kBar2Words u32 at 128-B stride
-                 kSyncSink = kSyncBar2 + kBar2Words * 128,            // 64 x u64 (DecodeScratch::sink)
-                 kSyncBytes = kSyncSink + 512;
-
-int ensure_decode_scratch(iggy_codec_ctx *c, uint64_t len) {
-    if (len <= c->dec_cap_len && c->dsync.p) return 0;
-    const uint64_t L = std::max<uint64_t>(len, 1 << 20);
-    const uint64_t max_frames = L / 48 + 2;
-    const uint64_t max_chunks = (max_frames + 6) / 256 + 2;
-    const uint64_t ntiles = L / kTileMin + 2;
-    const uint64_t ngroups = ntiles / kGrpTiles + 2;
-    const uint64_t max_blocks = (44 + 8 * max_frames) / 1024 + 2;
-    int r = 0;
-    if (!c->dsync.p) {
-        r |= c->dsync.ensure(kSyncBytes);
-        if (r) return r;
-        HIP_OK(hipMemset(c->dsync.p, 0, kSyncBytes));
-    }
-    // one 128-B block record per 128 frames (2 per chunk, decode_uniform.hip); zeroed
-    // so no stale tag can match a live epoch
-    r |= c->dsums.ensure(max_chunks * kChunkSumWords * 8 + 64);
-    if (!r && c->dsums.p) HIP_OK(hipMemset(c->dsums.p, 0, c->dsums.cap));
-    r |= c->derr.ensure(max_chunks * 32 * 16);  // (stored, computed) per 8-frame group
-    r |= c->gtiles_s.ensure(ntiles * 8);
-    r |= c->gtiles_x.ensure(ntiles * 8);
-    r |= c->gtiles_cnt.ensure(ntiles * 4);
-    r |= c->gtiles_e.ensure(ntiles * 8);
-    r |= c->gtiles_pre.ensure(ntiles * 4);
-    r |= c->gtiles_list.ensure(tile_list_words(L) * 4);
-    r |= c->ggrp.ensure(ngroups * kGrpWords * 8);
-    r |= c->gtiles_base.ensure(ntiles * 8);
-    r |= c->gfpos.ensure(max_frames * 8);
-    r |= c->gcs.ensure(max_frames * 8 + 16);       // verify_frames_dma reads aligned pairs
-    r |= c->gvrec.ensure((max_frames + 1) * 16);   // walk-order frame records + "none"
-    r |= c->gtiles_lcs.ensure(tile_list_words(L) * 8);
-    r |= c->gbsums.ensure(max_blocks * 64);
-    if (r) return IGGY_ERR_DEVICE;
-    c->dec_cap_len = L;
-    return 0;
-}
-
-DecodeScratch dscratch(iggy_codec_ctx *c) {
-    DecodeScratch s;
-    s.exited = c->dsync.as<uint32_t>(kSyncExited);
-    s.first_bad = c->dsync.as<uint64_t>(kSyncFirstBad);
-    s.spec_fail = c->dsync.as<uint64_t>(kSyncSpecFail);
-    s.sums = c->dsums.as<uint64_t>();
-    s.errslot = c->derr.as<uint64_t>();
-    s.small = c->dsync.as<uint8_t>(kSyncSmall);
-    s.sink = c->dsync.as<uint64_t>(kSyncSink);
-    s.gbar = c->dsync.as<uint32_t>(kSyncBar);
-    s.gbar2 = c->dsync.as<uint32_t>(kSyncBar2);
-    s.gmisc = c->dsync.as<uint64_t>(kSyncMisc);
-    s.max_chunks = (c->dsums.cap - 64) / (kChunkSumWords * 8);
-    return s;
-}
-
-// diagnostic ablation bits, zero in the product build
-inline uint32_t diag_bits(const iggy_codec_ctx *c) { return c->dbg & kDiagMask; }
-
-GeneralScratch gscratch(iggy_codec_ctx *c) {
-    GeneralScratch g;
-    g.tile_s = c->gtiles_s.as<uint64_t>();
-    g.tile_x = c->gtiles_x.as<uint64_t>();
-    g.tile_cnt = c->gtiles_cnt.as<uint32_t>();
-    g.tile_e = c->gtiles_e.as<uint64_t>();
-    g.tile_pre = c->gtiles_pre.as<uint32_t>();
-    g.tile_list = c->gtiles_list.as<uint32_t>();
-    g.grp = c->ggrp.as<uint64_t>();
-    g.tile_base = c->gtiles_base.as<uint64_t>();
-    g.fpos = c->gfpos.as<uint64_t>();
-    g.cs = c->gcs.as<uint64_t>();
-    g.vrec = c->gvrec.as<uint64_t>();
-    g.tile_lcs = c->gtiles_lcs.as<uint64_t>();
-    g.bsums = c->gbsums.as<uint64_t>();
-    g.misc = c->dsync.as<uint64_t>(kSyncMisc);
-    g.bar = c->dsync.as<uint32_t>(kSyncBar);
-    g.bar2 = c->dsync.as<uint32_t>(kSyncBar2);
-    g.u_exited = c->dsync.as<uint32_t>(kSyncExited);
-    g.u_first_bad = c->dsync.as<uint64_t>(kSyncFirstBad);
-    g.u_spec_fail = c->dsync.as<uint64_t>(kSyncSpecFail);
-    g.small = c->dsync.as<uint8_t>(kSyncSmall);
-    g.ntiles = c->gtiles_s.cap / 8;
-    g.max_frames = c->gfpos.cap / 8;
-    g.max_blocks = c->gbsums.cap / 64;
-    g.dbg = diag_bits(c);
-    return g;
-}
-
-// Every enqueue of a context runs in ONE stream order: the scratch it uses (sync
-// words, unit sums, walk tables, result staging) belongs to the context. An
-// enqueue on another stream than the previous one first makes that stream wait
-// for everything enqueued before (an event recorded on the previous stream, which
-// must therefore still exist). Enqueues on one stream pay nothing.
-hipStream_t bind(iggy_codec_ctx *c, void *stream) {
-    hipStream_t s = stream ? (hipStream_t)stream : c->stream;
-    if (s != c->last) {
-        if (c->last && c->order_ev && hipEventRecord(c->order_ev, c->last) == hipSuccess)
-            (void)hipStreamWaitEvent(s, c->order_ev, 0);
-        c->last = s;
-    }
-    return s;
-}
-
-// The context's device is current for the duration of an entry point; the
-// caller's current device is restored on return (multi-GPU processes keep
-// one context per GPU on arbitrary threads).
-struct DevGuard {
-    int prev = -1, dev;
-    explicit DevGuard(int d) : dev(d) {
-        int cur = -1;
-        if (hipGetDevice(&cur) == hipSuccess && cur != d && hipSetDevice(d) == hipSuccess) prev = cur;
-    }
-    ~DevGuard() {
-        if (prev >= 0) (void)hipSetDevice(prev);
-    }
-};
-
-// ------------------------------------------------------- caller host memory
-// Every byte of caller host memory that crosses PCIe goes through put_host / get_host.
-// The reference codec borrows `&[u8]` for the call only (batch.rs:391); the caller may
-// free or reuse the memory the moment a call returns. Pinned memory (hipHostMalloc,
-// hipHostRegister, iggy_codec_host_register: the server's socket and segment buffers)
-// is a DMA source / target as it is. PAGEABLE memory is never handed to the runtime's
-// copy engine: for such a copy ROCclr pins (locks) the caller's range and releases
-// the lock only when it retires the copy command, at a later synchronisation of that
-// stream. The host-flag entries (round 3) returned without one, so a lock could
-// outlive the call, the caller freed the range, and a later copy to a new allocation
-// at the same addresses went through the stale lock: the hipErrorIllegalAddress /
-// "Memory Fault" faults of GPUTEST_r03 and round 4. Pageable bytes are
-// therefore staged through the context's own two pinned chunks (memcpy of chunk k+1
-// under the DMA of chunk k), so no runtime lock on caller memory ever exists.
-constexpr uint64_t kXferChunk = 4ull << 20;
-// Ranges registered through iggy_codec_host_register. The registry is process-wide
-// (iggy_codec_host_pinned takes no context), but each entry belongs to the context that
-// registered it: iggy_codec_destroy unregisters that context's leftovers, so no entry
-// outlives its registration. Entries are trusted without a HIP query on every hit: a
-// range must be unregistered through the codec (iggy_codec_host_unregister), never with
-// a bare hipHostUnregister, or a later lookup would DMA from / map an unpinned range.
-std::mutex g_reg_mu;
-struct RegRange {
-    uintptr_t h;   // host address
-    uint64_t len;
-    uintptr_t d;   // its device-mapped address on `device` (0: not mapped)
-    int device;
-    const iggy_codec_ctx *owner;
-};
-std::vector<RegRange> g_reg;
-
-bool host_pinned(const void *p, uint64_t n) {
-    if (!p || !n) return true;
-    const uintptr_t a = (uintptr_t)p;
-    {
-        std::lock_guard<std::mutex> lk(g_reg_mu);
-        for (const auto &r : g_reg)
-            if (a >= r.h && a - r.h <= r.len && n <= r.len - (a - r.h)) return true;
-    }
-    hipPointerAttribute_t at;
-    if (hipPointerGetAttributes(&at, p) != hipSuccess) {
-        (void)hipGetLastError();  // pageable: not an error for the caller's HIP code
-        return false;
-    }
-    if (at.type != hipMemoryTypeHost) return false;
-    void *start = nullptr;
-    size_t size = 0;
-    if (hipPointerGetAttribute(&start, HIP_POINTER_ATTRIBUTE_RANGE_START_ADDR, (hipDeviceptr_t)p) != hipSuccess ||
-        hipPointerGetAttribute(&size, HIP_POINTER_ATTRIBUTE_RANGE_SIZE, (hipDeviceptr_t)p) != hipSuccess) {
-        (void)hipGetLastError();
-        return false;
-    }
-    // only a range the query reports in host addresses that covers [p, p + n) counts;
-    // anything else is staged (always correct, only slower)
-    const uintptr_t s0 = (uintptr_t)start;
-    return a >= s0 && a - s0 <= size && n <= size - (a - s0);
-}
-
-// the device-mapped address of pinned host memory [p, p + n) (nullptr: not pinned or
-// not mapped); ranges registered through the codec answer from the registry
-const uint8_t *host_device_ptr(const void *p, uint64_t n) {
-    const uintptr_t a = (uintptr_t)p;
-    int dev = -1;
-    (void)hipGetDevice(&dev);  // (the calling entry's DevGuard: the context's device)
-    {
-        std::lock_guard<std::mutex> lk(g_reg_mu);
-        for (const auto &r : g_reg)
-            if (a >= r.h && a - r.h <= r.len && n <= r.len - (a - r.h) && r.device == dev)
-                return r.d ? (const uint8_t *)(r.d + (a - r.h)) : nullptr;
-    }
-    if (!host_pinned(p, n)) return nullptr;
-    void *dp = nullptr;
-    if (hipHostGetDevicePointer(&dp, (void *)p, 0) != hipSuccess || !dp) {
-        (void)hipGetLastError();
-        return nullptr;
-    }
-    return (const uint8_t *)dp;
-}
-
-int xfer_init(iggy_codec_ctx *c) {
-    if (c->xst) return 0;
-    if (hipHostMalloc(&c->xst, 2 * kXferChunk, hipHostMallocDefault) != hipSuccess) {
-        c->xst = nullptr;
-        return IGGY_ERR_DEVICE;
-    }
-    for (auto &ev : c->xev)
-        if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) return IGGY_ERR_DEVICE;
-    return 0;
-}
-
-// the next staging chunk, free for the host (its previous copy has run)
-int xfer_chunk(iggy_codec_ctx *c, uint8_t **chunk, int *idx) {
-    const int b = (int)(c->xnext++ & 1);
-    if (c->xlive[b]) {
-        c->hs.host_waits++;
-        HIP_OK(hipEventSynchronize(c->xev[b]));
-        c->xlive[b] = false;
-    }
-    *chunk = (uint8_t *)c->xst + (size_t)b * kXferChunk;
-    *idx = b;
-    return 0;
-}
-
-// H2D of n caller bytes on stream s. Returns with the caller's bytes consumed as far
-// as the caller is concerned: staged into pinned chunks (pageable), or enqueued from
-// memory the caller keeps pinned (a plain DMA source: the caller keeps it alive until
-// the call, or the ticket, completes; nothing of the runtime's outlives that copy).
-// Only a staged copy records xin_ev, the event a synchronous entry settles before it
-// returns (xfer_settle): an asynchronous submit of pinned memory issues no event and
-// no wait here, so its copy overlaps everything else in flight (round 5 recorded the
-// event for every copy, and its H2D / D2H no longer overlapped: C4 24.7 -> 17.6 GiB/s,
-// scripts/c4_diag.py).
-int put_host(iggy_codec_ctx *c, void *d_dst, const void *h_src, uint64_t n, hipStream_t s) {
-    if (!n) return 0;
-    if (host_pinned(h_src, n)) {
-        HIP_OK(hipMemcpyAsync(d_dst, h_src, n, hipMemcpyHostToDevice, s));
-        c->hs.pinned_h2d_bytes += n;
-        return 0;
-    }
-    c->hs.staged_bytes += n;
-    if (xfer_init(c)) return IGGY_ERR_DEVICE;
-    for (uint64_t off = 0; off < n; off += kXferChunk) {
-        const uint64_t m = std::min(kXferChunk, n - off);
-        uint8_t *st;
-        int b;
-        int r = xfer_chunk(c, &st, &b);
-        if (r) return r;
-        memcpy(st, (const uint8_t *)h_src + off, m);
-        HIP_OK(hipMemcpyAsync((uint8_t *)d_dst + off, st, m, hipMemcpyHostToDevice, s));
-        HIP_OK(hipEventRecord(c->xev[b], s));
-        c->xlive[b] = true;
-    }
-    if (!c->xin_ev && hipEventCreateWithFlags(&c->xin_ev, hipEventDisableTiming) != hipSuccess) {
-        c->xin_ev = nullptr;
-        return IGGY_ERR_DEVICE;
-    }
-    HIP_OK(hipEventRecord(c->xin_ev, s));
-    c->hs.settle_events++;
-    c->xin_live = true;
-    return 0;
-}
-
-// Before a synchronous entry that saw its completion through a host-mapped flag (no
-// stream sync) returns: its staged H2D copies are done. They ran before the kernel that
-// raised the flag, so this costs one signal read (nothing at all after pinned copies).
-int xfer_settle(iggy_codec_ctx *c) {
-    if (c->xin_live) {
-        c->hs.host_waits++;
-        HIP_OK(hipEventSynchronize(c->xin_ev));
-        c->xin_live = false;
-    }
-    return 0;
-}
-
-// D2H of n bytes into caller memory on stream s; synchronous (returns with the bytes
-// in h_dst and nothing of the call outstanding on s).
-int get_host(iggy_codec_ctx *c, void *h_dst, const void *d_src, uint64_t n, hipStream_t s) {
-    if (!n) return 0;
-    c->hs.host_waits++;  // (returns with the bytes in h_dst)
-    if (host_pinned(h_dst, n)) {
-        HIP_OK(hipMemcpyAsync(h_dst, d_src, n, hipMemcpyDeviceToHost, s));
-        HIP_OK(hipStreamSynchronize(s));
-        return 0;
-    }
-    if (xfer_init(c)) return IGGY_ERR_DEVICE;
-    const uint64_t nk = (n + kXferChunk - 1) / kXferChunk;
-    uint8_t *st[2] = {nullptr, nullptr};
-    int bi[2] = {0, 0};
-    auto issue = [&](uint64_t k) -> int {
-        const uint64_t off = k * kXferChunk, m = std::min(kXferChunk, n - off);
-        int r = xfer_chunk(c, &st[k & 1], &bi[k & 1]);
-        if (r) return r;
-        HIP_OK(hipMemcpyAsync(st[k & 1], (const uint8_t *)d_src + off, m, hipMemcpyDeviceToHost, s));
-        HIP_OK(hipEventRecord(c->xev[bi[k & 1]], s));
-        c->xlive[bi[k & 1]] = true;
-        return 0;
-    };
-    int r = issue(0);
-    for (uint64_t k = 0; k < nk && !r; ++k) {
-        HIP_OK(hipEventSynchronize(c->xev[bi[k & 1]]));
-        c->xlive[bi[k & 1]] = false;
-        const uint8_t *src = st[k & 1];
-        if (k + 1 < nk) r = issue(k + 1);  // the next chunk's copy runs under this memcpy
-        const uint64_t off = k * kXferChunk;
-        memcpy((uint8_t *)h_dst + off, src, std::min(kXferChunk, n - off));
-    }
-    return r;
-}
-
-
-void prof_begin(iggy_codec_ctx *c, int which, hipStream_t s) {
-    if (!c->profile) return;
-    if (c->ev_pending[which]) {
-        float ms = 0;
-        if (hipEventSynchronize(c->ev1[which]) == hipSuccess &&
-            hipEventElapsedTime(&ms, c->ev0[which], c->ev1[which]) == hipSuccess) {
-            c->prof_ms[which] += ms;
-            c->prof_n[which] += 1;
-        }
-        c->ev_pending[which] = false;
-    }
-    (void)hipEventRecord(c->ev0[which], s);
-}
-void prof_end(iggy_codec_ctx *c, int which, hipStream_t s) {
-    if (!c->profile) return;
-    (void)hipEventRecord(c->ev1[which], s);
-    c->ev_pending[which] = true;
-}
-
-// launch the whole decode (uniform kernel + guarded general kernel)
-// k_bsum_blocks grid: one wave per 1024-B block of the checksum input (44 + 8 N
-// bytes, N <= max_frames), at most 4 WGs per CU; small inputs launch a small grid
-static uint32_t bsum_grid(const iggy_codec_ctx *c, uint64_t max_frames) {
-    const uint64_t blocks = (44 + 8 * max_frames) / 1024 + 1;
-    return (uint32_t)std::min<uint64_t>((uint64_t)c->ncu * 4, (blocks + 3) / 4);
-}
-
-// k_decode_general after a first-pass kernel on stream s: it returns at once unless that
-// kernel left d_res->status == kStatusNeedGeneral (ensure_decode_scratch done by the caller)
-void launch_general(iggy_codec_ctx *c, const uint8_t *d_body, uint64_t len, int integrity, uint64_t *d_pos,
-                    uint64_t cap, iggy_decode_result *d_res, hipStream_t s) {
-    GeneralScratch gs = gscratch(c);
-    const uint32_t ggrid = (uint32_t)std::min<uint64_t>((uint64_t)c->gen_grid, len / (64 << 10) + 2);
-    if (integrity == IGGY_INTEGRITY_VERIFY)
-        hipLaunchKernelGGL(k_decode_general<true>, dim3(ggrid), dim3(kGenThreads), kGenLds, s, d_body, len, d_pos,
-                           cap, d_res, gs);
-    else
-        hipLaunchKernelGGL(k_decode_general<false>, dim3(ggrid), dim3(kGenThreads), 0, s, d_body, len, d_pos, cap,
-                           d_res, gs);
-}
-
-int enqueue_decode(iggy_codec_ctx *c, const uint8_t *d_body, uint64_t len, int integrity,
-                   uint64_t *d_pos, uint64_t cap, iggy_decode_result *d_res, hipStream_t s) {
-    int r = ensure_decode_scratch(c, len);
-    if (r) return r;
-    if (++c->epoch > kEpochMask) {  // 24-bit tags: re-zero the block records before reusing one
-        c->epoch = 1;
-        HIP_OK(hipMemsetAsync(c->dsums.p, 0, c->dsums.cap, s));
-    }
-    const bool verify = integrity == IGGY_INTEGRITY_VERIFY;
-    DecodeScratch ds = dscratch(c);
-    // one persistent grid: one WG per CU, block 0 the consumer (chain) WG. Small
-    // records get grids sized to their work (at most one producer WG per 128-frame
-    // block of 48-B frames; one general WG per 64 KiB): dispatching two full
-    // persistent grids dominated a 300-KB decode. Both kernels split their work
-    // over whatever grid they get.
-    const uint64_t ub_blocks = len / (48 * 128) + 2;
-    const uint32_t grid = (uint32_t)std::min<uint64_t>((uint64_t)c->ugrid, ub_blocks + 1);
-    const uint32_t au = (uint32_t)c->allow_unaligned;
-    prof_begin(c, 0, s);
-    if (verify)
-        hipLaunchKernelGGL(k_decode_uniform<true>, dim3(grid), dim3(kUniformThreads), kUniformLds, s, d_body, len, d_pos,
-                           cap, d_res, ds, c->epoch, au, diag_bits(c));
-    else
-        hipLaunchKernelGGL(k_decode_uniform<false>, dim3(grid), dim3(kUniformThreads), kUniformLds, s, d_body, len, d_pos,
-                           cap, d_res, ds, c->epoch, au, diag_bits(c));
-    HIP_OK(hipGetLastError());
-    launch_general(c, d_body, len, integrity, d_pos, cap, d_res, s);
-    // the profiled interval is the whole decode: both kernels (the general one writes a
-    // lane-group decode's frame positions, decode_uniform.hip kPosEpilogue)
-    prof_end(c, 0, s);
-    HIP_OK(hipGetLastError());
-    return 0;
-}
-
-void fill_err(iggy_wire_error *err, const iggy_wire_error &e) {
-    if (err) *err = e;
-}
-void set_err(iggy_wire_error *err, uint32_t kind, uint32_t reason = 0, uint64_t a = 0,
-             uint64_t b = 0, uint64_t cc = 0) {
-    if (!err) return;
-    err->kind = kind;
-    err->reason = reason;
-    err->a = a;
-    err->b = b;
-    err->c = cc;
-}
-
-int reset_after_timeout(iggy_codec_ctx *c) {
-    HIP_OK(hipStreamSynchronize(c->stream));
-    HIP_OK(hipMemset(c->dsync.p, 0, kSyncBytes));
-    return 0;
-}
-
-// synchronous decode of a host buffer; also used by stamp / checksum helpers
-constexpr uint64_t kHostFastBytes = 16ull << 20;
-#ifndef IGGY_ZERO_COPY_BYTES
-#define IGGY_ZERO_COPY_BYTES (4ull << 20)  // (build knob for same-box A/B: 1 MiB measured slower)
-#endif
-constexpr uint64_t kZeroCopyBytes = IGGY_ZERO_COPY_BYTES;  // host inputs up to this size are read in place
-#ifndef IGGY_POLL_IN_PLACE
-#define IGGY_POLL_IN_PLACE 1  // (build knob for same-box A/B: poll bodies read in place)
-#endif
-int decode_host_fast(iggy_codec_ctx *c, const uint8_t *body, uint64_t len, int integrity,
-                     iggy_decode_result *res_out, uint64_t *frame_pos, uint64_t cap, bool *done);
-int decode_host(iggy_codec_ctx *c, const uint8_t *body, uint64_t len, int integrity,
-                iggy_decode_result *res_out, uint64_t *frame_pos, uint64_t cap, bool keep_on_device) {
-    bool done = false;
-    int r = decode_host_fast(c, body, len, integrity, res_out, frame_pos, cap, &done);
-    if (r || done) return r;
-    r |= c->din.ensure(len + 16);
-    const uint64_t pcap = frame_pos ? std::min<uint64_t>(cap, len / 48 + 1) : 0;
-    r |= c->dpos.ensure((pcap + 1) * 8);
-    if (r) return IGGY_ERR_DEVICE;
-    r = put_host(c, c->din.p, body, len, c->stream);
-    if (r) return r;
-    iggy_decode_result *d_res = c->dresult.as<iggy_decode_result>();
-    r = enqueue_decode(c, c->din.as<uint8_t>(), len, integrity, pcap ? c->dpos.as<uint64_t>() : nullptr,
-                       pcap, d_res, c->stream);
-    if (r) return r;
-    iggy_decode_result *h_res = (iggy_decode_result *)c->h_pinned;
-    HIP_OK(hipMemcpyAsync(h_res, d_res, sizeof(*h_res), hipMemcpyDeviceToHost, c->stream));
-    HIP_OK(hipStreamSynchronize(c->stream));
-    *res_out = *h_res;
-    if (res_out->error.kind == IGGY_ERR_TIMEOUT) reset_after_timeout(c);
-    if (frame_pos && pcap && res_out->error.kind == IGGY_OK) {
-        const uint64_t n = std::min<uint64_t>(res_out->frame_count, pcap);
-        if (n) return get_host(c, frame_pos, c->dpos.p, n * 8, c->stream);
-    }
-    (void)keep_on_device;
-    return 0;
-}
-
-
-// ------------------------------------------------------- multi-record decode
-// The walks over a sequence of batches (disk chunk, segment recovery, transferred
-// segment, poll body) decode every record in ONE launch of k_decode_records
-// (decode_records.hip). The host plans the launch from its own copy of the bytes
-// with the same stride speculation as make_plan: each single-stride record gets one
-// workgroup per 128-frame checksum block; a record that is not single-stride (or
-// is large enough to fill the chip on its own) takes the single-record path.
-struct RecIn {
-    uint64_t off, len;           // record start in the buffer, bytes available from there
-    uint64_t pos_base, pos_cap;  // frame positions (device buffer passed to enqueue_records)
-    uint64_t msg_base;           // polled messages (idem)
-};
-constexpr uint64_t kRecSingleBytes = 64ull << 20;  // larger records: the persistent single-record decode
-
-// -> workgroups of record [h, h + len) in k_decode_records (>= 1), 0 = single-record path
-uint64_t rec_plan(const uint8_t *h, uint64_t len, uint64_t *n_frames) {
-    *n_frames = 0;
-    if (len < kHdr) return 1;  // UnexpectedEof: resolved by the kernel from the header alone
-    uint64_t bl;
-    memcpy(&bl, h + 32, 8);
-    if (bl < kHdr) return 1;
-    for (uint32_t i = 52; i < kHdr; ++i)
-        if (h[i]) return 1;
-    if (len < bl) return 1;
-    const uint64_t blob = bl - kHdr;
-    if (blob == 0) return 1;
-    uint64_t resv;
-    if (blob < kFrameHdr) return 1;
-    memcpy(&resv, h + kHdr + 40, 8);
-    if (resv) return 1;
-    uint32_t uh, pl;
-    memcpy(&uh, h + kHdr + 32, 4);
-    memcpy(&pl, h + kHdr + 36, 4);
-    const uint64_t S = kFrameHdr + (uint64_t)uh + pl;
-    if (S > blob) return 1;
-    if (blob % S != 0 || S > (1u << 20) || bl > kRecSingleBytes) return 0;
-    *n_frames = blob / S;
-    return rec_blocks(blob / S);
-}
-
-// Enqueue the decode of K records of the device buffer d_base (h_base: the host
-// copy of the same bytes) on the context's stream: one k_decode_records launch for
-// every planned record, then the single-record decode of the others (appended to
-// *single). d_res[k] receives record k's verdict (device or host-mapped memory when
-// no record takes the single path); a record left with status kStatusNeedGeneral
-// (its stride breaks mid-record) is re-decoded by redo_general. host_flag (device
-// address of host-mapped memory, nullable): raised to flag_value when the launch is
-// complete. n_frames[k] (nullable) = the planned frame count (0 for single-path
-// records).
-constexpr uint64_t kRecZeroCopyWgs = 4096;  // larger launches upload their tables (H2D)
-
-int enqueue_records(iggy_codec_ctx *c, const uint8_t *d_base, const uint8_t *h_base, const RecIn *recs, size_t K,
-                    int integrity, uint64_t *d_pos, iggy_polled_message *d_msgs, iggy_decode_result *d_res,
-                    std::vector<size_t> *single, std::vector<uint64_t> *n_frames = nullptr,
-                    uint32_t *host_flag = nullptr, uint32_t flag_value = 0, HostMap *tab = nullptr,
-                    GenRearm rearm = GenRearm{nullptr, nullptr, nullptr}, Slot *own = nullptr) {
-    // tab (nullable): host-mapped memory for the launch's task table that stays the
-    // caller's until the launch completes (asynchronous submits); else the context's.
-    // own (nullable): a fast-path slot whose stream and scratch the launch uses (no
-    // context scratch: every record must plan, so nothing takes the single path)
-    hipStream_t s = own ? own->st : c->stream;
-    HostMap &rm = tab ? *tab : c->rmap;
-    DevBuf &rbsums = own ? own->rbsums : c->rbsums;
-    DevBuf &rstate = own ? own->rstate : c->rstate;
-    DevBuf &rcount = own ? own->rcount : c->rcount;
-    std::vector<RecTask> tasks(K);
-    std::vector<uint32_t> wgmap;
-    uint64_t nbs = 0, maxlen = 0;
-    if (n_frames) n_frames->assign(K, 0);
-    for (size_t k = 0; k < K; ++k) {
-        uint64_t nf = 0;
-        const uint64_t nw = rec_plan(h_base + recs[k].off, recs[k].len, &nf);
-        RecTask &t = tasks[k];
-        t.off = recs[k].off;
-        t.len = recs[k].len;
-        t.pos_base = recs[k].pos_base;
-        t.pos_cap = d_pos ? recs[k].pos_cap : 0;
-        t.msg_base = recs[k].msg_base;
-        t.bsum_base = nbs;
-        t.wg0 = (uint32_t)wgmap.size();
-        t.nwg = (uint32_t)nw;
-        if (!nw) {
-            single->push_back(k);
-            maxlen = std::max(maxlen, recs[k].len);
-            continue;
-        }
-        if (n_frames) (*n_frames)[k] = nf;
-        nbs += nw;
-        wgmap.insert(wgmap.end(), nw, (uint32_t)k);
-    }
-    const uint64_t W = wgmap.size();
-    if (W) {
-        const size_t tb = K * sizeof(RecTask), wb = W * 4;
-        int r = rm.ensure(tb + wb);
-        r |= rbsums.ensure(nbs * 64 + 64);
-        const size_t st_before = rstate.cap;
-        r |= rstate.ensure(K * sizeof(RecState));
-        if (!rcount.p) {
-            r |= rcount.ensure(64);
-            if (!r) HIP_OK(hipMemsetAsync(rcount.p, 0, rcount.cap, s));
-        }
-        if (r) return IGGY_ERR_DEVICE;
-        if (rstate.cap != st_before)  // fresh state: zero (the resolvers keep it zero after)
-            HIP_OK(hipMemsetAsync(rstate.p, 0, rstate.cap, s));
-        memcpy(rm.hp<uint8_t>(), tasks.data(), tb);
-        memcpy(rm.hp<uint8_t>(tb), wgmap.data(), wb);
-        const RecTask *dt = rm.dp<RecTask>();
-        const uint32_t *dw = rm.dp<uint32_t>(tb);
-        const RecTask inl = tasks[0];
-        if (K == 1) {  // one record: the task rides in the kernel arguments
-            dt = nullptr;
-            dw = nullptr;
-        } else if (W > kRecZeroCopyWgs && !tab) {  // a big launch: every workgroup would read its task over PCIe
-            r = c->rtab.ensure(tb + wb);
-            if (r) return IGGY_ERR_DEVICE;
-            HIP_OK(hipMemcpyAsync(c->rtab.p, rm.h, tb + wb, hipMemcpyHostToDevice, s));
-            dt = c->rtab.as<RecTask>();
-            dw = c->rtab.as<uint32_t>(tb);
-        }
-        RecState *ds = rstate.as<RecState>();
-        uint32_t *flag = single->empty() ? host_flag : nullptr;
-        if (integrity == IGGY_INTEGRITY_VERIFY)
-            hipLaunchKernelGGL(k_decode_records<true>, dim3((uint32_t)W), dim3(kRecThreads), 0, s, d_base, dt, dw, ds,
-                               rbsums.as<uint64_t>(), d_pos, d_msgs, d_res, rcount.as<uint32_t>(), flag,
-                               flag_value, rearm, inl);
-        else
-            hipLaunchKernelGGL(k_decode_records<false>, dim3((uint32_t)W), dim3(kRecThreads), 0, s, d_base, dt, dw,
-                               ds, rbsums.as<uint64_t>(), d_pos, d_msgs, d_res, rcount.as<uint32_t>(), flag,
-                               flag_value, rearm, inl);
-        HIP_OK(hipGetLastError());
-    }
-    if (!single->empty()) {
-        if (own) return IGGY_ERR_DEVICE;  // (the caller planned every record)
-        int r = ensure_decode_scratch(c, maxlen);
-        if (r) return r;
-        for (size_t k : *single) {
-            r = enqueue_decode(c, d_base + recs[k].off, recs[k].len, integrity,
-                               d_pos ? d_pos + recs[k].pos_base : nullptr, d_pos ? recs[k].pos_cap : 0, d_res + k, s);
-            if (r) return r;
-        }
-    }
-    return 0;
-}
-
-// true when every record goes to the multi-record kernel (the launch can raise the
-// host flag: results straight into host-mapped memory, no copy, no stream sync)
-bool records_all_planned(const uint8_t *h_base, const RecIn *recs, size_t K) {
-    for (size_t k = 0; k < K; ++k) {
-        uint64_t nf;
-        if (!rec_plan(h_base + recs[k].off, recs[k].len, &nf)) return false;
-    }
-    return true;
-}
-
-// Wait for a kernel to raise the host-mapped completion flag (a spin: the host
-// round trip of a stream sync or a result copy is what small host-buffer calls pay
-// most for). If the stream drains without the flag, the launch failed.
-// Bounded: a launch that neither raises the flag nor drains within kHostWaitLimit
-// (the kernels' own spin guards are 4 s) returns IGGY_ERR_TIMEOUT to the caller's
-// thread instead of holding it.
-constexpr double kHostWaitLimitS = 10.0;
-int wait_host_flag(iggy_codec_ctx *c, uint32_t v) {
-    volatile uint32_t *flag = c->omap.hp<volatile uint32_t>();
-    auto dbg = [&](const char *what, int rc) {
-        if (getenv("IGGY_CODEC_DEBUG"))
-            fprintf(stderr, "iggy_codec: wait_host_flag(%u): %s (flag %u)\n", v, what, *flag);
-        return rc;
-    };
-    const auto t0 = std::chrono::steady_clock::now();
-    for (uint64_t i = 1;; ++i) {
-        if (__atomic_load_n(flag, __ATOMIC_ACQUIRE) == v) return 0;
-        if ((i & 1023) == 0) {
-            const hipError_t q = hipStreamQuery(c->stream);
-            if (q == hipSuccess) {
-                // the stream drained: the flag store (system scope, over PCIe) may still be
-                // in flight behind the completion signal for a moment; then it is final
-                for (int k = 0; k < 100000; ++k) {
-                    if (__atomic_load_n(flag, __ATOMIC_ACQUIRE) == v) return 0;
-                    __builtin_ia32_pause();
-                }
-                return dbg("stream drained without the flag", IGGY_ERR_DEVICE);
-            }
-            if (q != hipErrorNotReady) return dbg(hipGetErrorString(q), IGGY_ERR_DEVICE);
-            if ((i & 0xfffff) == 0 &&
-                std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > kHostWaitLimitS)
-                return dbg("time limit", IGGY_ERR_TIMEOUT);
-        }
-        __builtin_ia32_pause();
-    }
-}
-uint32_t next_flag(iggy_codec_ctx *c) {
-    if (++c->hseq == 0) c->hseq = 1;
-    return c->hseq;
-}
-
-// After the launch: records the multi-record kernel left with status
-// kStatusNeedGeneral are decoded again by the single-record path (general walk, into
-// the device results buffer) and res (host) is refreshed for them. Returns
-// IGGY_ERR_TIMEOUT if a bug guard fired anywhere.
-int redo_general(iggy_codec_ctx *c, const uint8_t *d_base, const RecIn *recs, size_t K, int integrity,
-                 uint64_t *d_pos, iggy_decode_result *res, std::vector<size_t> *redone) {
-    std::vector<size_t> redo;
-    uint64_t maxlen = 0;
-    for (size_t k = 0; k < K; ++k) {
-        if (res[k].error.kind == IGGY_ERR_TIMEOUT) {
-            reset_after_timeout(c);
-            return IGGY_ERR_TIMEOUT;
-        }
-        if (res[k].status == kStatusNeedGeneral) {
-            redo.push_back(k);
-            maxlen = std::max(maxlen, recs[k].len);
-        }
-    }
-    if (redo.empty()) return 0;
-    int r = ensure_decode_scratch(c, maxlen);
-    r |= c->rres.ensure(K * sizeof(iggy_decode_result));
-    if (r) return r ? r : IGGY_ERR_DEVICE;
-    iggy_decode_result *d_res = c->rres.as<iggy_decode_result>();
-    for (size_t k : redo) {
-        r = enqueue_decode(c, d_base + recs[k].off, recs[k].len, integrity, d_pos ? d_pos + recs[k].pos_base : nullptr,
-                           d_pos ? recs[k].pos_cap : 0, d_res + k, c->stream);
-        if (r) return r;
-    }
-    for (size_t k : redo) {
-        r = get_host(c, res + k, d_res + k, sizeof(iggy_decode_result), c->stream);
-        if (r) return r;
-    }
-    for (size_t k : redo)
-        if (res[k].error.kind == IGGY_ERR_TIMEOUT) {
-            reset_after_timeout(c);
-            return IGGY_ERR_TIMEOUT;
-        }
-    if (redone) *redone = redo;
-    return 0;
-}
-
-// Every record of the device buffer d_base decoded, the verdicts in res (host): one
-// launch; when every record is planned for the multi-record kernel its results land
-// in host-mapped memory and the host spins on the completion flag, otherwise device
-// results, one copy and a stream sync; then the general re-walks, if any.
-int decode_records_to_host(iggy_codec_ctx *c, const uint8_t *d_base, const uint8_t *h_base, const RecIn *recs,
-                           size_t K, int integrity, iggy_decode_result *res) {
-    std::vector<size_t> single;
-    const size_t rb = K * sizeof(iggy_decode_result);
-    if (records_all_planned(h_base, recs, K)) {
-        if (c->omap.ensure(64 + rb)) return IGGY_ERR_DEVICE;
-        const uint32_t v = next_flag(c);
-        int r = enqueue_records(c, d_base, h_base, recs, K, integrity, nullptr, nullptr,
-                                c->omap.dp<iggy_decode_result>(64), &single, nullptr, c->omap.dp<uint32_t>(), v);
-        if (r) return r;
-        r = wait_host_flag(c, v);
-        if (!r) r = xfer_settle(c);
-        if (r) return r;
-        memcpy(res, c->omap.hp<uint8_t>(64), rb);
-    } else {
-        if (c->rres.ensure(rb)) return IGGY_ERR_DEVICE;
-        iggy_decode_result *d_res = c->rres.as<iggy_decode_result>();
-        int r = enqueue_records(c, d_base, h_base, recs, K, integrity, nullptr, nullptr, d_res, &single);
-        if (!r) r = get_host(c, res, d_res, rb, c->stream);
-        if (r) return r;
-    }
-    return redo_general(c, d_base, recs, K, integrity, nullptr, res, nullptr);
-}
-
-// A small single-stride record from host memory (iggy_codec_decode_batch and the
-// host entry points built on it): one H2D copy and ONE k_decode_records launch that
-// writes the verdict and the frame positions straight into host-mapped memory, the
-// host spinning on its completion flag -- two stream operations instead of the
-// persistent pair's five (H2D, two kernels, two copies back, a sync). *done = false
-// leaves the record to the persistent path (not single-stride, too large, or the
-// stride broke mid-record).
-int decode_host_fast(iggy_codec_ctx *c, const uint8_t *body, uint64_t len, int integrity,
-                     iggy_decode_result *res_out, uint64_t *frame_pos, uint64_t cap, bool *done) {
-    *done = false;
-    uint64_t nf = 0;
-    if (len > kHostFastBytes || !rec_plan(body, len, &nf)) return 0;
-    // (diagnostic build, IGGY_CODEC_TIMING=N: mean stage times of the next N calls)
-    static int timing = kDiagMask && getenv("IGGY_CODEC_TIMING") ? atoi(getenv("IGGY_CODEC_TIMING")) : 0;
-    static double tsum[4] = {0, 0, 0, 0};
-    static int tn = 0;
-    using tclk = std::chrono::steady_clock;
-    const auto tt0 = tclk::now();
-    auto tmark = [&](int k) {
-        if (timing) tsum[k] += std::chrono::duration<double, std::micro>(tclk::now() - tt0).count();
-    };
-    const uint64_t pcap = frame_pos ? std::min<uint64_t>(cap, len / 48 + 1) : 0;
-    if (c->omap.ensure(64 + 128 + pcap * 8)) return IGGY_ERR_DEVICE;
-    // a registered (page-locked, device-mapped) record of at most kZeroCopyBytes is read
-    // by the kernel in place over the host link: no H2D, one launch and the flag
-    const uint8_t *d_base = nullptr;
-    if (len <= kZeroCopyBytes) d_base = host_device_ptr(body, len);
-    int r = 0;
-    if (!d_base && len <= kZeroCopyBytes && !host_pinned(body, len)) {
-        // pageable: into the context's own mapped staging, read in place (the previous
-        // fast call's kernel is done: every synchronous entry waits for its flag)
-        if (c->zin.ensure(len + 16)) return IGGY_ERR_DEVICE;
-        memcpy(c->zin.h, body, len);
-        d_base = c->zin.d;
-    }
-    if (!d_base) {
-        if (c->din.ensure(len + 16)) return IGGY_ERR_DEVICE;
-        r = put_host(c, c->din.p, body, len, c->stream);
-        if (r) return r;
-        d_base = c->din.as<uint8_t>();
-    }
-    tmark(0);
-    const RecIn rec{0, len, 0, pcap, 0};
-    std::vector<size_t> single;
-    const uint32_t v = next_flag(c);
-    r = enqueue_records(c, d_base, body, &rec, 1, integrity,
-                        pcap ? c->omap.dp<uint64_t>(192) : nullptr, nullptr, c->omap.dp<iggy_decode_result>(64),
-                        &single, nullptr, c->omap.dp<uint32_t>(), v);
-    if (r) return r;
-    tmark(1);
-    r = wait_host_flag(c, v);
-    if (!r) r = xfer_settle(c);
-    if (r) return r;
-    tmark(2);
-    const iggy_decode_result res = *c->omap.hp<iggy_decode_result>(64);
-    if (res.status == kStatusNeedGeneral) return 0;
-    *res_out = res;
-    if (frame_pos && pcap && res.error.kind == IGGY_OK)
-        memcpy(frame_pos, c->omap.hp<uint64_t>(192), std::min<uint64_t>(res.frame_count, pcap) * 8);
-    *done = true;
-    tmark(3);
-    if (timing && ++tn == timing) {
-        fprintf(stderr, "iggy_codec timing (%d calls, us from entry): staged %.2f launched %.2f flag %.2f done %.2f\n",
-                tn, tsum[0] / tn, tsum[1] / tn, tsum[2] / tn, tsum[3] / tn);
-        tn = 0;
-        tsum[0] = tsum[1] = tsum[2] = tsum[3] = 0;
-    }
-    return 0;
-}
-
-}  // namespace
 
 // ===================================================================== ABI
 extern "C" {
@@ -1307,2188 +267,6 @@ int iggy_codec_synchronize(iggy_codec_ctx *c) {
 
 // iggy_batch_header_decode / _encode and iggy_encoded_batch_size (host pure) live in
 // sdk.cpp, which also builds alone for the host sanitizer run (tests/fuzz/).
-
-// ------------------------------------------------------------ synchronous
-int iggy_codec_decode_batch(iggy_codec_ctx *c, const uint8_t *body, uint64_t len, int integrity,
-                            iggy_batch_header *hdr, uint64_t *frame_pos, uint64_t cap,
-                            uint64_t *nframes, iggy_wire_error *err) {
-    if (!c || (!body && len)) return IGGY_ERR_INVALID_ARGUMENT;
-    DevGuard dg(c->device);
-    bind(c, nullptr);
-    iggy_decode_result res;
-    int r = decode_host(c, body, len, integrity, &res, frame_pos, cap, false);
-    if (r) return r;
-    fill_err(err, res.error);
-    if (hdr) *hdr = res.header;
-    if (nframes) *nframes = res.frame_count;
-    if (res.error.kind != IGGY_OK) return (int)res.error.kind;
-    if (frame_pos && res.frame_count > cap) {
-        set_err(err, IGGY_ERR_CAPACITY, 0, res.frame_count, cap);
-        return IGGY_ERR_CAPACITY;
-    }
-    return 0;
-}
-
-// Stage [256-B header built from *h][blob] in the context's input buffer: two
-// copies straight from the caller's memory (no host-side concatenation).
-static int stage_record(iggy_codec_ctx *c, const iggy_batch_header &h, const uint8_t *blob, uint64_t blob_len) {
-    if (c->din.ensure(256 + blob_len + 16)) return IGGY_ERR_DEVICE;
-    uint8_t *hb = (uint8_t *)c->h_pinned + 2048;  // pinned: the copy is truly async
-    iggy_batch_header_encode(&h, hb);
-    HIP_OK(hipMemcpyAsync(c->din.p, hb, 256, hipMemcpyHostToDevice, c->stream));
-    return put_host(c, c->din.as<uint8_t>(256), blob, blob_len, c->stream);
-}
-
-int iggy_codec_verify_and_recompute_batch_checksum(iggy_codec_ctx *c, const iggy_batch_header *hdr,
-                                                   const uint8_t *blob, uint64_t blob_len,
-                                                   uint64_t *out, iggy_wire_error *err) {
-    if (!c || !hdr || (!blob && blob_len)) return IGGY_ERR_INVALID_ARGUMENT;
-    DevGuard dg(c->device);
-    bind(c, nullptr);
-    // the BatchRef's header fields as given; batch_length is the record's own
-    // (256 + blob), as for every BatchRef a decode hands out (batch.rs:391-406)
-    iggy_batch_header h = *hdr;
-    h.batch_length = 256 + blob_len;
-    int r = stage_record(c, h, blob, blob_len);
-    if (r) return r;
-    iggy_decode_result *d_res = c->dresult.as<iggy_decode_result>();
-    r = enqueue_decode(c, c->din.as<uint8_t>(), 256 + blob_len, IGGY_INTEGRITY_VERIFY, nullptr, 0, d_res, c->stream);
-    if (r) return r;
-    iggy_decode_result *h_res = (iggy_decode_result *)c->h_pinned;
-    HIP_OK(hipMemcpyAsync(h_res, d_res, sizeof(*h_res), hipMemcpyDeviceToHost, c->stream));
-    HIP_OK(hipStreamSynchronize(c->stream));
-    const iggy_decode_result res = *h_res;
-    if (res.error.kind == IGGY_ERR_TIMEOUT) reset_after_timeout(c);
-    // the stored batch checksum is the caller's business here (batch.rs:474-506)
-    if (res.error.kind == IGGY_ERR_INVALID_BATCH_CHECKSUM || res.error.kind == IGGY_OK) {
-        if (out) *out = res.computed_checksum;
-        set_err(err, IGGY_OK);
-        return 0;
-    }
-    fill_err(err, res.error);
-    return (int)res.error.kind;
-}
-
-static int checksum_of_walk(iggy_codec_ctx *c, const iggy_batch_header *hdr, uint64_t nframes,
-                            const uint8_t *d_blob, const uint64_t *d_pos, uint64_t *d_out, hipStream_t s) {
-    // header fields and frame count travel as kernel arguments (no host copy)
-    iggy_batch_header *dh = c->dresult.as<iggy_batch_header>(2048);
-    uint64_t *d_n = c->dresult.as<uint64_t>(3096);
-    hipLaunchKernelGGL(k_put_header, dim3(1), dim3(64), 0, s, *hdr, nframes, (const uint64_t *)nullptr, dh, d_n);
-    CsSource src{nullptr, d_blob, d_pos};
-    hipLaunchKernelGGL(k_bsum_blocks, dim3(bsum_grid(c, nframes)), dim3(256), 0, s, dh, d_n, src,
-                       c->gbsums.as<uint64_t>(), nullptr);
-    hipLaunchKernelGGL(k_bsum_chain, dim3(1), dim3(128), 0, s, dh, d_n, src,
-                       (const uint64_t *)c->gbsums.as<uint64_t>(), c->dsync.as<uint8_t>(kSyncSmall), d_out,
-                       nullptr);
-    HIP_OK(hipGetLastError());
-    return 0;
-}
-
-// The frames BatchIteratorWithOffsets yields over the staged record (a LayoutOnly
-// decode: its frame_count is the walk's, whatever error ends it) and the batch
-// checksum over them with header fields *hdr, all in one enqueue.
-static int enqueue_checksum_of_staged(iggy_codec_ctx *c, const iggy_batch_header &hdr, uint64_t blob_len,
-                                      uint64_t *d_out) {
-    const uint64_t cap = blob_len / 48 + 1;
-    int r = c->dpos.ensure((cap + 1) * 8);
-    r |= c->gbsums.ensure(((44 + 8 * cap) / 1024 + 2) * 64);
-    if (r) return IGGY_ERR_DEVICE;
-    iggy_decode_result *d_res = c->dresult.as<iggy_decode_result>();
-    r = enqueue_decode(c, c->din.as<uint8_t>(), 256 + blob_len, IGGY_INTEGRITY_LAYOUT_ONLY, c->dpos.as<uint64_t>(),
-                       cap, d_res, c->stream);
-    if (r) return r;
-    iggy_batch_header *dh = c->dresult.as<iggy_batch_header>(2048);
-    uint64_t *d_n = c->dresult.as<uint64_t>(3096);
-    hipLaunchKernelGGL(k_put_header, dim3(1), dim3(64), 0, c->stream, hdr, (uint64_t)0,
-                       (const uint64_t *)&d_res->frame_count, dh, d_n);
-    CsSource src{nullptr, c->din.as<uint8_t>(256), c->dpos.as<uint64_t>()};
-    hipLaunchKernelGGL(k_bsum_blocks, dim3(bsum_grid(c, cap)), dim3(256), 0, c->stream, dh, d_n, src,
-                       c->gbsums.as<uint64_t>(), nullptr);
-    hipLaunchKernelGGL(k_bsum_chain, dim3(1), dim3(128), 0, c->stream, dh, d_n, src,
-                       (const uint64_t *)c->gbsums.as<uint64_t>(), c->dsync.as<uint8_t>(kSyncSmall), d_out, nullptr);
-    HIP_OK(hipGetLastError());
-    return 0;
-}
-
-int iggy_codec_calculate_batch_checksum(iggy_codec_ctx *c, const iggy_batch_header *hdr,
-                                        const uint8_t *blob, uint64_t blob_len, uint64_t *out) {
-    if (!c || !hdr || !out || (!blob && blob_len)) return IGGY_ERR_INVALID_ARGUMENT;
-    DevGuard dg(c->device);
-    bind(c, nullptr);
-    // the walk sees a header of this blob's length and no message count (only the
-    // frames matter); the checksum hashes the caller's header fields
-    iggy_batch_header h = *hdr;
-    h.batch_length = 256 + blob_len;
-    h.message_count = 0;
-    h.batch_checksum = 0;
-    int r = stage_record(c, h, blob, blob_len);
-    if (r) return r;
-    uint64_t *d_out = c->dresult.as<uint64_t>(3080);
-    r = enqueue_checksum_of_staged(c, *hdr, blob_len, d_out);
-    if (r) return r;
-    uint64_t *h_out = (uint64_t *)((uint8_t *)c->h_pinned + 1536);
-    HIP_OK(hipMemcpyAsync(h_out, d_out, 8, hipMemcpyDeviceToHost, c->stream));
-    HIP_OK(hipStreamSynchronize(c->stream));
-    *out = *h_out;
-    return 0;
-}
-
-int iggy_codec_stamp_batch(iggy_codec_ctx *c, uint8_t *batch, uint64_t len, uint64_t base_offset,
-                           uint64_t base_timestamp, iggy_batch_header *out, iggy_wire_error *err) {
-    if (!c || (!batch && len)) return IGGY_ERR_INVALID_ARGUMENT;
-    iggy_batch_header h;
-    int r = iggy_batch_header_decode(batch, len, &h, err);
-    if (r) return r;
-    if (len < h.batch_length) {
-        set_err(err, IGGY_ERR_UNEXPECTED_EOF, 0, 0, h.batch_length, len);
-        return IGGY_ERR_UNEXPECTED_EOF;
-    }
-    h.base_offset = base_offset;
-    h.base_timestamp = base_timestamp;
-    uint64_t cs = 0;
-    r = iggy_codec_calculate_batch_checksum(c, &h, batch + 256, h.batch_length - 256, &cs);
-    if (r) return r;
-    h.batch_checksum = cs;
-    uint8_t hb[256];
-    iggy_batch_header_encode(&h, hb);
-    memcpy(batch, hb, 256);
-    if (out) *out = h;
-    set_err(err, IGGY_OK);
-    return 0;
-}
-
-// batch_error (server_common/src/send_messages.rs:52-66): integrity errors keep
-// their payloads, every other wire error becomes InvalidCommand
-static int server_error(int rc, iggy_wire_error *err) {
-    if (rc == IGGY_OK || rc == IGGY_ERR_INVALID_BATCH_CHECKSUM || rc == IGGY_ERR_INVALID_MESSAGE_CHECKSUM ||
-        rc >= IGGY_ERR_DEVICE)
-        return rc;
-    set_err(err, IGGY_ERR_INVALID_COMMAND);
-    return IGGY_ERR_INVALID_COMMAND;
-}
-
-// decode_prepare_slice_inner (server_common/src/send_messages.rs:581-622): the
-// structural checks on the host, the per-message + batch checksum pass on the GPU
-int iggy_codec_decode_prepare(iggy_codec_ctx *c, const uint8_t *frame, uint64_t len, int validate,
-                              iggy_batch_header *hdr_out, iggy_wire_error *err) {
-    if (!c || (!frame && len)) return IGGY_ERR_INVALID_ARGUMENT;
-    set_err(err, IGGY_OK);
-    const uint64_t hs = IGGY_PREPARE_HEADER_SIZE;
-    if (len < hs) return server_error(IGGY_ERR_VALIDATION, err);
-    uint32_t total = 0;
-    memcpy(&total, frame + IGGY_PREPARE_SIZE_OFFSET, 4);
-    if (total < hs || len < total) return server_error(IGGY_ERR_VALIDATION, err);
-    const uint8_t *body = frame + hs;
-    const uint64_t body_len = total - hs;
-    if (body_len < 256) return server_error(IGGY_ERR_VALIDATION, err);
-    iggy_batch_header h;
-    int r = iggy_batch_header_decode(body, 256, &h, err);
-    if (r) return server_error(r, err);
-    if (body_len != h.batch_length) return server_error(IGGY_ERR_VALIDATION, err);
-    if (hdr_out) *hdr_out = h;
-    if (!validate) return 0;
-    r = iggy_codec_decode_batch(c, body, body_len, IGGY_INTEGRITY_VERIFY, nullptr, nullptr, 0, nullptr, err);
-    return server_error(r, err);
-}
-
-// admit_wire_request after SendMessagesMetadata::decode
-// (server_common/src/send_messages.rs:505-540)
-int iggy_codec_admit_batch(iggy_codec_ctx *c, const uint8_t *batch, uint64_t len,
-                           uint32_t metadata_messages_count, uint64_t partition_id, int checksum_mode,
-                           uint8_t *out, uint64_t cap, iggy_batch_header *hdr_out, iggy_wire_error *err) {
-    if (!c || (!batch && len) || !out) return IGGY_ERR_INVALID_ARGUMENT;
-    DevGuard dg(c->device);
-    bind(c, nullptr);
-    set_err(err, IGGY_OK);
-    // one H2D copy and one Verify decode (positions kept on the device); the stamped
-    // header's checksum (send_messages.rs:529-537) is computed from those positions in
-    // the same enqueue, before the host has seen the verdict (discarded on failure)
-    const uint64_t pcap = len / 48 + 1;
-    int r = c->din.ensure(len + 16);
-    r |= c->dpos.ensure((pcap + 1) * 8);
-    r |= c->gbsums.ensure(((44 + 8 * pcap) / 1024 + 2) * 64);
-    if (r) return IGGY_ERR_DEVICE;
-    r = put_host(c, c->din.p, batch, len, c->stream);
-    if (r) return r;
-    iggy_decode_result *d_res = c->dresult.as<iggy_decode_result>();
-    r = enqueue_decode(c, c->din.as<uint8_t>(), len, IGGY_INTEGRITY_VERIFY, c->dpos.as<uint64_t>(), pcap, d_res,
-                       c->stream);
-    if (r) return r;
-    uint64_t *d_cs = c->dresult.as<uint64_t>(3080);
-    const bool compute = checksum_mode == IGGY_CHECKSUM_COMPUTE;
-    if (compute) {
-        iggy_batch_header *dh = c->dresult.as<iggy_batch_header>(2048);
-        uint64_t *d_n = c->dresult.as<uint64_t>(3096);
-        hipLaunchKernelGGL(k_admit_header, dim3(1), dim3(64), 0, c->stream, (const iggy_decode_result *)d_res,
-                           partition_id, dh, d_n);
-        CsSource src{nullptr, c->din.as<uint8_t>(256), c->dpos.as<uint64_t>()};
-        hipLaunchKernelGGL(k_bsum_blocks, dim3(bsum_grid(c, pcap)), dim3(256), 0, c->stream, dh, d_n, src,
-                           c->gbsums.as<uint64_t>(), nullptr);
-        hipLaunchKernelGGL(k_bsum_chain, dim3(1), dim3(128), 0, c->stream, dh, d_n, src,
-                           (const uint64_t *)c->gbsums.as<uint64_t>(), c->dsync.as<uint8_t>(kSyncSmall), d_cs,
-                           nullptr);
-        HIP_OK(hipGetLastError());
-    }
-    iggy_decode_result *h_res = (iggy_decode_result *)c->h_pinned;
-    uint64_t *h_cs = (uint64_t *)((uint8_t *)c->h_pinned + 1536);
-    HIP_OK(hipMemcpyAsync(h_res, d_res, sizeof(*h_res), hipMemcpyDeviceToHost, c->stream));
-    if (compute) HIP_OK(hipMemcpyAsync(h_cs, d_cs, 8, hipMemcpyDeviceToHost, c->stream));
-    HIP_OK(hipStreamSynchronize(c->stream));
-    const iggy_decode_result res = *h_res;
-    if (res.error.kind == IGGY_ERR_TIMEOUT) reset_after_timeout(c);
-    if (res.error.kind != IGGY_OK) {
-        fill_err(err, res.error);
-        return server_error((int)res.error.kind, err);
-    }
-    iggy_batch_header h = res.header;
-    if (h.message_count == 0 || h.message_count != metadata_messages_count || len != h.batch_length) {
-        set_err(err, IGGY_ERR_INVALID_COMMAND);
-        return IGGY_ERR_INVALID_COMMAND;
-    }
-    if (cap < len) {
-        set_err(err, IGGY_ERR_CAPACITY, 0, len);
-        return IGGY_ERR_CAPACITY;
-    }
-    memcpy(out, batch, len);
-    h.partition_id = partition_id;
-    h.batch_checksum = compute ? *h_cs : 0;
-    uint8_t hb[256];
-    iggy_batch_header_encode(&h, hb);
-    memcpy(out, hb, 256);
-    if (hdr_out) *hdr_out = h;
-    set_err(err, IGGY_OK);
-    return 0;
-}
-
-int iggy_codec_decode_records(iggy_codec_ctx *c, const uint8_t *buf, uint64_t len, const uint64_t *offsets,
-                              uint64_t nrec, int integrity, iggy_decode_result *out) {
-    if (!c || (!buf && len) || (nrec && (!offsets || !out))) return IGGY_ERR_INVALID_ARGUMENT;
-    if (integrity != IGGY_INTEGRITY_VERIFY && integrity != IGGY_INTEGRITY_LAYOUT_ONLY) return IGGY_ERR_INVALID_ARGUMENT;
-    for (uint64_t k = 0; k < nrec; ++k)
-        if (offsets[k] > len) return IGGY_ERR_INVALID_ARGUMENT;
-    if (!nrec) return 0;
-    DevGuard dg(c->device);
-    bind(c, nullptr);
-    if (c->din.ensure(len + 16)) return IGGY_ERR_DEVICE;
-    int r = put_host(c, c->din.p, buf, len, c->stream);
-    if (r) return r;
-    std::vector<RecIn> recs(nrec);
-    for (uint64_t k = 0; k < nrec; ++k) recs[k] = RecIn{offsets[k], len - offsets[k], 0, 0, 0};
-    return decode_records_to_host(c, c->din.as<uint8_t>(), buf, recs.data(), nrec, integrity, out);
-}
-
-// recover_segment_bounds' index-less walk (core/partitions/src/segment_recovery.rs:425-530).
-// The chain of candidate batches depends on headers only (decode, extent, offset
-// contiguity), so the host walks it first; every candidate is then verified on the
-// GPU from one copy of the file (decodes queued back to back, one sync), and the
-// first candidate that fails verification ends the accepted chain.
-int iggy_codec_recover_segment(iggy_codec_ctx *c, const uint8_t *messages, uint64_t len,
-                               uint64_t start_offset, iggy_segment_recovery *out) {
-    if (!c || !out || (!messages && len)) return IGGY_ERR_INVALID_ARGUMENT;
-    DevGuard dg(c->device);
-    bind(c, nullptr);
-    memset(out, 0, sizeof(*out));
-    auto sat = [](uint64_t a, uint64_t b) { return a + b < a ? ~0ull : a + b; };
-    struct Cand { uint64_t pos; iggy_batch_header h; };
-    std::vector<Cand> cand;
-    uint64_t pos = 0, expected = start_offset, maxlen = 0;
-    while (pos < len) {
-        iggy_batch_header h;
-        iggy_wire_error e;
-        if (len - pos < 256 || iggy_batch_header_decode(messages + pos, 256, &h, &e)) break;
-        const uint64_t extent = sat(pos, h.batch_length);
-        if (extent > len || h.base_offset != expected) break;
-        cand.push_back({pos, h});
-        maxlen = std::max(maxlen, h.batch_length);
-        if (h.message_count > 0) expected = sat(sat(h.base_offset, (uint64_t)h.message_count - 1), 1);
-        pos = extent;
-    }
-    size_t accepted = 0;
-    if (!cand.empty()) {
-        // one copy of the file, every candidate verified in one multi-record launch
-        // (the single-record decode for the rest), one sync
-        const uint64_t span = cand.back().pos + cand.back().h.batch_length;
-        const size_t K = cand.size();
-        if (c->din.ensure(span + 16)) return IGGY_ERR_DEVICE;
-        (void)maxlen;
-        int r = put_host(c, c->din.p, messages, span, c->stream);
-        if (r) return r;
-        std::vector<RecIn> recs(K);
-        for (size_t k = 0; k < K; ++k) recs[k] = RecIn{cand[k].pos, cand[k].h.batch_length, 0, 0, 0};
-        std::vector<iggy_decode_result> res(K);
-        r = decode_records_to_host(c, c->din.as<uint8_t>(), messages, recs.data(), K, IGGY_INTEGRITY_VERIFY,
-                                   res.data());
-        if (r) return r;
-        for (; accepted < K; ++accepted)
-            if (res[accepted].error.kind != IGGY_OK) break;
-    }
-    uint64_t end_offset = start_offset, end_ts = 0, start_ts = 0, walked = 0;
-    bool have_start = false;
-    for (size_t k = 0; k < accepted; ++k) {
-        const iggy_batch_header &h = cand[k].h;
-        if (h.message_count > 0) {
-            end_offset = sat(h.base_offset, (uint64_t)h.message_count - 1);
-            end_ts = h.base_timestamp;
-            if (!have_start) { start_ts = h.base_timestamp; have_start = true; }
-        }
-        walked = cand[k].pos + h.batch_length;
-    }
-    out->found = have_start ? 1 : 0;
-    out->start_timestamp = start_ts;
-    out->end_timestamp = end_ts;
-    out->end_offset = end_offset;
-    out->walked_bytes = walked;
-    out->batches = accepted;
-    return 0;
-}
-
-// walk_segment_payload (core/partitions/src/state_transfer.rs:715-833). The batch
-// extents follow from the headers (host); every batch is Verify-decoded on the GPU
-// (one copy, all queued, one sync); the verdicts and the header-level checks are
-// then applied in walk order, so the first invalid byte decides, as in the reference.
-int iggy_codec_walk_segment_payload(iggy_codec_ctx *c, const uint8_t *bytes, uint64_t len, uint64_t base_offset,
-                                    uint8_t *index_out, uint64_t index_cap, iggy_segment_walk *out) {
-    if (!c || !out || (!bytes && len)) return IGGY_ERR_INVALID_ARGUMENT;
-    DevGuard dg(c->device);
-    bind(c, nullptr);
-    memset(out, 0, sizeof(*out));
-    struct Cand { uint64_t pos; iggy_batch_header h; bool ok; };
-    std::vector<Cand> cand;
-    uint64_t pos = 0, maxlen = 256;
-    while (pos < len) {
-        iggy_batch_header h{};
-        iggy_wire_error e;
-        const bool ok = iggy_batch_header_decode(bytes + pos, len - pos, &h, &e) == 0 && h.batch_length <= len - pos;
-        cand.push_back({pos, h, ok});
-        if (!ok) break;  // its decode reports the error at this position
-        maxlen = std::max(maxlen, h.batch_length);
-        pos += h.batch_length;
-    }
-    std::vector<iggy_decode_result> res(cand.size());
-    if (!cand.empty()) {
-        // one copy, every batch in one multi-record launch (single-record decode for the
-        // rest), one sync
-        const size_t K = cand.size();
-        if (c->din.ensure(len + 16)) return IGGY_ERR_DEVICE;
-        (void)maxlen;
-        int r = put_host(c, c->din.p, bytes, len, c->stream);
-        if (r) return r;
-        std::vector<RecIn> recs(K);
-        for (size_t k = 0; k < K; ++k) recs[k] = RecIn{cand[k].pos, len - cand[k].pos, 0, 0, 0};
-        r = decode_records_to_host(c, c->din.as<uint8_t>(), bytes, recs.data(), K, IGGY_INTEGRITY_VERIFY,
-                                       res.data());
-        if (r) return r;
-    }
-    uint64_t next_offset = base_offset, indexed = 0, nidx = 0;
-    bool have_stats = false, have_index = false;
-    for (size_t k = 0; k < cand.size(); ++k) {
-        const iggy_decode_result &rs = res[k];
-        const uint64_t position = cand[k].pos;
-        if (rs.error.kind == IGGY_ERR_TIMEOUT) {
-            reset_after_timeout(c);
-            return IGGY_ERR_TIMEOUT;
-        }
-        if (rs.error.kind != IGGY_OK) {  // :750-755, batch_error's mapping
-            out->error = IGGY_SEG_BATCH;
-            out->position = position;
-            out->source = rs.error;
-            server_error((int)rs.error.kind, &out->source);
-            return 0;
-        }
-        const iggy_batch_header &h = rs.header;
-        if (!have_stats && h.base_offset != base_offset) {
-            out->error = IGGY_SEG_BASE_OFFSET_MISMATCH;
-            out->expected = base_offset;
-            out->actual = h.base_offset;
-            return 0;
-        }
-        if (h.base_offset != next_offset) {
-            out->error = IGGY_SEG_NON_CONTIGUOUS;
-            out->expected = next_offset;
-            out->actual = h.base_offset;
-            return 0;
-        }
-        if (h.message_count == 0) {
-            out->error = IGGY_SEG_BATCH;
-            out->position = position;
-            set_err(&out->source, IGGY_ERR_INVALID_MESSAGES_COUNT);
-            return 0;
-        }
-        const uint64_t add = (uint64_t)h.message_count - 1;
-        if (h.base_offset > ~0ull - add) {
-            out->error = IGGY_SEG_OFFSET_OVERFLOW;
-            out->position = position;
-            return 0;
-        }
-        const uint64_t batch_end = h.base_offset + add, ts = h.base_timestamp;
-        if (!have_index || position - indexed >= 64 * 1024) {  // INDEX_STRIDE_BYTES (:2799)
-            have_index = true;
-            indexed = position;
-            if (index_out && nidx < index_cap) {
-                memcpy(index_out + 24 * nidx + 0, &h.base_offset, 8);
-                memcpy(index_out + 24 * nidx + 8, &ts, 8);
-                memcpy(index_out + 24 * nidx + 16, &position, 8);
-            }
-            ++nidx;
-        }
-        if (!have_stats) {
-            out->start_timestamp = ts;
-            out->max_timestamp = ts;
-        } else if (ts > out->max_timestamp) {
-            out->max_timestamp = ts;
-        }
-        have_stats = true;
-        out->end_offset = batch_end;
-        out->end_timestamp = ts;
-        out->batches++;
-        if (batch_end == ~0ull) {
-            out->error = IGGY_SEG_OFFSET_OVERFLOW;
-            out->position = position;
-            return 0;
-        }
-        next_offset = batch_end + 1;
-    }
-    out->index_entries = nidx;
-    if (!have_stats) {
-        out->error = IGGY_SEG_EMPTY;
-        return 0;
-    }
-    return nidx > index_cap && index_out ? IGGY_ERR_CAPACITY : 0;
-}
-
-int iggy_codec_segment_write_device(iggy_codec_ctx *c, int fd, uint64_t position, const uint8_t *d_bytes,
-                                    uint64_t len, int fsync, uint64_t *written) {
-    if (!c || fd < 0 || (!d_bytes && len)) return IGGY_ERR_INVALID_ARGUMENT;
-    DevGuard dg(c->device);
-    bind(c, nullptr);
-    if (written) *written = 0;
-    constexpr uint64_t kPiece = 8ull << 20;  // two 8 MiB pinned halves
-    if (!c->wstage) {
-        if (hipHostMalloc(&c->wstage, 2 * kPiece, hipHostMallocDefault) != hipSuccess) {
-            c->wstage = nullptr;
-            return IGGY_ERR_DEVICE;
-        }
-        for (auto &ev : c->wev)
-            if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) return IGGY_ERR_DEVICE;
-    }
-    const uint64_t npieces = (len + kPiece - 1) / kPiece;
-    auto issue = [&](uint64_t k) -> int {
-        const uint64_t off = k * kPiece, n = std::min(kPiece, len - off);
-        HIP_OK(hipMemcpyAsync((uint8_t *)c->wstage + (k & 1) * kPiece, d_bytes + off, n, hipMemcpyDeviceToHost,
-                              c->stream));
-        HIP_OK(hipEventRecord(c->wev[k & 1], c->stream));
-        return 0;
-    };
-    int r = npieces ? issue(0) : 0;
-    for (uint64_t k = 0; k < npieces && !r; ++k) {
-        HIP_OK(hipEventSynchronize(c->wev[k & 1]));
-        if (k + 1 < npieces) r = issue(k + 1);  // the next piece's copy runs under this pwrite
-        const uint64_t off = k * kPiece, n = std::min(kPiece, len - off);
-        const uint8_t *src = (const uint8_t *)c->wstage + (k & 1) * kPiece;
-        uint64_t done = 0;
-        while (done < n) {
-            const ssize_t w = pwrite(fd, src + done, n - done, (off_t)(position + off + done));
-            if (w <= 0) {
-                if (w < 0 && errno == EINTR) continue;
-                (void)hipStreamSynchronize(c->stream);
-                return IGGY_ERR_DEVICE;
-            }
-            done += (uint64_t)w;
-        }
-        if (written) *written += n;
-    }
-    if (r) return r;
-    if (fsync && fdatasync(fd) != 0) return IGGY_ERR_DEVICE;
-    return 0;
-}
-
-int iggy_codec_xxh3_64(iggy_codec_ctx *c, const void *data, uint64_t len, uint64_t *out) {
-    if (!c || !out || (!data && len)) return IGGY_ERR_INVALID_ARGUMENT;
-    DevGuard dg(c->device);
-    bind(c, nullptr);
-    int r = c->din.ensure(len + 16);
-    const uint64_t nb = len ? (len - 1) / 1024 + 1 : 1;
-    r |= c->hbsums.ensure(nb * 64 + 64);
-    if (r) return IGGY_ERR_DEVICE;
-    r = put_host(c, c->din.p, data, len, c->stream);
-    if (r) return r;
-    uint64_t *dout = c->dresult.as<uint64_t>(3088);
-    if (len > 240)
-        hipLaunchKernelGGL(k_xxh3_big_blocks, dim3(c->ncu * 4), dim3(256), 0, c->stream,
-                           c->din.as<uint8_t>(), len, c->hbsums.as<uint64_t>());
-    hipLaunchKernelGGL(k_xxh3_big_chain, dim3(1), dim3(64), 0, c->stream, c->din.as<uint8_t>(), len,
-                       (const uint64_t *)c->hbsums.as<uint64_t>(), dout);
-    HIP_OK(hipGetLastError());
-    return get_host(c, out, dout, 8, c->stream);
-}
-
-// ---------------------------------------------------------------- encode
-// A small encode's SoA input as device-visible host memory: every array read in place
-// when all are registered (and non-empty), else all copied with one memcpy each into
-// `stage` (mapped, every array 256-B aligned with 16 B of slack). dm: the result.
-static int stage_soa(const iggy_raw_messages *m, uint64_t n, uint64_t spl, uint64_t suh, HostMap &stage,
-                     iggy_raw_messages *dm) {
-    const bool has_uh = m->user_headers_lengths != nullptr;
-    struct Arr { const void *h; uint64_t len; const uint8_t *d; };
-    Arr a[6] = {{m->ids, n * 16, nullptr}, {m->origin_timestamps, n * 8, nullptr},
-                {m->payloads, spl, nullptr}, {m->payload_lengths, n * 4, nullptr},
-                {has_uh ? m->user_headers : nullptr, has_uh ? suh : 0, nullptr},
-                {has_uh ? m->user_headers_lengths : nullptr, has_uh ? n * 4 : 0, nullptr}};
-    bool mapped = true;  // (an empty array takes the staging too: a valid address behind it)
-    for (int i = 0; i < (has_uh ? 6 : 4); ++i)
-        mapped &= a[i].len && (a[i].d = host_device_ptr(a[i].h, a[i].len)) != nullptr;
-    if (!mapped) {
-        uint64_t off[6], tot = 0;
-        for (int i = 0; i < 6; ++i) {
-            off[i] = tot;
-            tot += (a[i].len + 16 + 255) & ~(uint64_t)255;
-        }
-        if (stage.ensure(tot)) return IGGY_ERR_DEVICE;
-        for (int i = 0; i < 6; ++i) {
-            if (a[i].len) memcpy(stage.hp<uint8_t>(off[i]), a[i].h, a[i].len);
-            a[i].d = stage.d + off[i];
-        }
-    }
-    dm->count = n;
-    dm->ids = (const uint64_t *)a[0].d;
-    dm->origin_timestamps = (const uint64_t *)a[1].d;
-    dm->payloads = a[2].d;
-    dm->payload_lengths = (const uint32_t *)a[3].d;
-    dm->user_headers = has_uh ? a[4].d : nullptr;
-    dm->user_headers_lengths = has_uh ? (const uint32_t *)a[5].d : nullptr;
-    return 0;
-}
-
-static int enqueue_encode(iggy_codec_ctx *c, const iggy_raw_messages *dm, uint64_t partition_id,
-                          uint8_t *d_out, uint64_t cap, iggy_encode_result *d_res, hipStream_t s,
-                          EncOwn *own = nullptr) {
-    // own (nullable): scratch of an asynchronous slot, so unsegmented encodes of
-    // different slots run side by side on their own streams (else the context's)
-    const uint64_t n = dm->count;
-    DevBuf &epl = own ? own->epl : c->epl, &euh = own ? own->euh : c->euh, &etile = own ? own->etile : c->etile;
-    DevBuf &ecs = own ? own->ecs : c->ecs, &emisc = own ? own->emisc : c->emisc, &bsums = own ? own->bsums : c->gbsums;
-    const uint64_t ntiles = (n + kEncTile - 1) / kEncTile;
-    int r = 0;
-    r |= epl.ensure(n * 8);
-    r |= euh.ensure(n * 8);
-    r |= etile.ensure(ntiles * 24 + 64);
-    r |= ecs.ensure(n * 8);
-    r |= emisc.ensure(1024);  // misc | header | checksum | small | chain state (512)
-    const uint64_t nbk = (44 + 8 * n) / 1024 + 2;
-    r |= bsums.ensure(nbk * 64);
-    if (r) return IGGY_ERR_DEVICE;
-    EncScratch es;
-    es.pl_local = epl.as<uint64_t>();
-    es.uh_local = euh.as<uint64_t>();
-    es.tile_pl = etile.as<uint64_t>();
-    es.tile_uh = etile.as<uint64_t>(ntiles * 8);
-    es.tile_min = etile.as<uint64_t>(ntiles * 16);
-    es.cs = ecs.as<uint64_t>();
-    es.misc = emisc.as<uint64_t>();
-    es.hdr = emisc.as<iggy_batch_header>(128);
-    es.dbg = diag_bits(c);
-    iggy_raw_messages m = *dm;
-    if (!own) prof_begin(c, 1, s);
-    hipLaunchKernelGGL(k_enc_prep, dim3(ntiles), dim3(256), 0, s, m, es, partition_id, cap, (uint32_t)(ntiles == 1));
-    if (ntiles != 1) hipLaunchKernelGGL(k_enc_scan, dim3(1), dim3(256), 0, s, ntiles, n, partition_id, cap, es);
-    const uint64_t waves = std::min<uint64_t>(n, (uint64_t)c->ncu * 32);
-    CsSource src{es.cs, nullptr, nullptr};
-    // checksum blocks: 44 + 8n bytes; full blocks nb (the chain), then the last one
-    const uint64_t csb = 44 + 8 * n;
-    const uint64_t nb = csb > 240 ? (csb - 1) / 1024 : 0;
-    bool segmented = false;
-    if (!m.user_headers_lengths) {
-        // no user headers: lane-group kernel (k_enc_frames only covers a < 16-B payload
-        // area, and runs first so the segments' checksum chain sees its output)
-        int nseg = 1;
-        if (!own && n >= kEncSegMinFrames && nb >= 4 * kEncSegs && c->side) {
-            nseg = kEncSegs;
-            for (auto ev : c->seg_ev)
-                if (!ev) nseg = 1;
-        }
-        segmented = nseg > 1;
-        // frames of <= 240 hashed bytes (one lane each, latency-bound): segmented, they
-        // run at the head of the side stream beside the first segment, ahead of every
-        // block-sum range that reads their checksums; k_enc_lanes never writes their
-        // checksum words. Unsegmented, the one k_enc_lanes launch hashes them after its
-        // loop and runs the < 16-B payload-area fallback itself (own_tail).
-        const bool ring = segmented && IGGY_ENC_RING;
-        // writer waves beside the hashers (k_enc_ring<true>) when every frame's payload
-        // keeps its source offset mod 16 in the output (P - out = 0 mod 16, encode.hip)
-        const bool split = IGGY_ENC_SPLIT && ((((uintptr_t)m.payloads) - (uintptr_t)d_out) & 15) == 0;
-        if (ring) {
-            if (c->erec.ensure((n + 1) * 32) || c->esink.ensure(kErSinkBytes)) return IGGY_ERR_DEVICE;
-            hipLaunchKernelGGL(k_enc_recs, dim3((uint32_t)std::min<uint64_t>((n + 256) / 256, (uint64_t)c->ncu * 8)),
-                               dim3(256), 0, s, m, es, c->erec.as<uint4>());
-        }
-        if (segmented) {
-            hipLaunchKernelGGL(k_enc_frames, dim3((waves + 3) / 4), dim3(256), 0, s, m, es, d_out, 1u);
-            const dim3 sgrid((uint32_t)std::min<uint64_t>((n + 255) / 256, (uint64_t)c->ncu * 4));
-            HIP_OK(hipEventRecord(c->seg_ev[kEncSegs + 1], s));
-            HIP_OK(hipStreamWaitEvent(c->side, c->seg_ev[kEncSegs + 1], 0));
-            hipLaunchKernelGGL(k_enc_short, sgrid, dim3(256), 0, c->side, m, es, d_out);
-        }
-        // one resident round of lane-group waves (2 WGs of 256 per CU at 240 VGPRs)
-        // segmented: one CU stays free of lane-group waves, so the side stream's
-        // single-wave chain (k_chain_partial) issues on a SIMD of its own (sharing one
-        // with lane-group waves it ran 132 ns/step instead of ~31)
-        const uint64_t lcu = (segmented && !(diag_bits(c) & 16384)) ? (uint64_t)c->ncu - 1 : (uint64_t)c->ncu;
-        const uint64_t lwg = std::min<uint64_t>((n + 31) / 32, lcu * ((diag_bits(c) & 2048) ? 8 : 2));
-        uint64_t *state = emisc.as<uint64_t>(512);
-        for (int k = 0; k < nseg; ++k) {
-            // blocks [B_k, B_k+1) need frames up to 128 B_k+1 - 6: segment k encodes
-            // frames [F_k, F_k+1), F_k = 128 B_k - 5
-            // uneven segments: the last one (whose chain cannot overlap) is ~6 % of the blocks
-            // (same box: 60 / 30 / 8 / 2 % measured no better once the segment chains
-            // stopped starving: 1.383-1.389 vs 1.376-1.386 ms)
-            static const uint32_t kSegPermille[kEncSegs + 1] = {0, 400, 750, 940, 1000};
-            auto bound = [&](int q) {
-                if (nseg == 1) return q ? nb : (uint64_t)0;
-                if (diag_bits(c) & 1024) return nb * q / nseg;  // diagnostics: even segments
-                return nb * kSegPermille[q] / 1000;
-            };
-            const uint64_t B0 = bound(k), B1 = bound(k + 1);
-            const uint64_t F0 = k == 0 ? 0 : std::min<uint64_t>(n, 128 * B0 - 5);
-            const uint64_t F1 = k == nseg - 1 ? n : std::min<uint64_t>(n, 128 * B1 - 5);
-            if (ring && split)
-                hipLaunchKernelGGL(k_enc_ring<true>, dim3((uint32_t)std::min<uint64_t>((n + 63) / 64, lcu)),
-                                   dim3(2 * kErThreads), kEsLds, s, m, es, d_out, F0, F1,
-                                   (const uint4 *)c->erec.as<uint4>(), c->esink.as<uint8_t>());
-            else if (ring)
-                hipLaunchKernelGGL(k_enc_ring<false>, dim3((uint32_t)std::min<uint64_t>((n + 63) / 64, lcu)),
-                                   dim3(kErThreads), kErLds, s, m, es, d_out, F0, F1,
-                                   (const uint4 *)c->erec.as<uint4>(), c->esink.as<uint8_t>());
-            else if (segmented)
-                hipLaunchKernelGGL(k_enc_lanes<false>, dim3(lwg), dim3(256), 0, s, m, es, d_out, F0, F1);
-            else
-                hipLaunchKernelGGL(k_enc_lanes<true>, dim3(lwg), dim3(256), 0, s, m, es, d_out, F0, F1);
-            if (segmented && k < nseg - 1) {
-                HIP_OK(hipEventRecord(c->seg_ev[k], s));
-                HIP_OK(hipStreamWaitEvent(c->side, c->seg_ev[k], 0));
-                hipLaunchKernelGGL(k_bsum_blocks_range, dim3(c->ncu / 2), dim3(256), 0, c->side,
-                                   (const iggy_batch_header *)es.hdr, (const uint64_t *)&es.misc[3], src,
-                                   bsums.as<uint64_t>(), B0, B1);
-                hipLaunchKernelGGL(k_chain_partial, dim3(1), dim3(256), 0, c->side, (const uint64_t *)&es.misc[3],
-                                   (const uint64_t *)bsums.as<uint64_t>(), state, B0, B1);
-            }
-        }
-        if (segmented) {
-            // the last segment's blocks and the partial one, after every frame
-            const uint64_t Bl = (diag_bits(c) & 1024) ? nb * (nseg - 1) / nseg : nb * 940 / 1000;  // last segment
-            HIP_OK(hipEventRecord(c->seg_ev[kEncSegs], c->side));
-            HIP_OK(hipStreamWaitEvent(s, c->seg_ev[kEncSegs], 0));
-            hipLaunchKernelGGL(k_bsum_blocks_range, dim3(c->ncu), dim3(256), 0, s, (const iggy_batch_header *)es.hdr,
-                               (const uint64_t *)&es.misc[3], src, bsums.as<uint64_t>(), Bl, nb + 1);
-            hipLaunchKernelGGL(k_chain_partial, dim3(1), dim3(256), 0, s, (const uint64_t *)&es.misc[3],
-                               (const uint64_t *)bsums.as<uint64_t>(), state, Bl, nb);
-        }
-    } else {
-        hipLaunchKernelGGL(k_enc_frames, dim3((waves + 3) / 4), dim3(256), 0, s, m, es, d_out, 0u);
-    }
-    if (!own) prof_end(c, 1, s);
-    uint64_t *dcs = emisc.as<uint64_t>(256);
-    if (!segmented && nb + 1 <= kEncTailBlocks) {  // small batch: sums, chain and finish in one launch
-        hipLaunchKernelGGL(k_enc_tail_small, dim3(1), dim3(256), 0, s, m, es, partition_id, cap,
-                           emisc.as<uint8_t>(320), d_out, d_res);
-        HIP_OK(hipGetLastError());
-        return 0;
-    }
-    if (segmented) {
-        hipLaunchKernelGGL(k_chain_finish, dim3(1), dim3(64), 0, s, (const iggy_batch_header *)es.hdr,
-                           (const uint64_t *)&es.misc[3], src, (const uint64_t *)bsums.as<uint64_t>(),
-                           (const uint64_t *)emisc.as<uint64_t>(512), emisc.as<uint8_t>(320), dcs);
-    } else {
-        hipLaunchKernelGGL(k_bsum_blocks, dim3(bsum_grid(c, n)), dim3(256), 0, s, (const iggy_batch_header *)es.hdr,
-                           (const uint64_t *)&es.misc[3], src, bsums.as<uint64_t>(), nullptr);
-        hipLaunchKernelGGL(k_bsum_chain, dim3(1), dim3(128), 0, s, (const iggy_batch_header *)es.hdr,
-                           (const uint64_t *)&es.misc[3], src, (const uint64_t *)bsums.as<uint64_t>(),
-                           emisc.as<uint8_t>(320) /* 192 B of small */, dcs, nullptr);
-    }
-    hipLaunchKernelGGL(k_enc_finish, dim3(1), dim3(64), 0, s, m, es, partition_id, cap,
-                       (const uint64_t *)dcs, d_out, d_res);
-    HIP_OK(hipGetLastError());
-    return 0;
-}
-
-int iggy_codec_encode_batch(iggy_codec_ctx *c, const iggy_raw_messages *m, uint64_t partition_id,
-                            uint8_t *out, uint64_t cap, uint64_t *out_len, iggy_wire_error *err) {
-    if (!c || !m) return IGGY_ERR_INVALID_ARGUMENT;
-    set_err(err, IGGY_OK);
-    if (m->count == 0) {
-        set_err(err, IGGY_ERR_VALIDATION, IGGY_V_EMPTY_BATCH);
-        return IGGY_ERR_VALIDATION;
-    }
-    if (m->count > 0xFFFFFFFFull) {
-        set_err(err, IGGY_ERR_PAYLOAD_TOO_LARGE, 0, m->count, 0xFFFFFFFFull);
-        return IGGY_ERR_PAYLOAD_TOO_LARGE;
-    }
-    DevGuard dg(c->device);
-    bind(c, nullptr);
-    const uint64_t n = m->count;
-    uint64_t spl = 0, suh = 0;
-    for (uint64_t i = 0; i < n; ++i) {
-        spl += m->payload_lengths[i];
-        suh += m->user_headers_lengths ? m->user_headers_lengths[i] : 0;
-    }
-    const uint64_t need = 256 + 48 * n + spl + suh;
-    if (cap < need || !out) {
-        set_err(err, IGGY_ERR_CAPACITY, 0, need, cap);
-        return IGGY_ERR_CAPACITY;
-    }
-    int r = 0;
-    const uint64_t in_bytes = n * 28 + spl + (m->user_headers_lengths ? suh + n * 4 : 0);
-    if (in_bytes <= kZeroCopyBytes && n < kEncSegMinFrames) {
-        // a small batch in place (as encode_submit's): the SoA arrays read over the host
-        // link, the wire bytes into the caller's registered `out` or the context's
-        // mapped bounce, the verdict into mapped memory; one stream sync, no copy
-        iggy_raw_messages dm;
-        if (stage_soa(m, n, spl, suh, c->zin, &dm)) return IGGY_ERR_DEVICE;
-        uint8_t *d_out = (uint8_t *)host_device_ptr(out, need);
-        const bool bounce = !d_out;
-        if (bounce) {
-            if (c->zout.ensure(need + 16)) return IGGY_ERR_DEVICE;
-            d_out = c->zout.d;
-        }
-        if (c->omap.ensure(64 + 256)) return IGGY_ERR_DEVICE;
-        iggy_encode_result *d_res = c->omap.dp<iggy_encode_result>(64);
-        hipStream_t s = c->stream;
-        r = enqueue_encode(c, &dm, partition_id, d_out, need, d_res, s);
-        if (r) return r;
-        HIP_OK(hipStreamSynchronize(s));
-        const iggy_encode_result res = *c->omap.hp<iggy_encode_result>(64);
-        if (res.error.kind != IGGY_OK) {
-            fill_err(err, res.error);
-            return (int)res.error.kind;
-        }
-        if (bounce) memcpy(out, c->zout.h, need);
-        if (out_len) *out_len = need;
-        return 0;
-    }
-    r |= c->eids.ensure(n * 16);
-    r |= c->eots.ensure(n * 8);
-    r |= c->epay.ensure(spl + 16);
-    r |= c->eplen.ensure(n * 4);
-    r |= c->euhb.ensure(suh + 16);
-    r |= c->euhl.ensure(n * 4);
-    r |= c->dout.ensure(need + 16);
-    if (r) return IGGY_ERR_DEVICE;
-    hipStream_t s = c->stream;
-    r |= put_host(c, c->eids.p, m->ids, n * 16, s);
-    r |= put_host(c, c->eots.p, m->origin_timestamps, n * 8, s);
-    r |= put_host(c, c->epay.p, m->payloads, spl, s);
-    r |= put_host(c, c->eplen.p, m->payload_lengths, n * 4, s);
-    const bool has_uh = m->user_headers_lengths != nullptr;
-    if (has_uh) {
-        r |= put_host(c, c->euhb.p, m->user_headers, suh, s);
-        r |= put_host(c, c->euhl.p, m->user_headers_lengths, n * 4, s);
-    }
-    if (r) return IGGY_ERR_DEVICE;
-    iggy_raw_messages dm;
-    dm.count = n;
-    dm.ids = c->eids.as<uint64_t>();
-    dm.origin_timestamps = c->eots.as<uint64_t>();
-    dm.payloads = c->epay.as<uint8_t>();
-    dm.payload_lengths = c->eplen.as<uint32_t>();
-    dm.user_headers = has_uh ? c->euhb.as<uint8_t>() : nullptr;
-    dm.user_headers_lengths = has_uh ? c->euhl.as<uint32_t>() : nullptr;
-    iggy_encode_result *d_res = c->dresult.as<iggy_encode_result>(512);
-    r = enqueue_encode(c, &dm, partition_id, c->dout.as<uint8_t>(), need, d_res, s);
-    if (r) return r;
-    iggy_encode_result *h_res = (iggy_encode_result *)((uint8_t *)c->h_pinned + 512);
-    HIP_OK(hipMemcpyAsync(h_res, d_res, sizeof(*h_res), hipMemcpyDeviceToHost, s));
-    HIP_OK(hipStreamSynchronize(s));
-    if (h_res->error.kind != IGGY_OK) {
-        fill_err(err, h_res->error);
-        return (int)h_res->error.kind;
-    }
-    r = get_host(c, out, c->dout.p, need, s);
-    if (r) return r;
-    if (out_len) *out_len = need;
-    return 0;
-}
-
-int iggy_codec_encode_batch_device(iggy_codec_ctx *c, const iggy_raw_messages *msgs,
-                                   uint64_t partition_id, uint8_t *d_out, uint64_t cap,
-                                   iggy_encode_result *d_result, void *stream) {
-    if (!c || !msgs || !d_out || !d_result || msgs->count == 0 || msgs->count > 0xFFFFFFFFull)
-        return IGGY_ERR_INVALID_ARGUMENT;
-    DevGuard dg(c->device);
-    // cap is checked on the device against the scanned batch length: a batch that
-    // does not fit writes nothing and reports IGGY_ERR_CAPACITY in *d_result
-    return enqueue_encode(c, msgs, partition_id, d_out, cap, d_result, bind(c, stream));
-}
-
-// ------------------------------------------------------------- poll decode
-int iggy_codec_poll_decode(iggy_codec_ctx *c, const uint8_t *buf, uint64_t len, int mode,
-                           iggy_polled_message *out, uint64_t cap, uint64_t *n_out,
-                           iggy_wire_error *err) {
-    if (!c || (!buf && len)) return IGGY_ERR_INVALID_ARGUMENT;
-    DevGuard dg(c->device);
-    bind(c, nullptr);
-    set_err(err, IGGY_OK);
-    if (n_out) *n_out = 0;
-    // 1. the record chain from the 256-B headers (polled_messages.rs:99-106,
-    //    poll_messages.rs:123-125); the header walk's own failure, if any, comes
-    //    after every record before it
-    struct Rec { uint64_t pos, bl, pbase; };
-    std::vector<Rec> recs;
-    int stop_rc = 0;
-    iggy_wire_error stop_err{};
-    uint64_t position = 0, pwords = 0;
-    while (position < len) {
-        iggy_batch_header h;
-        iggy_wire_error he;
-        const int hr = iggy_batch_header_decode(buf + position, len - position, &h, &he);
-        if (mode == IGGY_POLL_MODE_SDK) {
-            if (hr || h.batch_length > len - position) {
-                set_err(err, IGGY_ERR_INVALID_MESSAGE_PAYLOAD_LENGTH);
-                return IGGY_ERR_INVALID_MESSAGE_PAYLOAD_LENGTH;
-            }
-        } else if (hr) {
-            stop_rc = hr;
-            stop_err = he;
-            break;
-        }
-        const uint64_t avail = std::min<uint64_t>(h.batch_length, len - position);
-        recs.push_back({position, h.batch_length, pwords});
-        pwords += avail / 48 + 1;
-        if (h.batch_length > len - position) break;  // its decode reports the EOF
-        position += h.batch_length;
-    }
-    // 2. every record's frame walk (LayoutOnly) in ONE multi-record launch, which also
-    //    writes the message descriptors of the single-stride records; the others take
-    //    the single-record decode and k_poll_fill. Descriptor slots: record k's planned
-    //    frame count, consecutive, so a body of well-formed records comes back in one
-    //    copy; single-path and re-walked records fill a tail area instead.
-    const size_t K = recs.size();
-    std::vector<RecIn> rin(K);
-    std::vector<uint64_t> slot(K), tailb(K);
-    uint64_t nslots = 0;
-    for (size_t k = 0; k < K; ++k) {
-        const uint64_t avail = std::min<uint64_t>(recs[k].bl, len - recs[k].pos);
-        uint64_t nf = 0;
-        const uint64_t nw = rec_plan(buf + recs[k].pos, len - recs[k].pos, &nf);
-        slot[k] = nslots;
-        nslots += nw ? nf : 0;
-        rin[k] = RecIn{recs[k].pos, len - recs[k].pos, recs[k].pbase, avail / 48 + 1, slot[k]};
-    }
-    for (size_t k = 0; k < K; ++k) tailb[k] = nslots + recs[k].pbase;
-    if (K && records_all_planned(buf, rin.data(), K)) {
-        // every record single-stride: descriptors and verdicts straight into host-mapped
-        // memory, the host spinning on the launch's completion flag (one H2D, one launch)
-        const size_t rb = K * sizeof(iggy_decode_result), mo = (64 + rb + 127) & ~(size_t)127;
-        if (c->din.ensure(len + 16) || c->omap.ensure(mo + (nslots + 1) * sizeof(iggy_polled_message)))
-            return IGGY_ERR_DEVICE;
-        // a body of <= kZeroCopyBytes is read in place (registered: where it is;
-        // pageable: one memcpy into the context's mapped staging), larger ones copied
-        const uint8_t *d_body = nullptr;
-        if (IGGY_POLL_IN_PLACE && len <= kZeroCopyBytes) {
-            d_body = host_device_ptr(buf, len);
-            if (!d_body && !host_pinned(buf, len)) {
-                if (c->zin.ensure(len + 16)) return IGGY_ERR_DEVICE;
-                memcpy(c->zin.h, buf, len);
-                d_body = c->zin.d;
-            }
-        }
-        int r = 0;
-        if (!d_body) {
-            r = put_host(c, c->din.p, buf, len, c->stream);
-            if (r) return r;
-            d_body = c->din.as<uint8_t>();
-        }
-        std::vector<size_t> single;
-        const uint32_t v = next_flag(c);
-        r = enqueue_records(c, d_body, buf, rin.data(), K, IGGY_INTEGRITY_LAYOUT_ONLY, nullptr,
-                            c->omap.dp<iggy_polled_message>(mo), c->omap.dp<iggy_decode_result>(64), &single,
-                            nullptr, c->omap.dp<uint32_t>(), v);
-        if (r) return r;
-        r = wait_host_flag(c, v);
-        if (!r) r = xfer_settle(c);
-        if (r) return r;
-        const iggy_decode_result *res = c->omap.hp<iggy_decode_result>(64);
-        bool general = false;
-        for (size_t k = 0; k < K; ++k) {
-            if (res[k].error.kind == IGGY_ERR_TIMEOUT) {
-                reset_after_timeout(c);
-                set_err(err, IGGY_ERR_TIMEOUT);
-                return IGGY_ERR_TIMEOUT;
-            }
-            general |= res[k].status == kStatusNeedGeneral;
-        }
-        if (!general) {  // (a stride that broke mid-record: the path below, from scratch)
-            const iggy_polled_message *msgs = c->omap.hp<iggy_polled_message>(mo);
-            uint64_t n = 0;
-            int rc = 0;
-            for (size_t k = 0; k < K && !rc; ++k) {
-                const iggy_decode_result &rs = res[k];
-                if (mode == IGGY_POLL_MODE_SDK) {
-                    if (rs.covered != recs[k].bl - 256) {
-                        set_err(err, IGGY_ERR_INVALID_MESSAGE_PAYLOAD_LENGTH);
-                        return IGGY_ERR_INVALID_MESSAGE_PAYLOAD_LENGTH;
-                    }
-                } else if (rs.error.kind != IGGY_OK) {
-                    fill_err(err, rs.error);
-                    rc = (int)rs.error.kind;
-                    break;
-                }
-                const uint64_t nf = rs.frame_count;
-                if (n + nf > cap) {
-                    set_err(err, IGGY_ERR_CAPACITY, 0, n + nf, cap);
-                    rc = IGGY_ERR_CAPACITY;
-                    break;
-                }
-                if (nf) memcpy(out + n, msgs + slot[k], nf * sizeof(iggy_polled_message));
-                n += nf;
-            }
-            if (!rc && stop_rc) {
-                fill_err(err, stop_err);
-                rc = stop_rc;
-            }
-            if (n_out) *n_out = n;
-            return rc;
-        }
-    }
-    int r = c->din.ensure(len + 16);
-    r |= c->ppos.ensure((pwords + 1) * 8);
-    r |= c->pres.ensure((K + 1) * sizeof(iggy_decode_result));
-    r |= c->pmsgs.ensure((nslots + pwords + 1) * sizeof(iggy_polled_message));
-    if (r) return IGGY_ERR_DEVICE;
-    r = put_host(c, c->din.p, buf, len, c->stream);
-    if (r) return r;
-    iggy_decode_result *d_res = c->pres.as<iggy_decode_result>();
-    iggy_polled_message *d_msgs = c->pmsgs.as<iggy_polled_message>();
-    std::vector<size_t> single, redone;
-    r = enqueue_records(c, c->din.as<uint8_t>(), buf, rin.data(), K, IGGY_INTEGRITY_LAYOUT_ONLY, c->ppos.as<uint64_t>(),
-                        d_msgs, d_res, &single);
-    if (r) return r;
-    std::vector<iggy_decode_result> res(K);
-    r = get_host(c, res.data(), d_res, K * sizeof(iggy_decode_result), c->stream);
-    if (r) return r;
-    r = redo_general(c, c->din.as<uint8_t>(), rin.data(), K, IGGY_INTEGRITY_LAYOUT_ONLY, c->ppos.as<uint64_t>(),
-                     res.data(), &redone);
-    if (r) {
-        if (r == IGGY_ERR_TIMEOUT) set_err(err, IGGY_ERR_TIMEOUT);
-        return r;
-    }
-    std::vector<uint8_t> in_tail(K, 0);
-    for (size_t k : single) in_tail[k] = 1;
-    for (size_t k : redone) in_tail[k] = 1;
-    // 3. verdicts in record order; descriptors of tail records expanded, one copy out
-    uint64_t n = 0;
-    int rc = 0;
-    struct Span { uint64_t src, n; };
-    std::vector<Span> spans;
-    for (size_t k = 0; k < K && !rc; ++k) {
-        const iggy_decode_result &rs = res[k];
-        if (mode == IGGY_POLL_MODE_SDK) {
-            // the SDK walk only needs the frames to tile the record (no count check)
-            if (rs.covered != recs[k].bl - 256) {
-                set_err(err, IGGY_ERR_INVALID_MESSAGE_PAYLOAD_LENGTH);
-                return IGGY_ERR_INVALID_MESSAGE_PAYLOAD_LENGTH;
-            }
-        } else if (rs.error.kind != IGGY_OK) {  // yielded after the messages before it
-            fill_err(err, rs.error);
-            rc = (int)rs.error.kind;
-            break;
-        }
-        const uint64_t nf = rs.frame_count;
-        if (n + nf > cap) {
-            set_err(err, IGGY_ERR_CAPACITY, 0, n + nf, cap);
-            rc = IGGY_ERR_CAPACITY;
-            break;
-        }
-        if (nf) {
-            uint64_t src = slot[k];
-            if (in_tail[k]) {
-                src = tailb[k];
-                hipLaunchKernelGGL(k_poll_fill, dim3((uint32_t)std::min<uint64_t>((nf + 255) / 256, 65535)), dim3(256),
-                                   0, c->stream, c->din.as<uint8_t>(), recs[k].pos,
-                                   c->ppos.as<uint64_t>(8 * recs[k].pbase), nf, d_msgs + src);
-                HIP_OK(hipGetLastError());
-            }
-            if (!spans.empty() && spans.back().src + spans.back().n == src) spans.back().n += nf;
-            else spans.push_back({src, nf});
-        }
-        n += nf;
-    }
-    if (!rc && stop_rc) {
-        fill_err(err, stop_err);
-        rc = stop_rc;
-    }
-    uint64_t o = 0;
-    for (const Span &sp : spans) {
-        r = get_host(c, out + o, d_msgs + sp.src, sp.n * sizeof(iggy_polled_message), c->stream);
-        if (r) return r;
-        o += sp.n;
-    }
-    HIP_OK(hipStreamSynchronize(c->stream));
-    if (n_out) *n_out = n;
-    return rc;
-}
-
-// ------------------------------------------------------------ device APIs
-int iggy_codec_decode_batch_device(iggy_codec_ctx *c, const uint8_t *d_body, uint64_t len,
-                                   int integrity, uint64_t *d_frame_pos, uint64_t cap,
-                                   iggy_decode_result *d_result, void *stream) {
-    if (!c || !d_result || (!d_body && len)) return IGGY_ERR_INVALID_ARGUMENT;
-    DevGuard dg(c->device);
-    return enqueue_decode(c, d_body, len, integrity, d_frame_pos, d_frame_pos ? cap : 0, d_result,
-                          bind(c, stream));
-}
-
-int iggy_codec_batch_checksum_device(iggy_codec_ctx *c, const iggy_batch_header *hdr,
-                                     const uint8_t *d_blob, const uint64_t *d_frame_pos,
-                                     uint64_t nframes, uint64_t *d_out, void *stream) {
-    if (!c || !hdr || !d_out || (nframes && (!d_blob || !d_frame_pos))) return IGGY_ERR_INVALID_ARGUMENT;
-    DevGuard dg(c->device);
-    hipStream_t s = bind(c, stream);
-    int r = c->gbsums.ensure(((44 + 8 * nframes) / 1024 + 2) * 64);
-    if (r) return r;
-    return checksum_of_walk(c, hdr, nframes, d_blob, d_frame_pos, d_out, s);
-}
-
-int iggy_codec_xxh3_64_ranges_device(iggy_codec_ctx *c, const uint8_t *d_data, const uint64_t *d_offsets,
-                                     const uint32_t *d_lengths, uint64_t n, uint64_t *d_out,
-                                     void *stream) {
-    if (!c || !d_out || (n && (!d_data || !d_offsets || !d_lengths))) return IGGY_ERR_INVALID_ARGUMENT;
-    if (!n) return 0;
-    DevGuard dg(c->device);
-    const uint64_t blocks = std::min<uint64_t>((n + 255) / 256, (uint64_t)c->ncu * 16);
-    hipLaunchKernelGGL(k_xxh3_ranges, dim3((uint32_t)blocks), dim3(256), 0, bind(c, stream), d_data,
-                       d_offsets, d_lengths, n, d_out);
-    HIP_OK(hipGetLastError());
-    return 0;
-}
-
-// ------------------------------------------------- at-rest encryption (crypt.hip)
-namespace {
-const uint8_t kAesSboxHost[256] = {
-    0x63, 0x7c, 0x77, 0x7b, 0xf2, 0x6b, 0x6f, 0xc5, 0x30, 0x01, 0x67, 0x2b, 0xfe, 0xd7, 0xab, 0x76,
-    0xca, 0x82, 0xc9, 0x7d, 0xfa, 0x59, 0x47, 0xf0, 0xad, 0xd4, 0xa2, 0xaf, 0x9c, 0xa4, 0x72, 0xc0,
-    0xb7, 0xfd, 0x93, 0x26, 0x36, 0x3f, 0xf7, 0xcc, 0x34, 0xa5, 0xe5, 0xf1, 0x71, 0xd8, 0x31, 0x15,
-    0x04, 0xc7, 0x23, 0xc3, 0x18, 0x96, 0x05, 0x9a, 0x07, 0x12, 0x80, 0xe2, 0xeb, 0x27, 0xb2, 0x75,
-    0x09, 0x83, 0x2c, 0x1a, 0x1b, 0x6e, 0x5a, 0xa0, 0x52, 0x3b, 0xd6, 0xb3, 0x29, 0xe3, 0x2f, 0x84,
-    0x53, 0xd1, 0x00, 0xed, 0x20, 0xfc, 0xb1, 0x5b, 0x6a, 0xcb, 0xbe, 0x39, 0x4a, 0x4c, 0x58, 0xcf,
-    0xd0, 0xef, 0xaa, 0xfb, 0x43, 0x4d, 0x33, 0x85, 0x45, 0xf9, 0x02, 0x7f, 0x50, 0x3c, 0x9f, 0xa8,
-    0x51, 0xa3, 0x40, 0x8f, 0x92, 0x9d, 0x38, 0xf5, 0xbc, 0xb6, 0xda, 0x21, 0x10, 0xff, 0xf3, 0xd2,
-    0xcd, 0x0c, 0x13, 0xec, 0x5f, 0x97, 0x44, 0x17, 0xc4, 0xa7, 0x7e, 0x3d, 0x64, 0x5d, 0x19, 0x73,
-    0x60, 0x81, 0x4f, 0xdc, 0x22, 0x2a, 0x90, 0x88, 0x46, 0xee, 0xb8, 0x14, 0xde, 0x5e, 0x0b, 0xdb,
-    0xe0, 0x32, 0x3a, 0x0a, 0x49, 0x06, 0x24, 0x5c, 0xc2, 0xd3, 0xac, 0x62, 0x91, 0x95, 0xe4, 0x79,
-    0xe7, 0xc8, 0x37, 0x6d, 0x8d, 0xd5, 0x4e, 0xa9, 0x6c, 0x56, 0xf4, 0xea, 0x65, 0x7a, 0xae, 0x08,
-    0xba, 0x78, 0x25, 0x2e, 0x1c, 0xa6, 0xb4, 0xc6, 0xe8, 0xdd, 0x74, 0x1f, 0x4b, 0xbd, 0x8b, 0x8a,
-    0x70, 0x3e, 0xb5, 0x66, 0x48, 0x03, 0xf6, 0x0e, 0x61, 0x35, 0x57, 0xb9, 0x86, 0xc1, 0x1d, 0x9e,
-    0xe1, 0xf8, 0x98, 0x11, 0x69, 0xd9, 0x8e, 0x94, 0x9b, 0x1e, 0x87, 0xe9, 0xce, 0x55, 0x28, 0xdf,
-    0x8c, 0xa1, 0x89, 0x0d, 0xbf, 0xe6, 0x42, 0x68, 0x41, 0x99, 0x2d, 0x0f, 0xb0, 0x54, 0xbb, 0x16};
-
-uint32_t sub_word(uint32_t w) {
-    return ((uint32_t)kAesSboxHost[w >> 24] << 24) | ((uint32_t)kAesSboxHost[(w >> 16) & 0xff] << 16) |
-           ((uint32_t)kAesSboxHost[(w >> 8) & 0xff] << 8) | kAesSboxHost[w & 0xff];
-}
-// FIPS-197 5.2, Nk = 8: words w[0..59], big-endian byte order
-void aes256_key_schedule(const uint8_t key[32], uint32_t w[60]) {
-    for (int i = 0; i < 8; ++i)
-        w[i] = ((uint32_t)key[4 * i] << 24) | ((uint32_t)key[4 * i + 1] << 16) | ((uint32_t)key[4 * i + 2] << 8) |
-               key[4 * i + 3];
-    uint32_t rcon = 0x01000000u;
-    for (int i = 8; i < 60; ++i) {
-        uint32_t t = w[i - 1];
-        if (i % 8 == 0) {
-            t = sub_word((t << 8) | (t >> 24)) ^ rcon;
-            rcon = ((rcon << 1) ^ ((rcon & 0x80000000u) ? 0x1b000000u : 0)) & 0xff000000u;
-        } else if (i % 8 == 4) {
-            t = sub_word(t);
-        }
-        w[i] = w[i - 8] ^ t;
-    }
-}
-uint8_t gf_xtime(uint8_t x) { return (uint8_t)((x << 1) ^ ((x & 0x80) ? 0x1b : 0)); }
-// one block, byte-oriented rounds (only H = E_K(0) is computed on the host)
-void aes256_block_host(const uint32_t w[60], const uint8_t in[16], uint8_t out[16]) {
-    uint8_t s[16];
-    auto add_key = [&](int r) {
-        for (int c = 0; c < 4; ++c)
-            for (int k = 0; k < 4; ++k) s[4 * c + k] ^= (uint8_t)(w[4 * r + c] >> (24 - 8 * k));
-    };
-    memcpy(s, in, 16);
-    add_key(0);
-    for (int r = 1; r <= 14; ++r) {
-        uint8_t t[16];
-        for (int i = 0; i < 16; ++i) t[i] = kAesSboxHost[s[i]];
-        for (int c = 0; c < 4; ++c)
-            for (int k = 0; k < 4; ++k) s[4 * c + k] = t[4 * ((c + k) % 4) + k];
-        if (r != 14)
-            for (int c = 0; c < 4; ++c) {
-                uint8_t *a = s + 4 * c;
-                const uint8_t a0 = a[0], a1 = a[1], a2 = a[2], a3 = a[3], x = (uint8_t)(a0 ^ a1 ^ a2 ^ a3);
-                a[0] ^= (uint8_t)(x ^ gf_xtime((uint8_t)(a0 ^ a1)));
-                a[1] ^= (uint8_t)(x ^ gf_xtime((uint8_t)(a1 ^ a2)));
-                a[2] ^= (uint8_t)(x ^ gf_xtime((uint8_t)(a2 ^ a3)));
-                a[3] ^= (uint8_t)(x ^ gf_xtime((uint8_t)(a3 ^ a0)));
-            }
-        add_key(r);
-    }
-    memcpy(out, s, 16);
-}
-// GF(2^128) product, GCM bit order, (hi, lo) big-endian halves
-void gf128_mul(uint64_t xh, uint64_t xl, uint64_t yh, uint64_t yl, uint64_t &zh, uint64_t &zl) {
-    zh = zl = 0;
-    for (int i = 0; i < 128; ++i) {
-        const uint64_t bit = i < 64 ? (xh >> (63 - i)) & 1 : (xl >> (127 - i)) & 1;
-        if (bit) { zh ^= yh; zl ^= yl; }
-        const uint64_t lsb = yl & 1;
-        yl = (yl >> 1) | (yh << 63);
-        yh >>= 1;
-        if (lsb) yh ^= 0xe100000000000000ull;
-    }
-}
-// Shoup 4-bit table of P: t[2 i] = HL[i], t[2 i + 1] = HH[i] (entry 8 = P itself)
-void ghash_table(uint64_t ph, uint64_t pl, uint64_t *t) {
-    uint64_t HL[16] = {}, HH[16] = {};
-    uint64_t vh = ph, vl = pl;
-    HL[8] = vl; HH[8] = vh;
-    for (int i = 4; i > 0; i >>= 1) {
-        const uint64_t T = (vl & 1) ? 0xe1000000ull : 0;
-        vl = (vh << 63) | (vl >> 1);
-        vh = (vh >> 1) ^ (T << 32);
-        HL[i] = vl; HH[i] = vh;
-    }
-    for (int i = 2; i <= 8; i *= 2)
-        for (int j = 1; j < i; ++j) {
-            HH[i + j] = HH[i] ^ HH[j];
-            HL[i + j] = HL[i] ^ HL[j];
-        }
-    for (int i = 0; i < 16; ++i) { t[2 * i] = HL[i]; t[2 * i + 1] = HH[i]; }
-}
-constexpr size_t kCrMisc = 0, kCrHdr = 64, kCrN = 192, kCrSum = 200, kCrRes = 256, kCrTab = 1024,
-                 kCrTabBytes = (size_t)kGhPowers * 32 * 8, kCrArrays = kCrTab + kCrTabBytes;
-
-// every scratch buffer a crypt enqueue of a record of up to len bytes uses, sized
-// before the first enqueue of a sequence (a buffer grown between two enqueues of one
-// stream order would be freed under the earlier one's kernels)
-int crypt_reserve(iggy_codec_ctx *c, uint64_t len) {
-    const uint64_t nmax = (len > kHdr ? (len - kHdr) / kFrameHdr : 0) + 1;
-    const uint64_t ntiles = (nmax + kCryptTile - 1) / kCryptTile;
-    const void *cr_before = c->cr.p;
-    int r = c->cr.ensure(kCrArrays + (2 * nmax + ntiles + 2) * 8);
-    if (c->cr.p != cr_before) c->cr_key_set = false;  // a grown buffer lost the tables
-    r |= c->dpos.ensure((nmax + 1) * 8);
-    r |= c->gbsums.ensure(((44 + 8 * nmax) / 1024 + 2) * 64);
-    if (r) return IGGY_ERR_DEVICE;
-    return ensure_decode_scratch(c, len);
-}
-
-int enqueue_crypt(iggy_codec_ctx *c, bool enc, const uint8_t *key, const uint8_t *d_record, uint64_t len,
-                  const uint8_t *d_nonces, uint8_t *d_out, uint64_t cap, iggy_crypt_result *d_result, void *stream) {
-    if (!c || !key || !d_record || !d_out || !d_result || (enc && !d_nonces)) return IGGY_ERR_INVALID_ARGUMENT;
-    DevGuard dg(c->device);
-    hipStream_t s = bind(c, stream);
-    const uint64_t nmax = (len > kHdr ? (len - kHdr) / kFrameHdr : 0) + 1;
-    const uint64_t ntiles = (nmax + kCryptTile - 1) / kCryptTile;
-    int r = crypt_reserve(c, len);
-    if (r) return r;
-    if (!c->cr_pinned && hipHostMalloc(&c->cr_pinned, kCrTabBytes, hipHostMallocDefault) != hipSuccess) {
-        c->cr_pinned = nullptr;
-        return IGGY_ERR_DEVICE;
-    }
-    CryptKey ck;
-    aes256_key_schedule(key, ck.rk);
-    uint8_t fp[32] = {};
-    fp[16 + 15] = 1;
-    aes256_block_host(ck.rk, fp, fp);            // E_K(0)
-    aes256_block_host(ck.rk, fp + 16, fp + 16);  // E_K(1)
-    if (!c->cr_key_set || memcmp(c->cr_fp, fp, 32) != 0) {
-        // new key: H = E_K(0), tables of H^1 .. H^64 (the staging buffer is rewritten
-        // only after every earlier upload on this stream order has run)
-        HIP_OK(hipStreamSynchronize(s));
-        uint8_t zero[16] = {}, hb[16];
-        aes256_block_host(ck.rk, zero, hb);
-        uint64_t hh = 0, hl = 0;
-        for (int k = 0; k < 8; ++k) { hh = (hh << 8) | hb[k]; hl = (hl << 8) | hb[8 + k]; }
-        uint64_t ph = hh, pl = hl;
-        uint64_t *tab = (uint64_t *)c->cr_pinned;
-        for (uint32_t e = 1; e <= kGhPowers; ++e) {
-            ghash_table(ph, pl, tab + 32 * (e - 1));
-            uint64_t nh, nl;
-            gf128_mul(ph, pl, hh, hl, nh, nl);
-            ph = nh; pl = nl;
-        }
-        HIP_OK(hipMemcpyAsync(c->cr.as<uint8_t>(kCrTab), c->cr_pinned, kCrTabBytes, hipMemcpyHostToDevice, s));
-        memcpy(c->cr_fp, fp, 32);
-        c->cr_key_set = true;
-    }
-    CryptScratch cs;
-    iggy_decode_result *dres = c->cr.as<iggy_decode_result>(kCrRes);
-    cs.dres = dres;
-    cs.pos = c->dpos.as<uint64_t>();
-    cs.osize = c->cr.as<uint64_t>(kCrArrays);
-    cs.opos = cs.osize + nmax;
-    cs.tsum = cs.opos + nmax;
-    cs.misc = c->cr.as<uint64_t>(kCrMisc);
-    cs.gtab = c->cr.as<uint64_t>(kCrTab);
-    cs.dh = c->cr.as<iggy_batch_header>(kCrHdr);
-    cs.dn = c->cr.as<uint64_t>(kCrN);
-    cs.dsum = c->cr.as<uint64_t>(kCrSum);
-    HIP_OK(hipMemsetAsync(cs.misc, 0, 64, s));
-    r = enqueue_decode(c, d_record, len, enc ? IGGY_INTEGRITY_VERIFY : IGGY_INTEGRITY_LAYOUT_ONLY,
-                       c->dpos.as<uint64_t>(), nmax, dres, s);
-    if (r) return r;
-    const uint32_t sg = (uint32_t)std::min<uint64_t>(ntiles, (uint64_t)c->ncu * 4);
-    if (enc) {
-        hipLaunchKernelGGL(k_crypt_sizes<true>, dim3(sg), dim3(256), 0, s, d_record, cs);
-    } else {
-        hipLaunchKernelGGL(k_crypt_sizes<false>, dim3(sg), dim3(256), 0, s, d_record, cs);
-    }
-    hipLaunchKernelGGL(k_crypt_scan, dim3(1), dim3(1024), 0, s, cs);
-    if (enc) {
-        hipLaunchKernelGGL(k_crypt_frames<true>, dim3(c->ncu * 8), dim3(256), kCryptLds, s, d_record, d_out, cap,
-                           d_nonces, ck, cs);
-    } else {
-        hipLaunchKernelGGL(k_crypt_frames<false>, dim3(c->ncu * 8), dim3(256), kCryptLds, s, d_record, d_out, cap,
-                           (const uint8_t *)nullptr, ck, cs);
-    }
-    hipLaunchKernelGGL(k_crypt_checksums, dim3(c->ncu * 16), dim3(256), 0, s, d_out, cap, cs);
-    hipLaunchKernelGGL(k_crypt_header, dim3(1), dim3(64), 0, s, cap, cs);
-    CsSource src{nullptr, d_out + kHdr, cs.opos};
-    hipLaunchKernelGGL(k_bsum_blocks, dim3(bsum_grid(c, cap / 48 + 1)), dim3(256), 0, s, cs.dh, cs.dn, src,
-                       c->gbsums.as<uint64_t>(), nullptr);
-    hipLaunchKernelGGL(k_bsum_chain, dim3(1), dim3(128), 0, s, cs.dh, cs.dn, src,
-                       (const uint64_t *)c->gbsums.as<uint64_t>(), c->dsync.as<uint8_t>(kSyncSmall), cs.dsum,
-                       nullptr);
-    if (enc) {
-        hipLaunchKernelGGL(k_crypt_finish<true>, dim3(1), dim3(64), 0, s, d_record, len, d_out, cap, cs, d_result);
-    } else {
-        hipLaunchKernelGGL(k_crypt_finish<false>, dim3(1), dim3(64), 0, s, d_record, len, d_out, cap, cs, d_result);
-    }
-    HIP_OK(hipGetLastError());
-    return 0;
-}
-}  // namespace
-
-int iggy_codec_encrypt_batch_device(iggy_codec_ctx *c, const uint8_t *key, const uint8_t *d_record, uint64_t len,
-                                    const uint8_t *d_nonces, uint8_t *d_out, uint64_t cap,
-                                    iggy_crypt_result *d_result, void *stream) {
-    return enqueue_crypt(c, true, key, d_record, len, d_nonces, d_out, cap, d_result, stream);
-}
-
-int iggy_codec_decrypt_batch_device(iggy_codec_ctx *c, const uint8_t *key, const uint8_t *d_record, uint64_t len,
-                                    uint8_t *d_out, uint64_t cap, iggy_crypt_result *d_result, void *stream) {
-    return enqueue_crypt(c, false, key, d_record, len, nullptr, d_out, cap, d_result, stream);
-}
-
-// ----------------------------------------------- poll reply body
-// build_polled_messages_body (core/server/src/responses.rs:1666-1714): the fragments
-// concatenated into one stream, walked record by record (BatchHeader::decode,
-// batch_end = position + total_size checked against the stream), each record copied or
-// -- with an encryptor -- decrypted (decrypt_batch_record, send_messages.rs:364-415,
-// on the GPU: one H2D of the stream, every record's decrypt enqueued back to back on
-// the context stream, one D2H of the verdicts and the plaintext), the message count
-// summed with checked_add and backpatched into [partition_id u32][current_offset u64]
-// [count u32]. Errors in the reference's order: record k's header / bounds, then its
-// decrypt, then the count overflow, before anything of record k + 1.
-namespace {
-uint32_t poll_error_kind(uint32_t kind) {
-    // decrypt_batch_record's `?` on decode_batch_slice_with (LayoutOnly) goes through
-    // batch_error (send_messages.rs:52-66): checksum kinds keep their identity (never
-    // produced by a layout walk), everything else is InvalidCommand
-    switch (kind) {
-        case IGGY_OK:
-        case IGGY_ERR_CANNOT_DECRYPT_DATA:
-        case IGGY_ERR_INVALID_COMMAND:
-        case IGGY_ERR_INVALID_BATCH_CHECKSUM:
-        case IGGY_ERR_INVALID_MESSAGE_CHECKSUM:
-        case IGGY_ERR_TIMEOUT:
-        case IGGY_ERR_DEVICE:
-            return kind;
-        default:
-            return IGGY_ERR_INVALID_COMMAND;
-    }
-}
-int pb_pinned_ensure(iggy_codec_ctx *c, size_t n) {
-    // grown past kHostMapKeep by one large decrypting poll: given back at the next
-    // ordinary-sized one instead of staying pinned for the context's life
-    if (n <= c->pb_cap && !(c->pb_cap > kHostMapKeep && n <= kHostMapKeep)) return 0;
-    if (c->pb_pinned) (void)hipHostFree(c->pb_pinned);
-    c->pb_pinned = nullptr;
-    c->pb_cap = 0;
-    const size_t want = std::max<size_t>(n, 1 << 20);
-    if (hipHostMalloc(&c->pb_pinned, want, hipHostMallocDefault) != hipSuccess) {
-        c->pb_pinned = nullptr;
-        return IGGY_ERR_DEVICE;
-    }
-    c->pb_cap = want;
-    return 0;
-}
-}  // namespace
-
-int iggy_codec_build_polled_body(iggy_codec_ctx *c, uint32_t partition_id, uint64_t current_offset,
-                                 const iggy_poll_fragment *frags, uint64_t nfrags, const uint8_t *key, uint8_t *out,
-                                 uint64_t cap, uint64_t *out_len, iggy_wire_error *err) {
-    if (!c || (!frags && nfrags) || !out_len || (!out && cap)) return IGGY_ERR_INVALID_ARGUMENT;
-    set_err(err, IGGY_OK);
-    *out_len = 0;
-    uint64_t total = 0;
-    for (uint64_t f = 0; f < nfrags; ++f) {
-        if (!frags[f].data && frags[f].len) return IGGY_ERR_INVALID_ARGUMENT;
-        total += frags[f].len;
-    }
-    auto fail = [&](uint32_t kind, uint64_t a = 0, uint64_t b = 0) {
-        set_err(err, kind, 0, a, b);
-        return (int)kind;
-    };
-    // 1. the concatenated stream: straight into the body when it fits and nothing is
-    //    decrypted (the reply IS the stored encoding); into host memory when it does
-    //    not fit (only walked, for the reference's error order, then CAPACITY); into
-    //    the pinned staging (stream, then the plaintext) when records are decrypted
-    uint8_t *stream;
-    std::vector<uint8_t> walk_only;
-    if (!key && cap >= 16 + total) {
-        stream = out + 16;
-    } else if (!key) {
-        walk_only.resize(total + 1);
-        stream = walk_only.data();
-    } else {
-        if (pb_pinned_ensure(c, 2 * total + 64)) return IGGY_ERR_DEVICE;
-        stream = (uint8_t *)c->pb_pinned;
-    }
-    {
-        uint64_t o = 0;
-        for (uint64_t f = 0; f < nfrags; ++f) {
-            if (frags[f].len) memcpy(stream + o, frags[f].data, frags[f].len);
-            o += frags[f].len;
-        }
-    }
-    // 2. the record walk (headers only)
-    struct Rec { uint64_t pos, len; uint32_t count; };
-    std::vector<Rec> recs;
-    bool walk_failed = false;
-    for (uint64_t pos = 0; pos < total;) {
-        iggy_batch_header h;
-        iggy_wire_error e;
-        if (iggy_batch_header_decode(stream + pos, total - pos, &h, &e) != 0) {
-            walk_failed = true;  // BatchHeader::decode -> InvalidCommand
-            break;
-        }
-        const uint64_t end = pos + h.batch_length;
-        if (end < pos || end > total) {  // checked_add / batch_end > stream.len()
-            walk_failed = true;
-            break;
-        }
-        recs.push_back({pos, h.batch_length, h.message_count});
-        pos = end;
-    }
-    // 3. decrypt every walked record on the device
-    std::vector<iggy_crypt_result> res;
-    uint64_t dec_total = 0;
-    if (key && !recs.empty()) {
-        const uint64_t span = recs.back().pos + recs.back().len;
-        uint64_t maxlen = 0;
-        for (const Rec &r : recs) maxlen = std::max(maxlen, r.len);
-        DevGuard dg(c->device);
-        bind(c, nullptr);
-        int r = c->din.ensure(span + 16);
-        r |= c->dout.ensure(span + 16);
-        r |= c->pbres.ensure(recs.size() * sizeof(iggy_crypt_result));
-        if (r) return IGGY_ERR_DEVICE;
-        r = crypt_reserve(c, maxlen);
-        if (r) return r;
-        HIP_OK(hipMemcpyAsync(c->din.p, stream, span, hipMemcpyHostToDevice, c->stream));
-        iggy_crypt_result *d_res = c->pbres.as<iggy_crypt_result>();
-        for (size_t k = 0; k < recs.size(); ++k) {
-            r = enqueue_crypt(c, false, key, c->din.as<uint8_t>(recs[k].pos), recs[k].len, nullptr,
-                              c->dout.as<uint8_t>(recs[k].pos), recs[k].len, d_res + k, c->stream);
-            if (r) return r;
-        }
-        // verdicts and plaintext back into the staging's second half
-        uint8_t *hout = stream + total + 32;
-        res.resize(recs.size());
-        HIP_OK(hipMemcpyAsync(hout, c->dout.p, span, hipMemcpyDeviceToHost, c->stream));
-        r = get_host(c, res.data(), d_res, recs.size() * sizeof(iggy_crypt_result), c->stream);
-        if (r) return r;
-        for (const iggy_crypt_result &q : res)
-            if (q.error.kind == IGGY_ERR_TIMEOUT) { reset_after_timeout(c); break; }
-    }
-    // 4. the reference's per-record order: decrypt verdict, then the count
-    uint32_t count = 0;
-    for (size_t k = 0; k < recs.size(); ++k) {
-        if (key) {
-            const iggy_crypt_result &q = res[k];
-            const uint32_t kind = poll_error_kind(q.error.kind);
-            if (kind != IGGY_OK) {
-                if (err) {
-                    *err = q.error;
-                    err->kind = kind;
-                    if (kind != q.error.kind) err->reason = 0, err->a = err->b = err->c = 0;
-                }
-                return (int)kind;
-            }
-            dec_total += q.out_len;
-        }
-        if ((uint64_t)count + recs[k].count > 0xFFFFFFFFull) return fail(IGGY_ERR_INVALID_COMMAND);
-        count += recs[k].count;
-    }
-    if (walk_failed) return fail(IGGY_ERR_INVALID_COMMAND);
-    const uint64_t body_len = 16 + (key ? dec_total : total);
-    if (cap < body_len) return fail(IGGY_ERR_CAPACITY, body_len, cap);
-    if (key) {
-        const uint8_t *hout = stream + total + 32;
-        uint64_t o = 16;
-        for (size_t k = 0; k < recs.size(); ++k) {
-            memcpy(out + o, hout + recs[k].pos, res[k].out_len);
-            o += res[k].out_len;
-        }
-    } else if (stream != out + 16) {
-        memcpy(out + 16, stream, total);
-    }
-    memcpy(out, &partition_id, 4);
-    memcpy(out + 4, &current_offset, 8);
-    memcpy(out + 12, &count, 4);
-    *out_len = body_len;
-    return 0;
-}
-
-// ------------------------------------------------- poll-path slicing / stamp
-// select_batch_slice + served header on a decoded device record (gate / d_matched:
-// chunk walks, see k_chunk_gate)
-static int enqueue_select(iggy_codec_ctx *c, const uint8_t *d_record, const uint64_t *d_frame_pos, uint64_t nframes,
-                          const iggy_slice_query &qq, iggy_slice_result *d_out, uint8_t *d_header_out, hipStream_t s,
-                          const uint32_t *gate = nullptr, const uint32_t *d_matched = nullptr) {
-    const uint64_t ntiles = (nframes + kSliceTile - 1) / kSliceTile;
-    int r = c->sl.ensure(512 + ntiles * 4);
-    r |= c->gbsums.ensure(((44 + 8 * nframes) / 1024 + 2) * 64);
-    if (r) return IGGY_ERR_DEVICE;
-    SliceScratch ss;
-    ss.stop = c->sl.as<uint64_t>(0);
-    ss.nsel = c->sl.as<uint64_t>(8);
-    ss.first = c->sl.as<uint64_t>(16);
-    ss.computed = c->sl.as<uint64_t>(24);
-    ss.skip = c->sl.as<uint32_t>(32);
-    ss.hdr = c->sl.as<iggy_batch_header>(64);
-    ss.tile_cnt = c->sl.as<uint32_t>(512);
-    HIP_OK(hipMemsetAsync(ss.stop, 0xff, 8, s));
-    if (nframes) {
-        const uint32_t g = (uint32_t)std::min<uint64_t>((nframes + 255) / 256, (uint64_t)c->ncu * 8);
-        hipLaunchKernelGGL(k_slice_stop, dim3(g), dim3(256), 0, s, d_record, d_frame_pos, nframes, qq, ss.stop, gate);
-        hipLaunchKernelGGL(k_slice_count, dim3((uint32_t)ntiles), dim3(256), 0, s, d_record, d_frame_pos, nframes, qq,
-                           (const uint64_t *)ss.stop, ss.tile_cnt, gate);
-    }
-    hipLaunchKernelGGL(k_slice_pick, dim3(1), dim3(256), 0, s, d_record, d_frame_pos, nframes, qq,
-                       (const uint32_t *)ss.tile_cnt, ntiles, ss, d_out, gate, d_matched);
-    CsSource src{nullptr, d_record + kHdr, d_frame_pos, ss.first};
-    hipLaunchKernelGGL(k_bsum_blocks, dim3(bsum_grid(c, nframes)), dim3(256), 0, s, (const iggy_batch_header *)ss.hdr,
-                       (const uint64_t *)ss.nsel, src, c->gbsums.as<uint64_t>(), (const uint32_t *)ss.skip);
-    hipLaunchKernelGGL(k_bsum_chain, dim3(1), dim3(128), 0, s, (const iggy_batch_header *)ss.hdr,
-                       (const uint64_t *)ss.nsel, src, (const uint64_t *)c->gbsums.as<uint64_t>(),
-                       c->sl.as<uint8_t>(128), ss.computed, (const uint32_t *)ss.skip);
-    hipLaunchKernelGGL(k_slice_finish, dim3(1), dim3(64), 0, s, d_record, ss, d_out, d_header_out);
-    HIP_OK(hipGetLastError());
-    return 0;
-}
-
-int iggy_codec_select_slice_device(iggy_codec_ctx *c, const uint8_t *d_record, const uint64_t *d_frame_pos,
-                                   uint64_t nframes, const iggy_slice_query *q, iggy_slice_result *d_out,
-                                   uint8_t *d_header_out, void *stream) {
-    if (!c || !d_record || !q || !d_out || (nframes && !d_frame_pos)) return IGGY_ERR_INVALID_ARGUMENT;
-    if (q->kind != IGGY_LOOKUP_OFFSET && q->kind != IGGY_LOOKUP_TIMESTAMP) return IGGY_ERR_INVALID_ARGUMENT;
-    DevGuard dg(c->device);
-    hipStream_t s = bind(c, stream);
-    return enqueue_select(c, d_record, d_frame_pos, nframes, *q, d_out, d_header_out, s);
-}
-
-// The per-batch form of the chunk walk: every batch's decode, gate, selection and
-// fragment push enqueued one after the other (~11 stream operations per batch). Used
-// for chunks holding a batch that is not single-stride, or that the one-launch form
-// (below) found to need the general walk.
-static int walk_chunk_per_batch(iggy_codec_ctx *c, const uint8_t *chunk, uint64_t len, const iggy_slice_query *q,
-                                int integrity, iggy_chunk_fragment *frags, uint8_t *headers, uint64_t cap,
-                                iggy_chunk_walk *out) {
-    memset(out, 0, sizeof(*out));
-    // the batch extents follow from the 256-B headers alone (host); a header that does
-    // not decode or a batch that does not fit is the last candidate (its decode fails)
-    struct Cand { uint64_t pos, bl, nframes, pbase; };
-    std::vector<Cand> cand;
-    uint64_t cursor = 0, pwords = 0, maxn = 0;
-    while (cursor + 256 <= len) {
-        iggy_batch_header h;
-        iggy_wire_error he;
-        const bool ok = iggy_batch_header_decode(chunk + cursor, len - cursor, &h, &he) == 0;
-        const bool fits = ok && h.batch_length <= len - cursor;
-        const uint64_t nf = fits ? (h.batch_length - 256) / 48 + 1 : 1;
-        cand.push_back({cursor, fits ? h.batch_length : 0, fits ? (uint64_t)h.message_count : 0, pwords});
-        pwords += nf;
-        maxn = std::max(maxn, nf);
-        if (!fits) break;
-        cursor += h.batch_length;
-    }
-    const uint64_t K = cand.size();
-    // device: the chunk once; per batch its Verify / LayoutOnly decode, the gate, the
-    // selection (match count from the previous batch) and the fragment push; one sync
-    const uint64_t kState = 256, kSlot = 512;
-    int r = c->din.ensure(len + 16);
-    r |= c->dpos.ensure((pwords + 1) * 8);
-    r |= c->pres.ensure((K + 1) * sizeof(iggy_decode_result));
-    r |= c->cwk.ensure(kState + K * (kSlot + 8) + cap * (sizeof(iggy_chunk_fragment) + 256) + 64);
-    if (!r) r = ensure_decode_scratch(c, len);
-    if (r) return IGGY_ERR_DEVICE;
-    hipStream_t s = c->stream;
-    ChunkState *st = c->cwk.as<ChunkState>(0);
-    uint32_t *gates = c->cwk.as<uint32_t>(kState);
-    uint8_t *slots = c->cwk.as<uint8_t>(kState + K * 8);
-    iggy_chunk_fragment *d_frags = c->cwk.as<iggy_chunk_fragment>(kState + K * (kSlot + 8));
-    uint8_t *d_hdrs = (uint8_t *)(d_frags + cap);
-    r = put_host(c, c->din.p, chunk, len, s);
-    if (r) return r;
-    hipLaunchKernelGGL(k_chunk_init, dim3(1), dim3(64), 0, s, st, q->already_matched);
-    iggy_decode_result *d_res = c->pres.as<iggy_decode_result>();
-    for (uint64_t k = 0; k < K; ++k) {
-        const Cand &cd = cand[k];
-        const uint8_t *rec = c->din.as<uint8_t>(cd.pos);
-        uint64_t *pos = c->dpos.as<uint64_t>(8 * cd.pbase);
-        r = enqueue_decode(c, rec, len - cd.pos, integrity, pos, cd.bl ? (cd.bl - 256) / 48 + 1 : 0, d_res + k, s);
-        if (r) return r;
-        hipLaunchKernelGGL(k_chunk_gate, dim3(1), dim3(64), 0, s, (const iggy_decode_result *)(d_res + k), cd.pos,
-                           q->count, st, gates + k);
-        if (!cd.bl) break;  // its decode failed (the gate stops the walk there)
-        iggy_slice_result *sr = (iggy_slice_result *)(slots + k * kSlot);
-        uint8_t *hb = slots + k * kSlot + 256;
-        r = enqueue_select(c, rec, pos, cd.nframes, *q, sr, hb, s, gates + k, &st->matched);
-        if (r) return r;
-        hipLaunchKernelGGL(k_chunk_after, dim3(1), dim3(64), 0, s, (const iggy_slice_result *)sr,
-                           (const uint8_t *)hb, cd.pos, cd.bl, st, (const uint32_t *)(gates + k), d_frags, d_hdrs, cap);
-    }
-    HIP_OK(hipGetLastError());
-    ChunkState hs{};
-    r = get_host(c, &hs, st, sizeof(hs), s);
-    if (r) return r;
-    const uint64_t nf = std::min<uint64_t>(hs.nfrag, cap);
-    if (nf) {
-        r = get_host(c, frags, d_frags, nf * sizeof(iggy_chunk_fragment), s);
-        if (!r && headers) r = get_host(c, headers, d_hdrs, nf * 256, s);
-        if (r) return r;
-    }
-    if (hs.error.kind == IGGY_ERR_TIMEOUT) {  // a bug guard fired, not a verdict on the chunk
-        reset_after_timeout(c);
-        return IGGY_ERR_TIMEOUT;
-    }
-    out->consumed = std::min<uint64_t>(hs.consumed, len);
-    out->corrupt = hs.corrupt;
-    out->matched = hs.matched;
-    out->last_matching_offset = hs.last_matching_offset;
-    out->has_last_matching_offset = (uint32_t)hs.has_last;
-    out->fragments = hs.nfrag;
-    out->error = hs.error;
-    out->batches = hs.batches;
-    return hs.nfrag > cap ? IGGY_ERR_CAPACITY : 0;
-}
-
-int iggy_codec_walk_disk_chunk(iggy_codec_ctx *c, const uint8_t *chunk, uint64_t len, const iggy_slice_query *q,
-                               int integrity, iggy_chunk_fragment *frags, uint8_t *headers, uint64_t cap,
-                               iggy_chunk_walk *out) {
-    if (!c || !q || !out || (!chunk && len) || (cap && !frags)) return IGGY_ERR_INVALID_ARGUMENT;
-    if (q->kind != IGGY_LOOKUP_OFFSET && q->kind != IGGY_LOOKUP_TIMESTAMP) return IGGY_ERR_INVALID_ARGUMENT;
-    DevGuard dg(c->device);
-    bind(c, nullptr);
-    memset(out, 0, sizeof(*out));
-    // the batch extents follow from the 256-B headers alone (host); a header that does
-    // not decode or a batch that does not fit is the last candidate (its decode fails)
-    std::vector<ChunkCand> cand;
-    uint64_t cursor = 0, pwords = 0, nbb = 0;
-    bool one_launch = true;
-    while (cursor + 256 <= len) {
-        iggy_batch_header h;
-        iggy_wire_error he;
-        const bool ok = iggy_batch_header_decode(chunk + cursor, len - cursor, &h, &he) == 0;
-        const bool fits = ok && h.batch_length <= len - cursor;
-        uint64_t nfp = 0;
-        if (!rec_plan(chunk + cursor, len - cursor, &nfp)) one_launch = false;
-        const uint64_t nf = fits ? (h.batch_length - 256) / 48 + 1 : 1;
-        cand.push_back({cursor, fits ? h.batch_length : 0, pwords, nbb});
-        pwords += nf;
-        nbb += rec_blocks(nfp) + 2;
-        if (!fits) break;
-        cursor += h.batch_length;
-    }
-    const uint64_t K = cand.size();
-    if (K == 0) {  // no header fits: the loop does not run (poll_plan.rs:963)
-        out->matched = q->already_matched;
-        return 0;
-    }
-    if (!one_launch) return walk_chunk_per_batch(c, chunk, len, q, integrity, frags, headers, cap, out);
-    // One copy of the chunk, ONE multi-record decode launch, ONE k_chunk_walk launch
-    // (one workgroup per batch: gate, selection, partial checksum, fragment push, the
-    // match count handed batch to batch). The tables are read and the outputs written
-    // by the kernels in host-mapped memory; the host spins on the completion flag.
-    const uint64_t capk = std::min<uint64_t>(cap, K);  // at most one fragment per batch
-    const size_t res_bytes = 256 + capk * (sizeof(iggy_chunk_fragment) + 256);
-    const size_t cand_bytes = K * sizeof(ChunkCand), link_bytes = K * sizeof(ChunkLink);
-    int r = c->din.ensure(len + 16);
-    r |= c->dpos.ensure((pwords + 1) * 8);
-    r |= c->pres.ensure((K + 1) * sizeof(iggy_decode_result));
-    r |= c->sl.ensure(nbb * 64 + 64);
-    r |= c->cmap.ensure(cand_bytes);
-    r |= c->omap.ensure(64 + res_bytes);
-    // the links live in a buffer of their own that only ever holds links: a stale one
-    // carries an older epoch, never the current one (zeroed whenever it is new)
-    const size_t links_cap_before = c->clinks.cap;
-    r |= c->clinks.ensure(link_bytes);
-    if (r) return IGGY_ERR_DEVICE;
-    hipStream_t s = c->stream;
-    // the chunk is copied (read in place over the host link, a registered 1 MiB chunk
-    // walked 98-103 us against 90-93 us copied, Verify, same box: k_chunk_walk's
-    // scattered reads pay a link round trip each)
-    r = put_host(c, c->din.p, chunk, len, s);
-    if (r) return r;
-    const uint8_t *d_chunk = c->din.as<uint8_t>();
-    std::vector<RecIn> rin(K);
-    for (uint64_t k = 0; k < K; ++k)
-        rin[k] = RecIn{cand[k].pos, len - cand[k].pos, cand[k].pbase, cand[k].bl ? (cand[k].bl - 256) / 48 + 1 : 0, 0};
-    iggy_decode_result *d_res = c->pres.as<iggy_decode_result>();
-    std::vector<size_t> single;
-    r = enqueue_records(c, d_chunk, chunk, rin.data(), K, integrity, c->dpos.as<uint64_t>(), nullptr,
-                        d_res, &single);
-    if (r) return r;
-    memcpy(c->cmap.h, cand.data(), cand_bytes);
-    uint8_t *pin_res = c->omap.hp<uint8_t>(64);
-    ChunkState *d_state = c->omap.dp<ChunkState>(64);
-    iggy_chunk_fragment *d_frags = c->omap.dp<iggy_chunk_fragment>(64 + 256);
-    uint8_t *d_hdrs = c->omap.dp<uint8_t>(64 + 256 + capk * sizeof(iggy_chunk_fragment));
-    ChunkLink *d_links = c->clinks.as<ChunkLink>();
-    if (++c->chunk_epoch == 0 || c->clinks.cap != links_cap_before) {  // new buffer or wrapped tags
-        if (c->chunk_epoch == 0) c->chunk_epoch = 1;
-        HIP_OK(hipMemsetAsync(c->clinks.p, 0, c->clinks.cap, s));
-    }
-    const uint32_t v = next_flag(c);
-    hipLaunchKernelGGL(k_chunk_walk, dim3((uint32_t)K), dim3(kChunkThreads), 0, s, d_chunk,
-                       c->cmap.dp<const ChunkCand>(), (uint32_t)K, (const iggy_decode_result *)d_res,
-                       (const uint64_t *)c->dpos.as<uint64_t>(), *q, c->chunk_epoch, d_links, d_state, d_frags,
-                       headers ? d_hdrs : nullptr, capk, c->sl.as<uint64_t>(), c->omap.dp<uint32_t>(), v);
-    HIP_OK(hipGetLastError());
-    r = wait_host_flag(c, v);
-    if (!r) r = xfer_settle(c);
-    if (r) return r;
-    ChunkState hs;
-    memcpy(&hs, pin_res, sizeof(hs));
-    if (hs.error.kind == IGGY_ERR_PENDING)  // a batch needs the general walk: the per-batch form
-        return walk_chunk_per_batch(c, chunk, len, q, integrity, frags, headers, cap, out);
-    if (hs.error.kind == IGGY_ERR_TIMEOUT) {  // a bug guard fired, not a verdict on the chunk
-        reset_after_timeout(c);
-        return IGGY_ERR_TIMEOUT;
-    }
-    const uint64_t nf = std::min<uint64_t>(hs.nfrag, capk);
-    if (nf) {
-        memcpy(frags, pin_res + 256, nf * sizeof(iggy_chunk_fragment));
-        if (headers) memcpy(headers, pin_res + 256 + capk * sizeof(iggy_chunk_fragment), nf * 256);
-    }
-    out->consumed = std::min<uint64_t>(hs.consumed, len);
-    out->corrupt = hs.corrupt;
-    out->matched = hs.matched;
-    out->last_matching_offset = hs.last_matching_offset;
-    out->has_last_matching_offset = (uint32_t)hs.has_last;
-    out->fragments = hs.nfrag;
-    out->error = hs.error;
-    out->batches = hs.batches;
-    return hs.nfrag > cap ? IGGY_ERR_CAPACITY : 0;
-}
-
-int iggy_codec_select_slice(iggy_codec_ctx *c, const uint8_t *record, uint64_t len, const iggy_slice_query *q,
-                            iggy_slice_result *out, uint8_t *header_out, iggy_wire_error *err) {
-    if (!c || !q || !out || (!record && len)) return IGGY_ERR_INVALID_ARGUMENT;
-    DevGuard dg(c->device);
-    bind(c, nullptr);
-    set_err(err, IGGY_OK);
-    const uint64_t cap = len / kFrameHdr + 1;
-    int r = c->din.ensure(len + 16);
-    r |= c->dpos.ensure((cap + 1) * 8);
-    r |= c->slres.ensure(512);
-    if (r) return IGGY_ERR_DEVICE;
-    r = put_host(c, c->din.p, record, len, c->stream);
-    if (r) return r;
-    // the reference selects on a decoded batch: decode it (layout) first
-    iggy_decode_result *d_res = c->dresult.as<iggy_decode_result>();
-    r = enqueue_decode(c, c->din.as<uint8_t>(), len, IGGY_INTEGRITY_LAYOUT_ONLY, c->dpos.as<uint64_t>(), cap, d_res,
-                       c->stream);
-    if (r) return r;
-    iggy_decode_result *h_res = (iggy_decode_result *)c->h_pinned;
-    HIP_OK(hipMemcpyAsync(h_res, d_res, sizeof(*h_res), hipMemcpyDeviceToHost, c->stream));
-    HIP_OK(hipStreamSynchronize(c->stream));
-    const iggy_decode_result res = *h_res;
-    if (res.error.kind == IGGY_ERR_TIMEOUT) reset_after_timeout(c);
-    if (res.error.kind != IGGY_OK) {
-        fill_err(err, res.error);
-        return (int)res.error.kind;
-    }
-    iggy_slice_result *d_out = c->slres.as<iggy_slice_result>(0);
-    uint8_t *d_hdr = c->slres.as<uint8_t>(256);
-    r = iggy_codec_select_slice_device(c, c->din.as<uint8_t>(), c->dpos.as<uint64_t>(), res.frame_count, q, d_out,
-                                       d_hdr, c->stream);
-    if (r) return r;
-    uint8_t *h = (uint8_t *)c->h_pinned + 1024;
-    HIP_OK(hipMemcpyAsync(h, d_out, 512, hipMemcpyDeviceToHost, c->stream));
-    HIP_OK(hipStreamSynchronize(c->stream));
-    memcpy(out, h, sizeof(*out));
-    if (header_out && out->selected) memcpy(header_out, h + 256, 256);
-    return 0;
-}
-
-int iggy_codec_stamp_batch_device(iggy_codec_ctx *c, uint8_t *d_record, const uint64_t *d_frame_pos,
-                                  uint64_t nframes, uint64_t base_offset, uint64_t base_timestamp,
-                                  iggy_batch_header *d_header, void *stream) {
-    if (!c || !d_record || (nframes && !d_frame_pos)) return IGGY_ERR_INVALID_ARGUMENT;
-    DevGuard dg(c->device);
-    hipStream_t s = bind(c, stream);
-    int r = c->sl.ensure(512 + 4);
-    r |= c->gbsums.ensure(((44 + 8 * nframes) / 1024 + 2) * 64);
-    if (r) return IGGY_ERR_DEVICE;
-    iggy_batch_header *dh = c->sl.as<iggy_batch_header>(64);
-    uint64_t *dn = c->sl.as<uint64_t>(8), *dcs = c->sl.as<uint64_t>(24);
-    hipLaunchKernelGGL(k_stamp_prep, dim3(1), dim3(64), 0, s, (const uint8_t *)d_record, base_offset, base_timestamp,
-                       nframes, dh, dn);
-    CsSource src{nullptr, d_record + kHdr, d_frame_pos};
-    hipLaunchKernelGGL(k_bsum_blocks, dim3(bsum_grid(c, nframes)), dim3(256), 0, s, (const iggy_batch_header *)dh,
-                       (const uint64_t *)dn, src, c->gbsums.as<uint64_t>(), nullptr);
-    hipLaunchKernelGGL(k_bsum_chain, dim3(1), dim3(128), 0, s, (const iggy_batch_header *)dh, (const uint64_t *)dn,
-                       src, (const uint64_t *)c->gbsums.as<uint64_t>(), c->sl.as<uint8_t>(128), dcs, nullptr);
-    hipLaunchKernelGGL(k_stamp_finish, dim3(1), dim3(64), 0, s, d_record, (const iggy_batch_header *)dh,
-                       (const uint64_t *)dcs, d_header);
-    HIP_OK(hipGetLastError());
-    return 0;
-}
-
-// ------------------------------------------------ asynchronous host buffers
-// Shard threads have no blocking pool (server_common/src/executor.rs:80-88): a
-// host-buffer decode/encode is submitted (async H2D into a device slot on the copy-in
-// stream, the kernels on the context's stream, results and outputs back on the
-// copy-out stream) and its ticket polled from the reactor. Kernels only ever read
-// device memory; a caller buffer registered with iggy_codec_host_register is copied
-// at link speed without a bounce.
-namespace {
-int async_init(iggy_codec_ctx *c) {
-    if (c->h2d) return 0;
-    if (hipStreamCreateWithFlags(&c->h2d, hipStreamNonBlocking) != hipSuccess ||
-        hipStreamCreateWithFlags(&c->d2h, hipStreamNonBlocking) != hipSuccess ||
-        hipHostMalloc(&c->slot_pinned, kSlots * 256, hipHostMallocDefault) != hipSuccess)
-        return IGGY_ERR_DEVICE;
-    {
-        void *dp = nullptr;
-        if (hipHostGetDevicePointer(&dp, c->slot_pinned, 0) != hipSuccess) {
-            (void)hipGetLastError();
-            dp = nullptr;
-        }
-        c->slot_pinned_d = (uint8_t *)dp;
-    }
-    for (Slot &sl : c->slots)
-        if (hipEventCreateWithFlags(&sl.ev_in, hipEventDisableTiming) != hipSuccess ||
-            hipEventCreateWithFlags(&sl.ev_k, hipEventDisableTiming) != hipSuccess ||
-            hipEventCreateWithFlags(&sl.ev_done, hipEventDisableTiming) != hipSuccess)
-            return IGGY_ERR_DEVICE;
-    return 0;
-}
-int take_slot(iggy_codec_ctx *c, uint32_t op, int *idx) {
-    int r = async_init(c);
-    if (r) return r;
-    for (int k = 0; k < kSlots; ++k)
-        if (!c->slots[k].busy) {
-            Slot &sl = c->slots[k];
-            sl.busy = true;
-            sl.op = op;
-            sl.ticket = (++c->seq << 4) | (uint64_t)k;
-            *idx = k;
-            return 0;
-        }
-    return IGGY_ERR_BUSY;
-}
-}  // namespace
-
-int iggy_codec_host_register(iggy_codec_ctx *c, void *ptr, uint64_t len) {
-    if (!c || !ptr || !len) return IGGY_ERR_INVALID_ARGUMENT;
-    DevGuard dg(c->device);
-    HIP_OK(hipHostRegister(ptr, len, hipHostRegisterDefault));
-    void *dp = nullptr;
-    if (hipHostGetDevicePointer(&dp, ptr, 0) != hipSuccess) {
-        (void)hipGetLastError();
-        dp = nullptr;
-    }
-    hostmem_log("register", ptr, len);
-    std::lock_guard<std::mutex> lk(g_reg_mu);
-    for (const auto &r : g_reg)  // (the runtime accepted it, so any overlap is a stale entry)
-        if ((uintptr_t)ptr < r.h + r.len && r.h < (uintptr_t)ptr + len)
-            hostmem_log("register overlaps a registry entry", (const void *)r.h, r.len);
-    g_reg.push_back(RegRange{(uintptr_t)ptr, len, (uintptr_t)dp, c->device, c});
-    return 0;
-}
-
-int iggy_codec_host_unregister(iggy_codec_ctx *c, void *ptr) {
-    if (!c || !ptr) return IGGY_ERR_INVALID_ARGUMENT;
-    DevGuard dg(c->device);
-    uint64_t len = 0;
-    {
-        std::lock_guard<std::mutex> lk(g_reg_mu);
-        for (size_t i = 0; i < g_reg.size(); ++i)
-            if (g_reg[i].h == (uintptr_t)ptr) {
-                len = g_reg[i].len;
-                g_reg.erase(g_reg.begin() + (long)i);
-                break;
-            }
-    }
-    hostmem_log("unregister", ptr, len);
-    HIP_OK(hipHostUnregister(ptr));
-    return 0;
-}
-
-int iggy_codec_host_pinned(const void *ptr, uint64_t len) { return host_pinned(ptr, len) ? 1 : 0; }
-
-int iggy_codec_decode_submit(iggy_codec_ctx *c, const uint8_t *body, uint64_t len, int integrity,
-                             uint64_t *frame_pos, uint64_t cap, iggy_ticket *ticket) {
-    if (!c || !ticket || (!body && len)) return IGGY_ERR_INVALID_ARGUMENT;
-    DevGuard dg(c->device);
-    int k = 0;
-    int r = take_slot(c, IGGY_OP_DECODE, &k);
-    if (r) return r;
-    Slot &sl = c->slots[k];
-    const uint64_t pcap = frame_pos ? std::min<uint64_t>(cap, len / 48 + 1) : 0;
-    r = sl.in.ensure(len + 16);
-    r |= sl.pos.ensure((pcap + 1) * 8);
-    r |= sl.res.ensure(256);
-    if (!r) r = ensure_decode_scratch(c, len);
-    if (r) {
-        sl.busy = false;
-        return IGGY_ERR_DEVICE;
-    }
-    sl.cap = cap;
-    sl.frame_pos = frame_pos;
-    sl.hout_dst = nullptr;
-    sl.hout_len = 0;
-    const bool pos_pinned = host_pinned(frame_pos, pcap * 8);
-    if (pcap && !pos_pinned && sl.hout_ensure(pcap * 8)) r = IGGY_ERR_DEVICE;
-    uint64_t nf = 0;
-    if (!r && c->slot_pinned_d && len <= kHostFastBytes && rec_plan(body, len, &nf)) {
-        // a single-stride record of <= 16 MiB, on the slot's own stream with the slot's
-        // own k_decode_records scratch (so the slots' launches overlap): the input
-        // (read in place when <= kZeroCopyBytes, else copied), one launch whose verdict
-        // lands in the slot's host-mapped completion record, the positions back, the
-        // completion event; k_decode_general, for a stride that breaks mid-record, is
-        // started by iggy_codec_poll on the context's stream
-        if (!sl.st && hipStreamCreateWithFlags(&sl.st, hipStreamNonBlocking) != hipSuccess) {
-            sl.st = nullptr;
-            sl.busy = false;
-            return IGGY_ERR_DEVICE;
-        }
-        hipStream_t s = sl.st;
-        const uint8_t *d_in = len <= kZeroCopyBytes ? host_device_ptr(body, len) : nullptr;
-        if (!d_in && !host_pinned(body, len)) {
-            // pageable: copied into the slot's own pinned staging now (the caller's bytes
-            // are free when submit returns), then read in place or DMA'd from there; the
-            // slot holds the staging until the ticket completes, so nothing here waits
-            if (sl.zin.ensure(len + 16)) {
-                r = IGGY_ERR_DEVICE;
-            } else {
-                memcpy(sl.zin.h, body, len);
-                if (len <= kZeroCopyBytes) {
-                    d_in = sl.zin.d;
-                } else {
-                    if (hipMemcpyAsync(sl.in.p, sl.zin.h, len, hipMemcpyHostToDevice, s) != hipSuccess)
-                        r = IGGY_ERR_DEVICE;
-                    d_in = sl.in.as<uint8_t>();
-                }
-            }
-        }
-        if (!d_in && !r) {  // pinned caller memory above kZeroCopyBytes: one DMA, no wait
-            r = put_host(c, sl.in.p, body, len, s);
-            d_in = sl.in.as<uint8_t>();
-        }
-        iggy_decode_result *d_res = (iggy_decode_result *)(c->slot_pinned_d + 256 * k);
-        // positions straight into host memory the device can write: the caller's pinned
-        // array, else the slot's pinned bounce (copied out in iggy_codec_poll); a device
-        // buffer and a D2H copy only when neither is mapped
-        uint64_t *d_pos = nullptr;
-        bool pos_copy = false;
-        if (pcap) {
-            if (pos_pinned) d_pos = (uint64_t *)host_device_ptr(frame_pos, pcap * 8);
-            if (!d_pos && !pos_pinned) {
-                void *dp = nullptr;
-                if (hipHostGetDevicePointer(&dp, sl.hout, 0) == hipSuccess && dp) d_pos = (uint64_t *)dp;
-                else (void)hipGetLastError();
-                if (d_pos) sl.hout_dst = (uint8_t *)frame_pos;
-            }
-            if (!d_pos) {
-                d_pos = sl.pos.as<uint64_t>();
-                pos_copy = true;
-            }
-        }
-        std::vector<size_t> single;
-        const RecIn rec{0, len, 0, pcap, 0};
-        if (!r) {
-            // a stride break mid-record is left to iggy_codec_poll (k_decode_general)
-            r = enqueue_records(c, d_in, body, &rec, 1, integrity, d_pos, nullptr, d_res, &single, nullptr, nullptr,
-                                0, &sl.tab, GenRearm{nullptr, nullptr, nullptr}, &sl);
-        }
-        if (!r && hipGetLastError() != hipSuccess) r = IGGY_ERR_DEVICE;
-        if (!r && pos_copy) {
-            if (!pos_pinned) sl.hout_dst = (uint8_t *)frame_pos;
-            if (hipMemcpyAsync(pos_pinned ? (void *)frame_pos : sl.hout, sl.pos.p, pcap * 8, hipMemcpyDeviceToHost,
-                               s) != hipSuccess)
-                r = IGGY_ERR_DEVICE;
-        }
-        sl.fast = true;
-        sl.g_pending = false;
-        sl.g_in = d_in;
-        sl.g_len = len;
-        sl.g_pcap = pcap;
-        sl.g_pos = d_pos;
-        sl.g_integ = integrity;
-        sl.g_pos_copy = pos_copy;
-        if (!r && hipEventRecord(sl.ev_done, s) != hipSuccess) r = IGGY_ERR_DEVICE;
-        if (r) {
-            sl.busy = false;
-            return r;
-        }
-        *ticket = sl.ticket;
-        return 0;
-    }
-    sl.fast = false;
-    if (!r) r = put_host(c, sl.in.p, body, len, c->h2d);
-    if (r) {
-        sl.busy = false;
-        return r;
-    }
-    HIP_OK(hipEventRecord(sl.ev_in, c->h2d));
-    hipStream_t s = bind(c, nullptr);
-    HIP_OK(hipStreamWaitEvent(s, sl.ev_in, 0));
-    iggy_decode_result *d_res = sl.res.as<iggy_decode_result>();
-    r = enqueue_decode(c, sl.in.as<uint8_t>(), len, integrity, pcap ? sl.pos.as<uint64_t>() : nullptr, pcap, d_res, s);
-    if (r) {
-        sl.busy = false;
-        return r;
-    }
-    HIP_OK(hipEventRecord(sl.ev_k, s));
-    HIP_OK(hipStreamWaitEvent(c->d2h, sl.ev_k, 0));
-    HIP_OK(hipMemcpyAsync((uint8_t *)c->slot_pinned + 256 * k, d_res, sizeof(iggy_decode_result),
-                          hipMemcpyDeviceToHost, c->d2h));
-    // positions: straight into pinned caller memory; a pageable array gets them from the
-    // slot's pinned bounce in iggy_codec_poll (and only when the decode succeeded)
-    if (pcap) {
-        if (!pos_pinned) sl.hout_dst = (uint8_t *)frame_pos;
-        HIP_OK(hipMemcpyAsync(pos_pinned ? (void *)frame_pos : sl.hout, sl.pos.p, pcap * 8, hipMemcpyDeviceToHost,
-                              c->d2h));
-    }
-    HIP_OK(hipEventRecord(sl.ev_done, c->d2h));
-    *ticket = sl.ticket;
-    return 0;
-}
-
-int iggy_codec_encode_submit(iggy_codec_ctx *c, const iggy_raw_messages *m, uint64_t partition_id, uint8_t *out,
-                             uint64_t cap, iggy_ticket *ticket) {
-    if (!c || !m || !ticket) return IGGY_ERR_INVALID_ARGUMENT;
-    if (m->count == 0 || m->count > 0xFFFFFFFFull || !out) return IGGY_ERR_INVALID_ARGUMENT;
-    DevGuard dg(c->device);
-    const uint64_t n = m->count;
-    uint64_t spl = 0, suh = 0;
-    for (uint64_t i = 0; i < n; ++i) {
-        spl += m->payload_lengths[i];
-        suh += m->user_headers_lengths ? m->user_headers_lengths[i] : 0;
-    }
-    const uint64_t need = 256 + 48 * n + spl + suh;
-    int k = 0;
-    int r = take_slot(c, IGGY_OP_ENCODE, &k);
-    if (r) return r;
-    Slot &sl = c->slots[k];
-    const bool has_uh = m->user_headers_lengths != nullptr;
-    r = sl.ids.ensure(n * 16);
-    r |= sl.ots.ensure(n * 8);
-    r |= sl.pay.ensure(spl + 16);
-    r |= sl.plen.ensure(n * 4);
-    r |= sl.uhb.ensure(suh + 16);
-    r |= sl.uhl.ensure(n * 4);
-    r |= sl.out.ensure(need + 16);
-    r |= sl.res.ensure(256);
-    if (r) {
-        sl.busy = false;
-        return IGGY_ERR_DEVICE;
-    }
-    sl.cap = cap;
-    sl.out_len = need;
-    sl.fast = false;
-    sl.frame_pos = nullptr;
-    sl.hout_dst = nullptr;
-    sl.hout_len = 0;
-    const bool out_pinned = host_pinned(out, need);
-    if (cap >= need && !out_pinned && sl.hout_ensure(need)) r = IGGY_ERR_DEVICE;
-    // Small batches (SoA input of <= kZeroCopyBytes, one segment) in place: the kernels
-    // read the SoA arrays over the host link (registered ones where they are, anything
-    // else copied with one memcpy per array into the slot's mapped staging, so the
-    // caller's bytes are free when submit returns) and write the wire bytes and the
-    // verdict straight into mapped host memory (the caller's pinned `out`, else the
-    // slot's bounce). No copy operation on any stream; the kernels on the slot's own
-    // stream with the slot's own scratch, so the slots' encodes run side by side.
-    const uint64_t in_bytes = n * 28 + spl + (has_uh ? suh + n * 4 : 0);
-    if (!r && c->slot_pinned_d && cap >= need && in_bytes <= kZeroCopyBytes && n < kEncSegMinFrames) {
-        iggy_raw_messages dm;
-        if (stage_soa(m, n, spl, suh, sl.zin, &dm)) {
-            sl.busy = false;
-            return IGGY_ERR_DEVICE;
-        }
-        uint8_t *d_out = out_pinned ? (uint8_t *)host_device_ptr(out, need) : nullptr;
-        if (!d_out) {
-            void *dp = nullptr;
-            if (out_pinned || !sl.hout || hipHostGetDevicePointer(&dp, sl.hout, 0) != hipSuccess || !dp) {
-                (void)hipGetLastError();
-                dp = nullptr;
-            }
-            d_out = (uint8_t *)dp;
-            if (d_out) sl.hout_dst = out;
-        }
-        if (d_out) {
-            if (!sl.st && hipStreamCreateWithFlags(&sl.st, hipStreamNonBlocking) != hipSuccess) {
-                sl.st = nullptr;
-                sl.busy = false;
-                return IGGY_ERR_DEVICE;
-            }
-            iggy_encode_result *d_res = (iggy_encode_result *)(c->slot_pinned_d + 256 * k);
-            r = enqueue_encode(c, &dm, partition_id, d_out, cap, d_res, sl.st, &sl.eown);
-            if (!r && hipEventRecord(sl.ev_done, sl.st) != hipSuccess) r = IGGY_ERR_DEVICE;
-            if (r) {
-                sl.busy = false;
-                return r;
-            }
-            *ticket = sl.ticket;
-            return 0;
-        }
-        sl.hout_dst = nullptr;  // (no mapped destination: the copy path below)
-    }
-    hipStream_t h = c->h2d;
-    if (!r) {
-        r |= put_host(c, sl.ids.p, m->ids, n * 16, h);
-        r |= put_host(c, sl.ots.p, m->origin_timestamps, n * 8, h);
-        r |= put_host(c, sl.pay.p, m->payloads, spl, h);
-        r |= put_host(c, sl.plen.p, m->payload_lengths, n * 4, h);
-        if (has_uh) {
-            r |= put_host(c, sl.uhb.p, m->user_headers, suh, h);
-            r |= put_host(c, sl.uhl.p, m->user_headers_lengths, n * 4, h);
-        }
-    }
-    if (r) {
-        sl.busy = false;
-        return IGGY_ERR_DEVICE;
-    }
-    HIP_OK(hipEventRecord(sl.ev_in, h));
-    hipStream_t s = bind(c, nullptr);
-    HIP_OK(hipStreamWaitEvent(s, sl.ev_in, 0));
-    iggy_raw_messages dm;
-    dm.count = n;
-    dm.ids = sl.ids.as<uint64_t>();
-    dm.origin_timestamps = sl.ots.as<uint64_t>();
-    dm.payloads = sl.pay.as<uint8_t>();
-    dm.payload_lengths = sl.plen.as<uint32_t>();
-    dm.user_headers = has_uh ? sl.uhb.as<uint8_t>() : nullptr;
-    dm.user_headers_lengths = has_uh ? sl.uhl.as<uint32_t>() : nullptr;
-    iggy_encode_result *d_res = sl.res.as<iggy_encode_result>();
-    // a batch that does not fit `cap` is reported by the device (nothing is written)
-    r = enqueue_encode(c, &dm, partition_id, sl.out.as<uint8_t>(), cap, d_res, s);
-    if (r) {
-        sl.busy = false;
-        return r;
-    }
-    HIP_OK(hipEventRecord(sl.ev_k, s));
-    HIP_OK(hipStreamWaitEvent(c->d2h, sl.ev_k, 0));
-    HIP_OK(hipMemcpyAsync((uint8_t *)c->slot_pinned + 256 * k, d_res, sizeof(iggy_encode_result),
-                          hipMemcpyDeviceToHost, c->d2h));
-    if (cap >= need) {  // (a pageable `out` from the slot's pinned bounce, in iggy_codec_poll)
-        if (!out_pinned) sl.hout_dst = out;
-        HIP_OK(hipMemcpyAsync(out_pinned ? (void *)out : sl.hout, sl.out.p, need, hipMemcpyDeviceToHost, c->d2h));
-    }
-    HIP_OK(hipEventRecord(sl.ev_done, c->d2h));
-    *ticket = sl.ticket;
-    return 0;
-}
-
-int iggy_codec_poll(iggy_codec_ctx *c, iggy_ticket ticket, iggy_completion *out) {
-    if (!c || !out) return IGGY_ERR_INVALID_ARGUMENT;
-    Slot &sl = c->slots[ticket & (kSlots - 1)];
-    if (!sl.busy || sl.ticket != ticket) return IGGY_ERR_INVALID_ARGUMENT;
-    DevGuard dg(c->device);
-    const hipError_t q = hipEventQuery(sl.ev_done);
-    if (q == hipErrorNotReady) {
-        (void)hipGetLastError();  // not an error: leave no sticky status for the caller's HIP code
-        return IGGY_ERR_PENDING;
-    }
-    if (q == hipSuccess && sl.op == IGGY_OP_DECODE && sl.fast && !sl.g_pending) {
-        // the records launch found a stride break the walk goes past: the general walk
-        // (its barrier words re-armed first), the positions, the completion event again
-        const size_t k = ticket & (kSlots - 1);
-        const iggy_decode_result *rr = (const iggy_decode_result *)((const uint8_t *)c->slot_pinned + 256 * k);
-        if (rr->status == kStatusNeedGeneral) {
-            hipStream_t s = bind(c, nullptr);
-            const DecodeScratch dsc = dscratch(c);
-            iggy_decode_result *d_res = (iggy_decode_result *)(c->slot_pinned_d + 256 * k);
-            // each operation checked where it is issued: the thread's last-error status is
-            // cleared first, so a launch failure is this launch's and not an unrelated
-            // earlier error of the caller's own HIP code
-            (void)hipGetLastError();
-            hipError_t e = hipSuccess;
-            hipLaunchKernelGGL(k_general_rearm, dim3(1), dim3(64), 0, s, GenRearm{dsc.gbar, dsc.gbar2, dsc.gmisc});
-            e = hipGetLastError();
-            if (e == hipSuccess) {
-                launch_general(c, sl.g_in, sl.g_len, sl.g_integ, sl.g_pos, sl.g_pcap, d_res, s);
-                e = hipGetLastError();
-            }
-            if (e == hipSuccess && sl.g_pos_copy)
-                e = hipMemcpyAsync(host_pinned(sl.frame_pos, sl.g_pcap * 8) ? (void *)sl.frame_pos : sl.hout,
-                                   sl.pos.p, sl.g_pcap * 8, hipMemcpyDeviceToHost, s);
-            if (e == hipSuccess) e = hipEventRecord(sl.ev_done, s);
-            sl.g_pending = true;
-            if (e != hipSuccess) {
-                // whatever was issued may still use the slot's buffers and the caller's
-                // memory: drain the stream before the slot is free again
-                (void)hipGetLastError();
-                (void)hipStreamSynchronize(s);
-                sl.busy = false;
-                return IGGY_ERR_DEVICE;
-            }
-            return IGGY_ERR_PENDING;
-        }
-    }
-    sl.busy = false;
-    if (q != hipSuccess) return IGGY_ERR_DEVICE;
-    memset(out, 0, sizeof(*out));
-    out->op = sl.op;
-    const uint8_t *rec = (const uint8_t *)c->slot_pinned + 256 * (ticket & (kSlots - 1));
-    if (sl.op == IGGY_OP_DECODE) {
-        iggy_decode_result res;
-        memcpy(&res, rec, sizeof(res));
-        if (res.error.kind == IGGY_ERR_TIMEOUT) reset_after_timeout(c);
-        out->header = res.header;
-        out->error = res.error;
-        out->frame_count = res.frame_count;
-        out->computed_checksum = res.computed_checksum;
-        if (res.error.kind == IGGY_OK && sl.frame_pos && res.frame_count > sl.cap) {
-            out->error = iggy_wire_error{IGGY_ERR_CAPACITY, 0, res.frame_count, sl.cap, 0};
-        } else if (res.error.kind == IGGY_OK && sl.hout_dst && res.frame_count) {
-            memcpy(sl.hout_dst, sl.hout, std::min<uint64_t>(res.frame_count, sl.cap) * 8);
-        }
-    } else {
-        iggy_encode_result res;
-        memcpy(&res, rec, sizeof(res));
-        out->header = res.header;
-        out->error = res.error;
-        out->bytes = res.error.kind == IGGY_OK ? res.batch_length : 0;
-        if (res.error.kind == IGGY_OK && sl.hout_dst) memcpy(sl.hout_dst, sl.hout, sl.out_len);
-    }
-    return 0;
-}
-
-int iggy_codec_wait(iggy_codec_ctx *c, iggy_ticket ticket, iggy_completion *out) {
-    if (!c || !out) return IGGY_ERR_INVALID_ARGUMENT;
-    Slot &sl = c->slots[ticket & (kSlots - 1)];
-    if (!sl.busy || sl.ticket != ticket) return IGGY_ERR_INVALID_ARGUMENT;
-    while (true) {  // (a fast-path decode's general walk, started by poll, means one more round)
-        {
-            DevGuard dg(c->device);
-            HIP_OK(hipEventSynchronize(sl.ev_done));
-        }
-        const int r = iggy_codec_poll(c, ticket, out);
-        if (r != IGGY_ERR_PENDING) return r;
-    }
-}
 
 // -------------------------------------------------------------- profiling
 int iggy_codec_host_stats(iggy_codec_ctx *c, iggy_host_stats *out) {

@@ -5,7 +5,7 @@ Plumbing for the Python callers of the codec that move their own buffers with to
 locking the caller's range on the fly (ROCclr, transfers above GPU_PINNED_MIN_XFER_SIZE).
 On this pool that path faulted (hipErrorIllegalAddress inside a pageable copy) in rounds
 3-5, once inside torch's own `.to("cuda")` with no codec call since the last stream
-synchronisation. The codec never uses that path (codec_api.hip put_host /
+synchronisation. The codec never uses that path (host_mem.hpp put_host /
 get_host stage pageable bytes through its own pinned chunks); these helpers keep the
 callers' own copies off it too: a host memcpy into torch's pinned (hipHostMalloc) cache,
 then a DMA from page-locked memory.

@@ -587,7 +587,14 @@ typedef struct iggy_completion {
     uint64_t _pad1[3];
 } iggy_completion;
 
-/* Page-lock a caller buffer for the context's device (hipHostRegister) / undo it. */
+/* Page-lock a caller buffer for the context's device (hipHostRegister) / undo it.
+ * The pages a registration touches ([ptr & ~4095, ptr + len rounded up to 4096)) must
+ * not meet those of another live registration (IGGY_ERR_INVALID_ARGUMENT otherwise):
+ * the runtime pins whole pages, and two registrations over one page leave a dead
+ * mapping behind when either is undone. Register page-aligned buffers (the server's
+ * 4096-aligned Owned<MESSAGE_ALIGN> pool). Unregister only through the codec (never a
+ * bare hipHostUnregister); ranges a context registered are unregistered when it is
+ * destroyed. */
 int iggy_codec_host_register(iggy_codec_ctx *ctx, void *ptr, uint64_t len);
 int iggy_codec_host_unregister(iggy_codec_ctx *ctx, void *ptr);
 /* 1 when every host entry point copies [ptr, ptr + len) by DMA directly (pinned:

@@ -19,7 +19,7 @@ import torch  # noqa: E402,F401  (the HIP runtime the codec shares)
 from iggy_amd import codec as _codec  # noqa: E402
 if os.environ.get("IGGY_LIB"):  # a library build to compare (same-box A/B)
     _codec.use_library(os.environ["IGGY_LIB"])
-from iggy_amd.codec import Codec, raw_messages  # noqa: E402
+from iggy_amd.codec import Codec, host_buffer, page_aligned, raw_messages  # noqa: E402
 from oracle import oracle as O  # noqa: E402  (the CPU leg and the check)
 
 
@@ -32,13 +32,14 @@ def main():
         ots = (1_700_000_000_000_000 + b * n + np.arange(n)).astype(np.uint64)
         pay = rng.integers(0, 256, size=n * pl, dtype=np.uint8)
         pls = np.full(n, pl, dtype=np.uint32)
+        ids, ots, pay, pls = (page_aligned(a) for a in (ids, ots, pay, pls))
         soas.append((ids, ots, pay, pls))
         raws.append(raw_messages(ids, ots, pay, pls))
         rc, e, out = O.encode_batch(raws[-1], 0)
         assert rc == 0
         wants.append(np.frombuffer(out, dtype=np.uint8))
     size = wants[0].size
-    outs = [np.zeros(size, dtype=np.uint8) for _ in range(nb)]
+    outs = [host_buffer(size) for _ in range(nb)]  # (registrations may not share a page)
     cx = Codec(0)
 
     def run(reps):

@@ -12,12 +12,13 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from iggy_amd import abi  # noqa: E402
 from iggy_amd import codec as _codec  # noqa: E402
 _codec.use_library(os.environ.get("IGGY_DIAG_LIB", _codec.DIAG_LIB_PATH))
-from iggy_amd.codec import Codec  # noqa: E402
+from iggy_amd.codec import Codec, host_buffer, page_aligned  # noqa: E402
 from oracle import oracle as O  # noqa: E402
 
 
 def run(cx, rec, label, reg):
-    pos = np.zeros(rec.size // 48 + 1, dtype=np.uint64)
+    rec = page_aligned(rec)  # (registrations may not share a page)
+    pos = host_buffer(rec.size // 48 + 1, np.uint64)
     if reg:
         cx.host_register(rec)
         cx.host_register(pos)

@@ -22,7 +22,7 @@ sys.path.insert(0, ROOT)
 from iggy_amd import codec as _codec  # noqa: E402
 if os.environ.get("IGGY_LIB"):  # a library build to compare (same-box A/B)
     _codec.use_library(os.environ["IGGY_LIB"])
-from iggy_amd.codec import Codec  # noqa: E402
+from iggy_amd.codec import Codec, host_buffer, page_aligned  # noqa: E402
 from oracle import oracle as O  # noqa: E402  (the CPU leg)
 
 
@@ -36,8 +36,8 @@ def main():
     rows = []
     for kib in (64, 256, 1024, 2048, 4096, 16384, 65536):
         n = max(1, kib * 1024 // 1072)
-        rec = O.synth_batch(n, 1024, 1024, seed=kib)
-        pos = np.zeros(rec.size // 48 + 1, dtype=np.uint64)
+        rec = page_aligned(O.synth_batch(n, 1024, 1024, seed=kib))  # (registrations may not share a page)
+        pos = host_buffer(rec.size // 48 + 1, np.uint64)
         if args.registered:
             cx.host_register(rec)
             cx.host_register(pos)

@@ -11,7 +11,7 @@ if ROOT not in sys.path:
 # environment is dropped before anything initialises the runtime.
 os.environ.pop("GPU_PINNED_MIN_XFER_SIZE", None)
 
-# Host-memory history of this test process (codec_api.hip hostmem_log): every range the
+# Host-memory history of this test process (iggy_amd/csrc/host_ctx.hpp hostmem_log): every range the
 # codec registers, maps or pins, and its release, with test boundaries between; the tail
 # is attached to a failing test's report, so a fault can be checked against earlier
 # pinned or mapped ranges without running anything again.

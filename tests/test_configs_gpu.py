@@ -53,12 +53,13 @@ def _stream_encode_decode(cx, batches, in_flight):
     """Encode each SoA batch (encode_submit) into a registered wire buffer, then decode
     the wire bytes (decode_submit) into registered position buffers, `in_flight`
     batches deep; -> [(wire bytes, completion of the decode, positions)]."""
+    from iggy_amd.codec import host_buffer
     outs = []
     for m in batches:
         n = len(m["pls"])
         need = 256 + 48 * n + int(m["pls"].sum())
-        wire = np.zeros(need, dtype=np.uint8)
-        pos = np.zeros(n, dtype=np.uint64)
+        wire = host_buffer(need)  # (registrations may not share a page)
+        pos = host_buffer(n, np.uint64)
         outs.append((wire, pos))
     for wire, pos in outs:
         cx.host_register(wire)

@@ -12,7 +12,7 @@ import numpy as np
 import pytest
 
 from iggy_amd import abi
-from iggy_amd.codec import frame_read, raw_messages
+from iggy_amd.codec import frame_read, page_aligned, raw_messages
 from oracle import oracle as O
 from oracle import sdk_ref as S
 
@@ -92,6 +92,7 @@ def test_socket_frame_to_admitted_batch(cx):
         for f in frames:
             rc, e, buf = frame_read(b.fileno(), 8 << 20)
             assert rc == 0 and buf.tobytes() == f
+            buf = page_aligned(buf)  # (registrations may not share a page)
             cx.host_register(buf)
             try:
                 rc, e, h, out = cx.convert_request(buf, 5, 0)

@@ -10,7 +10,7 @@ import pytest
 
 from crypt_util import frame_sections, key_for, nonces_for, raw_record
 from iggy_amd import abi
-from iggy_amd.torch_io import to_device, to_host
+from iggy_amd.torch_io import to_host
 from oracle import oracle as O
 
 pytestmark = pytest.mark.gpu
@@ -25,8 +25,11 @@ def cx():
 
 
 def _dev(a):
+    """A plain pageable torch copy, on purpose: the module where round 5's fault surfaced
+    runs the runtime's pageable path again, now that the suite's registrations no longer
+    share pages; the other modules copy through pinned staging."""
     import torch
-    return to_device(a)
+    return torch.from_numpy(np.ascontiguousarray(a)).to("cuda")
 
 
 def _run(cx, enc: bool, key, rec, nonces=None, cap=None, length=None):

@@ -35,9 +35,10 @@ def test_runtime_defaults_in_this_process():
 
 def test_host_pinned_classification(cx):
     import torch
+    from iggy_amd.codec import host_buffer
     a = np.zeros(1 << 20, dtype=np.uint8)
     assert not cx.host_pinned(a.ctypes.data, a.size)
-    b = np.zeros(3 << 20, dtype=np.uint8)
+    b = host_buffer(3 << 20)
     cx.host_register(b)
     try:
         assert cx.host_pinned(b.ctypes.data, b.size)
@@ -117,6 +118,7 @@ def test_registered_record_read_in_place(cx):
     host-mapped bytes, no H2D): same verdicts as the oracle, at the start of the
     registered range and at an interior, unaligned offset, clean and corrupted, and a
     larger registered record (copied as before)."""
+    from iggy_amd.codec import host_buffer
     recs = [O.synth_batch(1000, 256, seed=31), O.synth_batch(700, 100, 900, seed=32),
             O.synth_batch(1500, 1024, seed=33),  # 1.6 MB: in place
             O.synth_batch(5000, 1024, seed=34)]  # 5.4 MB: above the in-place limit, copied
@@ -126,9 +128,9 @@ def test_registered_record_read_in_place(cx):
     for rec in recs:
         want = O.decode_batch_slice_with(rec, 0)
         for off in (0, 4099):
-            buf = np.zeros(off + rec.size + 64, dtype=np.uint8)
+            buf = host_buffer(off + rec.size + 64)
             buf[off:off + rec.size] = rec
-            pos = np.zeros(rec.size // 48 + 1, dtype=np.uint64)
+            pos = host_buffer(rec.size // 48 + 1, np.uint64)
             cx.host_register(buf)
             cx.host_register(pos)
             try:
@@ -169,9 +171,11 @@ def test_submit_single_stride_fast_path(cx, registered):
     clean = O.synth_batch(1000, 256, seed=43)
     bad = clean.copy()
     bad[256 + 304 * 700 + 100] ^= 1
+    from iggy_amd.codec import host_buffer, page_aligned
     recs = [clean, bad, _stride_break_record(), O.synth_batch(3000, 1000, seed=44),  # 3.1 MB: in place
             O.synth_batch(5000, 1000, seed=45)]  # 5.2 MB: copied (pageable: from the slot's staging)
-    poss = [np.zeros(r.size // 48 + 1, dtype=np.uint64) for r in recs]
+    recs = [page_aligned(r) for r in recs]  # (registrations may not share a page)
+    poss = [host_buffer(r.size // 48 + 1, np.uint64) for r in recs]
     if registered:
         for a in recs + poss:
             cx.host_register(a)
@@ -270,16 +274,17 @@ def test_destroy_with_fast_submits_in_flight():
 
 
 def _soa(n, lo, hi, seed, uh=False):
-    from iggy_amd.codec import raw_messages
+    """SoA arrays in page-aligned buffers (registrations may not share a page)."""
+    from iggy_amd.codec import page_aligned, raw_messages
     rng = np.random.default_rng(seed)
-    ids = rng.integers(1, 2**63, size=2 * n, dtype=np.uint64)
-    ots = (1_700_000_000_000_000 + rng.integers(0, 10**6, size=n)).astype(np.uint64)
-    pls = rng.integers(lo, hi + 1, size=n).astype(np.uint32)
-    pay = rng.integers(0, 256, size=int(pls.sum()), dtype=np.uint8)
+    ids = page_aligned(rng.integers(1, 2**63, size=2 * n, dtype=np.uint64))
+    ots = page_aligned((1_700_000_000_000_000 + rng.integers(0, 10**6, size=n)).astype(np.uint64))
+    pls = page_aligned(rng.integers(lo, hi + 1, size=n).astype(np.uint32))
+    pay = page_aligned(rng.integers(0, 256, size=int(pls.sum()), dtype=np.uint8))
     arrs = [ids, ots, pay, pls]
     if uh:
-        uhl = rng.integers(0, 40, size=n).astype(np.uint32)
-        uhb = rng.integers(0, 256, size=int(uhl.sum()), dtype=np.uint8)
+        uhl = page_aligned(rng.integers(0, 40, size=n).astype(np.uint32))
+        uhb = page_aligned(rng.integers(0, 256, size=int(uhl.sum()), dtype=np.uint8))
         arrs += [uhb, uhl]
         return arrs, raw_messages(ids, ots, pay, pls, uhb, uhl)
     return arrs, raw_messages(ids, ots, pay, pls)
@@ -293,6 +298,7 @@ def test_encode_submit_small_batches_in_place(cx, registered):
     without user headers, empty payloads, the caller's SoA arrays overwritten right
     after each submit, each output byte-exact against the oracle; plus one batch whose
     output capacity is too small (nothing written, capacity error)."""
+    from iggy_amd.codec import page_aligned
     cases = [(1000, 256, 256, False), (700, 0, 300, True), (3000, 1, 900, False), (64, 0, 0, False),
              (1000, 256, 256, True), (5, 2000, 5000, False), (2000, 100, 1000, True), (1, 17, 17, False)]
     wants, outs, tks, keep = [], [], [], []
@@ -301,7 +307,7 @@ def test_encode_submit_small_batches_in_place(cx, registered):
         rc, e, w = O.encode_batch(raw, 3)
         assert rc == 0
         wants.append(np.frombuffer(w, dtype=np.uint8))
-        out = np.full(len(w) + 32, 0xEE, dtype=np.uint8)
+        out = page_aligned(np.full(len(w) + 32, 0xEE, dtype=np.uint8))
         outs.append(out)
         if registered:
             for a in arrs + [out]:
@@ -378,3 +384,27 @@ def test_pinned_submits_never_wait(cx):
     assert np.array_equal(poss[1].numpy(), np.arange(n, dtype=np.int64) * (48 + pl))
     orc, oe, oh, of = O.decode_batch_slice_with(small, 0)
     assert done[2].error.kind == 0 == orc and np.array_equal(p_small.numpy().view(np.uint64), np.asarray(of, dtype=np.uint64))
+
+
+def test_registrations_may_not_share_a_page(cx):
+    """iggy_codec_host_register refuses a range whose pages meet a live registration's
+    (the runtime pins whole pages: two objects over one page leave a dead mapping when
+    either is undone); page-aligned neighbours register side by side, and
+    the refused range registers once its neighbour is gone."""
+    from iggy_amd.codec import CodecError, host_buffer
+    raw = host_buffer(3 * 4096)
+    a, b = raw[:5000], raw[5000:9000]   # b starts inside a's second page
+    cx.host_register(a)
+    try:
+        with pytest.raises(CodecError) as ei:
+            cx.host_register(b)
+        assert ei.value.rc == abi.ERR_INVALID_ARGUMENT
+        c, d = host_buffer(5000), host_buffer(100)
+        cx.host_register(c)
+        cx.host_register(d)
+        cx.host_unregister(d)
+        cx.host_unregister(c)
+    finally:
+        cx.host_unregister(a)
+    cx.host_register(b)
+    cx.host_unregister(b)

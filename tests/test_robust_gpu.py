@@ -93,10 +93,10 @@ def test_submit_poll_decode_matches_oracle(cx):
 
 
 def test_submit_registered_buffers_and_busy(cx):
+    from iggy_amd.codec import host_buffer, page_aligned
     rec = O.synth_batch(20000, 100, 2000, seed=9)
-    buf = np.empty(rec.size, dtype=np.uint8)
-    buf[:] = rec
-    pos = np.zeros(20000, dtype=np.uint64)
+    buf = page_aligned(rec)
+    pos = host_buffer(20000, np.uint64)
     cx.host_register(buf)
     cx.host_register(pos)
     try:
