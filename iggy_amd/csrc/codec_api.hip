@@ -178,7 +178,6 @@ void iggy_codec_destroy(iggy_codec_ctx *c) {
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     if (c->last && c->last != c->stream) (void)hipStreamSynchronize(c->last);
     if (c->side) (void)hipStreamSynchronize(c->side);
-    if (c->trail) (void)hipStreamSynchronize(c->trail);
     if (c->h2d) (void)hipStreamSynchronize(c->h2d);
     if (c->d2h) (void)hipStreamSynchronize(c->d2h);
     for (Slot &sl : c->slots)  // the fast-path decodes' own streams
@@ -243,9 +242,6 @@ void iggy_codec_destroy(iggy_codec_ctx *c) {
     if (c->h2d) (void)hipStreamSynchronize(c->h2d), (void)hipStreamDestroy(c->h2d);
     if (c->d2h) (void)hipStreamSynchronize(c->d2h), (void)hipStreamDestroy(c->d2h);
     if (c->side) (void)hipStreamDestroy(c->side);
-    if (c->trail) (void)hipStreamDestroy(c->trail);
-    for (auto &ev : c->trail_ev)
-        if (ev) (void)hipEventDestroy(ev);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
 }

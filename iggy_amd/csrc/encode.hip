@@ -1167,79 +1167,6 @@ __global__ __launch_bounds__(SPLIT ? 2 * kErThreads : kErThreads, 1) void k_enc_
     wait_vm_const<0>();
 }
 
-// ---- trailing copier (IGGY_ENC_TRAIL, a timing prototype): the frame bytes written by a
-// kernel of their own, one wave per frame, beside a ring encode that hashes only
-#ifndef IGGY_ENC_TRAIL
-#define IGGY_ENC_TRAIL 0
-#endif
-struct TrailFrame {
-    uint8_t *D;           // payload destination (frame + 48)
-    const uint8_t *S;     // payload source
-    uint64_t pl, head, body;
-    bool valid;
-};
-__device__ __forceinline__ TrailFrame trail_frame(const uint8_t *P, uint8_t *out, const uint4 *erec, uint64_t f,
-                                                  uint64_t f_hi, int lane) {
-    TrailFrame t;
-    t.valid = f < f_hi;
-    const uint4 r = erec[2 * (t.valid ? f : f_hi)];  // (erec[2 N] is the zero "no frame" record)
-    const uint4 ids = erec[2 * (t.valid ? f : f_hi) + 1];
-    const uint64_t po = (uint64_t)r.x | ((uint64_t)r.y << 32);
-    t.pl = t.valid ? r.z : 0;
-    uint8_t *F = out + 256 + 48 * f + po;
-    t.D = F + 48;
-    t.S = P + po;
-    t.head = min<uint64_t>((16 - ((uintptr_t)t.D & 15)) & 15, t.pl);
-    t.body = (t.pl - t.head) & ~15ull;
-    if (t.valid && lane < 5) {
-        const uint64_t hw = lane == 0 ? ((uint64_t)ids.x | ((uint64_t)ids.y << 32))
-                          : lane == 1 ? ((uint64_t)ids.z | ((uint64_t)ids.w << 32))
-                          : lane == 2 ? ((f & 0xFFFFFFFFull) | ((uint64_t)r.w << 32))
-                          : lane == 3 ? (t.pl << 32) : 0ull;
-        st64_any(F + 8 + 8 * lane, hw);
-    }
-    return t;
-}
-// one wave per frame, TRAIL_F frames per pass with every load of the pass in flight
-// before the first store (payloads are at most 4 KiB + 15 B of head: 4 body loads a lane)
-constexpr int kTrailF = 2;
-__global__ __launch_bounds__(256) void k_enc_trailcopy(iggy_raw_messages m, uint8_t *__restrict__ out,
-                                                        const uint4 *__restrict__ erec, uint64_t f_lo, uint64_t f_hi) {
-    const int lane = threadIdx.x & 63;
-    const uint64_t w = (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
-    const uint64_t nw = (uint64_t)gridDim.x * (blockDim.x >> 6);
-    const uint8_t *__restrict__ P = m.payloads;
-    for (uint64_t f = f_lo + w; f < f_hi; f += kTrailF * nw) {
-        TrailFrame t[kTrailF];
-#pragma unroll
-        for (int i = 0; i < kTrailF; ++i) t[i] = trail_frame(P, out, erec, f + i * nw, f_hi, lane);
-        uint4 v[kTrailF][4];
-        uint32_t hb[kTrailF], tb[kTrailF];
-#pragma unroll
-        for (int i = 0; i < kTrailF; ++i) {
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                const uint64_t o = t[i].head + 16 * (uint64_t)(64 * k + lane);
-                v[i][k] = o + 16 <= t[i].head + t[i].body ? ld128_any(t[i].S + o) : make_uint4(0, 0, 0, 0);
-            }
-            hb[i] = (uint64_t)lane < t[i].head ? t[i].S[lane] : 0u;
-            const uint64_t t0 = t[i].head + t[i].body;
-            tb[i] = (uint64_t)lane < t[i].pl - t0 ? t[i].S[t0 + lane] : 0u;
-        }
-#pragma unroll
-        for (int i = 0; i < kTrailF; ++i) {
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                const uint64_t o = t[i].head + 16 * (uint64_t)(64 * k + lane);
-                if (o + 16 <= t[i].head + t[i].body) *(uint4 *)(t[i].D + o) = v[i][k];
-            }
-            if ((uint64_t)lane < t[i].head) t[i].D[lane] = (uint8_t)hb[i];
-            const uint64_t t0 = t[i].head + t[i].body;
-            if ((uint64_t)lane < t[i].pl - t0) t[i].D[t0 + lane] = (uint8_t)tb[i];
-        }
-    }
-}
-
 // Frames of <= 240 hashed bytes of a lane-group encode: one lane each hashes the
 // stream (XXH3 17-128 / 129-240 paths) from the SoA input and backpatches.
 __device__ inline void enc_short_frame(const iggy_raw_messages &m, EncScratch es, uint8_t *out, uint64_t origin,

@@ -220,8 +220,6 @@ struct iggy_codec_ctx {
     // while later segments are encoded on the call's stream
     hipStream_t side = nullptr;
     hipEvent_t seg_ev[kEncSegs + 2] = {};  // segment ends, side-stream end, fork ([kEncSegs + 1])
-    hipStream_t trail = nullptr;           // (IGGY_ENC_TRAIL timing prototype) the copier's stream
-    hipEvent_t trail_ev[2] = {};
     DevBuf dresult;  // iggy_decode_result + iggy_encode_result + u64 scratch
     // sync-API staging
     DevBuf din, dpos, dout;

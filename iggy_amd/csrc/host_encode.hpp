@@ -105,18 +105,6 @@ static int enqueue_encode(iggy_codec_ctx *c, const iggy_raw_messages *dm, uint64
             if (c->erec.ensure((n + 1) * 32) || c->esink.ensure(kErSinkBytes)) return IGGY_ERR_DEVICE;
             hipLaunchKernelGGL(k_enc_recs, dim3((uint32_t)std::min<uint64_t>((n + 256) / 256, (uint64_t)c->ncu * 8)),
                                dim3(256), 0, s, m, es, c->erec.as<uint4>());
-            if (IGGY_ENC_TRAIL) {  // (timing prototype) the frame bytes from a copier on its own stream
-                if (!c->trail && hipStreamCreateWithFlags(&c->trail, hipStreamNonBlocking) != hipSuccess)
-                    return IGGY_ERR_DEVICE;
-                if (!c->trail_ev[0])
-                    for (auto &ev : c->trail_ev)
-                        if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) return IGGY_ERR_DEVICE;
-                HIP_OK(hipEventRecord(c->trail_ev[0], s));
-                HIP_OK(hipStreamWaitEvent(c->trail, c->trail_ev[0], 0));
-                hipLaunchKernelGGL(k_enc_trailcopy, dim3((uint32_t)c->ncu * ((diag_bits(c) >> 24) & 0xf ? (diag_bits(c) >> 24) & 0xf : 1)),
-                                   dim3(256), 0, c->trail, m, d_out, (const uint4 *)c->erec.as<uint4>(), (uint64_t)0, n);
-                HIP_OK(hipEventRecord(c->trail_ev[1], c->trail));
-            }
         }
         if (segmented) {
             hipLaunchKernelGGL(k_enc_frames, dim3((waves + 3) / 4), dim3(256), 0, s, m, es, d_out, 1u);
@@ -190,7 +178,6 @@ static int enqueue_encode(iggy_codec_ctx *c, const iggy_raw_messages *dm, uint64
         HIP_OK(hipGetLastError());
         return 0;
     }
-    if (IGGY_ENC_TRAIL && segmented && IGGY_ENC_RING) HIP_OK(hipStreamWaitEvent(s, c->trail_ev[1], 0));
     if (segmented) {
         hipLaunchKernelGGL(k_chain_finish, dim3(1), dim3(64), 0, s, (const iggy_batch_header *)es.hdr,
                            (const uint64_t *)&es.misc[3], src, (const uint64_t *)bsums.as<uint64_t>(),
