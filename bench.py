@@ -391,6 +391,16 @@ def c1_leg(cx, dev, seconds: float):
     try:
         sync_registered_us = sync_us()
         assert all(int(p[1]) == 48 + pl for p in poss)
+        # the same synchronous calls with the context's resident decode service
+        # (iggy_codec_service_start: no launch per call)
+        cx.service_start()
+        try:
+            for p in poss:
+                p[:] = 0
+            sync_registered_svc_us = sync_us()
+            assert all(int(p[1]) == 48 + pl for p in poss)
+        finally:
+            cx.service_stop()
         for p in poss:
             p[:] = 0
         async_us(1)
@@ -412,6 +422,7 @@ def c1_leg(cx, dev, seconds: float):
         "gpu_host_roundtrip_us_per_batch": round(host_us, 1),
         "gpu_host_sync_us_per_batch": round(sync_pageable_us, 1),
         "gpu_host_sync_registered_us_per_batch": round(sync_registered_us, 1),
+        "gpu_host_sync_registered_service_us_per_batch": round(sync_registered_svc_us, 1),
         "gpu_host_async_registered_us_per_batch": round(async_registered_us, 1),
         "gpu_host_async_registered_submit_cpu_us_per_batch": round(submit_cpu[0], 1),
         "gpu_host_encode_async_registered_us_per_batch": round(enc_async_registered_us, 1),

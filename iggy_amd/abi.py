@@ -185,7 +185,8 @@ class HostStats(ctypes.Structure):
         ("host_waits", u64),
         ("device_allocs", u64),
         ("pinned_allocs", u64),
-        ("_reserved", u64 * 2),
+        ("service_posts", u64),
+        ("service_launches", u64),
     ]
 
     def as_dict(self) -> dict:

@@ -123,6 +123,8 @@ def load(path: str) -> ctypes.CDLL:
     L.iggy_codec_profile_enable.argtypes = [vp, ci]
     L.iggy_codec_profile_read.argtypes = [vp, ci, vp, vp]
     L.iggy_codec_host_stats.argtypes = [vp, vp]
+    L.iggy_codec_service_start.argtypes = [vp]
+    L.iggy_codec_service_stop.argtypes = [vp]
     L.iggy_codec_host_register.argtypes = [vp, vp, u64]
     L.iggy_codec_host_unregister.argtypes = [vp, vp]
     L.iggy_codec_host_pinned.argtypes = [vp, u64]
@@ -542,6 +544,17 @@ class Codec:
         ms = ctypes.c_double(0)
         self._L.iggy_codec_profile_read(self._h, which, ctypes.byref(n), ctypes.byref(ms))
         return n.value, ms.value
+
+    def service_start(self):
+        """iggy_codec_service_start: small synchronous host decodes go to resident workgroups."""
+        rc = self._L.iggy_codec_service_start(self._h)
+        if rc:
+            raise CodecError(rc, None, "service_start")
+
+    def service_stop(self):
+        rc = self._L.iggy_codec_service_stop(self._h)
+        if rc:
+            raise CodecError(rc, None, "service_stop")
 
     def host_stats(self) -> dict:
         """iggy_codec_host_stats: cumulative copy / wait / allocation counters."""

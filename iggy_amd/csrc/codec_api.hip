@@ -175,6 +175,8 @@ void iggy_codec_destroy(iggy_codec_ctx *c) {
     // every stream that may still run this context's work (the caller's last stream,
     // the side stream of segmented encodes, the copy streams of the asynchronous host
     // operations) drains before any buffer it reads or writes goes back to the allocator
+    (void)svc_disable(c);  // the resident service's grid stops and drains first
+    if (c->svc.s) (void)hipStreamSynchronize(c->svc.s);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     if (c->last && c->last != c->stream) (void)hipStreamSynchronize(c->last);
     if (c->side) (void)hipStreamSynchronize(c->side);
@@ -242,6 +244,11 @@ void iggy_codec_destroy(iggy_codec_ctx *c) {
     if (c->h2d) (void)hipStreamSynchronize(c->h2d), (void)hipStreamDestroy(c->h2d);
     if (c->d2h) (void)hipStreamSynchronize(c->d2h), (void)hipStreamDestroy(c->d2h);
     if (c->side) (void)hipStreamDestroy(c->side);
+    c->svc.mb.release();
+    c->svc.ctl.release();
+    c->svc.st.release();
+    c->svc.bsums.release();
+    if (c->svc.s) (void)hipStreamDestroy(c->svc.s);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
 }
@@ -274,7 +281,21 @@ int iggy_codec_host_stats(iggy_codec_ctx *c, iggy_host_stats *out) {
     *out = c->hs;
     out->device_allocs = g_dev_allocs.load(std::memory_order_relaxed);
     out->pinned_allocs = g_pin_allocs.load(std::memory_order_relaxed);
+    out->service_posts = c->svc.posts;
+    out->service_launches = c->svc.launches;
     return 0;
+}
+
+int iggy_codec_service_start(iggy_codec_ctx *c) {
+    if (!c) return IGGY_ERR_INVALID_ARGUMENT;
+    DevGuard dg(c->device);
+    return svc_enable(c);
+}
+
+int iggy_codec_service_stop(iggy_codec_ctx *c) {
+    if (!c) return IGGY_ERR_INVALID_ARGUMENT;
+    DevGuard dg(c->device);
+    return svc_disable(c);
 }
 
 int iggy_codec_profile_enable(iggy_codec_ctx *c, int enable) {

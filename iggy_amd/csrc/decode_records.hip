@@ -133,16 +133,24 @@ __device__ __forceinline__ void decode_record_block(const RecTask &inl, const ui
                                                     const RecTask *__restrict__ tasks,
                                                     const uint32_t *__restrict__ wg_task, RecState *st,
                                                     uint64_t *bsums, uint64_t *frame_pos, iggy_polled_message *msgs,
-                                                    iggy_decode_result *results) {
+                                                    iggy_decode_result *results, uint32_t vblock = ~0u,
+                                                    const uint8_t *pre_head = nullptr, uint64_t *stamp = nullptr) {
+    // (diagnostic build: stage times of thread 0 into stamp[k], the service's LDS)
+    auto mark = [&](int k) {
+        if (kDiagMask && stamp && threadIdx.x == 0) stamp[k] = rt_now();
+    };
+    mark(1);
     __shared__ uint64_t s_cs[kRecFrames + 2];  // stored checksums of frames 128b - 6 + k
     __shared__ uint64_t s_min[4];
     __shared__ uint32_t s_last;
     __shared__ uint8_t s_small[256];  // short checksum inputs (N <= 24): 44 + 8 N bytes
     // one record: its task comes in the kernel arguments (tasks == nullptr), not from a
     // table in host-mapped memory (two dependent PCIe reads before anything else)
-    const uint32_t t = tasks ? wg_task[blockIdx.x] : 0u;
+    // vblock: the workgroup's block when a resident service workgroup runs it (k_decode_service)
+    const uint32_t wg = vblock != ~0u ? vblock : blockIdx.x;
+    const uint32_t t = tasks ? wg_task[wg] : 0u;
     const RecTask tk = tasks ? tasks[t] : inl;
-    const uint32_t blk = blockIdx.x - tk.wg0;
+    const uint32_t blk = wg - tk.wg0;
     const uint8_t *body = base + tk.off;
     const uint8_t *blob = body + kHdr;
     const int lane = threadIdx.x & 63;
@@ -150,17 +158,19 @@ __device__ __forceinline__ void decode_record_block(const RecTask &inl, const ui
     // the batch header and the first frame header (304 B) staged in LDS with one load
     // round, so the header parse and the plan cost no further memory round trips (each
     // one is microseconds for a registered record read in place over the host link)
+    // (pre_head: the same 304 B already in LDS, the resident service's relay)
     __shared__ __attribute__((aligned(16))) uint8_t s_head[kHdr + kFrameHdr];
     const bool staged = tk.len >= kHdr + kFrameHdr;
-    if (staged) {
+    if (staged && !pre_head) {
         if (threadIdx.x < (kHdr + kFrameHdr) / 16)
             *(uint4 *)(s_head + 16 * threadIdx.x) = ld128_any(body + 16 * threadIdx.x);
         __syncthreads();
     }
+    const uint8_t *head = pre_head ? pre_head : s_head;
     HeaderInfo hi;
-    parse_header(staged ? s_head : body, tk.len, hi);
+    parse_header(staged ? head : body, tk.len, hi);
     UPlan pl;
-    make_plan(hi, staged ? s_head + kHdr : blob, tk.len, VERIFY, ~0ull, true, pl);
+    make_plan(hi, staged ? head + kHdr : blob, tk.len, VERIFY, ~0ull, true, pl);
     iggy_decode_result *res = results + t;
 
     if (pl.state != 0 || tk.nwg < rec_blocks(pl.N)) {
@@ -253,18 +263,20 @@ __device__ __forceinline__ void decode_record_block(const RecTask &inl, const ui
             constexpr uint32_t K = kRecFrames / 32;
             uint4 hdr[K], pc[K][8], lastp[K];
             uint64_t stored[K];
+            // (no loads for the slots past the record's ends: a small record read in place
+            // would otherwise fetch frame 0 again over the host link for each of them)
 #pragma unroll
             for (uint32_t k = 0; k < K; ++k) {
                 const int64_t i = i0 + g + 32 * k;
                 const bool valid = i >= 0 && (uint64_t)i < N;
                 const uint8_t *fb = blob + (valid ? (uint64_t)i : 0) * S;
                 const uint8_t *hb = fb + 8 + poff;
-                hdr[k] = l == 0 ? ld128_any(fb + 32) : make_uint4(0, 0, 0, 0);
-                stored[k] = l == 0 ? ld64_any(fb) : 0;
+                hdr[k] = valid && l == 0 ? ld128_any(fb + 32) : make_uint4(0, 0, 0, 0);
+                stored[k] = valid && l == 0 ? ld64_any(fb) : 0;
 #pragma unroll
                 for (int q = 0; q < 8; ++q)
-                    pc[k][q] = (2 * (uint64_t)q + par < ns) ? ld128_any(hb + 128 * q) : make_uint4(0, 0, 0, 0);
-                lastp[k] = par ? make_uint4(0, 0, 0, 0) : ld128_any(fb + 8 + L - 64 + 16 * m);
+                    pc[k][q] = valid && (2 * (uint64_t)q + par < ns) ? ld128_any(hb + 128 * q) : make_uint4(0, 0, 0, 0);
+                lastp[k] = valid && !par ? ld128_any(fb + 8 + L - 64 + 16 * m) : make_uint4(0, 0, 0, 0);
             }
 #pragma unroll
             for (uint32_t k = 0; k < K; ++k) {
@@ -280,12 +292,12 @@ __device__ __forceinline__ void decode_record_block(const RecTask &inl, const ui
             const uint8_t *hb = fb + 8 + poff;
             uint4 hdr = make_uint4(0, 0, 0, 0);
             uint64_t stored = 0;
-            if (l == 0) {
+            if (valid && l == 0) {
                 hdr = ld128_any(fb + 32);  // user_headers_length, payload_length, reserved
                 stored = ld64_any(fb);
             }
             uint64_t a0 = init0, a1 = init1;
-            for (uint64_t b = 0; b < nbF; ++b) {
+            for (uint64_t b = 0; b < (valid ? nbF : 0); ++b) {
                 uint4 pc[8];
 #pragma unroll
                 for (int q = 0; q < 8; ++q) pc[q] = ld128_any(hb + 1024 * b + 128 * q);
@@ -303,8 +315,9 @@ __device__ __forceinline__ void decode_record_block(const RecTask &inl, const ui
             uint4 pc[8];
 #pragma unroll
             for (int q = 0; q < 8; ++q)
-                pc[q] = (2 * (uint64_t)q + par < ns) ? ld128_any(hb + 1024 * nbF + 128 * q) : make_uint4(0, 0, 0, 0);
-            const uint4 lastp = par ? make_uint4(0, 0, 0, 0) : ld128_any(fb + 8 + L - 64 + 16 * m);
+                pc[q] = valid && (2 * (uint64_t)q + par < ns) ? ld128_any(hb + 1024 * nbF + 128 * q)
+                                                              : make_uint4(0, 0, 0, 0);
+            const uint4 lastp = valid && !par ? ld128_any(fb + 8 + L - 64 + 16 * m) : make_uint4(0, 0, 0, 0);
             finish(k, i, valid, hdr, stored, a0, a1, pc, lastp);
         }
     } else if (threadIdx.x < kRecFrames) {
@@ -331,12 +344,14 @@ __device__ __forceinline__ void decode_record_block(const RecTask &inl, const ui
         }
     }
     if (threadIdx.x == 0) s_cs[kRecFrames] = cs_next;
+    mark(2);  // (thread 0's own frames hashed)
     const uint64_t wbad = wg_min(mybad, s_min);  // (its barriers also publish s_cs)
     const uint64_t wsf = wg_min(mysf, s_min);
-    if (threadIdx.x == 0) {
+    if (threadIdx.x == 0 && nblk > 1) {  // (a one-block record's own minima are final)
         if (wbad != ~0ull) atomicMax((unsigned long long *)&st[t].first_bad, (unsigned long long)~wbad);
         if (wsf != ~0ull) atomicMax((unsigned long long *)&st[t].spec_fail, (unsigned long long)~wsf);
     }
+    uint64_t t8 = 0;  // (wave 0 lane j < 8: this block's partial sum j)
     if (VERIFY && pl.long_cs && wave == 0) {
         // words m = 128b + j of the checksum input, j = lane, lane + 64
         const uint64_t mb = (uint64_t)kRecFrames * blk;
@@ -344,8 +359,8 @@ __device__ __forceinline__ void decode_record_block(const RecTask &inl, const ui
         word_contrib_s(pl.Mreg, mb + lane, s_cs[lane], s_cs[lane + 1], true, kSecretW8[(lane >> 3) + (lane & 7)], x, y);
         word_contrib_s(pl.Mreg, mb + 64 + lane, s_cs[64 + lane], s_cs[65 + lane], true,
                        kSecretW8[8 + (lane >> 3) + (lane & 7)], x, y);
-        const uint64_t t8 = reduce_acc8(x, y);
-        if (lane < 8) bsums[8 * (tk.bsum_base + blk) + lane] = t8;
+        t8 = reduce_acc8(x, y);
+        if (lane < 8 && nblk > 1) bsums[8 * (tk.bsum_base + blk) + lane] = t8;
     }
     // the last block workgroup of the record resolves it (a one-block record: its only
     // workgroup, with no device-scope fence or counter)
@@ -365,8 +380,12 @@ __device__ __forceinline__ void decode_record_block(const RecTask &inl, const ui
 
     // the record's first-bad / stride-fail words: final now, loaded beside the chain's
     // block sums (one memory round trip, not two)
-    const uint64_t fb_enc = __hip_atomic_load(&st[t].first_bad, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const uint64_t sf_enc = __hip_atomic_load(&st[t].spec_fail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    mark(3);
+    // (one block: this workgroup's own minima and partial sums, no memory round trip)
+    const uint64_t fb_enc = nblk > 1 ? __hip_atomic_load(&st[t].first_bad, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                     : (wbad != ~0ull ? ~wbad : 0ull);
+    const uint64_t sf_enc = nblk > 1 ? __hip_atomic_load(&st[t].spec_fail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                     : (wsf != ~0ull ? ~wsf : 0ull);
     uint64_t computed = 0;
     if (VERIFY && pl.long_cs) {
         const int j = lane & 7;
@@ -386,7 +405,7 @@ __device__ __forceinline__ void decode_record_block(const RecTask &inl, const ui
         }
         // y = acc + S_0; y = scramble(y) + S_b for b = 1 .. nb (the partial block nb only adds)
         const uint64_t *src = bsums + 8 * tk.bsum_base + j;
-        uint64_t y = acc + src[0];
+        uint64_t y = acc + (nblk > 1 ? src[0] : __shfl(t8, j));  // (one block: pl.nb == 0)
         const uint64_t nb = pl.nb;
         uint64_t b = 1;
         uint64_t v[16];
@@ -416,15 +435,19 @@ __device__ __forceinline__ void decode_record_block(const RecTask &inl, const ui
                                hi.h.batch_length};
         for (int i = 0; i < 5; ++i) st64_any(s_small + 8 * i, w[i]);
         *(u32_ua *)(s_small + 40) = hi.h.message_count;
-        for (uint64_t i = 0; i < N; ++i) st64_any(s_small + 44 + 8 * i, ld64_any(blob + i * S));
+        // (the stored checksums are in s_cs already: frame i at s_cs[i + 6] of the one block)
+        for (uint64_t i = 0; i < N; ++i) st64_any(s_small + 44 + 8 * i, s_cs[i + 6]);
         computed = xxh3_64_lane(s_small, pl.n);
     }
     if (lane != 0) return;
+    mark(4);
     // precedence, as the uniform kernel's consumer (batch.rs:395-421, 461-506)
     // every block workgroup of the record has arrived: re-arm its state for the next launch
-    __hip_atomic_store(&st[t].first_bad, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(&st[t].spec_fail, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(&st[t].done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (nblk > 1) {
+        __hip_atomic_store(&st[t].first_bad, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&st[t].spec_fail, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&st[t].done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
     const bool has_fb = fb_enc != 0, has_sf = sf_enc != 0;
     const uint64_t fbi = ~fb_enc, sf = ~sf_enc;
     uint32_t kind = IGGY_OK, reason = 0, status = kStatusDone;
@@ -457,6 +480,7 @@ __device__ __forceinline__ void decode_record_block(const RecTask &inl, const ui
         a = hi.h.batch_checksum; b = computed; c = hi.h.base_offset;
     }
     write_result(res, hi, kind, reason, a, b, c, nframes, computed, 1, status, nframes * S);
+    mark(5);
 }
 
 // tasks / wg_task may live in host-mapped pinned memory (read once per workgroup);
@@ -483,6 +507,205 @@ __global__ __launch_bounds__(kRecThreads) void k_decode_records(const uint8_t *_
     }
     decode_record_block<VERIFY>(inl, base, tasks, wg_task, st, bsums, frame_pos, msgs, results);
     launch_done(counter, host_flag, flag_value);
+}
+
+// ------------------------------------------------------------ resident service
+// A synchronous host decode of a small single-stride record (iggy_codec_decode_batch
+// at C1, the reference's own call shape, batch.rs:391) spends most of its time on the
+// launch: the host's launch call and the dispatch before the first wave runs (a
+// 4-message record: ≈ 18 µs from the launch returning to its completion flag, of which
+// the kernel is a few). k_decode_service keeps kSvcWgs workgroups resident instead. The
+// leader (workgroup 0) polls a host-mapped mailbox and relays each post through a
+// device-memory control block; every workgroup then decodes block b = its index of the
+// posted record with the same block code as k_decode_records, the last one raising the
+// host flag. Only the leader decides to stop (the mailbox's stop word, kSvcIdleTicks
+// without a post, or the bug guard), and the followers stop on its word, so a post is
+// decoded by all of its workgroups or by none (the host relaunches and re-posts it
+// then). On its way out the leader clears the mailbox's `alive` word.
+constexpr uint32_t kSvcWgs = 8;                       // records of <= 8 blocks (C1: 1 000 frames)
+constexpr uint32_t kSvcPre = 26;                      // 12-B pieces of the record's first 304 B
+constexpr uint64_t kSvcIdleTicks = 100000ull * 20;    // 20 ms without a post: exit
+// Host-mapped mailbox: 8 chunks of 16 B, read by the leader's wave in ONE round of loads
+// (lane c takes chunk c). Chunks 0-5 hold the post and carry its sequence number in
+// their first word, written by the host after the chunk's other words, so a load
+// round that sees the same new number in all six saw the whole post.
+struct SvcMailbox {
+    uint32_t seq0, integrity; uint64_t len;                   // chunk 0
+    uint32_t seq1, nwg; uint64_t pos_cap;                     // 1
+    uint32_t seq2, flag_value; const uint8_t *base;           // 2: the record (device-visible)
+    uint32_t seq3, _r3; uint64_t *frame_pos;                  // 3: positions (device-visible, nullable)
+    uint32_t seq4, _r4; iggy_decode_result *result;           // 4: device-visible
+    uint32_t seq5, _r5; uint32_t *host_flag;                  // 5: raised to flag_value when done
+    uint32_t stop, alive, _r6[2];                             // 6: host: 1 = exit now; alive: see below
+    uint64_t _r7[2];                                          // 7
+    // 8..33: the record's first 304 B (batch header + frame 0's header) in 12-B pieces,
+    // each after its own copy of the sequence number, so the post's load round also
+    // stages what every block workgroup would otherwise fetch over the host link first
+    struct { uint32_t seq; uint8_t b[12]; } pre[kSvcPre];
+    uint64_t diag[8];  // (diagnostic build: stage times of the post, ticks after the leader saw it)
+};
+static_assert(sizeof(SvcMailbox) == 128 + 16 * kSvcPre + 64, "mailbox layout");
+struct SvcCtl {                       // device memory, zeroed before every launch
+    uint32_t go, cmd, counter, _pad;  // go: relays so far; cmd: 1 decode, 2 exit; counter: workgroups done
+    uint4 chunk[6];                   // the relayed post (mailbox chunks 0-5)
+    uint32_t _pad2[4];
+    uint4 head[19];                   // the record's first 304 B
+};
+static_assert(sizeof(SvcCtl) == 128 + 304, "control block layout");
+constexpr int kAuxSys = 17;  // buffer-load cache policy sc0 | sc1: system-coherent (host-mapped memory)
+
+__device__ __forceinline__ uint4 svc_chunk_sys(const SvcMailbox *mb, uint32_t c) {
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void *)mb, 0, sizeof(SvcMailbox), 0x00020000);
+    const g4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, 16u * c, 0, kAuxSys);
+    return make_uint4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ uint4 svc_chunk_dev(const SvcCtl *ctl, uint32_t c) {  // c: 16-B unit from ctl->chunk
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void *)ctl->chunk, 0, 96 + 16 + 304, 0x00020000);
+    const g4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, 16u * c, 0, kAuxSc1);
+    return make_uint4(v.x, v.y, v.z, v.w);
+}
+
+// (diagnostic build) ticks from the leader seeing the post to the flag store, into the
+// mailbox's chunk 7 (the host reads it beside the flag)
+__device__ __forceinline__ void svc_stamp(SvcMailbox *mb, SvcCtl *ctl, uint64_t *stamp) {
+    stamp[7] = rt_now();
+    const uint64_t t0 = (uint64_t)__hip_atomic_load(&ctl->_pad2[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) |
+                        ((uint64_t)__hip_atomic_load(&ctl->_pad2[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) << 32);
+    for (int k = 1; k < 8; ++k)
+        __hip_atomic_store(&mb->diag[k], stamp[k] - t0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(&mb->_r7[0], rt_now() - t0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+__global__ __launch_bounds__(kRecThreads) void k_decode_service(SvcMailbox *mb, uint32_t start_seq, SvcCtl *ctl,
+                                                                RecState *st, uint64_t *bsums) {
+    __shared__ uint32_t s_cmd, s_go;
+    __shared__ uint4 s_chunk[6];
+    __shared__ __attribute__((aligned(16))) uint8_t s_pre[16 * 19];  // the record's first 304 B
+    __shared__ uint64_t s_stamp[8];  // (diagnostic build)
+    const int lane = threadIdx.x & 63;
+    const uint32_t wave = threadIdx.x >> 6;
+    uint32_t seen = start_seq, go = 0;
+    uint64_t t_idle = rt_now();
+    const uint64_t t_guard = t_idle;
+    for (;;) {
+        if (wave == 0) {  // (wave-uniform control flow: every decision comes from a shuffle)
+            uint32_t cmd = 2;
+            bool relay = true;
+            if (blockIdx.x == 0) {  // the leader: the host's mailbox, one load round per poll
+                for (;;) {
+                    const uint32_t cidx = (uint32_t)min(lane, 8 + (int)kSvcPre - 1);
+                    const uint4 v = svc_chunk_sys(mb, cidx);
+                    if (__shfl((int)v.x, 6)) break;  // stop
+                    const uint32_t s0 = (uint32_t)__shfl((int)v.x, 0);
+                    const bool tagged = lane < 6 || (lane >= 8 && lane < 8 + (int)kSvcPre);
+                    if (s0 != seen && __ballot(tagged && v.x != s0) == 0) {  // a whole new post
+                        relay = (uint32_t)__shfl((int)v.y, 1) > 1;  // (a one-block post is the leader's alone)
+                        if (lane < 6) {
+                            s_chunk[lane] = v;
+                            if (relay) ctl->chunk[lane] = v;  // (published by the release store of go)
+                        }
+                        if (lane >= 8 && lane < 8 + (int)kSvcPre) {  // 12-B piece lane - 8 of the prefix
+                            uint32_t *d = (uint32_t *)s_pre + 3u * (uint32_t)(lane - 8);  // (76 dwords)
+                            d[0] = v.y;
+                            if (lane < 8 + (int)kSvcPre - 1) { d[1] = v.z; d[2] = v.w; }
+                        }
+                        __builtin_amdgcn_s_waitcnt(0);  // (LDS writes of the prefix: lgkm)
+                        if (relay && lane < 19) ctl->head[lane] = *(const uint4 *)(s_pre + 16 * lane);
+                        seen = s0;
+                        cmd = 1;
+                        if (kDiagMask && lane == 0) {  // (diagnostic build: when the post was seen)
+                            const uint64_t t = rt_now();
+                            ctl->_pad2[0] = (uint32_t)t;
+                            ctl->_pad2[1] = (uint32_t)(t >> 32);
+                        }
+                        break;
+                    }
+                    const uint64_t now = rt_now();
+                    if (now - t_idle > kSvcIdleTicks || now - t_guard > kSpinLimitTicks * 16) break;
+                    __builtin_amdgcn_s_sleep(2);
+                }
+                if (relay) {  // (the followers take only the latest relay they see)
+                    __builtin_amdgcn_s_waitcnt(0);  // the relayed chunks are written
+                    if (lane == 0) {
+                        __hip_atomic_store(&ctl->cmd, cmd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        __hip_atomic_store(&ctl->go, go + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+                    }
+                }
+                if (lane == 0) {
+                    s_go = relay ? go + 1 : go;
+                    s_cmd = cmd;
+                }
+            } else {  // a follower: the leader's latest relay, read as a seqlock (a relay the
+                      // follower has no block in can be overtaken by the next one meanwhile)
+                const uint64_t t0 = rt_now();
+                for (;;) {
+                    const uint32_t g1 = __hip_atomic_load(&ctl->go, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+                    if (g1 == go) {
+                        if (rt_now() - t0 > kSpinLimitTicks * 16) break;  // bug guard (the leader always relays)
+                        __builtin_amdgcn_s_sleep(1);
+                        continue;
+                    }
+                    const uint32_t c = __hip_atomic_load(&ctl->cmd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    // units 0-5: the post's chunks; 7-25: the record's first 304 B (ctl->head)
+                    const uint4 v = (lane < 6 || (lane >= 7 && lane < 26)) ? svc_chunk_dev(ctl, (uint32_t)lane)
+                                                                           : make_uint4(0, 0, 0, 0);
+                    __builtin_amdgcn_s_waitcnt(0);
+                    if (__hip_atomic_load(&ctl->go, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) == g1) {
+                        if (lane < 6) s_chunk[lane] = v;
+                        if (lane >= 7 && lane < 26) *(uint4 *)(s_pre + 16 * (lane - 7)) = v;
+                        cmd = c;
+                        if (lane == 0) s_go = g1;
+                        break;
+                    }
+                }
+                if (lane == 0) s_cmd = cmd;
+            }
+        }
+        __syncthreads();
+        if (s_cmd != 1) break;
+        go = s_go;  // (a follower may have skipped relays it had no block in)
+        t_idle = rt_now();
+        const uint4 c0 = s_chunk[0], c1 = s_chunk[1], c2 = s_chunk[2], c3 = s_chunk[3], c4 = s_chunk[4],
+                    c5 = s_chunk[5];
+        const uint32_t integ = c0.y, nwg = c1.y, flag_value = c2.y;
+        auto u64 = [](const uint4 &c) { return (uint64_t)c.z | ((uint64_t)c.w << 32); };
+        if (blockIdx.x < nwg && nwg <= kSvcWgs) {
+            RecTask tk;
+            tk.off = 0; tk.len = u64(c0); tk.pos_base = 0; tk.pos_cap = u64(c1); tk.msg_base = 0;
+            tk.bsum_base = 0; tk.wg0 = 0; tk.nwg = nwg;
+            const uint8_t *base = (const uint8_t *)u64(c2);
+            uint64_t *fpos = (uint64_t *)u64(c3);
+            iggy_decode_result *res = (iggy_decode_result *)u64(c4);
+            uint32_t *flag = (uint32_t *)u64(c5);
+            if (integ == IGGY_INTEGRITY_VERIFY)
+                decode_record_block<true>(tk, base, nullptr, nullptr, st, bsums, fpos, nullptr, res, blockIdx.x, s_pre,
+                                          kDiagMask ? s_stamp : nullptr);
+            else
+                decode_record_block<false>(tk, base, nullptr, nullptr, st, bsums, fpos, nullptr, res, blockIdx.x, s_pre,
+                                           kDiagMask ? s_stamp : nullptr);
+            // completion, as launch_done over the post's nwg workgroups (one workgroup: its
+            // own fence orders every host-visible write before the flag)
+            __threadfence_system();
+            if (kDiagMask && threadIdx.x == 0) s_stamp[6] = rt_now();
+            __syncthreads();
+            if (nwg == 1) {
+                if (kDiagMask && threadIdx.x == 0) {
+                    svc_stamp(mb, ctl, s_stamp);
+                    __threadfence_system();
+                }
+                if (threadIdx.x == 0) __hip_atomic_store(flag, flag_value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            } else if (threadIdx.x == 0 && atomicAdd(&ctl->counter, 1u) == nwg - 1) {
+                // every workgroup fenced its host-visible writes at system scope before it
+                // counted, so the last one's flag needs no second fence
+                __hip_atomic_store(&ctl->counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (kDiagMask) svc_stamp(mb, ctl, s_stamp);
+                __hip_atomic_store(flag, flag_value, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+            }
+        }
+        __syncthreads();  // (s_cmd / s_chunk are rewritten by the next relay)
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0)
+        __hip_atomic_store(&mb->alive, 0u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 template __global__ void k_decode_records<true>(const uint8_t *__restrict__, const RecTask *__restrict__,

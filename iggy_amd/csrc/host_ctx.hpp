@@ -273,6 +273,18 @@ struct iggy_codec_ctx {
     hipEvent_t xin_ev = nullptr;
     bool xin_live = false;
     iggy_host_stats hs = {};  // iggy_codec_host_stats (the allocation counts are process-wide)
+    // resident decode service (iggy_codec_service_start, k_decode_service): its mailbox
+    // (host-mapped), control block, record state and block sums, its stream, the last
+    // post's sequence number, and whether the context uses it
+    struct {
+        HostMap mb;
+        DevBuf ctl, st, bsums;
+        hipStream_t s = nullptr;
+        bool enabled = false, launched = false;
+        uint32_t seq = 0;
+        uint64_t posts = 0, launches = 0;
+        uint64_t dev_ticks[8] = {};  // (diagnostic build: summed device time of the posts)
+    } svc;
     // asynchronous host-buffer operations: copy-in stream -> the context's stream -> copy-out
     // stream, so one operation's H2D, another's kernels and a third's D2H overlap
     hipStream_t h2d = nullptr, d2h = nullptr;

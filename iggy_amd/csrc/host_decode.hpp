@@ -408,6 +408,112 @@ int decode_records_to_host(iggy_codec_ctx *c, const uint8_t *d_base, const uint8
     return redo_general(c, d_base, recs, K, integrity, nullptr, res, nullptr);
 }
 
+// ------------------------------------------------------- resident decode service
+// (k_decode_service, decode_records.hip) A context with the service enabled posts a
+// small single-stride record read in place (registered, or copied into the context's
+// mapped staging) to the resident workgroups instead of launching a kernel per call.
+SvcMailbox *svc_mb(iggy_codec_ctx *c) { return c->svc.mb.hp<SvcMailbox>(); }
+
+// (re)launch the service kernel; start_seq: the last post it must not decode again
+int svc_launch(iggy_codec_ctx *c, uint32_t start_seq) {
+    auto &v = c->svc;
+    if (v.launched) HIP_OK(hipStreamSynchronize(v.s));  // the previous grid has exited
+    volatile SvcMailbox *mb = svc_mb(c);
+    mb->stop = 0;
+    mb->alive = 1;
+    HIP_OK(hipMemsetAsync(v.ctl.p, 0, sizeof(SvcCtl), v.s));
+    hipLaunchKernelGGL(k_decode_service, dim3(kSvcWgs), dim3(kRecThreads), 0, v.s, v.mb.dp<SvcMailbox>(), start_seq,
+                       v.ctl.as<SvcCtl>(), v.st.as<RecState>(), v.bsums.as<uint64_t>());
+    HIP_OK(hipGetLastError());
+    v.launched = true;
+    v.launches++;
+    return 0;
+}
+
+int svc_enable(iggy_codec_ctx *c) {
+    auto &v = c->svc;
+    if (v.enabled) return 0;
+    if (!v.s && hipStreamCreateWithFlags(&v.s, hipStreamNonBlocking) != hipSuccess) {
+        v.s = nullptr;
+        return IGGY_ERR_DEVICE;
+    }
+    int r = v.mb.ensure(sizeof(SvcMailbox));
+    r |= v.ctl.ensure(sizeof(SvcCtl));
+    const bool fresh = !v.st.p;
+    r |= v.st.ensure(sizeof(RecState));
+    r |= v.bsums.ensure(8 * 8 * (kSvcWgs + 1));
+    if (r) return IGGY_ERR_DEVICE;
+    if (fresh) HIP_OK(hipMemsetAsync(v.st.p, 0, v.st.cap, v.s));  // (the resolver keeps it zero after)
+    memset(v.mb.h, 0, sizeof(SvcMailbox));
+    v.seq = 0;
+    v.enabled = true;
+    return svc_launch(c, v.seq);
+}
+
+int svc_disable(iggy_codec_ctx *c) {
+    auto &v = c->svc;
+    if (!v.enabled) return 0;
+    v.enabled = false;
+    if (!v.launched) return 0;
+    ((volatile SvcMailbox *)svc_mb(c))->stop = 1;
+    v.launched = false;
+    HIP_OK(hipStreamSynchronize(v.s));  // every workgroup has seen the stop word and exited
+    return 0;
+}
+
+// Post one record to the service and wait for its completion flag (the same flag and
+// host-mapped results as the launch path). A grid that exited idle is relaunched first;
+// one that exits while the post is pending (it never relays a post it has not read) is
+// relaunched to take it.
+int svc_post_wait(iggy_codec_ctx *c, const uint8_t *d_base, const uint8_t *host_prefix, uint64_t len, int integrity,
+                  uint32_t nwg, uint64_t pcap, uint32_t v) {
+    auto &s = c->svc;
+    volatile SvcMailbox *mb = svc_mb(c);
+    if (!mb->alive && svc_launch(c, s.seq)) return IGGY_ERR_DEVICE;
+    mb->integrity = (uint32_t)integrity;
+    mb->nwg = nwg;
+    mb->flag_value = v;
+    mb->len = len;
+    mb->pos_cap = pcap;
+    mb->base = d_base;
+    mb->frame_pos = pcap ? c->omap.dp<uint64_t>(192) : nullptr;
+    mb->result = c->omap.dp<iggy_decode_result>(64);
+    mb->host_flag = c->omap.dp<uint32_t>();
+    // the record's first 304 B (zero past its end), 12 B per tagged piece
+    uint8_t pre[12 * kSvcPre] = {};
+    memcpy(pre, host_prefix, std::min<uint64_t>(len, kHdr + kFrameHdr));
+    for (uint32_t k = 0; k < kSvcPre; ++k) memcpy((void *)mb->pre[k].b, pre + 12 * k, 12);
+    std::atomic_thread_fence(std::memory_order_release);
+    // every chunk's tag after its words (x86 keeps stores in order): a device load round
+    // that sees the new number in all 32 tagged chunks saw the whole post
+    const uint32_t seq = ++s.seq;
+    for (uint32_t k = 0; k < kSvcPre; ++k) mb->pre[k].seq = seq;
+    mb->seq0 = seq; mb->seq1 = seq; mb->seq2 = seq; mb->seq3 = seq; mb->seq4 = seq; mb->seq5 = seq;
+    s.posts++;
+    volatile uint32_t *flag = c->omap.hp<volatile uint32_t>();
+    const auto t0 = std::chrono::steady_clock::now();
+    for (uint64_t i = 1;; ++i) {
+        if (__atomic_load_n(flag, __ATOMIC_ACQUIRE) == v) {
+            if (kDiagMask) {  // (diagnostic build: the device's part, 100 MHz ticks)
+                s.dev_ticks[0] += mb->_r7[0];
+                for (int k = 1; k < 8; ++k) s.dev_ticks[k] += mb->diag[k];
+            }
+            return 0;
+        }
+        if (!mb->alive) {
+            HIP_OK(hipStreamSynchronize(s.s));  // the grid is gone; every store it made has landed
+            if (__atomic_load_n(flag, __ATOMIC_ACQUIRE) == v) return 0;
+            if (svc_launch(c, s.seq - 1)) return IGGY_ERR_DEVICE;  // it sees this post as new
+        }
+        if ((i & 0xfffff) == 0 &&
+            std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > kHostWaitLimitS) {
+            if (getenv("IGGY_CODEC_DEBUG")) fprintf(stderr, "iggy_codec: service post %u: time limit\n", s.seq);
+            return IGGY_ERR_TIMEOUT;
+        }
+        __builtin_ia32_pause();
+    }
+}
+
 // A small single-stride record from host memory (iggy_codec_decode_batch and the
 // host entry points built on it): one H2D copy and ONE k_decode_records launch that
 // writes the verdict and the frame positions straight into host-mapped memory, the
@@ -453,12 +559,19 @@ int decode_host_fast(iggy_codec_ctx *c, const uint8_t *body, uint64_t len, int i
     const RecIn rec{0, len, 0, pcap, 0};
     std::vector<size_t> single;
     const uint32_t v = next_flag(c);
-    r = enqueue_records(c, d_base, body, &rec, 1, integrity,
-                        pcap ? c->omap.dp<uint64_t>(192) : nullptr, nullptr, c->omap.dp<iggy_decode_result>(64),
-                        &single, nullptr, c->omap.dp<uint32_t>(), v);
-    if (r) return r;
-    tmark(1);
-    r = wait_host_flag(c, v);
+    const uint64_t nwg = rec_blocks(nf);
+    if (c->svc.enabled && nf && nwg <= kSvcWgs && len <= kZeroCopyBytes) {
+        // the resident service: no launch (d_base is host memory the device reads in place)
+        tmark(1);
+        r = svc_post_wait(c, d_base, body, len, integrity, (uint32_t)nwg, pcap, v);
+    } else {
+        r = enqueue_records(c, d_base, body, &rec, 1, integrity,
+                            pcap ? c->omap.dp<uint64_t>(192) : nullptr, nullptr, c->omap.dp<iggy_decode_result>(64),
+                            &single, nullptr, c->omap.dp<uint32_t>(), v);
+        if (r) return r;
+        tmark(1);
+        r = wait_host_flag(c, v);
+    }
     if (!r) r = xfer_settle(c);
     if (r) return r;
     tmark(2);
@@ -470,8 +583,14 @@ int decode_host_fast(iggy_codec_ctx *c, const uint8_t *body, uint64_t len, int i
     *done = true;
     tmark(3);
     if (timing && ++tn == timing) {
-        fprintf(stderr, "iggy_codec timing (%d calls, us from entry): staged %.2f launched %.2f flag %.2f done %.2f\n",
-                tn, tsum[0] / tn, tsum[1] / tn, tsum[2] / tn, tsum[3] / tn);
+        fprintf(stderr, "iggy_codec timing (%d calls, us from entry): staged %.2f launched %.2f flag %.2f done %.2f"
+                " service-device %.2f (block entry %.2f hashed %.2f resolver %.2f computed %.2f result %.2f"
+                " fenced %.2f counted %.2f)\n",
+                tn, tsum[0] / tn, tsum[1] / tn, tsum[2] / tn, tsum[3] / tn, c->svc.dev_ticks[0] * 0.01 / tn,
+                c->svc.dev_ticks[1] * 0.01 / tn, c->svc.dev_ticks[2] * 0.01 / tn, c->svc.dev_ticks[3] * 0.01 / tn,
+                c->svc.dev_ticks[4] * 0.01 / tn, c->svc.dev_ticks[5] * 0.01 / tn, c->svc.dev_ticks[6] * 0.01 / tn,
+                c->svc.dev_ticks[7] * 0.01 / tn);
+        for (auto &x : c->svc.dev_ticks) x = 0;
         tn = 0;
         tsum[0] = tsum[1] = tsum[2] = tsum[3] = 0;
     }

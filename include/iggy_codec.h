@@ -833,9 +833,24 @@ typedef struct iggy_host_stats {
     uint64_t host_waits;         /* blocking waits inside the codec's copy helpers */
     uint64_t device_allocs;      /* device scratch (re)allocations (process-wide) */
     uint64_t pinned_allocs;      /* pinned / mapped host (re)allocations (process-wide) */
-    uint64_t _reserved[2];
+    uint64_t service_posts;      /* records decoded by the resident service (iggy_codec_service_start) */
+    uint64_t service_launches;   /* launches of its grid (one per start, and one per idle exit re-entered) */
 } iggy_host_stats;
 int iggy_codec_host_stats(iggy_codec_ctx *ctx, iggy_host_stats *out);
+
+/* ----------------------------------------------------- resident decode service */
+/* Synchronous host decodes of small single-stride records (iggy_codec_decode_batch and
+ * the entries built on it: decode_batch_slice_with at C1, batch.rs:391, the reference's
+ * own call shape) without a kernel launch per call: the context keeps 8 workgroups
+ * resident that poll a host-mapped mailbox, and a record of at most 8 checksum blocks
+ * (1 018 frames) that the device can read in place (registered, or copied into the
+ * context's mapped staging) is posted to them. Results, errors and positions are those
+ * of the launch path. The grid exits after 20 ms without a post and is relaunched by
+ * the next call; it holds 8 workgroups of 256 threads and < 2 KiB of LDS while alive
+ * (the persistent C2 decode grid still fits beside it). Off by default; _stop (and
+ * iggy_codec_destroy) ends it. */
+int iggy_codec_service_start(iggy_codec_ctx *ctx);
+int iggy_codec_service_stop(iggy_codec_ctx *ctx);
 
 /* Human-readable text for an error kind / validation reason. */
 const char *iggy_codec_error_string(uint32_t kind, uint32_t reason);
