@@ -349,6 +349,30 @@ def c1_leg(cx, dev, seconds: float):
                 cx.decode_batch_into(r, abi.INTEGRITY_VERIFY, p)
         return (time.perf_counter() - t) / (reps * nb) * 1e6
 
+    # The same synchronous calls timed from C (scripts/c_loop.c), the way the native
+    # caller makes them: the Python loop above also pays ctypes' per-call argument
+    # building (about 2-3 us of each call), which no Rust caller of the C ABI does.
+    c_loop = None
+    c_loop_path = os.path.join(ROOT, "scripts", "_c_loop.so")
+    if os.path.exists(c_loop_path):
+        c_loop = ctypes.CDLL(c_loop_path)
+        c_loop.c_loop_decode.restype = ctypes.c_double
+        c_loop.c_loop_decode.argtypes = [ctypes.c_void_p] * 7 + [ctypes.c_int, ctypes.c_int, ctypes.c_int]
+
+    def sync_c_us(reps=50):
+        if c_loop is None:
+            return None
+        k = len(recs)
+        P = ctypes.c_void_p * k
+        U = ctypes.c_uint64 * k
+        args = (ctypes.cast(cx._L.iggy_codec_decode_batch, ctypes.c_void_p), cx._h,
+                P(*[r.ctypes.data for r in recs]), U(*[r.size for r in recs]), P(*[p.ctypes.data for p in poss]),
+                U(*[p.size for p in poss]), U(*[n] * k), k, abi.INTEGRITY_VERIFY)
+        assert c_loop.c_loop_decode(*args, 2) > 0
+        ns = c_loop.c_loop_decode(*args, reps)
+        assert ns > 0, ns
+        return ns / 1e3
+
     submit_cpu = [0.0]
 
     def async_us(reps=5, with_pos=True):
@@ -390,6 +414,7 @@ def c1_leg(cx, dev, seconds: float):
         cx.host_register(a)
     try:
         sync_registered_us = sync_us()
+        sync_registered_c_us = sync_c_us()
         assert all(int(p[1]) == 48 + pl for p in poss)
         # the same synchronous calls with the context's resident decode service
         # (iggy_codec_service_start: no launch per call)
@@ -398,6 +423,7 @@ def c1_leg(cx, dev, seconds: float):
             for p in poss:
                 p[:] = 0
             sync_registered_svc_us = sync_us()
+            sync_registered_svc_c_us = sync_c_us()
             assert all(int(p[1]) == 48 + pl for p in poss)
         finally:
             cx.service_stop()
@@ -423,6 +449,11 @@ def c1_leg(cx, dev, seconds: float):
         "gpu_host_sync_us_per_batch": round(sync_pageable_us, 1),
         "gpu_host_sync_registered_us_per_batch": round(sync_registered_us, 1),
         "gpu_host_sync_registered_service_us_per_batch": round(sync_registered_svc_us, 1),
+        # the two synchronous forms above, timed from C (scripts/c_loop.c): no ctypes per call
+        "gpu_host_sync_registered_c_loop_us_per_batch": (round(sync_registered_c_us, 1)
+                                                          if sync_registered_c_us is not None else None),
+        "gpu_host_sync_registered_service_c_loop_us_per_batch": (round(sync_registered_svc_c_us, 1)
+                                                                  if sync_registered_svc_c_us is not None else None),
         "gpu_host_async_registered_us_per_batch": round(async_registered_us, 1),
         "gpu_host_async_registered_submit_cpu_us_per_batch": round(submit_cpu[0], 1),
         "gpu_host_encode_async_registered_us_per_batch": round(enc_async_registered_us, 1),

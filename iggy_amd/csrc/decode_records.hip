@@ -16,9 +16,9 @@
 // XXH3 accumulator sums. 8 lanes per frame (lane-group XXH3, 16-B pieces, pairs
 // folded by DPP) for hashed lengths > 240 B; one lane per frame otherwise and
 // under LayoutOnly. The LAST workgroup of a record to finish (a per-record
-// counter after a release fence) runs the record's serial scramble chain over its
-// block sums and resolves precedence exactly as the uniform kernel's consumer
-// does. A record whose stride speculation breaks without the walk stopping is
+// counter; the block sums handed over as sc1 stores and loads) runs the record's
+// serial scramble chain over its block sums and resolves precedence exactly as the
+// uniform kernel's consumer does. A record whose stride speculation breaks without the walk stopping is
 // left with status kStatusNeedGeneral; the host re-decodes it with the general
 // walk (decode_general.hip).
 //
@@ -58,6 +58,8 @@ __global__ void k_general_rearm(GenRearm rearm) {
     if (threadIdx.x < kBar2Words)
         __hip_atomic_store(&rearm.gbar2[32 * threadIdx.x], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+
+typedef uint32_t rec_g2 __attribute__((ext_vector_type(2)));
 
 struct RecState {  // zero between launches: zeroed when allocated, reset by the record's resolver
     uint64_t first_bad;  // ~min index of a frame whose checksum mismatches (max-encoded), 0 = none
@@ -251,7 +253,6 @@ __device__ __forceinline__ void decode_record_block(const RecTask &inl, const ui
                 if (valid) {
                     if (hdr.z | hdr.w || (uint64_t)kFrameHdr + hdr.x + hdr.y != S) mysf = min(mysf, (uint64_t)i);
                     if (h != stored) mybad = min(mybad, (uint64_t)i);
-                    if (frame_pos && (uint64_t)i < tk.pos_cap) frame_pos[tk.pos_base + i] = (uint64_t)i * S;
                 }
                 s_cs[g + 32 * k] = valid ? stored : 0;
             }
@@ -332,7 +333,6 @@ __device__ __forceinline__ void decode_record_block(const RecTask &inl, const ui
             stored = ld64_any(fb);
             if (hdr.z | hdr.w || (uint64_t)kFrameHdr + hdr.x + hdr.y != S) mysf = (uint64_t)i;
             if (VERIFY && xxh3_64_lane(fb + 8, L) != stored) mybad = (uint64_t)i;
-            if (frame_pos && (uint64_t)i < tk.pos_cap) frame_pos[tk.pos_base + i] = (uint64_t)i * S;
         }
         s_cs[k] = stored;
     }
@@ -360,22 +360,41 @@ __device__ __forceinline__ void decode_record_block(const RecTask &inl, const ui
         word_contrib_s(pl.Mreg, mb + 64 + lane, s_cs[64 + lane], s_cs[65 + lane], true,
                        kSecretW8[8 + (lane >> 3) + (lane & 7)], x, y);
         t8 = reduce_acc8(x, y);
-        if (lane < 8 && nblk > 1) bsums[8 * (tk.bsum_base + blk) + lane] = t8;
+        // (sc1: written through, for the resolver's sc1 loads on another CU)
+        if (lane < 8 && nblk > 1)
+            __hip_atomic_store(&bsums[8 * (tk.bsum_base + blk) + lane], t8, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-    // the last block workgroup of the record resolves it (a one-block record: its only
-    // workgroup, with no device-scope fence or counter)
+    // The last block workgroup of the record resolves it (a one-block record: its only
+    // workgroup, with no counter). The hand-off needs no fence (round 6): the block sums
+    // are sc1 stores of wave 0 and the minima are atomics of its lane 0, which waits for
+    // all of them (vmcnt) before its counter add; the resolver is the wave whose add came
+    // last and reads them with sc1 loads after its add has returned
+    // (MI355X_MICROARCH.md, hand-off table, first row). A __threadfence() on each side
+    // (an L2 write-back and an L1 invalidate, microseconds each) was on every small
+    // record's critical path.
     __syncthreads();
+    // Frame positions (i * S; valid when the record decodes) are stored only now: ahead
+    // of the counter add, a store to host-mapped positions would put a host-link round
+    // trip into the wait before it.
+    auto store_positions = [&]() {
+        if (!frame_pos) return;
+        for (uint32_t k = threadIdx.x; k < kRecFrames; k += kRecThreads) {
+            const int64_t i = i0 + k;
+            if (i >= 0 && (uint64_t)i < N && (uint64_t)i < tk.pos_cap) frame_pos[tk.pos_base + i] = (uint64_t)i * S;
+        }
+    };
     if (nblk > 1) {
         if (threadIdx.x == 0) {
-            __threadfence();  // release: this WG's block sums, positions and atomics
-            const uint32_t old = atomicAdd(&st[t].done, 1u);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // wave 0's block sums and minima
+            const uint32_t old = __hip_atomic_fetch_add(&st[t].done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             s_last = old + 1 == (uint32_t)nblk;
         }
+        store_positions();
         __syncthreads();
         if (!s_last || wave != 0) return;
-        __threadfence();  // acquire: every block workgroup's stores of this record
-    } else if (wave != 0) {
-        return;
+    } else {
+        store_positions();
+        if (wave != 0) return;
     }
 
     // the record's first-bad / stride-fail words: final now, loaded beside the chain's
@@ -404,18 +423,25 @@ __device__ __forceinline__ void decode_record_block(const RecTask &inl, const ui
             }
         }
         // y = acc + S_0; y = scramble(y) + S_b for b = 1 .. nb (the partial block nb only adds)
-        const uint64_t *src = bsums + 8 * tk.bsum_base + j;
-        uint64_t y = acc + (nblk > 1 ? src[0] : __shfl(t8, j));  // (one block: pl.nb == 0)
+        // (the block sums of other workgroups: sc1 loads, see the hand-off above)
+        // (buffer loads with the sc1 policy: schedulable, so a group of 16 is one round)
         const uint64_t nb = pl.nb;
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+            (void *)(bsums + 8 * tk.bsum_base), 0, (int)min<uint64_t>(64 * (nb + 1), 1u << 30), 0x00020000);
+        auto sum_at = [&](uint64_t b) -> uint64_t {  // (lane j: sum j of block b)
+            const rec_g2 r = __builtin_amdgcn_raw_buffer_load_b64(rs, (uint32_t)(64 * b + 8 * j), 0, kAuxSc1);
+            return (uint64_t)r.x | ((uint64_t)r.y << 32);
+        };
+        uint64_t y = acc + (nblk > 1 ? sum_at(0) : __shfl(t8, j));  // (one block: pl.nb == 0)
         uint64_t b = 1;
         uint64_t v[16];
-        for (; b + 16 <= nb + 1; b += 16) {
+        for (; b <= nb; b += 16) {  // groups of up to 16 blocks: the group's loads, then its steps
 #pragma unroll
-            for (int q = 0; q < 16; ++q) v[q] = src[8 * (b + q)];
+            for (int q = 0; q < 16; ++q) v[q] = b + q <= nb ? sum_at(b + q) : 0;
 #pragma unroll
-            for (int q = 0; q < 16; ++q) y = chain_step(y, v[q], klo, khi);
+            for (int q = 0; q < 16; ++q)
+                if (b + q <= nb) y = chain_step(y, v[q], klo, khi);
         }
-        for (; b <= nb; ++b) y = chain_step(y, src[8 * b], klo, khi);
         acc = y;
         // last stripe = stored checksums of frames N-8 .. N-1 (secret offset 121)
         const uint64_t lv = __shfl(r_lv, j);
@@ -545,13 +571,21 @@ struct SvcMailbox {
     uint64_t diag[8];  // (diagnostic build: stage times of the post, ticks after the leader saw it)
 };
 static_assert(sizeof(SvcMailbox) == 128 + 16 * kSvcPre + 64, "mailbox layout");
-struct SvcCtl {                       // device memory, zeroed before every launch
-    uint32_t go, cmd, counter, _pad;  // go: relays so far; cmd: 1 decode, 2 exit; counter: workgroups done
-    uint4 chunk[6];                   // the relayed post (mailbox chunks 0-5)
-    uint32_t _pad2[4];
-    uint4 head[19];                   // the record's first 304 B
+// The leader relays a post to the followers as the mailbox's own tagged units, copied
+// verbatim: units 0-5 the post's chunks, 6-31 the 26 prefix pieces, each 16-B unit
+// carrying the post's sequence number in its first word. A follower's poll is one round
+// of sc1 loads of all of them (and the exit word): a round that sees one new number in
+// all 32 saw the whole relay (a 16-B sc1 store is observed whole). Round 6: the relay
+// had been a go word behind a release, read behind an acquire and re-checked behind a
+// second one, ~1.9 us from the leader seeing the post to the followers starting.
+constexpr uint32_t kSvcUnits = 6 + kSvcPre;
+struct SvcCtl {                        // device memory, zeroed before every launch
+    uint4 unit[kSvcUnits];             // the relayed post (tagged units, see above)
+    uint32_t exit, _e[3];              // unit kSvcUnits: the leader's exit word (1 = exit)
+    uint32_t counter, _c[3];           // workgroups done with the current post
+    uint32_t diag[4];                  // (diagnostic build) when the leader saw the post
 };
-static_assert(sizeof(SvcCtl) == 128 + 304, "control block layout");
+static_assert(sizeof(SvcCtl) == 16 * kSvcUnits + 48, "control block layout");
 constexpr int kAuxSys = 17;  // buffer-load cache policy sc0 | sc1: system-coherent (host-mapped memory)
 
 __device__ __forceinline__ uint4 svc_chunk_sys(const SvcMailbox *mb, uint32_t c) {
@@ -559,18 +593,23 @@ __device__ __forceinline__ uint4 svc_chunk_sys(const SvcMailbox *mb, uint32_t c)
     const g4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, 16u * c, 0, kAuxSys);
     return make_uint4(v.x, v.y, v.z, v.w);
 }
-__device__ __forceinline__ uint4 svc_chunk_dev(const SvcCtl *ctl, uint32_t c) {  // c: 16-B unit from ctl->chunk
-    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void *)ctl->chunk, 0, 96 + 16 + 304, 0x00020000);
+__device__ __forceinline__ uint4 svc_unit_dev(const SvcCtl *ctl, uint32_t c) {  // c: 16-B unit, kSvcUnits: exit
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void *)ctl, 0, sizeof(SvcCtl), 0x00020000);
     const g4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, 16u * c, 0, kAuxSc1);
     return make_uint4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ void svc_unit_store(SvcCtl *ctl, uint32_t c, uint4 v) {  // sc1: written through
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void *)ctl, 0, sizeof(SvcCtl), 0x00020000);
+    const g4 w = {v.x, v.y, v.z, v.w};
+    __builtin_amdgcn_raw_buffer_store_b128(w, rs, 16u * c, 0, kAuxSc1);
 }
 
 // (diagnostic build) ticks from the leader seeing the post to the flag store, into the
 // mailbox's chunk 7 (the host reads it beside the flag)
 __device__ __forceinline__ void svc_stamp(SvcMailbox *mb, SvcCtl *ctl, uint64_t *stamp) {
     stamp[7] = rt_now();
-    const uint64_t t0 = (uint64_t)__hip_atomic_load(&ctl->_pad2[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) |
-                        ((uint64_t)__hip_atomic_load(&ctl->_pad2[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) << 32);
+    const uint64_t t0 = (uint64_t)__hip_atomic_load(&ctl->diag[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) |
+                        ((uint64_t)__hip_atomic_load(&ctl->diag[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) << 32);
     for (int k = 1; k < 8; ++k)
         __hip_atomic_store(&mb->diag[k], stamp[k] - t0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     __hip_atomic_store(&mb->_r7[0], rt_now() - t0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -578,92 +617,98 @@ __device__ __forceinline__ void svc_stamp(SvcMailbox *mb, SvcCtl *ctl, uint64_t 
 
 __global__ __launch_bounds__(kRecThreads) void k_decode_service(SvcMailbox *mb, uint32_t start_seq, SvcCtl *ctl,
                                                                 RecState *st, uint64_t *bsums) {
-    __shared__ uint32_t s_cmd, s_go;
+    __shared__ uint32_t s_cmd;
     __shared__ uint4 s_chunk[6];
     __shared__ __attribute__((aligned(16))) uint8_t s_pre[16 * 19];  // the record's first 304 B
     __shared__ uint64_t s_stamp[8];  // (diagnostic build)
     const int lane = threadIdx.x & 63;
     const uint32_t wave = threadIdx.x >> 6;
-    uint32_t seen = start_seq, go = 0;
+    uint32_t seen = start_seq;  // the last post taken (posts are numbered from 1; 0 is never one)
     uint64_t t_idle = rt_now();
     const uint64_t t_guard = t_idle;
     for (;;) {
         if (wave == 0) {  // (wave-uniform control flow: every decision comes from a shuffle)
             uint32_t cmd = 2;
-            bool relay = true;
-            if (blockIdx.x == 0) {  // the leader: the host's mailbox, one load round per poll
-                for (;;) {
-                    const uint32_t cidx = (uint32_t)min(lane, 8 + (int)kSvcPre - 1);
-                    const uint4 v = svc_chunk_sys(mb, cidx);
-                    if (__shfl((int)v.x, 6)) break;  // stop
+            if (blockIdx.x == 0) {
+                // The leader: the host's mailbox, one load round per poll, four polls in
+                // flight (each waits only for the oldest), so a post is seen about one
+                // host-link round trip after it lands instead of up to two.
+                const uint32_t cidx = (uint32_t)min(lane, 8 + (int)kSvcPre - 1);
+                const bool tagged = lane < 6 || (lane >= 8 && lane < 8 + (int)kSvcPre);
+                // returns true when the poll v decides (a new post: cmd 1; stop, idle or
+                // the bug guard: cmd 2)
+                auto take = [&](const uint4 &v) -> bool {
+                    if (__shfl((int)v.x, 6)) return true;  // stop
                     const uint32_t s0 = (uint32_t)__shfl((int)v.x, 0);
-                    const bool tagged = lane < 6 || (lane >= 8 && lane < 8 + (int)kSvcPre);
-                    if (s0 != seen && __ballot(tagged && v.x != s0) == 0) {  // a whole new post
-                        relay = (uint32_t)__shfl((int)v.y, 1) > 1;  // (a one-block post is the leader's alone)
-                        if (lane < 6) {
-                            s_chunk[lane] = v;
-                            if (relay) ctl->chunk[lane] = v;  // (published by the release store of go)
-                        }
+                    if (s0 != 0 && s0 != seen && __ballot(tagged && v.x != s0) == 0) {  // a whole new post
+                        const bool relay = (uint32_t)__shfl((int)v.y, 1) > 1;  // (a one-block post is the leader's alone)
+                        if (lane < 6) s_chunk[lane] = v;
                         if (lane >= 8 && lane < 8 + (int)kSvcPre) {  // 12-B piece lane - 8 of the prefix
                             uint32_t *d = (uint32_t *)s_pre + 3u * (uint32_t)(lane - 8);  // (76 dwords)
                             d[0] = v.y;
                             if (lane < 8 + (int)kSvcPre - 1) { d[1] = v.z; d[2] = v.w; }
                         }
-                        __builtin_amdgcn_s_waitcnt(0);  // (LDS writes of the prefix: lgkm)
-                        if (relay && lane < 19) ctl->head[lane] = *(const uint4 *)(s_pre + 16 * lane);
-                        seen = s0;
-                        cmd = 1;
+                        if (relay && tagged) svc_unit_store(ctl, lane < 6 ? (uint32_t)lane : (uint32_t)lane - 2u, v);
                         if (kDiagMask && lane == 0) {  // (diagnostic build: when the post was seen)
                             const uint64_t t = rt_now();
-                            ctl->_pad2[0] = (uint32_t)t;
-                            ctl->_pad2[1] = (uint32_t)(t >> 32);
+                            ctl->diag[0] = (uint32_t)t;
+                            ctl->diag[1] = (uint32_t)(t >> 32);
                         }
-                        break;
+                        seen = s0;
+                        cmd = 1;
+                        return true;
                     }
                     const uint64_t now = rt_now();
-                    if (now - t_idle > kSvcIdleTicks || now - t_guard > kSpinLimitTicks * 16) break;
+                    return now - t_idle > kSvcIdleTicks || now - t_guard > kSpinLimitTicks * 16;
+                };
+                uint4 p0 = svc_chunk_sys(mb, cidx);
+                __builtin_amdgcn_s_sleep(2);
+                uint4 p1 = svc_chunk_sys(mb, cidx);
+                __builtin_amdgcn_s_sleep(2);
+                uint4 p2 = svc_chunk_sys(mb, cidx);
+                for (;;) {
                     __builtin_amdgcn_s_sleep(2);
+                    uint4 p3 = svc_chunk_sys(mb, cidx);
+                    if (take(p0)) break;
+                    __builtin_amdgcn_s_sleep(2);
+                    p0 = svc_chunk_sys(mb, cidx);
+                    if (take(p1)) break;
+                    __builtin_amdgcn_s_sleep(2);
+                    p1 = svc_chunk_sys(mb, cidx);
+                    if (take(p2)) break;
+                    __builtin_amdgcn_s_sleep(2);
+                    p2 = svc_chunk_sys(mb, cidx);
+                    if (take(p3)) break;
                 }
-                if (relay) {  // (the followers take only the latest relay they see)
-                    __builtin_amdgcn_s_waitcnt(0);  // the relayed chunks are written
-                    if (lane == 0) {
-                        __hip_atomic_store(&ctl->cmd, cmd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                        __hip_atomic_store(&ctl->go, go + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-                    }
-                }
-                if (lane == 0) {
-                    s_go = relay ? go + 1 : go;
-                    s_cmd = cmd;
-                }
-            } else {  // a follower: the leader's latest relay, read as a seqlock (a relay the
-                      // follower has no block in can be overtaken by the next one meanwhile)
+                __builtin_amdgcn_s_waitcnt(0);  // the polls still in flight, the relay stores and the LDS writes
+                if (cmd != 1 && lane == 0)  // the followers stop on this word
+                    __hip_atomic_store(&ctl->exit, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (lane == 0) s_cmd = cmd;
+            } else {  // a follower: the leader's latest relay (one sc1 load round per poll)
                 const uint64_t t0 = rt_now();
                 for (;;) {
-                    const uint32_t g1 = __hip_atomic_load(&ctl->go, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
-                    if (g1 == go) {
-                        if (rt_now() - t0 > kSpinLimitTicks * 16) break;  // bug guard (the leader always relays)
-                        __builtin_amdgcn_s_sleep(1);
-                        continue;
-                    }
-                    const uint32_t c = __hip_atomic_load(&ctl->cmd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    // units 0-5: the post's chunks; 7-25: the record's first 304 B (ctl->head)
-                    const uint4 v = (lane < 6 || (lane >= 7 && lane < 26)) ? svc_chunk_dev(ctl, (uint32_t)lane)
-                                                                           : make_uint4(0, 0, 0, 0);
-                    __builtin_amdgcn_s_waitcnt(0);
-                    if (__hip_atomic_load(&ctl->go, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) == g1) {
+                    const uint4 v = lane <= (int)kSvcUnits ? svc_unit_dev(ctl, (uint32_t)lane) : make_uint4(0, 0, 0, 0);
+                    if (__shfl((int)v.x, kSvcUnits)) break;  // the leader exits
+                    const uint32_t s0 = (uint32_t)__shfl((int)v.x, 0);
+                    if (s0 != 0 && s0 != seen && __ballot(lane < (int)kSvcUnits && v.x != s0) == 0) {
                         if (lane < 6) s_chunk[lane] = v;
-                        if (lane >= 7 && lane < 26) *(uint4 *)(s_pre + 16 * (lane - 7)) = v;
-                        cmd = c;
-                        if (lane == 0) s_go = g1;
+                        if (lane >= 6 && lane < (int)kSvcUnits) {  // prefix piece lane - 6
+                            uint32_t *d = (uint32_t *)s_pre + 3u * (uint32_t)(lane - 6);
+                            d[0] = v.y;
+                            if (lane < (int)kSvcUnits - 1) { d[1] = v.z; d[2] = v.w; }
+                        }
+                        seen = s0;
+                        cmd = 1;
                         break;
                     }
+                    if (rt_now() - t0 > kSpinLimitTicks * 16) break;  // bug guard (the leader always ends with exit)
+                    __builtin_amdgcn_s_sleep(1);
                 }
                 if (lane == 0) s_cmd = cmd;
             }
         }
         __syncthreads();
         if (s_cmd != 1) break;
-        go = s_go;  // (a follower may have skipped relays it had no block in)
         t_idle = rt_now();
         const uint4 c0 = s_chunk[0], c1 = s_chunk[1], c2 = s_chunk[2], c3 = s_chunk[3], c4 = s_chunk[4],
                     c5 = s_chunk[5];

@@ -486,7 +486,8 @@ int svc_post_wait(iggy_codec_ctx *c, const uint8_t *d_base, const uint8_t *host_
     std::atomic_thread_fence(std::memory_order_release);
     // every chunk's tag after its words (x86 keeps stores in order): a device load round
     // that sees the new number in all 32 tagged chunks saw the whole post
-    const uint32_t seq = ++s.seq;
+    if (++s.seq == 0) ++s.seq;  // (0 is never a post: a zeroed relay unit carries it)
+    const uint32_t seq = s.seq;
     for (uint32_t k = 0; k < kSvcPre; ++k) mb->pre[k].seq = seq;
     mb->seq0 = seq; mb->seq1 = seq; mb->seq2 = seq; mb->seq3 = seq; mb->seq4 = seq; mb->seq5 = seq;
     s.posts++;

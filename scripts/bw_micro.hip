@@ -120,6 +120,63 @@ __global__ __launch_bounds__(256, 1) void lds_frames(const uint8_t *__restrict__
     if (x == 0x12345678) out[0] = x;
 }
 
+// The C2 producers' order (decode_uniform.hip produce_lg), staging only: WG g of NP takes
+// 128-frame blocks g, g + NP, ...; at step k its wave w loads unit k & 3 (32 frames) of
+// block k >> 2, frame group w of it (frames 32 u - 6 + 8 w + fg), 9 loads per step, a
+// SLOTS ring per wave and a constant vmcnt (SLOTS - 1 steps in flight).
+// ORDER 1: the same blocks, but the chip's units in step order (unit-major: at step k all
+// WGs read unit k & 3 of ONE window of NP blocks -- the product); ORDER 2: a contiguous
+// window per step (WG g reads unit g & 3 of block 4 * (k div ... )): see issue()
+template <int SLOTS, int ORDER>
+__global__ __launch_bounds__(256, 1) void lds_blocks(const uint8_t *__restrict__ blob, uint64_t S, uint64_t N, uint64_t *out) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const int lane = threadIdx.x & 63;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t ring = wave * SLOTS * 9216;
+    const int l = lane & 7, fg = lane >> 3, m = l >> 1, par = l & 1;
+    const uint32_t poff = 16 * (m + 4 * par);
+    const uint64_t NP = gridDim.x, g = blockIdx.x;
+    const uint64_t blocks = (N + 6 + 127) / 128;
+    const uint64_t units = 4 * blocks;
+    // unit of step k for this WG
+    auto unit_of = [&](uint64_t k) -> uint64_t {
+        if (ORDER == 1) return 4 * (g + NP * (k >> 2)) + (k & 3);
+        // ORDER 2: at step k the NP WGs read NP consecutive units (a contiguous window);
+        // WG g's unit sequence still covers whole blocks? no: staging-only bound
+        return NP * k + g;
+    };
+    uint64_t mine = 0;
+    while (unit_of(mine) < units) ++mine;
+    auto issue = [&](uint64_t k) {
+        const uint64_t u = unit_of(k);
+        const int64_t i = (int64_t)(32 * u) - 6 + 8 * (int64_t)wave + fg;
+        const bool valid = i >= 0 && (uint64_t)i < N;
+        const uint8_t *fb = blob + (valid ? (uint64_t)i : 0) * S;
+        const uint32_t slot = ring + (uint32_t)(k % SLOTS) * 9216;
+        for (int q = 0; q < 8; ++q) glds(fb + 8 + 128 * q + poff, slot + 1024 * q);
+        glds(!par ? fb + 8 + 1000 + 16 * m : (m == 1 ? fb + S : fb), slot + 8192);
+    };
+    uint32_t x = 0;
+    uint64_t issued = 0;
+    for (; issued < SLOTS && issued < mine; ++issued) issue(issued);
+    for (uint64_t k = 0; k < mine; ++k) {
+        if (issued - 1 - k >= (uint64_t)SLOTS - 1) {
+            if (SLOTS == 4) asm volatile("s_waitcnt vmcnt(27)" ::: "memory");
+            else if (SLOTS == 3) asm volatile("s_waitcnt vmcnt(18)" ::: "memory");
+            else asm volatile("s_waitcnt vmcnt(9)" ::: "memory");
+        } else {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        const uint8_t *p = smem + ring + (k % SLOTS) * 9216 + 16 * lane;
+        uint4 v = *(const uint4 *)p;
+        x ^= v.x ^ v.w;
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if (issued < mine) { issue(issued); ++issued; }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (x == 0x12345678) out[0] = x;
+}
+
 __global__ void fill_random(uint64_t *p, uint64_t n) {
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
         uint64_t z = i * 0x9E3779B97F4A7C15ull + 0x1234567;
@@ -158,6 +215,24 @@ int main() {
         printf("%-40s %8.4f ms  %7.1f GB/s\n", name, ms, L / (ms * 1e-3) / 1e9);
     };
     char nm[128];
+    if (getenv("BW_ORDER")) {  // the C2 producers' block order vs a contiguous window, staging only
+        hipFuncSetAttribute((const void *)lds_blocks<4, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
+        hipFuncSetAttribute((const void *)lds_blocks<4, 2>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
+        hipFuncSetAttribute((const void *)lds_blocks<3, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
+        hipFuncSetAttribute((const void *)lds_frames<0, 8, 4>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
+        for (int rep = 0; rep < 2; ++rep) {
+            for (int np : {249, 255, 256}) {
+                snprintf(nm, sizeof nm, "blocks(product order) 4slot np=%d", np);
+                timeit(nm, [&] { hipLaunchKernelGGL((lds_blocks<4, 1>), np, 256, 4 * 4 * 9216, 0, d + 256, S, N, o); });
+                snprintf(nm, sizeof nm, "blocks(product order) 3slot np=%d", np);
+                timeit(nm, [&] { hipLaunchKernelGGL((lds_blocks<3, 1>), np, 256, 4 * 3 * 9216, 0, d + 256, S, N, o); });
+                snprintf(nm, sizeof nm, "units(contiguous window) 4slot np=%d", np);
+                timeit(nm, [&] { hipLaunchKernelGGL((lds_blocks<4, 2>), np, 256, 4 * 4 * 9216, 0, d + 256, S, N, o); });
+            }
+            timeit("ldsdma seg unit8 4slot (round 1)", [&] { hipLaunchKernelGGL((lds_frames<0, 8, 4>), 255, 256, 163840, 0, d + 256, S, N, o); });
+        }
+        return 0;
+    }
     if (getenv("BW_MISALIGN")) {  // the same frame-segment reads with 16-B / 4-B / 1-B aligned frame starts
         for (uint64_t S2 : {1072ull, 1076ull, 1073ull}) {
             for (uint64_t base : {256ull, 257ull}) {
