@@ -25,9 +25,6 @@
 #ifndef IGGY_ENC_RING
 #define IGGY_ENC_RING 1  // (build knob for same-box A/B: 0 = k_enc_lanes for segmented encodes too)
 #endif
-#ifndef IGGY_ENC_WAVE
-#define IGGY_ENC_WAVE 0  // (build knob for same-box A/B: 1 = k_enc_wave for congruent segmented encodes, a prototype)
-#endif
 #ifndef IGGY_ENC_SPLIT
 #define IGGY_ENC_SPLIT 0  // (build knob for same-box A/B: 1 = writer waves in k_enc_ring, encode.hip)
 #endif
@@ -36,7 +33,6 @@
 #include "decode_uniform.hip"
 #include "decode_records.hip"
 #include "encode.hip"
-#include "encode_wave.hip"
 #include "poll.hip"
 #include "slice.hip"
 #include "crypt.hip"
@@ -127,8 +123,6 @@ int iggy_codec_create(int device, iggy_codec_ctx **out) {
                                 hipFuncAttributeMaxDynamicSharedMemorySize, kGenLds) != hipSuccess ||
             hipFuncSetAttribute((const void *)k_enc_ring<false>,
                                 hipFuncAttributeMaxDynamicSharedMemorySize, kErLds) != hipSuccess ||
-            hipFuncSetAttribute((const void *)k_enc_wave,
-                                hipFuncAttributeMaxDynamicSharedMemorySize, kEwLds) != hipSuccess ||
             (IGGY_ENC_SPLIT && hipFuncSetAttribute((const void *)k_enc_ring<true>,
                                                    hipFuncAttributeMaxDynamicSharedMemorySize, kEsLds) != hipSuccess))
             r = IGGY_ERR_DEVICE;

@@ -101,10 +101,6 @@ static int enqueue_encode(iggy_codec_ctx *c, const iggy_raw_messages *dm, uint64
         // writer waves beside the hashers (k_enc_ring<true>) when every frame's payload
         // keeps its source offset mod 16 in the output (P - out = 0 mod 16, encode.hip)
         const bool split = IGGY_ENC_SPLIT && ((((uintptr_t)m.payloads) - (uintptr_t)d_out) & 15) == 0;
-        // one wave per frame, copy-shaped (k_enc_wave, encode_wave.hip): payload and output
-        // 16-B congruent, so every payload chunk is one aligned load and one aligned store
-        const bool wave = IGGY_ENC_WAVE && !(diag_bits(c) & 0x400000) &&
-                          ((((uintptr_t)m.payloads) - (uintptr_t)d_out) & 15) == 0;
         if (ring) {
             if (c->erec.ensure((n + 1) * 32) || c->esink.ensure(kErSinkBytes)) return IGGY_ERR_DEVICE;
             hipLaunchKernelGGL(k_enc_recs, dim3((uint32_t)std::min<uint64_t>((n + 256) / 256, (uint64_t)c->ncu * 8)),
@@ -139,10 +135,7 @@ static int enqueue_encode(iggy_codec_ctx *c, const iggy_raw_messages *dm, uint64
             const uint64_t B0 = bound(k), B1 = bound(k + 1);
             const uint64_t F0 = k == 0 ? 0 : std::min<uint64_t>(n, 128 * B0 - 5);
             const uint64_t F1 = k == nseg - 1 ? n : std::min<uint64_t>(n, 128 * B1 - 5);
-            if (ring && wave)
-                hipLaunchKernelGGL(k_enc_wave, dim3((uint32_t)std::min<uint64_t>((n + 15) / 16, lcu)), dim3(kEwThreads),
-                                   kEwLds, s, m, es, d_out, F0, F1, (const uint4 *)c->erec.as<uint4>());
-            else if (ring && split)
+            if (ring && split)
                 hipLaunchKernelGGL(k_enc_ring<true>, dim3((uint32_t)std::min<uint64_t>((n + 63) / 64, lcu)),
                                    dim3(2 * kErThreads), kEsLds, s, m, es, d_out, F0, F1,
                                    (const uint4 *)c->erec.as<uint4>(), c->esink.as<uint8_t>());

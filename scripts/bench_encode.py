@@ -34,8 +34,6 @@ def main():
     ap.add_argument("--hi", type=int, default=4096)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--zero-uh", action="store_true",
-                    help="pass zero-length user headers: the same bytes through k_enc_frames (one wave per frame)")
     ap.add_argument("--no-check", action="store_true",
                     help="ablation runs (wrong bytes by design): time the encode only, no decode check")
     args = ap.parse_args()
@@ -56,11 +54,6 @@ def main():
     out = torch.empty(total, dtype=torch.uint8, device=dev)
     res = torch.zeros(ctypes.sizeof(abi.EncodeResult), dtype=torch.uint8, device=dev)
     raw = abi.RawMessages(n, ids.data_ptr(), ots.data_ptr(), pay.data_ptr(), pls.data_ptr(), None, None)
-    if args.zero_uh:  # (the wire bytes are identical: every user-header length is 0)
-        uhl = torch.zeros(n, dtype=torch.int32, device=dev)
-        uhb = torch.zeros(64, dtype=torch.uint8, device=dev)
-        raw = abi.RawMessages(n, ids.data_ptr(), ots.data_ptr(), pay.data_ptr(), pls.data_ptr(), uhb.data_ptr(),
-                              uhl.data_ptr())
 
     def step():
         rc = cx.encode_device(raw, 0, out.data_ptr(), total, res.data_ptr(), s)
