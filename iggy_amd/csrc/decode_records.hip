@@ -130,13 +130,26 @@ __device__ __forceinline__ void launch_done(uint32_t *counter, uint32_t *host_fl
     }
 }
 
+// The resident service's block hand-off (k_decode_service; units == nullptr elsewhere):
+// block b > 0 of the post stores its record -- 8 partial sums, its first-bad and
+// stride-fail words, 80 B -- as 7 tagged 16-B units (the post's number, then 12 B), and
+// block 0 resolves once one load round has seen all of them. No counter, no sum
+// buffer read after it: one host-visible round trip fewer on a small record's path.
+constexpr uint32_t kSvcRecUnits = 7;
+constexpr uint32_t kSvcWgs_ = 8;  // (k_decode_service's kSvcWgs)
+struct SvcHand {
+    uint4 *units;  // [(block - 1) * kSvcRecUnits + u] (device memory, sc1)
+    uint32_t seq;
+};
+
 template <bool VERIFY>
 __device__ __forceinline__ void decode_record_block(const RecTask &inl, const uint8_t *__restrict__ base,
                                                     const RecTask *__restrict__ tasks,
                                                     const uint32_t *__restrict__ wg_task, RecState *st,
                                                     uint64_t *bsums, uint64_t *frame_pos, iggy_polled_message *msgs,
                                                     iggy_decode_result *results, uint32_t vblock = ~0u,
-                                                    const uint8_t *pre_head = nullptr, uint64_t *stamp = nullptr) {
+                                                    const uint8_t *pre_head = nullptr, uint64_t *stamp = nullptr,
+                                                    SvcHand hand = SvcHand{nullptr, 0}) {
     // (diagnostic build: stage times of thread 0 into stamp[k], the service's LDS)
     auto mark = [&](int k) {
         if (kDiagMask && stamp && threadIdx.x == 0) stamp[k] = rt_now();
@@ -201,6 +214,19 @@ __device__ __forceinline__ void decode_record_block(const RecTask &inl, const ui
     const uint64_t S = pl.S, N = pl.N, L = pl.L;
     const uint64_t nblk = rec_blocks(N);
     if (blk >= nblk) return;
+    const int64_t i0v = (int64_t)kRecFrames * blk - 6;
+    auto store_positions = [&]() {
+        if (!frame_pos) return;
+        for (uint32_t k = threadIdx.x; k < kRecFrames; k += kRecThreads) {
+            const int64_t i = i0v + k;
+            if (i >= 0 && (uint64_t)i < pl.N && (uint64_t)i < tk.pos_cap) frame_pos[tk.pos_base + i] = (uint64_t)i * pl.S;
+        }
+    };
+    // (service: the positions go out before the frame loads; their host-link acks are
+    // long in by the time the block fences them before handing over its record)
+    if (hand.units) store_positions();
+    // the resolver's per-lane constants, loaded now rather than on its critical path
+    const uint64_t rc_init = kAccInit[lane & 7], rc_key = kSecretW8[16 + (lane & 7)], rc_last = kSecretLast[lane & 7];
     const int64_t i0 = (int64_t)kRecFrames * blk - 6;
     const uint64_t base_offset = hi.h.base_offset, base_ts = hi.h.base_timestamp, origin = hi.h.origin_timestamp;
     uint64_t mybad = ~0ull, mysf = ~0ull;
@@ -344,10 +370,13 @@ __device__ __forceinline__ void decode_record_block(const RecTask &inl, const ui
         }
     }
     if (threadIdx.x == 0) s_cs[kRecFrames] = cs_next;
+    // the resolver's inputs from the record have landed by now (without this use the
+    // compiler sank their loads to the resolver, one host-link round trip on its path)
+    asm volatile("" ::"v"(r_cs0), "v"(r_lv));
     mark(2);  // (thread 0's own frames hashed)
     const uint64_t wbad = wg_min(mybad, s_min);  // (its barriers also publish s_cs)
     const uint64_t wsf = wg_min(mysf, s_min);
-    if (threadIdx.x == 0 && nblk > 1) {  // (a one-block record's own minima are final)
+    if (threadIdx.x == 0 && nblk > 1 && !hand.units) {  // (a one-block record's own minima are final)
         if (wbad != ~0ull) atomicMax((unsigned long long *)&st[t].first_bad, (unsigned long long)~wbad);
         if (wsf != ~0ull) atomicMax((unsigned long long *)&st[t].spec_fail, (unsigned long long)~wsf);
     }
@@ -361,7 +390,7 @@ __device__ __forceinline__ void decode_record_block(const RecTask &inl, const ui
                        kSecretW8[8 + (lane >> 3) + (lane & 7)], x, y);
         t8 = reduce_acc8(x, y);
         // (sc1: written through, for the resolver's sc1 loads on another CU)
-        if (lane < 8 && nblk > 1)
+        if (lane < 8 && nblk > 1 && !hand.units)
             __hip_atomic_store(&bsums[8 * (tk.bsum_base + blk) + lane], t8, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     // The last block workgroup of the record resolves it (a one-block record: its only
@@ -373,17 +402,65 @@ __device__ __forceinline__ void decode_record_block(const RecTask &inl, const ui
     // (an L2 write-back and an L1 invalidate, microseconds each) was on every small
     // record's critical path.
     __syncthreads();
-    // Frame positions (i * S; valid when the record decodes) are stored only now: ahead
-    // of the counter add, a store to host-mapped positions would put a host-link round
-    // trip into the wait before it.
-    auto store_positions = [&]() {
-        if (!frame_pos) return;
-        for (uint32_t k = threadIdx.x; k < kRecFrames; k += kRecThreads) {
-            const int64_t i = i0 + k;
-            if (i >= 0 && (uint64_t)i < N && (uint64_t)i < tk.pos_cap) frame_pos[tk.pos_base + i] = (uint64_t)i * S;
+    // Frame positions (i * S; valid when the record decodes) are stored after the
+    // counter add: ahead of it, a store to host-mapped positions would put a host-link
+    // round trip into the wait before it. (The service's blocks store them first of all,
+    // see store_positions' definition.)
+    // (service) every block's record, block 0 first: [8 sums, first-bad, stride-fail]
+    __shared__ uint64_t s_recs[kSvcWgs_ * 10];
+    bool svc_ok = true;
+    if (hand.units && nblk > 1) {
+        // (blocks > 0, every wave: its positions, stored before the frame loads, are
+        // host-visible before the block's units go out; block 0's are ordered before the
+        // flag by its completion fence. A vmcnt wait alone was measured not to be enough:
+        // positions of other blocks read back as zeros after the flag.)
+        if (blk != 0) __threadfence_system();
+        if (wave == 0) {
+            uint64_t *mine = s_recs + 10 * (blk == 0 ? 0 : 1);  // (a block > 0 stages its own record in slot 1)
+            if (lane < 8) mine[lane] = t8;
+            if (lane == 8) mine[8] = wbad != ~0ull ? ~wbad : 0ull;
+            if (lane == 9) mine[9] = wsf != ~0ull ? ~wsf : 0ull;
         }
-    };
-    if (nblk > 1) {
+        __syncthreads();
+        if (blk != 0) {
+            if (wave == 0 && lane < (int)kSvcRecUnits) {  // (LDS reads of the record's 12-B slice lane)
+                const uint32_t *r32 = (const uint32_t *)(s_recs + 10);
+                const uint32_t d0 = r32[3 * lane], d1 = r32[3 * lane + 1], d2 = lane < 6 ? r32[3 * lane + 2] : 0u;
+                const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+                    (void *)hand.units, 0, (int)(16 * kSvcRecUnits * kSvcWgs_), 0x00020000);
+                const g4 w = {hand.seq, d0, d1, d2};
+                __builtin_amdgcn_raw_buffer_store_b128(w, rs, 16u * (kSvcRecUnits * (blk - 1) + (uint32_t)lane), 0,
+                                                       kAuxSc1);
+            }
+            return;
+        }
+        if (wave != 0) return;
+        // block 0 resolves: one sc1 load round per poll over every other block's units
+        const uint32_t nu = kSvcRecUnits * (uint32_t)(nblk - 1);
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+            (void *)hand.units, 0, (int)(16 * kSvcRecUnits * kSvcWgs_), 0x00020000);
+        const uint64_t tw = rt_now();
+        for (;;) {
+            const g4 v = (uint32_t)lane < nu ? __builtin_amdgcn_raw_buffer_load_b128(rs, 16u * (uint32_t)lane, 0, kAuxSc1)
+                                             : g4{hand.seq, 0, 0, 0};
+            if (__ballot(v.x != hand.seq) == 0) {
+                if ((uint32_t)lane < nu) {  // unit u of block b + 1 into slot b + 1
+                    const uint32_t b = (uint32_t)lane / kSvcRecUnits, u = (uint32_t)lane % kSvcRecUnits;
+                    uint32_t *r32 = (uint32_t *)(s_recs + 10 * (b + 1)) + 3 * u;
+                    r32[0] = v.y;
+                    r32[1] = v.z;
+                    if (u < 6) r32[2] = v.w;
+                }
+                break;
+            }
+            if (rt_now() - tw > kSpinLimitTicks) {  // (bug guard: a block never arrived)
+                svc_ok = false;
+                break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+        }
+        __builtin_amdgcn_s_waitcnt(0);  // (the slots' LDS writes, before the chain reads them)
+    } else if (nblk > 1) {
         if (threadIdx.x == 0) {
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // wave 0's block sums and minima
             const uint32_t old = __hip_atomic_fetch_add(&st[t].done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -393,7 +470,7 @@ __device__ __forceinline__ void decode_record_block(const RecTask &inl, const ui
         __syncthreads();
         if (!s_last || wave != 0) return;
     } else {
-        store_positions();
+        if (!hand.units) store_positions();  // (the service's went out first)
         if (wave != 0) return;
     }
 
@@ -401,15 +478,23 @@ __device__ __forceinline__ void decode_record_block(const RecTask &inl, const ui
     // block sums (one memory round trip, not two)
     mark(3);
     // (one block: this workgroup's own minima and partial sums, no memory round trip)
-    const uint64_t fb_enc = nblk > 1 ? __hip_atomic_load(&st[t].first_bad, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                                     : (wbad != ~0ull ? ~wbad : 0ull);
-    const uint64_t sf_enc = nblk > 1 ? __hip_atomic_load(&st[t].spec_fail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                                     : (wsf != ~0ull ? ~wsf : 0ull);
+    uint64_t fb_enc = 0, sf_enc = 0;
+    if (hand.units && nblk > 1) {  // (service) the blocks' records, max-encoded minima
+        for (uint64_t b = 0; b < nblk; ++b) {
+            fb_enc = max(fb_enc, s_recs[10 * b + 8]);
+            sf_enc = max(sf_enc, s_recs[10 * b + 9]);
+        }
+    } else {
+        fb_enc = nblk > 1 ? __hip_atomic_load(&st[t].first_bad, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                          : (wbad != ~0ull ? ~wbad : 0ull);
+        sf_enc = nblk > 1 ? __hip_atomic_load(&st[t].spec_fail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                          : (wsf != ~0ull ? ~wsf : 0ull);
+    }
     uint64_t computed = 0;
     if (VERIFY && pl.long_cs) {
         const int j = lane & 7;
-        uint64_t acc = kAccInit[j];
-        const uint64_t key = kSecretW8[16 + j];
+        uint64_t acc = rc_init;
+        const uint64_t key = rc_key;
         const uint32_t klo = (uint32_t)key, khi = (uint32_t)(key >> 32);
         {  // words 0..5: header fields, then count | lo32(cs_0)
             const uint64_t cs0 = __shfl(r_cs0, 0);
@@ -428,7 +513,9 @@ __device__ __forceinline__ void decode_record_block(const RecTask &inl, const ui
         const uint64_t nb = pl.nb;
         const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
             (void *)(bsums + 8 * tk.bsum_base), 0, (int)min<uint64_t>(64 * (nb + 1), 1u << 30), 0x00020000);
+        const bool from_lds = hand.units != nullptr;  // (service: the records the poll staged)
         auto sum_at = [&](uint64_t b) -> uint64_t {  // (lane j: sum j of block b)
+            if (from_lds) return s_recs[10 * b + j];
             const rec_g2 r = __builtin_amdgcn_raw_buffer_load_b64(rs, (uint32_t)(64 * b + 8 * j), 0, kAuxSc1);
             return (uint64_t)r.x | ((uint64_t)r.y << 32);
         };
@@ -446,7 +533,7 @@ __device__ __forceinline__ void decode_record_block(const RecTask &inl, const ui
         // last stripe = stored checksums of frames N-8 .. N-1 (secret offset 121)
         const uint64_t lv = __shfl(r_lv, j);
         acc += __shfl_xor(lv, 1);
-        acc += mul32x32(lv ^ kSecretLast[j]);
+        acc += mul32x32(lv ^ rc_last);
         uint64_t a[8];
 #pragma unroll
         for (int i = 0; i < 8; ++i) a[i] = __shfl(acc, i);
@@ -469,7 +556,7 @@ __device__ __forceinline__ void decode_record_block(const RecTask &inl, const ui
     mark(4);
     // precedence, as the uniform kernel's consumer (batch.rs:395-421, 461-506)
     // every block workgroup of the record has arrived: re-arm its state for the next launch
-    if (nblk > 1) {
+    if (nblk > 1 && !hand.units) {
         __hip_atomic_store(&st[t].first_bad, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(&st[t].spec_fail, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(&st[t].done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -504,6 +591,9 @@ __device__ __forceinline__ void decode_record_block(const RecTask &inl, const ui
     } else if (VERIFY && computed != hi.h.batch_checksum) {
         kind = IGGY_ERR_INVALID_BATCH_CHECKSUM;
         a = hi.h.batch_checksum; b = computed; c = hi.h.base_offset;
+    }
+    if (!svc_ok) {  // (service: a block's record never arrived -- the bug guard)
+        kind = IGGY_ERR_TIMEOUT; reason = 0; a = b = c = 0; status = kStatusDone;
     }
     write_result(res, hi, kind, reason, a, b, c, nframes, computed, 1, status, nframes * S);
     mark(5);
@@ -548,7 +638,7 @@ __global__ __launch_bounds__(kRecThreads) void k_decode_records(const uint8_t *_
 // without a post, or the bug guard), and the followers stop on its word, so a post is
 // decoded by all of its workgroups or by none (the host relaunches and re-posts it
 // then). On its way out the leader clears the mailbox's `alive` word.
-constexpr uint32_t kSvcWgs = 8;                       // records of <= 8 blocks (C1: 1 000 frames)
+constexpr uint32_t kSvcWgs = kSvcWgs_;                // records of <= 8 blocks (C1: 1 000 frames)
 constexpr uint32_t kSvcPre = 26;                      // 12-B pieces of the record's first 304 B
 constexpr uint64_t kSvcIdleTicks = 100000ull * 20;    // 20 ms without a post: exit
 // Host-mapped mailbox: 8 chunks of 16 B, read by the leader's wave in ONE round of loads
@@ -582,10 +672,11 @@ constexpr uint32_t kSvcUnits = 6 + kSvcPre;
 struct SvcCtl {                        // device memory, zeroed before every launch
     uint4 unit[kSvcUnits];             // the relayed post (tagged units, see above)
     uint32_t exit, _e[3];              // unit kSvcUnits: the leader's exit word (1 = exit)
-    uint32_t counter, _c[3];           // workgroups done with the current post
+    uint32_t counter, _c[3];           // (unused since the block hand-off below)
     uint32_t diag[4];                  // (diagnostic build) when the leader saw the post
+    uint4 rec[kSvcRecUnits * (kSvcWgs - 1)];  // blocks 1.. of the current post hand their records to block 0 (SvcHand)
 };
-static_assert(sizeof(SvcCtl) == 16 * kSvcUnits + 48, "control block layout");
+static_assert(sizeof(SvcCtl) == 16 * kSvcUnits + 48 + 16 * kSvcRecUnits * (kSvcWgs - 1), "control block layout");
 constexpr int kAuxSys = 17;  // buffer-load cache policy sc0 | sc1: system-coherent (host-mapped memory)
 
 __device__ __forceinline__ uint4 svc_chunk_sys(const SvcMailbox *mb, uint32_t c) {
@@ -722,29 +813,26 @@ __global__ __launch_bounds__(kRecThreads) void k_decode_service(SvcMailbox *mb, 
             uint64_t *fpos = (uint64_t *)u64(c3);
             iggy_decode_result *res = (iggy_decode_result *)u64(c4);
             uint32_t *flag = (uint32_t *)u64(c5);
+            const SvcHand hand{ctl->rec, c0.x};  // (the post's number tags its blocks' records)
             if (integ == IGGY_INTEGRITY_VERIFY)
                 decode_record_block<true>(tk, base, nullptr, nullptr, st, bsums, fpos, nullptr, res, blockIdx.x, s_pre,
-                                          kDiagMask ? s_stamp : nullptr);
+                                          kDiagMask ? s_stamp : nullptr, hand);
             else
                 decode_record_block<false>(tk, base, nullptr, nullptr, st, bsums, fpos, nullptr, res, blockIdx.x, s_pre,
-                                           kDiagMask ? s_stamp : nullptr);
-            // completion, as launch_done over the post's nwg workgroups (one workgroup: its
-            // own fence orders every host-visible write before the flag)
-            __threadfence_system();
-            if (kDiagMask && threadIdx.x == 0) s_stamp[6] = rt_now();
-            __syncthreads();
-            if (nwg == 1) {
+                                           kDiagMask ? s_stamp : nullptr, hand);
+            // Completion: block 0 resolved the post after every other block had fenced its
+            // host-visible writes at system scope and handed over its record, so its own
+            // fence orders the verdict, and with it every position, before the flag.
+            if (blockIdx.x == 0) {
+                __threadfence_system();
+                if (kDiagMask && threadIdx.x == 0) s_stamp[6] = rt_now();
+                __syncthreads();
                 if (kDiagMask && threadIdx.x == 0) {
+                    s_stamp[7] = rt_now();  // (no counter round any more: "counted" = fenced)
                     svc_stamp(mb, ctl, s_stamp);
                     __threadfence_system();
                 }
-                if (threadIdx.x == 0) __hip_atomic_store(flag, flag_value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-            } else if (threadIdx.x == 0 && atomicAdd(&ctl->counter, 1u) == nwg - 1) {
-                // every workgroup fenced its host-visible writes at system scope before it
-                // counted, so the last one's flag needs no second fence
-                __hip_atomic_store(&ctl->counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                if (kDiagMask) svc_stamp(mb, ctl, s_stamp);
-                __hip_atomic_store(flag, flag_value, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+                if (threadIdx.x == 0) __hip_atomic_store(flag, flag_value, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
             }
         }
         __syncthreads();  // (s_cmd / s_chunk are rewritten by the next relay)
