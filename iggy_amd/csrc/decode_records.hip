@@ -131,11 +131,15 @@ __device__ __forceinline__ void launch_done(uint32_t *counter, uint32_t *host_fl
 }
 
 // The resident service's block hand-off (k_decode_service; units == nullptr elsewhere):
-// block b > 0 of the post stores its record -- 8 partial sums, its first-bad and
-// stride-fail words, 80 B -- as 7 tagged 16-B units (the post's number, then 12 B), and
-// block 0 resolves once one load round has seen all of them. No counter, no sum
-// buffer read after it: one host-visible round trip fewer on a small record's path.
-constexpr uint32_t kSvcRecUnits = 7;
+// block b > 0 of the post stores its record -- 8 partial sums and the low words of its
+// first-bad and stride-fail encodings, 18 dwords -- as 9 16-B units of two 8-B granules
+// {the post's number, one dword} each, and block 0 resolves once one load round has seen
+// the number in every granule. Each 8-B half of a 16-B sc1 store is observed untorn,
+// the whole 16 B is not (MI355X_MICROARCH.md: granules): a unit {number, 12 B} let a
+// load see the new number beside a stale second half -- the previous post's first-bad
+// word, a corrupt frame passed as clean. No counter, no sum buffer read after it: one
+// host-visible round trip fewer on a small record's path.
+constexpr uint32_t kSvcRecUnits = 9;
 constexpr uint32_t kSvcWgs_ = 8;  // (k_decode_service's kSvcWgs)
 struct SvcHand {
     uint4 *units;  // [(block - 1) * kSvcRecUnits + u] (device memory, sc1)
@@ -410,11 +414,12 @@ __device__ __forceinline__ void decode_record_block(const RecTask &inl, const ui
     __shared__ uint64_t s_recs[kSvcWgs_ * 10];
     bool svc_ok = true;
     if (hand.units && nblk > 1) {
-        // (blocks > 0, every wave: its positions, stored before the frame loads, are
-        // host-visible before the block's units go out; block 0's are ordered before the
-        // flag by its completion fence. A vmcnt wait alone was measured not to be enough:
-        // positions of other blocks read back as zeros after the flag.)
-        if (blk != 0) __threadfence_system();
+        // (blocks > 0, every wave, when the post asked for positions in host memory: they
+        // are host-visible before the block's units go out; block 0's are ordered before
+        // the flag by its completion fence. A vmcnt wait alone was measured not to be
+        // enough: positions of other blocks read back as zeros after the flag. The host's
+        // own posts ask for none, see svc_post_wait.)
+        if (blk != 0 && frame_pos) __threadfence_system();
         if (wave == 0) {
             uint64_t *mine = s_recs + 10 * (blk == 0 ? 0 : 1);  // (a block > 0 stages its own record in slot 1)
             if (lane < 8) mine[lane] = t8;
@@ -423,12 +428,14 @@ __device__ __forceinline__ void decode_record_block(const RecTask &inl, const ui
         }
         __syncthreads();
         if (blk != 0) {
-            if (wave == 0 && lane < (int)kSvcRecUnits) {  // (LDS reads of the record's 12-B slice lane)
+            if (wave == 0 && lane < (int)kSvcRecUnits) {  // (LDS reads: dwords 2 lane, 2 lane + 1)
                 const uint32_t *r32 = (const uint32_t *)(s_recs + 10);
-                const uint32_t d0 = r32[3 * lane], d1 = r32[3 * lane + 1], d2 = lane < 6 ? r32[3 * lane + 2] : 0u;
+                // (unit 8: the low words of the first-bad and stride-fail encodings; a frame
+                // index < 2^32 leaves their high words all ones, and none encodes as 0)
+                const uint32_t d0 = lane < 8 ? r32[2 * lane] : r32[16], d1 = lane < 8 ? r32[2 * lane + 1] : r32[18];
                 const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-                    (void *)hand.units, 0, (int)(16 * kSvcRecUnits * kSvcWgs_), 0x00020000);
-                const g4 w = {hand.seq, d0, d1, d2};
+                    (void *)hand.units, 0, (int)(16 * kSvcRecUnits * (kSvcWgs_ - 1)), 0x00020000);
+                const g4 w = {hand.seq, d0, hand.seq, d1};
                 __builtin_amdgcn_raw_buffer_store_b128(w, rs, 16u * (kSvcRecUnits * (blk - 1) + (uint32_t)lane), 0,
                                                        kAuxSc1);
             }
@@ -438,18 +445,21 @@ __device__ __forceinline__ void decode_record_block(const RecTask &inl, const ui
         // block 0 resolves: one sc1 load round per poll over every other block's units
         const uint32_t nu = kSvcRecUnits * (uint32_t)(nblk - 1);
         const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-            (void *)hand.units, 0, (int)(16 * kSvcRecUnits * kSvcWgs_), 0x00020000);
+            (void *)hand.units, 0, (int)(16 * kSvcRecUnits * (kSvcWgs_ - 1)), 0x00020000);
         const uint64_t tw = rt_now();
         for (;;) {
             const g4 v = (uint32_t)lane < nu ? __builtin_amdgcn_raw_buffer_load_b128(rs, 16u * (uint32_t)lane, 0, kAuxSc1)
-                                             : g4{hand.seq, 0, 0, 0};
-            if (__ballot(v.x != hand.seq) == 0) {
+                                             : g4{hand.seq, 0, hand.seq, 0};
+            if (__ballot(v.x != hand.seq || v.z != hand.seq) == 0) {
                 if ((uint32_t)lane < nu) {  // unit u of block b + 1 into slot b + 1
                     const uint32_t b = (uint32_t)lane / kSvcRecUnits, u = (uint32_t)lane % kSvcRecUnits;
-                    uint32_t *r32 = (uint32_t *)(s_recs + 10 * (b + 1)) + 3 * u;
-                    r32[0] = v.y;
-                    r32[1] = v.z;
-                    if (u < 6) r32[2] = v.w;
+                    uint64_t *slot = s_recs + 10 * (b + 1);
+                    if (u < 8) {
+                        slot[u] = (uint64_t)v.y | ((uint64_t)v.w << 32);
+                    } else {
+                        slot[8] = v.y ? (0xFFFFFFFF00000000ull | v.y) : 0ull;
+                        slot[9] = v.w ? (0xFFFFFFFF00000000ull | v.w) : 0ull;
+                    }
                 }
                 break;
             }
@@ -661,22 +671,24 @@ struct SvcMailbox {
     uint64_t diag[8];  // (diagnostic build: stage times of the post, ticks after the leader saw it)
 };
 static_assert(sizeof(SvcMailbox) == 128 + 16 * kSvcPre + 64, "mailbox layout");
-// The leader relays a post to the followers as the mailbox's own tagged units, copied
-// verbatim: units 0-5 the post's chunks, 6-31 the 26 prefix pieces, each 16-B unit
-// carrying the post's sequence number in its first word. A follower's poll is one round
-// of sc1 loads of all of them (and the exit word): a round that sees one new number in
-// all 32 saw the whole relay (a 16-B sc1 store is observed whole). Round 6: the relay
-// had been a go word behind a release, read behind an acquire and re-checked behind a
-// second one, ~1.9 us from the leader seeing the post to the followers starting.
-constexpr uint32_t kSvcUnits = 6 + kSvcPre;
+// Every workgroup keeps the post in LDS as kSvcPost dwords: the record's first 304 B
+// (dwords 0-75, the block code's pre_head), then chunks 0-5's words y, z, w (76-93).
+// The leader relays them to the followers as 47 16-B units of two 8-B granules
+// {the post's sequence number, one dword} each. A follower's poll is one round of sc1
+// loads of all of them (and the exit word): a round that sees one new number in all 94
+// granules saw the whole relay. Each 8-B half of a 16-B sc1 store is observed untorn,
+// the whole 16 B is not (see kSvcRecUnits). Round 6: the relay had been a go word
+// behind a release, read behind an acquire and re-checked behind a second one, ~1.9 us
+// from the leader seeing the post to the followers starting.
+constexpr uint32_t kSvcPost = 76 + 18;
+constexpr uint32_t kSvcUnits = kSvcPost / 2;
 struct SvcCtl {                        // device memory, zeroed before every launch
-    uint4 unit[kSvcUnits];             // the relayed post (tagged units, see above)
+    uint4 unit[kSvcUnits];             // the relayed post (tagged granules, see above)
     uint32_t exit, _e[3];              // unit kSvcUnits: the leader's exit word (1 = exit)
-    uint32_t counter, _c[3];           // (unused since the block hand-off below)
     uint32_t diag[4];                  // (diagnostic build) when the leader saw the post
     uint4 rec[kSvcRecUnits * (kSvcWgs - 1)];  // blocks 1.. of the current post hand their records to block 0 (SvcHand)
 };
-static_assert(sizeof(SvcCtl) == 16 * kSvcUnits + 48 + 16 * kSvcRecUnits * (kSvcWgs - 1), "control block layout");
+static_assert(sizeof(SvcCtl) == 16 * kSvcUnits + 32 + 16 * kSvcRecUnits * (kSvcWgs - 1), "control block layout");
 constexpr int kAuxSys = 17;  // buffer-load cache policy sc0 | sc1: system-coherent (host-mapped memory)
 
 __device__ __forceinline__ uint4 svc_chunk_sys(const SvcMailbox *mb, uint32_t c) {
@@ -709,8 +721,7 @@ __device__ __forceinline__ void svc_stamp(SvcMailbox *mb, SvcCtl *ctl, uint64_t 
 __global__ __launch_bounds__(kRecThreads) void k_decode_service(SvcMailbox *mb, uint32_t start_seq, SvcCtl *ctl,
                                                                 RecState *st, uint64_t *bsums) {
     __shared__ uint32_t s_cmd;
-    __shared__ uint4 s_chunk[6];
-    __shared__ __attribute__((aligned(16))) uint8_t s_pre[16 * 19];  // the record's first 304 B
+    __shared__ __attribute__((aligned(16))) uint32_t s_post[kSvcPost + 2];  // (see kSvcPost; [kSvcPost]: its number)
     __shared__ uint64_t s_stamp[8];  // (diagnostic build)
     const int lane = threadIdx.x & 63;
     const uint32_t wave = threadIdx.x >> 6;
@@ -733,13 +744,21 @@ __global__ __launch_bounds__(kRecThreads) void k_decode_service(SvcMailbox *mb, 
                     const uint32_t s0 = (uint32_t)__shfl((int)v.x, 0);
                     if (s0 != 0 && s0 != seen && __ballot(tagged && v.x != s0) == 0) {  // a whole new post
                         const bool relay = (uint32_t)__shfl((int)v.y, 1) > 1;  // (a one-block post is the leader's alone)
-                        if (lane < 6) s_chunk[lane] = v;
+                        if (lane < 6) {  // chunk lane's words
+                            uint32_t *d = s_post + 76 + 3u * (uint32_t)lane;
+                            d[0] = v.y; d[1] = v.z; d[2] = v.w;
+                        }
                         if (lane >= 8 && lane < 8 + (int)kSvcPre) {  // 12-B piece lane - 8 of the prefix
-                            uint32_t *d = (uint32_t *)s_pre + 3u * (uint32_t)(lane - 8);  // (76 dwords)
+                            uint32_t *d = s_post + 3u * (uint32_t)(lane - 8);  // (76 dwords)
                             d[0] = v.y;
                             if (lane < 8 + (int)kSvcPre - 1) { d[1] = v.z; d[2] = v.w; }
                         }
-                        if (relay && tagged) svc_unit_store(ctl, lane < 6 ? (uint32_t)lane : (uint32_t)lane - 2u, v);
+                        if (lane == 0) s_post[kSvcPost] = s0;
+                        // (this wave's own LDS writes have landed; the memory clobber keeps
+                        // the reads below after them)
+                        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                        if (relay && lane < (int)kSvcUnits)
+                            svc_unit_store(ctl, (uint32_t)lane, make_uint4(s0, s_post[2 * lane], s0, s_post[2 * lane + 1]));
                         if (kDiagMask && lane == 0) {  // (diagnostic build: when the post was seen)
                             const uint64_t t = rt_now();
                             ctl->diag[0] = (uint32_t)t;
@@ -781,13 +800,12 @@ __global__ __launch_bounds__(kRecThreads) void k_decode_service(SvcMailbox *mb, 
                     const uint4 v = lane <= (int)kSvcUnits ? svc_unit_dev(ctl, (uint32_t)lane) : make_uint4(0, 0, 0, 0);
                     if (__shfl((int)v.x, kSvcUnits)) break;  // the leader exits
                     const uint32_t s0 = (uint32_t)__shfl((int)v.x, 0);
-                    if (s0 != 0 && s0 != seen && __ballot(lane < (int)kSvcUnits && v.x != s0) == 0) {
-                        if (lane < 6) s_chunk[lane] = v;
-                        if (lane >= 6 && lane < (int)kSvcUnits) {  // prefix piece lane - 6
-                            uint32_t *d = (uint32_t *)s_pre + 3u * (uint32_t)(lane - 6);
-                            d[0] = v.y;
-                            if (lane < (int)kSvcUnits - 1) { d[1] = v.z; d[2] = v.w; }
+                    if (s0 != 0 && s0 != seen && __ballot(lane < (int)kSvcUnits && (v.x != s0 || v.z != s0)) == 0) {
+                        if (lane < (int)kSvcUnits) {
+                            s_post[2 * lane] = v.y;
+                            s_post[2 * lane + 1] = v.w;
                         }
+                        if (lane == 0) s_post[kSvcPost] = s0;
                         seen = s0;
                         cmd = 1;
                         break;
@@ -801,19 +819,20 @@ __global__ __launch_bounds__(kRecThreads) void k_decode_service(SvcMailbox *mb, 
         __syncthreads();
         if (s_cmd != 1) break;
         t_idle = rt_now();
-        const uint4 c0 = s_chunk[0], c1 = s_chunk[1], c2 = s_chunk[2], c3 = s_chunk[3], c4 = s_chunk[4],
-                    c5 = s_chunk[5];
-        const uint32_t integ = c0.y, nwg = c1.y, flag_value = c2.y;
-        auto u64 = [](const uint4 &c) { return (uint64_t)c.z | ((uint64_t)c.w << 32); };
+        // chunk k's words: y = s_post[76 + 3k], z | w << 32 = u64(k)
+        const uint32_t *cw = s_post + 76;
+        const uint32_t integ = cw[0], nwg = cw[3], flag_value = cw[6];
+        auto u64 = [&](int k) { return (uint64_t)cw[3 * k + 1] | ((uint64_t)cw[3 * k + 2] << 32); };
         if (blockIdx.x < nwg && nwg <= kSvcWgs) {
             RecTask tk;
-            tk.off = 0; tk.len = u64(c0); tk.pos_base = 0; tk.pos_cap = u64(c1); tk.msg_base = 0;
+            tk.off = 0; tk.len = u64(0); tk.pos_base = 0; tk.pos_cap = u64(1); tk.msg_base = 0;
             tk.bsum_base = 0; tk.wg0 = 0; tk.nwg = nwg;
-            const uint8_t *base = (const uint8_t *)u64(c2);
-            uint64_t *fpos = (uint64_t *)u64(c3);
-            iggy_decode_result *res = (iggy_decode_result *)u64(c4);
-            uint32_t *flag = (uint32_t *)u64(c5);
-            const SvcHand hand{ctl->rec, c0.x};  // (the post's number tags its blocks' records)
+            const uint8_t *base = (const uint8_t *)u64(2);
+            uint64_t *fpos = (uint64_t *)u64(3);
+            iggy_decode_result *res = (iggy_decode_result *)u64(4);
+            uint32_t *flag = (uint32_t *)u64(5);
+            const uint8_t *s_pre = (const uint8_t *)s_post;
+            const SvcHand hand{ctl->rec, s_post[kSvcPost]};  // (the post's number tags its blocks' records)
             if (integ == IGGY_INTEGRITY_VERIFY)
                 decode_record_block<true>(tk, base, nullptr, nullptr, st, bsums, fpos, nullptr, res, blockIdx.x, s_pre,
                                           kDiagMask ? s_stamp : nullptr, hand);
@@ -835,7 +854,14 @@ __global__ __launch_bounds__(kRecThreads) void k_decode_service(SvcMailbox *mb, 
                 if (threadIdx.x == 0) __hip_atomic_store(flag, flag_value, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
             }
         }
-        __syncthreads();  // (s_cmd / s_chunk are rewritten by the next relay)
+        // Every workgroup drops what its caches hold of the record before the next post:
+        // the host rewrites its buffers between calls (a pageable record goes through the
+        // same mapped staging every time), and the next post's in-place loads would hit
+        // this one's lines -- a corrupt frame judged on the clean bytes of the call before
+        // (measured). The launch path gets this from every launch's acquire. Here it comes
+        // after the flag (block 0) or the hand-over (the others): off the post's path.
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+        __syncthreads();  // (s_cmd / s_post are rewritten by the next relay)
     }
     if (blockIdx.x == 0 && threadIdx.x == 0)
         __hip_atomic_store(&mb->alive, 0u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);

@@ -476,7 +476,7 @@ int svc_post_wait(iggy_codec_ctx *c, const uint8_t *d_base, const uint8_t *host_
     mb->len = len;
     mb->pos_cap = pcap;
     mb->base = d_base;
-    mb->frame_pos = pcap ? c->omap.dp<uint64_t>(192) : nullptr;
+    mb->frame_pos = pcap ? c->omap.dp<uint64_t>(192) : nullptr;  // (decode_host_fast passes 0)
     mb->result = c->omap.dp<iggy_decode_result>(64);
     mb->host_flag = c->omap.dp<uint32_t>();
     // the record's first 304 B (zero past its end), 12 B per tagged piece
@@ -561,10 +561,16 @@ int decode_host_fast(iggy_codec_ctx *c, const uint8_t *body, uint64_t len, int i
     std::vector<size_t> single;
     const uint32_t v = next_flag(c);
     const uint64_t nwg = rec_blocks(nf);
+    bool svc_pos = false;
     if (c->svc.enabled && nf && nwg <= kSvcWgs && len <= kZeroCopyBytes) {
         // the resident service: no launch (d_base is host memory the device reads in place)
+        // No positions from the device: a record the service decodes is single-stride
+        // (every frame's header was checked against the stride S), so its positions are
+        // i * S, written below from the verdict -- no blocks fencing 8 KB of host-mapped
+        // stores before they hand over, no copy of them back out of the mapped buffer.
         tmark(1);
-        r = svc_post_wait(c, d_base, body, len, integrity, (uint32_t)nwg, pcap, v);
+        r = svc_post_wait(c, d_base, body, len, integrity, (uint32_t)nwg, 0, v);
+        svc_pos = true;
     } else {
         r = enqueue_records(c, d_base, body, &rec, 1, integrity,
                             pcap ? c->omap.dp<uint64_t>(192) : nullptr, nullptr, c->omap.dp<iggy_decode_result>(64),
@@ -579,8 +585,15 @@ int decode_host_fast(iggy_codec_ctx *c, const uint8_t *body, uint64_t len, int i
     const iggy_decode_result res = *c->omap.hp<iggy_decode_result>(64);
     if (res.status == kStatusNeedGeneral) return 0;
     *res_out = res;
-    if (frame_pos && pcap && res.error.kind == IGGY_OK)
-        memcpy(frame_pos, c->omap.hp<uint64_t>(192), std::min<uint64_t>(res.frame_count, pcap) * 8);
+    if (frame_pos && pcap && res.error.kind == IGGY_OK) {
+        const uint64_t n = std::min<uint64_t>(res.frame_count, pcap);
+        if (svc_pos) {
+            const uint64_t S = res.frame_count ? (res.header.batch_length - kHdr) / res.frame_count : 0;
+            for (uint64_t i = 0; i < n; ++i) frame_pos[i] = i * S;
+        } else {
+            memcpy(frame_pos, c->omap.hp<uint64_t>(192), n * 8);
+        }
+    }
     *done = true;
     tmark(3);
     if (timing && ++tn == timing) {

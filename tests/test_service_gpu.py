@@ -89,6 +89,44 @@ def test_service_matches_oracle(cx, registered):
 
 
 @pytest.mark.parametrize("registered", [False, True])
+def test_service_back_to_back_posts_of_one_shape(cx, registered):
+    """Records of one shape posted back to back, each verdict judged against its own
+    oracle result: a clean record, the same with one payload bit of a late block flipped
+    (its stored checksums unchanged, so only that block's first-bad word tells them
+    apart), and the same with another base offset (only the relayed prefix differs).
+    A stale relay granule or block record from the previous post would pass one for the
+    other."""
+    from iggy_amd.codec import host_buffer, page_aligned
+    clean = O.synth_batch(1000, 256, seed=51)
+    bad = clean.copy()
+    bad[256 + 304 * 990 + 200] ^= 0x01                  # frame 990: block 7, the last
+    moved = clean.copy()
+    moved[8:16].view(np.uint64)[0] += 1000
+    recs = [page_aligned(r) for r in (clean, bad, moved)]
+    wants = [O.decode_batch_slice_with(r, abi.INTEGRITY_VERIFY) for r in recs]
+    assert wants[0][0] == 0 and wants[1][0] != 0
+    pos = host_buffer(clean.size // 48 + 1, np.uint64)
+    if registered:
+        for a in recs + [pos]:
+            cx.host_register(a)
+    try:
+        cx.service_start()
+        h, e = abi.BatchHeader(), abi.WireError()
+        for k in range(300):
+            i = (k * 7 + k // 3) % 3
+            rc, nf = cx.decode_batch_into(recs[i], abi.INTEGRITY_VERIFY, pos, h, e)
+            want = wants[i]
+            assert rc == want[0] and e.astuple() == want[1].astuple() and h.astuple() == want[2].astuple(), (k, i, rc)
+            if rc == 0:
+                assert nf == len(want[3]) and np.array_equal(pos[:nf], np.asarray(want[3], dtype=np.uint64))
+        cx.service_stop()
+    finally:
+        if registered:
+            for a in recs + [pos]:
+                cx.host_unregister(a)
+
+
+@pytest.mark.parametrize("registered", [False, True])
 def test_service_header_prefix_follows_each_post(cx, registered):
     """The post carries the record's first 304 B (batch header + frame 0's header) to
     the workgroups: the same buffer rewritten between calls (header fields, a reserved
