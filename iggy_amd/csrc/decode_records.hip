@@ -267,10 +267,12 @@ __device__ __forceinline__ void decode_record_block(const RecTask &inl, const ui
         const uint64_t nbF = pl.nbF, ns = pl.ns;
         // one frame's hash from its loaded pieces (the last, partial block and the last
         // stripe), the header checks and the outputs
-        auto finish = [&](uint32_t k, int64_t i, bool valid, uint4 hdr, uint64_t stored, uint64_t a0, uint64_t a1,
-                          const uint4 *pc, uint4 lastp) {
+        // (QT: the pieces pc holds, 2 or 8; a frame needs piece q when 2 q + par < ns)
+        auto finish = [&](auto QT, uint32_t k, int64_t i, bool valid, uint4 hdr, uint64_t stored, uint64_t a0,
+                          uint64_t a1, const uint4 *pc, uint4 lastp) {
+            constexpr int Q = decltype(QT)::value;
 #pragma unroll
-            for (int q = 0; q < 8; ++q)
+            for (int q = 0; q < Q; ++q)
                 if (2 * (uint64_t)q + par < ns) piece(a0, a1, pc[q], s0[q], s1[q]);
             a0 += gdpp64<0xB1>(a0);
             a1 += gdpp64<0xB1>(a1);
@@ -292,28 +294,53 @@ __device__ __forceinline__ void decode_record_block(const RecTask &inl, const ui
             // the hashes -- one memory round trip instead of four (a registered record
             // is read in place over the host link, where each round trip is microseconds)
             constexpr uint32_t K = kRecFrames / 32;
-            uint4 hdr[K], pc[K][8], lastp[K];
-            uint64_t stored[K];
-            // (no loads for the slots past the record's ends: a small record read in place
-            // would otherwise fetch frame 0 again over the host link for each of them)
+            // Buffer loads over the block's own frames, a piece a lane does not need given an
+            // offset past the range (the load returns zeros and fetches nothing: a small
+            // record read in place does not fetch frame 0 again over the host link for every
+            // slot past its end). No branch around any load, and frames of at most 4 stripes
+            // (C1's 296 B) hold 2 pieces a lane, not 8, so the loads land in VGPRs: the
+            // compiler then waits for each frame's own pieces (vmcnt(n)) and frame k's hash
+            // runs while frames k + 1.. are still on the way. Loads behind branches had been
+            // waited for all at once before the first hash.
+            const int64_t f0 = i0 < 0 ? 0 : i0;
+            const int64_t f1 = min<int64_t>(i0 + (int64_t)kRecFrames, (int64_t)N);
+            const __amdgpu_buffer_rsrc_t frs = __builtin_amdgcn_make_buffer_rsrc(
+                (void *)(blob + (uint64_t)f0 * S), 0, (int)((uint64_t)(f1 - f0) * S), 0x00020000);
+            constexpr uint32_t kOff = 0x80000000u;  // (past any block's range)
+            auto frames = [&](auto QT) {
+                constexpr int Q = decltype(QT)::value;
+                uint4 hdr[K], pc[K][Q], lastp[K];
+                uint64_t stored[K];
 #pragma unroll
-            for (uint32_t k = 0; k < K; ++k) {
-                const int64_t i = i0 + g + 32 * k;
-                const bool valid = i >= 0 && (uint64_t)i < N;
-                const uint8_t *fb = blob + (valid ? (uint64_t)i : 0) * S;
-                const uint8_t *hb = fb + 8 + poff;
-                hdr[k] = valid && l == 0 ? ld128_any(fb + 32) : make_uint4(0, 0, 0, 0);
-                stored[k] = valid && l == 0 ? ld64_any(fb) : 0;
+                for (uint32_t k = 0; k < K; ++k) {
+                    const int64_t i = i0 + g + 32 * k;
+                    const bool valid = i >= 0 && (uint64_t)i < N;
+                    const uint32_t fo = valid ? (uint32_t)((uint64_t)(i - f0) * S) : kOff;
+                    const uint32_t ho = fo + 8 + poff;
+                    const g4 h4 = __builtin_amdgcn_raw_buffer_load_b128(frs, l == 0 ? fo + 32 : kOff, 0, 0);
+                    hdr[k] = make_uint4(h4.x, h4.y, h4.z, h4.w);
+                    const rec_g2 s2 = __builtin_amdgcn_raw_buffer_load_b64(frs, l == 0 ? fo : kOff, 0, 0);
+                    stored[k] = (uint64_t)s2.x | ((uint64_t)s2.y << 32);
 #pragma unroll
-                for (int q = 0; q < 8; ++q)
-                    pc[k][q] = valid && (2 * (uint64_t)q + par < ns) ? ld128_any(hb + 128 * q) : make_uint4(0, 0, 0, 0);
-                lastp[k] = valid && !par ? ld128_any(fb + 8 + L - 64 + 16 * m) : make_uint4(0, 0, 0, 0);
-            }
+                    for (int q = 0; q < Q; ++q) {
+                        const g4 p4 = __builtin_amdgcn_raw_buffer_load_b128(
+                            frs, (2 * (uint64_t)q + par < ns) ? ho + 128 * q : kOff, 0, 0);
+                        pc[k][q] = make_uint4(p4.x, p4.y, p4.z, p4.w);
+                    }
+                    const g4 l4 = __builtin_amdgcn_raw_buffer_load_b128(
+                        frs, !par ? fo + 8 + (uint32_t)L - 64 + 16 * m : kOff, 0, 0);
+                    lastp[k] = make_uint4(l4.x, l4.y, l4.z, l4.w);
+                }
 #pragma unroll
-            for (uint32_t k = 0; k < K; ++k) {
-                const int64_t i = i0 + g + 32 * k;
-                finish(k, i, i >= 0 && (uint64_t)i < N, hdr[k], stored[k], init0, init1, pc[k], lastp[k]);
-            }
+                for (uint32_t k = 0; k < K; ++k) {
+                    const int64_t i = i0 + g + 32 * k;
+                    finish(QT, k, i, i >= 0 && (uint64_t)i < N, hdr[k], stored[k], init0, init1, pc[k], lastp[k]);
+                }
+            };
+            if (ns <= 4)
+                frames(std::integral_constant<int, 2>{});
+            else
+                frames(std::integral_constant<int, 8>{});
         } else
 #pragma unroll 1
         for (uint32_t k = 0; k < kRecFrames / 32; ++k) {
@@ -349,7 +376,7 @@ __device__ __forceinline__ void decode_record_block(const RecTask &inl, const ui
                 pc[q] = valid && (2 * (uint64_t)q + par < ns) ? ld128_any(hb + 1024 * nbF + 128 * q)
                                                               : make_uint4(0, 0, 0, 0);
             const uint4 lastp = valid && !par ? ld128_any(fb + 8 + L - 64 + 16 * m) : make_uint4(0, 0, 0, 0);
-            finish(k, i, valid, hdr, stored, a0, a1, pc, lastp);
+            finish(std::integral_constant<int, 8>{}, k, i, valid, hdr, stored, a0, a1, pc, lastp);
         }
     } else if (threadIdx.x < kRecFrames) {
         // one lane per frame: header checks, short-frame hashes (<= 240 B), positions
@@ -827,7 +854,12 @@ __global__ __launch_bounds__(kRecThreads) void k_decode_service(SvcMailbox *mb, 
             RecTask tk;
             tk.off = 0; tk.len = u64(0); tk.pos_base = 0; tk.pos_cap = u64(1); tk.msg_base = 0;
             tk.bsum_base = 0; tk.wg0 = 0; tk.nwg = nwg;
-            const uint8_t *base = (const uint8_t *)u64(2);
+            // (made a global-space pointer first: a plain pointer out of LDS words is
+            // loaded through with flat loads, which count on lgkmcnt too, and the frames'
+            // whole load round was then waited for with vmcnt(0) lgkmcnt(0) before the
+            // first frame's hash; global loads let each frame's hash start when its own
+            // bytes have landed)
+            const uint8_t *base = (const uint8_t *)(const __attribute__((address_space(1))) uint8_t *)u64(2);
             uint64_t *fpos = (uint64_t *)u64(3);
             iggy_decode_result *res = (iggy_decode_result *)u64(4);
             uint32_t *flag = (uint32_t *)u64(5);
