@@ -708,6 +708,14 @@ static_assert(sizeof(SvcMailbox) == 128 + 16 * kSvcPre + 64, "mailbox layout");
 // behind a release, read behind an acquire and re-checked behind a second one, ~1.9 us
 // from the leader seeing the post to the followers starting.
 constexpr uint32_t kSvcPost = 76 + 18;
+#ifndef IGGY_SVC_DIRECT
+#define IGGY_SVC_DIRECT 1
+#endif
+#ifndef IGGY_SVC_INFLIGHT
+#define IGGY_SVC_INFLIGHT 1
+#endif
+constexpr bool kSvcDirect = IGGY_SVC_DIRECT;      // followers poll the mailbox themselves (no relay)
+constexpr int kSvcInflight = IGGY_SVC_INFLIGHT;   // mailbox polls in flight per poller: 1 or 4
 constexpr uint32_t kSvcUnits = kSvcPost / 2;
 struct SvcCtl {                        // device memory, zeroed before every launch
     uint4 unit[kSvcUnits];             // the relayed post (tagged granules, see above)
@@ -758,19 +766,26 @@ __global__ __launch_bounds__(kRecThreads) void k_decode_service(SvcMailbox *mb, 
     for (;;) {
         if (wave == 0) {  // (wave-uniform control flow: every decision comes from a shuffle)
             uint32_t cmd = 2;
-            if (blockIdx.x == 0) {
-                // The leader: the host's mailbox, one load round per poll, four polls in
-                // flight (each waits only for the oldest), so a post is seen about one
-                // host-link round trip after it lands instead of up to two.
+            const bool leader = blockIdx.x == 0;
+            if (leader || kSvcDirect) {
+                // The host's mailbox, one load round per poll (kSvcInflight polls in
+                // flight, each waiting only for the oldest). The leader decides stop and
+                // idle exit; a follower (kSvcDirect) polls the mailbox too, so it starts
+                // with the leader instead of a device hand-off later, and stops on the
+                // leader's exit word, which its lane 34 loads beside the chunks.
                 const uint32_t cidx = (uint32_t)min(lane, 8 + (int)kSvcPre - 1);
                 const bool tagged = lane < 6 || (lane >= 8 && lane < 8 + (int)kSvcPre);
-                // returns true when the poll v decides (a new post: cmd 1; stop, idle or
-                // the bug guard: cmd 2)
+                const int xl = leader ? 6 : 34;  // (the stop word / the leader's exit word)
+                const uint64_t t0 = rt_now();
+                auto poll = [&]() -> uint4 {
+                    return !leader && lane == 34 ? svc_unit_dev(ctl, kSvcUnits) : svc_chunk_sys(mb, cidx);
+                };
+                // returns true when the poll v decides (a new post: cmd 1; stop, idle, the
+                // leader's exit or the bug guard: cmd 2)
                 auto take = [&](const uint4 &v) -> bool {
-                    if (__shfl((int)v.x, 6)) return true;  // stop
+                    if (__shfl((int)v.x, xl)) return true;
                     const uint32_t s0 = (uint32_t)__shfl((int)v.x, 0);
                     if (s0 != 0 && s0 != seen && __ballot(tagged && v.x != s0) == 0) {  // a whole new post
-                        const bool relay = (uint32_t)__shfl((int)v.y, 1) > 1;  // (a one-block post is the leader's alone)
                         if (lane < 6) {  // chunk lane's words
                             uint32_t *d = s_post + 76 + 3u * (uint32_t)lane;
                             d[0] = v.y; d[1] = v.z; d[2] = v.w;
@@ -781,12 +796,16 @@ __global__ __launch_bounds__(kRecThreads) void k_decode_service(SvcMailbox *mb, 
                             if (lane < 8 + (int)kSvcPre - 1) { d[1] = v.z; d[2] = v.w; }
                         }
                         if (lane == 0) s_post[kSvcPost] = s0;
-                        // (this wave's own LDS writes have landed; the memory clobber keeps
-                        // the reads below after them)
-                        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-                        if (relay && lane < (int)kSvcUnits)
-                            svc_unit_store(ctl, (uint32_t)lane, make_uint4(s0, s_post[2 * lane], s0, s_post[2 * lane + 1]));
-                        if (kDiagMask && lane == 0) {  // (diagnostic build: when the post was seen)
+                        if (leader && !kSvcDirect) {
+                            const bool relay = (uint32_t)__shfl((int)v.y, 1) > 1;  // (a one-block post is the leader's alone)
+                            // (this wave's own LDS writes have landed; the memory clobber
+                            // keeps the reads below after them)
+                            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                            if (relay && lane < (int)kSvcUnits)
+                                svc_unit_store(ctl, (uint32_t)lane,
+                                               make_uint4(s0, s_post[2 * lane], s0, s_post[2 * lane + 1]));
+                        }
+                        if (kDiagMask && leader && lane == 0) {  // (diagnostic build: when the post was seen)
                             const uint64_t t = rt_now();
                             ctl->diag[0] = (uint32_t)t;
                             ctl->diag[1] = (uint32_t)(t >> 32);
@@ -796,29 +815,35 @@ __global__ __launch_bounds__(kRecThreads) void k_decode_service(SvcMailbox *mb, 
                         return true;
                     }
                     const uint64_t now = rt_now();
+                    if (!leader) return now - t0 > kSpinLimitTicks * 16;  // bug guard (the leader always ends with exit)
                     return now - t_idle > kSvcIdleTicks || now - t_guard > kSpinLimitTicks * 16;
                 };
-                uint4 p0 = svc_chunk_sys(mb, cidx);
-                __builtin_amdgcn_s_sleep(2);
-                uint4 p1 = svc_chunk_sys(mb, cidx);
-                __builtin_amdgcn_s_sleep(2);
-                uint4 p2 = svc_chunk_sys(mb, cidx);
-                for (;;) {
+                if (kSvcInflight == 1) {
+                    for (;;)
+                        if (take(poll())) break;
+                } else {
+                    uint4 p0 = poll();
                     __builtin_amdgcn_s_sleep(2);
-                    uint4 p3 = svc_chunk_sys(mb, cidx);
-                    if (take(p0)) break;
+                    uint4 p1 = poll();
                     __builtin_amdgcn_s_sleep(2);
-                    p0 = svc_chunk_sys(mb, cidx);
-                    if (take(p1)) break;
-                    __builtin_amdgcn_s_sleep(2);
-                    p1 = svc_chunk_sys(mb, cidx);
-                    if (take(p2)) break;
-                    __builtin_amdgcn_s_sleep(2);
-                    p2 = svc_chunk_sys(mb, cidx);
-                    if (take(p3)) break;
+                    uint4 p2 = poll();
+                    for (;;) {
+                        __builtin_amdgcn_s_sleep(2);
+                        uint4 p3 = poll();
+                        if (take(p0)) break;
+                        __builtin_amdgcn_s_sleep(2);
+                        p0 = poll();
+                        if (take(p1)) break;
+                        __builtin_amdgcn_s_sleep(2);
+                        p1 = poll();
+                        if (take(p2)) break;
+                        __builtin_amdgcn_s_sleep(2);
+                        p2 = poll();
+                        if (take(p3)) break;
+                    }
                 }
                 __builtin_amdgcn_s_waitcnt(0);  // the polls still in flight, the relay stores and the LDS writes
-                if (cmd != 1 && lane == 0)  // the followers stop on this word
+                if (leader && cmd != 1 && lane == 0)  // the followers stop on this word
                     __hip_atomic_store(&ctl->exit, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 if (lane == 0) s_cmd = cmd;
             } else {  // a follower: the leader's latest relay (one sc1 load round per poll)
