@@ -5,7 +5,8 @@
 # failure ends the script.
 set -u
 cd ${GRAFT_REPO_ROOT:-$(pwd)}
-STEPS="tests smoke bench phase" bash scripts/gpu_round.sh r6f || exit $?
-bash scripts/profile_round.sh r06f || exit $?
+TAG=${1:-r6f}
+STEPS="tests smoke bench phase" bash scripts/gpu_round.sh $TAG || exit $?
+bash scripts/profile_round.sh r0${TAG#r} || exit $?
 bash scripts/c3_profile.sh || exit $?
 bash scripts/enc_pmc.sh || exit $?
