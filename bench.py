@@ -461,6 +461,9 @@ def c1_leg(cx, dev, seconds: float):
         "cpu_ref_encode_us_per_batch": round(recs[0].size / enc * 1e6, 1),
         "cpu_ref_decode_us_per_batch": round(recs[0].size / dec * 1e6, 1),
         "wire_bytes": wire,
+        "sync_note": ("gpu_host_sync_*: iggy_codec_decode_batch (decode_batch_slice_with's synchronous shape) per "
+                      "call; *_service_*: the same calls after iggy_codec_service_start (resident workgroups, no "
+                      "launch per call; opt-in per context), the others launch one kernel per call"),
     }
 
 
