@@ -144,6 +144,7 @@ constexpr uint32_t kSvcWgs_ = 8;  // (k_decode_service's kSvcWgs)
 struct SvcHand {
     uint4 *units;  // [(block - 1) * kSvcRecUnits + u] (device memory, sc1)
     uint32_t seq;
+    uint64_t *bdiag = nullptr;  // (diagnostic build) [2 b]: block b's entry / hashed clocks
 };
 
 template <bool VERIFY>
@@ -455,6 +456,10 @@ __device__ __forceinline__ void decode_record_block(const RecTask &inl, const ui
         }
         __syncthreads();
         if (blk != 0) {
+            if (kDiagMask && stamp && hand.bdiag && threadIdx.x == 0) {  // (diagnostic build)
+                __hip_atomic_store(&hand.bdiag[2 * blk], stamp[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(&hand.bdiag[2 * blk + 1], stamp[2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
             if (wave == 0 && lane < (int)kSvcRecUnits) {  // (LDS reads: dwords 2 lane, 2 lane + 1)
                 const uint32_t *r32 = (const uint32_t *)(s_recs + 10);
                 // (unit 8: the low words of the first-bad and stride-fail encodings; a frame
@@ -722,8 +727,10 @@ struct SvcCtl {                        // device memory, zeroed before every lau
     uint32_t exit, _e[3];              // unit kSvcUnits: the leader's exit word (1 = exit)
     uint32_t diag[4];                  // (diagnostic build) when the leader saw the post
     uint4 rec[kSvcRecUnits * (kSvcWgs - 1)];  // blocks 1.. of the current post hand their records to block 0 (SvcHand)
+    uint64_t bdiag[2 * kSvcWgs];       // (diagnostic build) every block's entry / hashed clocks
 };
-static_assert(sizeof(SvcCtl) == 16 * kSvcUnits + 32 + 16 * kSvcRecUnits * (kSvcWgs - 1), "control block layout");
+static_assert(sizeof(SvcCtl) == 16 * kSvcUnits + 32 + 16 * kSvcRecUnits * (kSvcWgs - 1) + 16 * kSvcWgs,
+              "control block layout");
 constexpr int kAuxSys = 17;  // buffer-load cache policy sc0 | sc1: system-coherent (host-mapped memory)
 
 __device__ __forceinline__ uint4 svc_chunk_sys(const SvcMailbox *mb, uint32_t c) {
@@ -743,9 +750,16 @@ __device__ __forceinline__ void svc_unit_store(SvcCtl *ctl, uint32_t c, uint4 v)
 }
 
 // (diagnostic build) ticks from the leader seeing the post to the flag store, into the
-// mailbox's chunk 7 (the host reads it beside the flag)
-__device__ __forceinline__ void svc_stamp(SvcMailbox *mb, SvcCtl *ctl, uint64_t *stamp) {
-    stamp[7] = rt_now();
+// mailbox's chunk 7 (the host reads it beside the flag); stamps 6 / 7: the latest
+// follower's entry / hashed clock
+__device__ __forceinline__ void svc_stamp(SvcMailbox *mb, SvcCtl *ctl, uint64_t *stamp, uint32_t nwg) {
+    uint64_t e = stamp[1], h = stamp[2];
+    for (uint32_t b = 1; b < nwg; ++b) {
+        e = max(e, __hip_atomic_load(&ctl->bdiag[2 * b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+        h = max(h, __hip_atomic_load(&ctl->bdiag[2 * b + 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    }
+    stamp[6] = e;
+    stamp[7] = h;
     const uint64_t t0 = (uint64_t)__hip_atomic_load(&ctl->diag[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) |
                         ((uint64_t)__hip_atomic_load(&ctl->diag[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) << 32);
     for (int k = 1; k < 8; ++k)
@@ -889,7 +903,7 @@ __global__ __launch_bounds__(kRecThreads) void k_decode_service(SvcMailbox *mb, 
             iggy_decode_result *res = (iggy_decode_result *)u64(4);
             uint32_t *flag = (uint32_t *)u64(5);
             const uint8_t *s_pre = (const uint8_t *)s_post;
-            const SvcHand hand{ctl->rec, s_post[kSvcPost]};  // (the post's number tags its blocks' records)
+            const SvcHand hand{ctl->rec, s_post[kSvcPost], kDiagMask ? ctl->bdiag : nullptr};  // (the post's number tags its blocks' records)
             if (integ == IGGY_INTEGRITY_VERIFY)
                 decode_record_block<true>(tk, base, nullptr, nullptr, st, bsums, fpos, nullptr, res, blockIdx.x, s_pre,
                                           kDiagMask ? s_stamp : nullptr, hand);
@@ -904,8 +918,7 @@ __global__ __launch_bounds__(kRecThreads) void k_decode_service(SvcMailbox *mb, 
                 if (kDiagMask && threadIdx.x == 0) s_stamp[6] = rt_now();
                 __syncthreads();
                 if (kDiagMask && threadIdx.x == 0) {
-                    s_stamp[7] = rt_now();  // (no counter round any more: "counted" = fenced)
-                    svc_stamp(mb, ctl, s_stamp);
+                    svc_stamp(mb, ctl, s_stamp, nwg);
                     __threadfence_system();
                 }
                 if (threadIdx.x == 0) __hip_atomic_store(flag, flag_value, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);

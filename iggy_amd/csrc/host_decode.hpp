@@ -599,7 +599,7 @@ int decode_host_fast(iggy_codec_ctx *c, const uint8_t *body, uint64_t len, int i
     if (timing && ++tn == timing) {
         fprintf(stderr, "iggy_codec timing (%d calls, us from entry): staged %.2f launched %.2f flag %.2f done %.2f"
                 " service-device %.2f (block entry %.2f hashed %.2f resolver %.2f computed %.2f result %.2f"
-                " fenced %.2f counted %.2f)\n",
+                " followers entered (max) %.2f followers hashed (max) %.2f)\n",
                 tn, tsum[0] / tn, tsum[1] / tn, tsum[2] / tn, tsum[3] / tn, c->svc.dev_ticks[0] * 0.01 / tn,
                 c->svc.dev_ticks[1] * 0.01 / tn, c->svc.dev_ticks[2] * 0.01 / tn, c->svc.dev_ticks[3] * 0.01 / tn,
                 c->svc.dev_ticks[4] * 0.01 / tn, c->svc.dev_ticks[5] * 0.01 / tn, c->svc.dev_ticks[6] * 0.01 / tn,
