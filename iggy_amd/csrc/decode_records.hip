@@ -232,6 +232,9 @@ __device__ __forceinline__ void decode_record_block(const RecTask &inl, const ui
     if (hand.units) store_positions();
     // the resolver's per-lane constants, loaded now rather than on its critical path
     const uint64_t rc_init = kAccInit[lane & 7], rc_key = kSecretW8[16 + (lane & 7)], rc_last = kSecretLast[lane & 7];
+    // and the block's partial sums' (wave 0, after the hashes: a constant-table load there
+    // waited out a cache miss behind the frames' stream)
+    const uint64_t ps_key0 = kSecretW8[(lane >> 3) + (lane & 7)], ps_key1 = kSecretW8[8 + (lane >> 3) + (lane & 7)];
     const int64_t i0 = (int64_t)kRecFrames * blk - 6;
     const uint64_t base_offset = hi.h.base_offset, base_ts = hi.h.base_timestamp, origin = hi.h.origin_timestamp;
     uint64_t mybad = ~0ull, mysf = ~0ull;
@@ -417,9 +420,8 @@ __device__ __forceinline__ void decode_record_block(const RecTask &inl, const ui
         // words m = 128b + j of the checksum input, j = lane, lane + 64
         const uint64_t mb = (uint64_t)kRecFrames * blk;
         uint64_t x = 0, y = 0;
-        word_contrib_s(pl.Mreg, mb + lane, s_cs[lane], s_cs[lane + 1], true, kSecretW8[(lane >> 3) + (lane & 7)], x, y);
-        word_contrib_s(pl.Mreg, mb + 64 + lane, s_cs[64 + lane], s_cs[65 + lane], true,
-                       kSecretW8[8 + (lane >> 3) + (lane & 7)], x, y);
+        word_contrib_s(pl.Mreg, mb + lane, s_cs[lane], s_cs[lane + 1], true, ps_key0, x, y);
+        word_contrib_s(pl.Mreg, mb + 64 + lane, s_cs[64 + lane], s_cs[65 + lane], true, ps_key1, x, y);
         t8 = reduce_acc8(x, y);
         // (sc1: written through, for the resolver's sc1 loads on another CU)
         if (lane < 8 && nblk > 1 && !hand.units)
