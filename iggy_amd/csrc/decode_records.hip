@@ -91,19 +91,38 @@ __device__ __forceinline__ void rec_fill_msg(const uint8_t *rec, uint64_t rec_of
     *out = m;
 }
 
-// min over the WG of per-thread candidates (~0 = none), via wave minima in LDS
-__device__ __forceinline__ uint64_t wg_min(uint64_t v, uint64_t *s4) {
-    for (int d = 32; d; d >>= 1) {
-        const uint64_t o = __shfl_xor(v, d);
-        v = o < v ? o : v;
+// lane l's 64-bit value, wave-uniform (v_readlane)
+__device__ __forceinline__ uint64_t rdlane64(uint64_t v, int l) {
+    return (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, l) |
+           ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), l) << 32);
+}
+
+// minima over the WG of two per-thread candidates (~0 = none), via wave minima in LDS
+// (s8: 2 per wave). A wave without a candidate (a clean block: every wave) skips its
+// shuffle ladder, six dependent 64-bit shuffles of ~0.3 us each pair; the two ladders of
+// a wave that has one run interleaved, and the two minima share one pair of barriers.
+__device__ __forceinline__ void wg_min2(uint64_t &v1, uint64_t &v2, uint64_t *s8) {
+    if (__ballot(v1 != ~0ull || v2 != ~0ull)) {
+        for (int d = 32; d; d >>= 1) {
+            const uint64_t o1 = __shfl_xor(v1, d), o2 = __shfl_xor(v2, d);
+            v1 = o1 < v1 ? o1 : v1;
+            v2 = o2 < v2 ? o2 : v2;
+        }
     }
-    if ((threadIdx.x & 63) == 0) s4[threadIdx.x >> 6] = v;
+    if ((threadIdx.x & 63) == 0) {
+        s8[2 * (threadIdx.x >> 6)] = v1;
+        s8[2 * (threadIdx.x >> 6) + 1] = v2;
+    }
     __syncthreads();
-    uint64_t m = s4[0];
+    uint64_t m1 = s8[0], m2 = s8[1];
 #pragma unroll
-    for (int w = 1; w < (int)(kRecThreads / 64); ++w) m = s4[w] < m ? s4[w] : m;
+    for (int w = 1; w < (int)(kRecThreads / 64); ++w) {
+        m1 = s8[2 * w] < m1 ? s8[2 * w] : m1;
+        m2 = s8[2 * w + 1] < m2 ? s8[2 * w + 1] : m2;
+    }
     __syncthreads();
-    return m;
+    v1 = m1;
+    v2 = m2;
 }
 
 // Launch completion for host callers that spin instead of synchronising the stream:
@@ -161,7 +180,7 @@ __device__ __forceinline__ void decode_record_block(const RecTask &inl, const ui
     };
     mark(1);
     __shared__ uint64_t s_cs[kRecFrames + 2];  // stored checksums of frames 128b - 6 + k
-    __shared__ uint64_t s_min[4];
+    __shared__ uint64_t s_min[2 * (kRecThreads / 64)];
     __shared__ uint32_t s_last;
     __shared__ uint8_t s_small[256];  // short checksum inputs (N <= 24): 44 + 8 N bytes
     // one record: its task comes in the kernel arguments (tasks == nullptr), not from a
@@ -409,8 +428,8 @@ __device__ __forceinline__ void decode_record_block(const RecTask &inl, const ui
     // compiler sank their loads to the resolver, one host-link round trip on its path)
     asm volatile("" ::"v"(r_cs0), "v"(r_lv));
     mark(2);  // (thread 0's own frames hashed)
-    const uint64_t wbad = wg_min(mybad, s_min);  // (its barriers also publish s_cs)
-    const uint64_t wsf = wg_min(mysf, s_min);
+    uint64_t wbad = mybad, wsf = mysf;
+    wg_min2(wbad, wsf, s_min);  // (its barriers also publish s_cs)
     if (threadIdx.x == 0 && nblk > 1 && !hand.units) {  // (a one-block record's own minima are final)
         if (wbad != ~0ull) atomicMax((unsigned long long *)&st[t].first_bad, (unsigned long long)~wbad);
         if (wsf != ~0ull) atomicMax((unsigned long long *)&st[t].spec_fail, (unsigned long long)~wsf);
@@ -541,7 +560,7 @@ __device__ __forceinline__ void decode_record_block(const RecTask &inl, const ui
         const uint64_t key = rc_key;
         const uint32_t klo = (uint32_t)key, khi = (uint32_t)(key >> 32);
         {  // words 0..5: header fields, then count | lo32(cs_0)
-            const uint64_t cs0 = __shfl(r_cs0, 0);
+            const uint64_t cs0 = rdlane64(r_cs0, 0);
             const uint64_t w6[6] = {hi.h.partition_id, hi.h.base_offset, hi.h.base_timestamp,
                                     hi.h.origin_timestamp, hi.h.batch_length,
                                     (uint64_t)hi.h.message_count | (cs0 << 32)};
@@ -563,7 +582,7 @@ __device__ __forceinline__ void decode_record_block(const RecTask &inl, const ui
             const rec_g2 r = __builtin_amdgcn_raw_buffer_load_b64(rs, (uint32_t)(64 * b + 8 * j), 0, kAuxSc1);
             return (uint64_t)r.x | ((uint64_t)r.y << 32);
         };
-        uint64_t y = acc + (nblk > 1 ? sum_at(0) : __shfl(t8, j));  // (one block: pl.nb == 0)
+        uint64_t y = acc + (nblk > 1 ? sum_at(0) : t8);  // (one block: pl.nb == 0; lane j < 8 holds sum j)
         uint64_t b = 1;
         uint64_t v[16];
         for (; b <= nb; b += 16) {  // groups of up to 16 blocks: the group's loads, then its steps
@@ -575,12 +594,12 @@ __device__ __forceinline__ void decode_record_block(const RecTask &inl, const ui
         }
         acc = y;
         // last stripe = stored checksums of frames N-8 .. N-1 (secret offset 121)
-        const uint64_t lv = __shfl(r_lv, j);
-        acc += __shfl_xor(lv, 1);
+        const uint64_t lv = r_lv;  // (lane j < 8 loaded frame N - 8 + j's; only lanes 0..7 carry on)
+        acc += gdpp64<0xB1>(lv);   // (lane j ^ 1's)
         acc += mul32x32(lv ^ rc_last);
         uint64_t a[8];
 #pragma unroll
-        for (int i = 0; i < 8; ++i) a[i] = __shfl(acc, i);
+        for (int i = 0; i < 8; ++i) a[i] = rdlane64(acc, i);  // (v_readlane: no LDS round trip)
         uint64_t r = pl.n * P64_1;
 #pragma unroll
         for (int i = 0; i < 4; ++i)
