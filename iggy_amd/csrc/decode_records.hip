@@ -543,9 +543,13 @@ __device__ __forceinline__ void decode_record_block(const RecTask &inl, const ui
     // (one block: this workgroup's own minima and partial sums, no memory round trip)
     uint64_t fb_enc = 0, sf_enc = 0;
     if (hand.units && nblk > 1) {  // (service) the blocks' records, max-encoded minima
-        for (uint64_t b = 0; b < nblk; ++b) {
-            fb_enc = max(fb_enc, s_recs[10 * b + 8]);
-            sf_enc = max(sf_enc, s_recs[10 * b + 9]);
+        // (lane b reads block b's pair, one LDS round; then v_readlane, not one LDS round
+        // trip per block)
+        const uint64_t f = (uint64_t)lane < nblk ? s_recs[10 * lane + 8] : 0ull;
+        const uint64_t g = (uint64_t)lane < nblk ? s_recs[10 * lane + 9] : 0ull;
+        for (uint32_t b = 0; b < (uint32_t)nblk; ++b) {
+            fb_enc = max(fb_enc, rdlane64(f, (int)b));
+            sf_enc = max(sf_enc, rdlane64(g, (int)b));
         }
     } else {
         fb_enc = nblk > 1 ? __hip_atomic_load(&st[t].first_bad, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
