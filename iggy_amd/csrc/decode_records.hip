@@ -597,6 +597,9 @@ __device__ __forceinline__ void decode_record_block(const RecTask &inl, const ui
                 if (b + q <= nb) y = chain_step(y, v[q], klo, khi);
         }
         acc = y;
+#ifdef IGGY_DIAG_CHAIN
+        mark(5);  // (diagnostic bisect build, -DIGGY_DIAG_CHAIN: the chain done, not the result written)
+#endif
         // last stripe = stored checksums of frames N-8 .. N-1 (secret offset 121)
         const uint64_t lv = r_lv;  // (lane j < 8 loaded frame N - 8 + j's; only lanes 0..7 carry on)
         acc += gdpp64<0xB1>(lv);   // (lane j ^ 1's)
@@ -663,7 +666,9 @@ __device__ __forceinline__ void decode_record_block(const RecTask &inl, const ui
         kind = IGGY_ERR_TIMEOUT; reason = 0; a = b = c = 0; status = kStatusDone;
     }
     write_result(res, hi, kind, reason, a, b, c, nframes, computed, 1, status, nframes * S);
+#ifndef IGGY_DIAG_CHAIN
     mark(5);
+#endif
 }
 
 // tasks / wg_task may live in host-mapped pinned memory (read once per workgroup);
@@ -955,6 +960,8 @@ __global__ __launch_bounds__(kRecThreads) void k_decode_service(SvcMailbox *mb, 
         // this one's lines -- a corrupt frame judged on the clean bytes of the call before
         // (measured). The launch path gets this from every launch's acquire. Here it comes
         // after the flag (block 0) or the hand-over (the others): off the post's path.
+        // (System scope: L1 and L2. Agent scope, the L1 alone, passed the service tests
+        // and saved 0.27 us per call, but nothing shows the L2 holds no host lines.)
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
         __syncthreads();  // (s_cmd / s_post are rewritten by the next relay)
     }
