@@ -750,7 +750,7 @@ constexpr uint32_t kSvcPost = 76 + 18;
 #define IGGY_SVC_INFLIGHT 1
 #endif
 constexpr bool kSvcDirect = IGGY_SVC_DIRECT;      // followers poll the mailbox themselves (no relay)
-constexpr int kSvcInflight = IGGY_SVC_INFLIGHT;   // mailbox polls in flight per poller: 1 or 4
+constexpr int kSvcInflight = IGGY_SVC_INFLIGHT;   // mailbox polls in flight per poller: 1, 2 or 4
 constexpr uint32_t kSvcUnits = kSvcPost / 2;
 struct SvcCtl {                        // device memory, zeroed before every launch
     uint4 unit[kSvcUnits];             // the relayed post (tagged granules, see above)
@@ -865,6 +865,16 @@ __global__ __launch_bounds__(kRecThreads) void k_decode_service(SvcMailbox *mb, 
                 if (kSvcInflight == 1) {
                     for (;;)
                         if (take(poll())) break;
+                } else if (kSvcInflight == 2) {
+                    uint4 p0 = poll();
+                    __builtin_amdgcn_s_sleep(8);
+                    uint4 p1 = poll();
+                    for (;;) {
+                        if (take(p0)) break;
+                        p0 = poll();
+                        if (take(p1)) break;
+                        p1 = poll();
+                    }
                 } else {
                     uint4 p0 = poll();
                     __builtin_amdgcn_s_sleep(2);
