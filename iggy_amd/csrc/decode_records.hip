@@ -713,6 +713,7 @@ __global__ __launch_bounds__(kRecThreads) void k_decode_records(const uint8_t *_
 constexpr uint32_t kSvcWgs = kSvcWgs_;                // records of <= 8 blocks (C1: 1 000 frames)
 constexpr uint32_t kSvcPre = 26;                      // 12-B pieces of the record's first 304 B
 constexpr uint64_t kSvcIdleTicks = 100000ull * 20;    // 20 ms without a post: exit
+constexpr uint64_t kSvcBackoffTicks = 100ull * 200;   // 200 us without a post: poll every ~4 us
 // Host-mapped mailbox: 8 chunks of 16 B, read by the leader's wave in ONE round of loads
 // (lane c takes chunk c). Chunks 0-5 hold the post and carry its sequence number in
 // their first word, written by the host after the chunk's other words, so a load
@@ -863,8 +864,13 @@ __global__ __launch_bounds__(kRecThreads) void k_decode_service(SvcMailbox *mb, 
                     return now - t_idle > kSvcIdleTicks || now - t_guard > kSpinLimitTicks * 16;
                 };
                 if (kSvcInflight == 1) {
-                    for (;;)
+                    for (;;) {
                         if (take(poll())) break;
+                        // (idle for kSvcBackoffTicks: ~4 us between polls, so a service
+                        // alive between sparse posts reads ~0.8 GB/s over the host link,
+                        // not ~3 GB/s; back-to-back posts never get here)
+                        if (rt_now() - t_idle > kSvcBackoffTicks) __builtin_amdgcn_s_sleep(127);
+                    }
                 } else if (kSvcInflight == 2) {
                     uint4 p0 = poll();
                     __builtin_amdgcn_s_sleep(8);

@@ -6,7 +6,8 @@ in one process, each library's service started and stopped within its own round.
 call's result is checked by the loop (rc, frame count); the positions once per round
 against the oracle.
 
-usage: python scripts/svc_ab.py <lib A .so> <lib B .so> [...] [--rounds 8] [--reps 300]
+usage: python scripts/svc_ab.py <lib A .so> <lib B .so> [...] [--rounds 8] [--reps 300] [--gap-us G]
+(--gap-us: sparse posts, G us of idle spin between calls, each call timed alone from Python)
 """
 import argparse
 import ctypes
@@ -14,6 +15,7 @@ import json
 import os
 import statistics
 import sys
+import time
 
 import numpy as np
 
@@ -30,6 +32,7 @@ def main():
     ap.add_argument("libs", nargs="+")
     ap.add_argument("--rounds", type=int, default=8)
     ap.add_argument("--reps", type=int, default=300)
+    ap.add_argument("--gap-us", type=float, default=0.0)
     args = ap.parse_args()
     torch.cuda.set_device(0)
     c_loop = ctypes.CDLL(os.path.join(ROOT, "scripts", "_c_loop.so"))
@@ -59,7 +62,19 @@ def main():
                  P(rec.ctypes.data), U(rec.size), P(pos.ctypes.data), U(pos.size), U(len(want[3])), 1,
                  abi.INTEGRITY_VERIFY)
             assert c_loop.c_loop_decode(*a, 20) > 0
-            ns = c_loop.c_loop_decode(*a, args.reps)
+            if args.gap_us > 0:
+                ts = []
+                for _ in range(args.reps // 4):
+                    t_end = time.perf_counter() + args.gap_us * 1e-6
+                    while time.perf_counter() < t_end:
+                        pass
+                    t0 = time.perf_counter()
+                    rc, nf = cx.decode_batch_into(rec, abi.INTEGRITY_VERIFY, pos)
+                    ts.append(time.perf_counter() - t0)
+                    assert rc == 0
+                ns = statistics.median(ts) * 1e9
+            else:
+                ns = c_loop.c_loop_decode(*a, args.reps)
             assert ns > 0, ns
             rc, nf = cx.decode_batch_into(rec, abi.INTEGRITY_VERIFY, pos)
             assert rc == 0 and np.array_equal(pos[:nf], np.asarray(want[3], dtype=np.uint64)), p
